@@ -1,0 +1,238 @@
+"""aniso_amd -- MI355X-native matvec of the lowrank/aniso anisotropic RTE solver.
+
+Host-side mirror of the reference's plugin interface: the MATLAB handle class
+`Aniso` (class/@Aniso/Aniso.m:1-34) over the MEX ops new/delete/getNodes/
+setCoeff/cache/mapping (AnisoWrapper.cpp:10-136).  Everything here calls the C ABI
+of `libaniso_mi355x.so` (include/aniso_mi355x.h); the compute runs in the HIP
+kernels of aniso_amd/csrc.  There is no CPU fallback: a missing library or a
+missing GPU raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libaniso_mi355x.so")
+_lib = None
+
+STAGE_FAR, STAGE_NEAR, STAGE_STENCIL, STAGE_SING, STAGE_ALL = 1, 2, 4, 8, 15
+
+
+class AnisoError(RuntimeError):
+    """Raised for any non-zero status of the C ABI (mexErrMsgIdAndTxt analogue)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"[aniso status {code}] {msg}")
+        self.code = code
+
+
+def lib():
+    """Load the C ABI library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise AnisoError(-1, f"{LIB_PATH} not built; run `make -C aniso_amd/csrc`")
+        L = ctypes.CDLL(LIB_PATH)
+        P, I, D, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_int64
+        dp, ip, lp = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int64)
+        fp = ctypes.POINTER(ctypes.c_float)
+        sig = {
+            "aniso_create": [I, I, I, D, I, I, I, ctypes.POINTER(P)],
+            "aniso_destroy": [P],
+            "aniso_num_nodes": [P, lp],
+            "aniso_get_nodes": [P, dp],
+            "aniso_get_weights": [P, dp],
+            "aniso_set_coeff": [P, dp, dp],
+            "aniso_cache": [P, I],
+            "aniso_mapping": [P, dp, I, dp],
+            "aniso_mapping_dev": [P, P, I, P, P],
+            "aniso_mapping_batched": [P, dp, I, I, dp],
+            "aniso_mapping_stages_dev": [P, P, I, I, P, P],
+            "aniso_set_shard": [P, I, I],
+            "aniso_get_shard": [P, lp, lp],
+            "aniso_tree_perm": [P, ip],
+            "aniso_permute_to_tree_dev": [P, P, P, P],
+            "aniso_tree_size": [P, ip, ip],
+            "aniso_tree_nodes": [P, ip, dp],
+            "aniso_tree_list": [P, I, lp, ip],
+            "aniso_stats": [P, lp],
+            "aniso_set_timing": [P, I],
+            "aniso_stage_times": [P, fp],
+            "aniso_line_integrals": [P, dp, I, dp],
+            "aniso_last_error": [ctypes.c_char_p, ctypes.c_size_t],
+        }
+        for name, args in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = I
+        L.aniso_version.restype = ctypes.c_char_p
+        L.aniso_version.argtypes = []
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    """Names of the entry points declared in include/aniso_mi355x.h."""
+    hdr = open(os.path.join(_HERE, "..", "include", "aniso_mi355x.h")).read()
+    import re
+
+    return sorted(set(re.findall(r"^(?:int|const char \*)\s*\**\s*(aniso_\w+)\s*\(", hdr, re.M)))
+
+
+def _check(code):
+    if code != 0:
+        buf = ctypes.create_string_buffer(4096)
+        lib().aniso_last_error(buf, len(buf))
+        raise AnisoError(code, buf.value.decode(errors="replace"))
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _f64(a, n, name):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1))
+    if a.size != n:
+        raise AnisoError(1, f"{name} has {a.size} entries, expected N = {n}")
+    return a
+
+
+class Aniso:
+    """Aniso(ds, qr, ks, as, sr, fn, fm) -- class/@Aniso/Aniso.m:8-11.
+
+    ds: squares per side, qr: quadrature rule, ks: kernel size (modes 0..2ks-2),
+    as: anisotropy g, sr: singular rule, fn: FMM np (4), fm: FMM maxLevel.
+    """
+
+    def __init__(self, ds, qr, ks, as_, sr, fn, fm):
+        h = ctypes.c_void_p()
+        _check(lib().aniso_create(int(ds), int(qr), int(ks), float(as_), int(sr), int(fn), int(fm), ctypes.byref(h)))
+        self.address = h
+        n = ctypes.c_int64()
+        _check(lib().aniso_num_nodes(h, ctypes.byref(n)))
+        self.N = n.value
+        self.sz, self.d, self.ks, self.g, self.ns, self.np, self.maxLevel = int(ds), int(qr), int(ks), float(as_), int(sr), int(fn), int(fm)
+
+    # 'delete' (Aniso.m:13-16)
+    def close(self):
+        if getattr(self, "address", None):
+            lib().aniso_destroy(self.address)
+            self.address = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def getNodes(self):
+        """N x 2 array of quadrature nodes (Aniso.m:22-24)."""
+        xy = np.zeros(2 * self.N)
+        _check(lib().aniso_get_nodes(self.address, _dp(xy)))
+        return xy.reshape(2, self.N).T.copy()
+
+    def getWeights(self):
+        w = np.zeros(self.N)
+        _check(lib().aniso_get_weights(self.address, _dp(w)))
+        return w
+
+    def setCoeff(self, sigma_s, sigma_t):
+        """Aniso.m:18-20."""
+        s = _f64(sigma_s, self.N, "sigma_s")
+        t = _f64(sigma_t, self.N, "sigma_t")
+        _check(lib().aniso_set_coeff(self.address, _dp(s), _dp(t)))
+
+    def cache(self, id_):
+        """Aniso.m:26-28."""
+        _check(lib().aniso_cache(self.address, int(id_)))
+
+    def mapping(self, charge, id_):
+        """Aniso.m:30-32: returns K_id * charge (N,)."""
+        c = _f64(charge, self.N, "charge")
+        out = np.zeros(self.N)
+        _check(lib().aniso_mapping(self.address, _dp(c), int(id_), _dp(out)))
+        return out
+
+    def mapping_batched(self, Q, id_):
+        Q = np.asfortranarray(np.asarray(Q, dtype=np.float64))
+        if Q.ndim != 2 or Q.shape[0] != self.N:
+            raise AnisoError(1, f"Q must be N x k with N = {self.N}")
+        out = np.zeros(Q.shape, order="F")
+        _check(lib().aniso_mapping_batched(self.address, _dp(Q), Q.shape[1], int(id_), _dp(out)))
+        return out
+
+    # ---- device-pointer variants (torch tensors on the current HIP device)
+    def mapping_dev(self, charge, id_, out, stream=None, mask=STAGE_ALL):
+        """charge/out: contiguous float64 torch tensors of N entries on the GPU."""
+        import torch
+
+        for t, nm in ((charge, "charge"), (out, "out")):
+            if not (t.is_cuda and t.dtype == torch.float64 and t.is_contiguous() and t.numel() == self.N):
+                raise AnisoError(1, f"{nm} must be a contiguous float64 CUDA tensor of {self.N} entries")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        if mask == STAGE_ALL:
+            _check(lib().aniso_mapping_dev(self.address, ctypes.c_void_p(charge.data_ptr()), int(id_),
+                                           ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(s)))
+        else:
+            _check(lib().aniso_mapping_stages_dev(self.address, ctypes.c_void_p(charge.data_ptr()), int(id_), int(mask),
+                                                  ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(s)))
+        return out
+
+    def set_shard(self, rank, nranks):
+        _check(lib().aniso_set_shard(self.address, int(rank), int(nranks)))
+
+    def shard(self):
+        b, e = ctypes.c_int64(), ctypes.c_int64()
+        _check(lib().aniso_get_shard(self.address, ctypes.byref(b), ctypes.byref(e)))
+        return b.value, e.value
+
+    def tree_perm(self):
+        p = np.zeros(self.N, dtype=np.int32)
+        _check(lib().aniso_tree_perm(self.address, p.ctypes.data_as(ctypes.POINTER(ctypes.c_int))))
+        return p
+
+    def tree_size(self):
+        nn, ml = ctypes.c_int(), ctypes.c_int()
+        _check(lib().aniso_tree_size(self.address, ctypes.byref(nn), ctypes.byref(ml)))
+        return nn.value, ml.value
+
+    def tree_nodes(self):
+        nn, _ = self.tree_size()
+        ints = np.zeros((nn, 11), dtype=np.int32)
+        geom = np.zeros((nn, 4))
+        _check(lib().aniso_tree_nodes(self.address, ints.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _dp(geom)))
+        return ints, geom
+
+    def tree_list(self, which):
+        nn, _ = self.tree_size()
+        ptr = np.zeros(nn + 1, dtype=np.int64)
+        _check(lib().aniso_tree_list(self.address, int(which), ptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
+        idx = np.zeros(int(ptr[-1]), dtype=np.int32)
+        _check(lib().aniso_tree_list(self.address, int(which), ptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                     idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int))))
+        return ptr, idx
+
+    def stats(self):
+        s = np.zeros(8, dtype=np.int64)
+        _check(lib().aniso_stats(self.address, s.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        keys = ["near_entries", "m2l_entries", "m2l_pairs", "leaves", "m2l_targets", "tree_nodes", "max_leaf", "N"]
+        return dict(zip(keys, (int(v) for v in s)))
+
+    def set_timing(self, on):
+        _check(lib().aniso_set_timing(self.address, int(bool(on))))
+
+    def stage_times(self):
+        t = (ctypes.c_float * 7)()
+        _check(lib().aniso_stage_times(self.address, t))
+        return dict(zip(["prep", "up", "m2l", "l2l", "near_l2p", "corr", "total"], list(t)))
+
+    def line_integrals(self, seg):
+        seg = np.ascontiguousarray(np.asarray(seg, dtype=np.float64).reshape(-1, 4))
+        out = np.zeros(seg.shape[0])
+        _check(lib().aniso_line_integrals(self.address, _dp(seg), seg.shape[0], _dp(out)))
+        return out
+
+
+def version():
+    return lib().aniso_version().decode()

@@ -1,0 +1,359 @@
+// aniso_op.hip -- host orchestration of the MI355X operator (one per handle).
+//
+// Lifecycle mirrors the reference's MEX ops (AnisoWrapper.cpp:10-136):
+//   Operator()  <- 'new'       geometry + quadtree + lists on the host (no GPU)
+//   setCoeff    <- 'setCoeff'  sigma coefficients; uploads geometry/tree to HBM
+//   cache(m)    <- 'cache'     device-side build of the merged pair operators
+//   mapping*    <- 'mapping'   one apply, all stages on the GPU
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+#include "aniso_op.hpp"
+#include "kernels.hpp"
+
+namespace aniso {
+
+[[noreturn]] void throw_hip(hipError_t e, const char* file, int line) {
+    throw std::runtime_error(std::string("HIP error ") + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ") at " +
+                             file + ":" + std::to_string(line));
+}
+
+#define HIP_CHECK(x)                                         \
+    do {                                                     \
+        hipError_t e__ = (x);                                \
+        if (e__ != hipSuccess) throw_hip(e__, __FILE__, __LINE__); \
+    } while (0)
+
+DevBuf::~DevBuf() {
+    if (p) (void)hipFree(p);
+}
+
+void DevBuf::alloc(size_t nbytes) {
+    if (p && bytes == nbytes) return;
+    if (p) {
+        HIP_CHECK(hipFree(p));
+        p = nullptr;
+    }
+    bytes = nbytes;
+    if (nbytes) HIP_CHECK(hipMalloc(&p, nbytes));
+}
+
+void DevBuf::upload(const void* host, size_t nbytes) {
+    alloc(nbytes);
+    if (nbytes) HIP_CHECK(hipMemcpy(p, host, nbytes, hipMemcpyHostToDevice));
+}
+
+template <class T>
+static void up(DevBuf& b, const std::vector<T>& v) {
+    b.upload(v.data(), v.size() * sizeof(T));
+}
+
+static int host_threads() {
+    unsigned n = std::thread::hardware_concurrency();
+    return n ? (int)std::min(n, 16u) : 4;
+}
+
+Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxLevel_)
+    : ks(ks_), ns(ns_), np(np_), maxLevel(maxLevel_), g(g_) {
+    if (ks < 1) throw std::invalid_argument("kernel size must be >= 1");
+    if (np != kNP) throw std::invalid_argument("np must be 4 on the MI355X path (rank-16 Chebyshev)");
+    if (d < 1 || d > kMaxD) throw std::invalid_argument("quadRule must be in 1..6 on the MI355X path");
+    if (maxLevel < 0) throw std::invalid_argument("maxLevel must be >= 0");
+    kernelSize = 2 * ks - 1;
+    geo.build(sz, d, ns);
+    tree.build(geo.px.data(), geo.py.data(), geo.N, np * np, maxLevel, host_threads());
+    plan.build(tree, np, 0, 1);
+    sigma_s.assign(geo.N, 0.0);
+    sigma_t.assign(geo.N, 0.0);
+    modes.resize(kernelSize);
+}
+
+Operator::~Operator() {
+    if (device >= 0) {
+        (void)hipSetDevice(device);
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (own) (void)hipStreamDestroy(own);
+    }
+}
+
+void Operator::getNodes(double* xy) const {
+    for (int64_t i = 0; i < geo.N; ++i) {
+        xy[i] = geo.px[i];
+        xy[i + geo.N] = geo.py[i];
+    }
+}
+
+void Operator::setShard(int rank, int nranks) {
+    plan.build(tree, np, rank, nranks);
+    for (auto& m : modes) {
+        m.Knear.alloc(0);
+        m.Km2l.alloc(0);
+        m.ready = false;
+    }
+    if (device >= 0) uploadPlan();
+}
+
+void Operator::ensureDevice() {
+    if (device >= 0) {
+        HIP_CHECK(hipSetDevice(device));
+        return;
+    }
+    HIP_CHECK(hipGetDevice(&device));
+    HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+    for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+    // tree-order coordinates
+    std::vector<double> pxT(geo.N), pyT(geo.N);
+    for (int64_t k = 0; k < geo.N; ++k) {
+        pxT[k] = geo.px[tree.perm[k]];
+        pyT[k] = geo.py[tree.perm[k]];
+    }
+    up(dPxT, pxT);
+    up(dPyT, pyT);
+    up(dPerm, tree.perm);
+    up(dW, geo.w);
+    up(dNcx, tree.ncx);
+    up(dNcy, tree.ncy);
+    up(dNrx, tree.nrx);
+    up(dNry, tree.nry);
+    up(dBegin, tree.begin);
+    up(dCount, tree.count);
+    up(dParent, tree.parent);
+    up(dSlot, tree.slot);
+    std::vector<int4> ch(tree.nn);
+    for (int i = 0; i < tree.nn; ++i) ch[i] = make_int4(tree.child[i][0], tree.child[i][1], tree.child[i][2], tree.child[i][3]);
+    for (auto& c : ch) {  // leaves: point children at self (never dereferenced for non-leaves)
+        if (c.x < 0) c = make_int4(0, 0, 0, 0);
+    }
+    up(dChild, ch);
+    // parameter block
+    Params P;
+    std::memset(&P, 0, sizeof(P));
+    P.sz = geo.sz;
+    P.d = geo.d;
+    P.d2 = geo.d2;
+    P.nsq = geo.nsq;
+    P.dx = geo.dx;
+    for (int i = 0; i < geo.d; ++i) {
+        P.gx[i] = geo.gx[i];
+        P.gw[i] = geo.gw[i];
+    }
+    // Chebyshev nodes / polynomials / transfer operators (bbfmm.h:597-693)
+    for (int i = 0; i < kNP; ++i) P.cheb[i] = -std::cos((i + 0.5) * M_PI / kNP);
+    for (int i = 0; i < kNP; ++i) {
+        double T[kNP];
+        T[0] = 1.0;
+        T[1] = P.cheb[i];
+        for (int l = 2; l < kNP; ++l) T[l] = 2.0 * P.cheb[i] * T[l - 1] - T[l - 2];
+        for (int l = 0; l < kNP; ++l) P.tnode[i + l * kNP] = T[l];
+    }
+    double S[2 * kNP][kNP];
+    for (int k = 0; k < 2 * kNP; ++k) {
+        double s = (k < kNP) ? -0.5 + 0.5 * P.cheb[k] : 0.5 + 0.5 * P.cheb[k - kNP];
+        double T[kNP];
+        T[0] = 1.0;
+        T[1] = s;
+        for (int l = 2; l < kNP; ++l) T[l] = 2.0 * s * T[l - 1] - T[l - 2];
+        for (int i = 0; i < kNP; ++i) {
+            double acc = 0.0;
+            for (int l = 0; l < kNP; ++l) acc += T[l] * P.tnode[i + l * kNP];
+            S[k][i] = (2.0 * acc - 1.0) * (1.0 / kNP);
+        }
+    }
+    for (int id = 0; id < 4; ++id) {
+        int b0 = id & 1, b1 = (id >> 1) & 1;
+        for (int i = 0; i < kNP; ++i)
+            for (int j = 0; j < kNP; ++j)
+                for (int k = 0; k < kNP; ++k)
+                    for (int l = 0; l < kNP; ++l)
+                        P.R[id][(i * kNP + j) + (k * kNP + l) * kRank] = S[b1 * kNP + i][k] * S[b0 * kNP + j][l];
+    }
+    const int d2 = geo.d2;
+    for (int i = 0; i < d2 * d2; ++i) P.interp[i] = geo.interp[i];
+    for (int i = 0; i < d2; ++i) P.sqrtW[i] = geo.sqrtW[i];
+    CorrTables ct;
+    ct.build(geo, 0);
+    for (size_t i = 0; i < ct.legB.size(); ++i) P.legB[i] = ct.legB[i];
+    for (int i = 0; i < d2; ++i) P.coefScale[i] = ct.coefScale[i];
+    dParams.upload(&P, sizeof(P));
+    // work arrays
+    dCharge.alloc(geo.N * sizeof(double));
+    dOut.alloc(geo.N * sizeof(double));
+    dFT.alloc(geo.N * sizeof(double));
+    dFO.alloc(geo.N * sizeof(double));
+    dMult.alloc((size_t)tree.nn * kRank * sizeof(double));
+    dLocal.alloc((size_t)tree.nn * kRank * sizeof(double));
+    HIP_CHECK(hipMemset(dMult.p, 0, dMult.bytes));
+    HIP_CHECK(hipMemset(dLocal.p, 0, dLocal.bytes));
+    uploadPlan();
+}
+
+void Operator::uploadPlan() {
+    up(dLeaves, plan.leaves);
+    up(dNearPtr, plan.nearPtr);
+    up(dNearSrc, plan.nearSrc);
+    up(dNearKOff, plan.nearKOff);
+    up(dM2LTgt, plan.m2lTgt);
+    up(dM2LPtr, plan.m2lPtr);
+    up(dM2LSrc, plan.m2lSrc);
+    std::vector<int> pairTgt(plan.m2lSrc.size());
+    for (size_t i = 0; i < plan.m2lTgt.size(); ++i)
+        for (int64_t p = plan.m2lPtr[i]; p < plan.m2lPtr[i + 1]; ++p) pairTgt[p] = plan.m2lTgt[i];
+    up(dM2LPairTgt, pairTgt);
+    up(dP2M, plan.p2mLeaves);
+    dM2M.clear();
+    dL2L.clear();
+    dM2M = std::vector<DevBuf>(plan.m2mLevels.size());
+    dL2L = std::vector<DevBuf>(plan.l2lLevels.size());
+    m2mCount.assign(plan.m2mLevels.size(), 0);
+    l2lCount.assign(plan.l2lLevels.size(), 0);
+    for (size_t L = 0; L < plan.m2mLevels.size(); ++L) {
+        up(dM2M[L], plan.m2mLevels[L]);
+        m2mCount[L] = (int)plan.m2mLevels[L].size();
+    }
+    for (size_t L = 0; L < plan.l2lLevels.size(); ++L) {
+        up(dL2L[L], plan.l2lLevels[L]);
+        l2lCount[L] = (int)plan.l2lLevels[L].size();
+    }
+    maxNearS = 1;
+    for (size_t li = 0; li < plan.leaves.size(); ++li) {
+        int64_t S = 0;
+        for (int64_t j = plan.nearPtr[li]; j < plan.nearPtr[li + 1]; ++j) S += tree.count[plan.nearSrc[j]];
+        maxNearS = std::max<int>(maxNearS, (int)S);
+    }
+}
+
+// setCoeff (AnisoWrapper.cpp:46-69): sigma copies + interpolation() (KernelFactory.cpp:212-227);
+// singPrecompute() lives in Geometry; the device keeps sigma_t's coefficients / legendreNorms.
+void Operator::setCoeff(const double* ss, const double* st) {
+    ensureDevice();
+    std::memcpy(sigma_s.data(), ss, geo.N * sizeof(double));
+    std::memcpy(sigma_t.data(), st, geo.N * sizeof(double));
+    const int d2 = geo.d2;
+    std::vector<double> coef((size_t)geo.nsq * d2);
+    std::vector<double> lt(d2);
+    for (int i = 0; i < geo.nsq; ++i) {
+        for (int j = 0; j < d2; ++j) lt[j] = geo.sqrtW[j] * st[(size_t)i * d2 + j];
+        for (int r = 0; r < d2; ++r) {
+            double s = 0.0;
+            for (int k = 0; k < d2; ++k) s += geo.interp[r + (size_t)k * d2] * lt[k];
+            coef[(size_t)i * d2 + r] = s / geo.lnorm[r];
+        }
+    }
+    up(dStCoef, coef);
+    for (auto& m : modes) m.ready = false;
+    coeffSet = true;
+}
+
+// cache(Id) (AnisoWrapper.cpp:72-90): runKernelsCache + runKernelsCacheSing
+// (merged operators, built on the GPU), refineAddOnCache + singularAddCache
+// (translation-invariant stencil tables, built on the host).
+void Operator::cache(int id) {
+    if (!coeffSet) throw std::runtime_error("cache called before setCoeff");
+    if (id < 0 || id >= kernelSize)
+        throw std::out_of_range("kernel id " + std::to_string(id) + " out of range [0, " + std::to_string(kernelSize) + ")");
+    ensureDevice();
+    ModeCache& mc = modes[id];
+    mc.Knear.alloc((size_t)plan.nearKTotal * sizeof(double));
+    mc.Km2l.alloc((size_t)plan.pairsM2L * 256 * sizeof(double));
+    const Params* P = dParams.as<Params>();
+    int maxSrc = 1;
+    for (size_t li = 0; li < plan.leaves.size(); ++li)
+        maxSrc = std::max<int>(maxSrc, (int)(plan.nearPtr[li + 1] - plan.nearPtr[li]));
+    launch_cache_m2l(plan.pairsM2L, dM2LPairTgt.as<int>(), dM2LSrc.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
+                     dNrx.as<double>(), dNry.as<double>(), dStCoef.as<double>(), P, id, mc.Km2l.as<double>(), own);
+    launch_cache_near((int)plan.leaves.size(), dLeaves.as<int>(), dNearPtr.as<int64_t>(), dNearSrc.as<int>(),
+                      dNearKOff.as<int64_t>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dPxT.as<double>(),
+                      dPyT.as<double>(), dStCoef.as<double>(), P, id, maxSrc, mc.Knear.as<double>(), own);
+    CorrTables ct;
+    ct.build(geo, id);
+    up(mc.C, ct.C);
+    up(mc.mu, ct.mu);
+    HIP_CHECK(hipStreamSynchronize(own));
+    mc.ready = true;
+}
+
+void Operator::mappingHost(const double* charge, int id, double* out) {
+    ensureDevice();
+    HIP_CHECK(hipMemcpyAsync(dCharge.p, charge, geo.N * sizeof(double), hipMemcpyHostToDevice, own));
+    if (plan.nranks > 1) HIP_CHECK(hipMemsetAsync(dOut.p, 0, dOut.bytes, own));
+    mappingDev(dCharge.as<double>(), id, dOut.as<double>(), own, kStageAll);
+    HIP_CHECK(hipMemcpyAsync(out, dOut.p, geo.N * sizeof(double), hipMemcpyDeviceToHost, own));
+    HIP_CHECK(hipStreamSynchronize(own));
+}
+
+// mapping (AnisoWrapper.cpp:92-136) on device pointers, enqueued on stream s.
+// Only owned targets of `out` are written when the operator is sharded.
+void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t s, int mask) {
+    if (id < 0 || id >= kernelSize) throw std::out_of_range("kernel id out of range");
+    if (!modes[id].ready) throw std::runtime_error("mapping on kernel id " + std::to_string(id) + " before cache(" + std::to_string(id) + ")");
+    ensureDevice();
+    const ModeCache& mc = modes[id];
+    const Params* P = dParams.as<Params>();
+    const bool tm = timeStages;
+    if (tm) HIP_CHECK(hipEventRecord(ev[0], s));
+    HIP_CHECK(hipMemsetAsync(dLocal.p, 0, dLocal.bytes, s));
+    launch_prepare(geo.N, dPerm.as<int>(), charge, dW.as<double>(), dFT.as<double>(), dFO.as<double>(), s);
+    if (tm) HIP_CHECK(hipEventRecord(ev[1], s));
+    // up pass (global, every rank): P2M at leaves, then M2M bottom-up
+    launch_p2m((int)plan.p2mLeaves.size(), dP2M.as<int>(), dBegin.as<int64_t>(), dCount.as<int64_t>(),
+               dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(),
+               dPyT.as<double>(), dFT.as<double>(), P, dMult.as<double>(), s);
+    for (int L = (int)m2mCount.size() - 1; L >= 0; --L)
+        launch_m2m(m2mCount[L], dM2M[L].as<int>(), dChild.as<int4>(), dCount.as<int64_t>(), P, dMult.as<double>(), s);
+    if (tm) HIP_CHECK(hipEventRecord(ev[2], s));
+    if (mask & kStageFar) {
+        launch_m2l((int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LSrc.as<int>(),
+                   mc.Km2l.as<double>(), dMult.as<double>(), dLocal.as<double>(), s);
+    }
+    if (tm) HIP_CHECK(hipEventRecord(ev[3], s));
+    if (mask & kStageFar) {
+        for (size_t L = 2; L < l2lCount.size(); ++L)
+            launch_l2l(l2lCount[L], dL2L[L].as<int>(), dParent.as<int>(), dSlot.as<int>(), P, dLocal.as<double>(), s);
+    }
+    if (tm) HIP_CHECK(hipEventRecord(ev[4], s));
+    launch_near_l2p((int)plan.leaves.size(), dLeaves.as<int>(), dNearPtr.as<int64_t>(), dNearSrc.as<int>(),
+                    dNearKOff.as<int64_t>(), mc.Knear.as<double>(), dBegin.as<int64_t>(), dCount.as<int64_t>(),
+                    dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(),
+                    dPyT.as<double>(), dFT.as<double>(), dLocal.as<double>(), dPerm.as<int>(), P, maxNearS, mask,
+                    out, s);
+    if (tm) HIP_CHECK(hipEventRecord(ev[5], s));
+    launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), charge, dFO.as<double>(), mc.C.as<double>(),
+                mc.mu.as<double>(), P, mask, M_1_PI / 2.0, out, s);
+    if (tm) {
+        HIP_CHECK(hipEventRecord(ev[6], s));
+        HIP_CHECK(hipEventSynchronize(ev[6]));
+        float t[6];
+        for (int i = 0; i < 6; ++i) HIP_CHECK(hipEventElapsedTime(&t[i], ev[i], ev[i + 1]));
+        lastTimes.prep = t[0];
+        lastTimes.up = t[1];
+        lastTimes.m2l = t[2];
+        lastTimes.down = t[3];
+        lastTimes.near = t[4];
+        lastTimes.corr = t[5];
+        lastTimes.total = t[0] + t[1] + t[2] + t[3] + t[4] + t[5];
+    }
+}
+
+void Operator::lineIntegrals(const double* seg, int n, double* out) {
+    if (!coeffSet) throw std::runtime_error("line integrals before setCoeff");
+    if (n < 0) throw std::invalid_argument("n must be >= 0");
+    if (n == 0) return;
+    ensureDevice();
+    DevBuf ds, dout;
+    ds.upload(seg, (size_t)n * 4 * sizeof(double));
+    dout.alloc((size_t)n * sizeof(double));
+    launch_line_integrals(n, ds.as<double>(), dStCoef.as<double>(), dParams.as<Params>(), dout.as<double>(), own);
+    HIP_CHECK(hipStreamSynchronize(own));
+    HIP_CHECK(hipMemcpy(out, dout.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+}
+
+void Operator::permuteToTree(const double* orig, double* treeOut, hipStream_t s) {
+    ensureDevice();
+    launch_permute(geo.N, dPerm.as<int>(), orig, treeOut, s);
+}
+
+}  // namespace aniso

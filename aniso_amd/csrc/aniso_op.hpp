@@ -1,0 +1,96 @@
+// aniso_op.hpp -- the MI355X operator behind the C ABI (one per handle).
+//
+// Host state (geometry, tree, plan) is built by the constructor without touching
+// the GPU; device buffers are created on first use (setCoeff), on the HIP device
+// that is current at that moment.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "host.hpp"
+
+namespace aniso {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+    ~DevBuf();
+    void alloc(size_t nbytes);
+    void upload(const void* host, size_t nbytes);
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct ModeCache {
+    DevBuf Knear, Km2l, C, mu;
+    bool ready = false;
+};
+
+struct StageTimes {
+    float prep = 0, up = 0, m2l = 0, down = 0, near = 0, corr = 0, total = 0;
+};
+
+class Operator {
+public:
+    Operator(int sz, int d, int ks, double g, int ns, int np, int maxLevel);
+    ~Operator();
+
+    // --- the reference's MEX ops (AnisoWrapper.cpp:10-136)
+    int64_t numNodes() const { return geo.N; }
+    void getNodes(double* xy) const;
+    void setCoeff(const double* sigma_s, const double* sigma_t);
+    void cache(int id);
+    void mappingHost(const double* charge, int id, double* out);
+    void mappingDev(const double* charge, int id, double* out, hipStream_t s, int stageMask = 0x3f);
+
+    // --- extensions
+    void setShard(int rank, int nranks);
+    void getShard(int64_t* ownBegin, int64_t* ownEnd) const { *ownBegin = plan.ownBegin; *ownEnd = plan.ownEnd; }
+    // sharded apply: writes only owned targets of out (original order), others untouched
+    void permuteToTree(const double* orig, double* tree, hipStream_t s);
+    void lineIntegrals(const double* seg, int n, double* out);
+    bool modeCached(int id) const { return id >= 0 && id < kernelSize && modes[id].ready; }
+    int kernelSize = 0;
+    StageTimes lastTimes;
+    bool timeStages = false;
+
+    Geometry geo;
+    Tree tree;
+    Plan plan;
+    int ks = 0, ns = 0, np = 0, maxLevel = 0;
+    double g = 0;
+    bool coeffSet = false;
+    std::vector<double> sigma_s, sigma_t;
+
+    // stats
+    int64_t nearEntries() const { return plan.pairsNear; }
+    int64_t m2lEntries() const { return plan.pairsM2L * 256; }
+    int maxNearSources() const { return maxNearS; }
+
+private:
+    void ensureDevice();
+    void uploadPlan();
+    int device = -1;
+    hipStream_t own = nullptr;
+    hipEvent_t ev[8] = {};
+    int maxNearS = 0;
+    // geometry / tree on device
+    DevBuf dPxT, dPyT, dPerm, dW, dNcx, dNcy, dNrx, dNry, dBegin, dCount, dParent, dSlot, dChild, dIsLeaf;
+    DevBuf dLeaves, dNearPtr, dNearSrc, dNearKOff, dM2LTgt, dM2LPtr, dM2LSrc, dM2LPairTgt, dP2M;
+    std::vector<DevBuf> dM2M, dL2L;
+    std::vector<int> m2mCount, l2lCount;
+    DevBuf dParams, dStCoef;
+    DevBuf dCharge, dOut, dFT, dFO, dMult, dLocal;
+    std::vector<ModeCache> modes;
+};
+
+}  // namespace aniso

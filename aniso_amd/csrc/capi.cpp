@@ -1,0 +1,299 @@
+// capi.cpp -- extern "C" boundary over aniso::Operator.  No exception crosses
+// the ABI: every failure becomes a status code + thread-local message.
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/aniso_mi355x.h"
+#include "aniso_op.hpp"
+#include "kernels.hpp"
+
+struct aniso_op_s {
+    uint64_t magic = 0xA2150A2150ULL;
+    aniso::Operator op;
+    template <class... A>
+    explicit aniso_op_s(A... a) : op(a...) {}
+};
+
+namespace {
+thread_local std::string g_err;
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        g_err.clear();
+        f();
+        return ANISO_OK;
+    } catch (const std::out_of_range& e) {
+        g_err = e.what();
+        return ANISO_ERR_RANGE;
+    } catch (const std::invalid_argument& e) {
+        g_err = e.what();
+        return ANISO_ERR_INVALID;
+    } catch (const std::logic_error& e) {
+        g_err = e.what();
+        return ANISO_ERR_STATE;
+    } catch (const std::bad_alloc&) {
+        g_err = "host out of memory";
+        return ANISO_ERR_RUNTIME;
+    } catch (const std::runtime_error& e) {
+        g_err = e.what();
+        std::string w = e.what();
+        return (w.find("before") != std::string::npos) ? ANISO_ERR_STATE : ANISO_ERR_RUNTIME;
+    } catch (...) {
+        g_err = "unknown error";
+        return ANISO_ERR_RUNTIME;
+    }
+}
+
+aniso::Operator& get(aniso_handle h) {
+    if (!h || h->magic != 0xA2150A2150ULL) throw std::invalid_argument("invalid aniso handle");
+    return h->op;
+}
+
+#define CHECK_HANDLE(h)                              \
+    do {                                             \
+        if (!h || h->magic != 0xA2150A2150ULL) {     \
+            g_err = "invalid aniso handle";          \
+            return ANISO_ERR_HANDLE;                 \
+        }                                            \
+    } while (0)
+
+#define CHECK_PTR(p)                                                         \
+    do {                                                                     \
+        if (!(p)) throw std::invalid_argument(std::string(#p) + " is NULL"); \
+    } while (0)
+}  // namespace
+
+extern "C" {
+
+int aniso_create(int sz, int d, int ks, double g, int ns, int np, int maxLevel, aniso_handle* out) {
+    return guarded([&] {
+        CHECK_PTR(out);
+        *out = nullptr;
+        *out = new aniso_op_s(sz, d, ks, g, ns, np, maxLevel);
+    });
+}
+
+int aniso_destroy(aniso_handle h) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        h->magic = 0;
+        delete h;
+    });
+}
+
+int aniso_num_nodes(aniso_handle h, int64_t* n) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(n);
+        *n = get(h).numNodes();
+    });
+}
+
+int aniso_get_nodes(aniso_handle h, double* xy) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(xy);
+        get(h).getNodes(xy);
+    });
+}
+
+int aniso_get_weights(aniso_handle h, double* w) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(w);
+        auto& op = get(h);
+        std::memcpy(w, op.geo.w.data(), op.geo.N * sizeof(double));
+    });
+}
+
+int aniso_set_coeff(aniso_handle h, const double* ss, const double* st) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(ss);
+        CHECK_PTR(st);
+        get(h).setCoeff(ss, st);
+    });
+}
+
+int aniso_cache(aniso_handle h, int id) {
+    CHECK_HANDLE(h);
+    return guarded([&] { get(h).cache(id); });
+}
+
+int aniso_mapping(aniso_handle h, const double* charge, int id, double* out) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(charge);
+        CHECK_PTR(out);
+        get(h).mappingHost(charge, id, out);
+    });
+}
+
+int aniso_mapping_dev(aniso_handle h, const double* charge, int id, double* out, void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(charge);
+        CHECK_PTR(out);
+        get(h).mappingDev(charge, id, out, (hipStream_t)stream, aniso::kStageAll);
+    });
+}
+
+int aniso_mapping_stages_dev(aniso_handle h, const double* charge, int id, int mask, double* out, void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(charge);
+        CHECK_PTR(out);
+        if (mask < 0 || mask > aniso::kStageAll) throw std::invalid_argument("bad stage mask");
+        get(h).mappingDev(charge, id, out, (hipStream_t)stream, mask);
+    });
+}
+
+int aniso_mapping_batched(aniso_handle h, const double* Q, int k, int id, double* Out) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(Q);
+        CHECK_PTR(Out);
+        if (k < 0) throw std::invalid_argument("k must be >= 0");
+        auto& op = get(h);
+        for (int j = 0; j < k; ++j) op.mappingHost(Q + (size_t)j * op.geo.N, id, Out + (size_t)j * op.geo.N);
+    });
+}
+
+int aniso_set_shard(aniso_handle h, int rank, int nranks) {
+    CHECK_HANDLE(h);
+    return guarded([&] { get(h).setShard(rank, nranks); });
+}
+
+int aniso_get_shard(aniso_handle h, int64_t* b, int64_t* e) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(b);
+        CHECK_PTR(e);
+        get(h).getShard(b, e);
+    });
+}
+
+int aniso_tree_perm(aniso_handle h, int* perm) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(perm);
+        auto& t = get(h).tree;
+        std::memcpy(perm, t.perm.data(), t.perm.size() * sizeof(int));
+    });
+}
+
+int aniso_permute_to_tree_dev(aniso_handle h, const double* orig, double* tree, void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(orig);
+        CHECK_PTR(tree);
+        get(h).permuteToTree(orig, tree, (hipStream_t)stream);
+    });
+}
+
+int aniso_tree_size(aniso_handle h, int* nnodes, int* max_level) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        auto& t = get(h).tree;
+        if (nnodes) *nnodes = t.nn;
+        if (max_level) *max_level = t.maxLevel;
+    });
+}
+
+int aniso_tree_nodes(aniso_handle h, int* ints, double* geom) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        auto& t = get(h).tree;
+        for (int i = 0; i < t.nn; ++i) {
+            if (ints) {
+                int* o = ints + 11 * (size_t)i;
+                o[0] = t.parent[i];
+                for (int c = 0; c < 4; ++c) o[1 + c] = t.child[i][c];
+                o[5] = t.level[i];
+                o[6] = t.slot[i];
+                o[7] = t.isLeaf[i];
+                o[8] = t.isEmpty[i];
+                o[9] = (int)t.count[i];
+                o[10] = (int)t.begin[i];
+            }
+            if (geom) {
+                double* g = geom + 4 * (size_t)i;
+                g[0] = t.ncx[i];
+                g[1] = t.ncy[i];
+                g[2] = t.nrx[i];
+                g[3] = t.nry[i];
+            }
+        }
+    });
+}
+
+int aniso_tree_list(aniso_handle h, int which, int64_t* ptr, int* idx) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        auto& t = get(h).tree;
+        const std::vector<int64_t>* P[4] = {&t.uPtr, &t.vPtr, &t.wPtr, &t.xPtr};
+        const std::vector<int>* I[4] = {&t.uIdx, &t.vIdx, &t.wIdx, &t.xIdx};
+        if (which < 0 || which > 3) throw std::invalid_argument("which must be 0..3");
+        CHECK_PTR(ptr);
+        std::memcpy(ptr, P[which]->data(), P[which]->size() * sizeof(int64_t));
+        if (idx) std::memcpy(idx, I[which]->data(), I[which]->size() * sizeof(int));
+    });
+}
+
+int aniso_stats(aniso_handle h, int64_t* s) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(s);
+        auto& op = get(h);
+        s[0] = op.nearEntries();
+        s[1] = op.m2lEntries();
+        s[2] = op.plan.pairsM2L;
+        s[3] = (int64_t)op.plan.leaves.size();
+        s[4] = (int64_t)op.plan.m2lTgt.size();
+        s[5] = op.tree.nn;
+        int64_t mx = 0;
+        for (int i = 0; i < op.tree.nn; ++i)
+            if (op.tree.isLeaf[i]) mx = std::max<int64_t>(mx, op.tree.count[i]);
+        s[6] = mx;
+        s[7] = op.geo.N;
+    });
+}
+
+int aniso_set_timing(aniso_handle h, int on) {
+    CHECK_HANDLE(h);
+    return guarded([&] { get(h).timeStages = on != 0; });
+}
+
+int aniso_stage_times(aniso_handle h, float* t) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(t);
+        auto& s = get(h).lastTimes;
+        t[0] = s.prep; t[1] = s.up; t[2] = s.m2l; t[3] = s.down; t[4] = s.near; t[5] = s.corr; t[6] = s.total;
+    });
+}
+
+int aniso_line_integrals(aniso_handle h, const double* seg, int n, double* out) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(seg);
+        CHECK_PTR(out);
+        get(h).lineIntegrals(seg, n, out);
+    });
+}
+
+int aniso_last_error(char* buf, size_t len) {
+    if (!buf || !len) return ANISO_ERR_INVALID;
+    size_t n = std::min(len - 1, g_err.size());
+    std::memcpy(buf, g_err.data(), n);
+    buf[n] = 0;
+    return ANISO_OK;
+}
+
+const char* aniso_version(void) { return "aniso_mi355x 0.1 (gfx950)"; }
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// host.hpp -- host-side (C++) state of the MI355X matvec: geometry, quadtree,
+// flattened interaction lists and the small translation-invariant tables.
+//
+// Everything here is built once per geometry (aniso_create) or per mode
+// (aniso_cache) and uploaded to HBM; the per-apply work is all on the GPU.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace aniso {
+
+constexpr double kEps = 1e-12;  // bbfmm/utils.h:46
+
+// Geometry::Geometry (Geometry.cpp:10-114) + the singular Duffy rule
+// (KernelFactory.cpp:15-16, 863-986).
+struct Geometry {
+    int sz = 0, d = 0, d2 = 0, ns = 0;
+    double dx = 0;
+    int nsq = 0;
+    int64_t N = 0;
+    std::vector<double> px, py, w;            // nodes + weights, square-major order
+    std::vector<double> gx, gw;               // 1-D volume rule on [-1,1]
+    std::vector<double> qx, qy, qw, sqrtW;    // tensor rule (d2)
+    int nref = 0;
+    std::vector<double> refx, refy, refw;     // two-level refinement rule (16 d2)
+    std::vector<double> interp;               // d2 x d2, col-major
+    std::vector<double> nearMap;              // nref x d2, col-major
+    std::vector<double> lnorm;                // d2 (norms of the *refinement* matrix: quirk)
+    std::vector<double> sgx, sgw;             // singular rule on [0,1] (affine)
+    int nsing = 0;                            // 8 ns^2
+    std::vector<double> singX, singY, singW;  // d2 x nsing
+
+    void build(int sz_, int d_, int ns_);
+};
+
+// bbfmm::tree (bbfmm.h:146-449) flattened: node ids follow the reference's
+// assignment order (4 consecutive ids per split, depth-first), points are
+// stored in leaf-contiguous tree order (perm), lists as sorted CSR.
+struct Tree {
+    int nn = 0, maxLevel = 0;
+    double cx = 0, cy = 0, rx = 0, ry = 0;
+    std::vector<int> parent, level, slot, isLeaf, isEmpty;
+    std::vector<std::array<int, 4>> child;
+    std::vector<double> ncx, ncy, nrx, nry;
+    std::vector<int64_t> begin, count;        // point range in tree order
+    std::vector<int> perm;                    // tree position -> original index
+    std::vector<int64_t> uPtr, vPtr, wPtr, xPtr;
+    std::vector<int> uIdx, vIdx, wIdx, xIdx;
+
+    void build(const double* x, const double* y, int64_t n, int rank, int maxLevelArg, int nthreads);
+};
+
+// Per-shard work lists (all of them when nranks == 1).
+struct Plan {
+    int rank = 0, nranks = 1;
+    int64_t ownBegin = 0, ownEnd = 0;          // owned tree-position range
+    std::vector<int> leaves;                   // non-empty leaves whose points are owned
+    std::vector<int64_t> nearPtr;              // CSR over leaves -> source nodes
+    std::vector<int> nearSrc;
+    std::vector<int64_t> nearKOff;             // per leaf: offset of its K block (doubles)
+    int64_t nearKTotal = 0;
+    std::vector<int> m2lTgt;                   // active target nodes with M2L work
+    std::vector<int64_t> m2lPtr;               // CSR over m2lTgt -> source nodes
+    std::vector<int> m2lSrc;
+    std::vector<int> p2mLeaves;                // every non-empty leaf (up pass is global)
+    std::vector<std::vector<int>> m2mLevels;   // non-leaf nodes per level (global)
+    std::vector<std::vector<int>> l2lLevels;   // active non-empty nodes per level >= 2
+    int64_t pairsNear = 0, pairsM2L = 0;       // kernel entries per apply
+
+    void build(const Tree& t, int np, int rank, int nranks);
+};
+
+// Small per-mode tables for the correction stencil (nearRemoval + refineAddOn,
+// KernelFactory.cpp:445-478, 662-709) and the singular add-on moments
+// (KernelFactory.cpp:828-860).  See DESIGN.md "Corrections".
+struct CorrTables {
+    std::vector<double> C;        // d2 (target) x 9 (3x3 squares) x d2 (source)
+    std::vector<double> mu;       // d2 x d x d singular moments
+    std::vector<double> legB;     // d x d x d : beta_{n,a} polynomial coefficients in X
+    std::vector<double> coefScale;// d2: 1/lnorm
+    void build(const Geometry& g, int mode);
+};
+
+double legendre_tr1(unsigned l, double x);  // std::tr1::legendre restated
+void gauss_rule(int deg, double* x, double* w);
+
+}  // namespace aniso

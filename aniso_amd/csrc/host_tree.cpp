@@ -1,0 +1,291 @@
+// host_tree.cpp -- quadtree + U/V/W/X lists, bit-exact with bbfmm::tree
+// (bbfmm.h:146-449), and the flattened per-shard work plan uploaded to HBM.
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <stdexcept>
+#include <thread>
+
+#include "host.hpp"
+
+namespace aniso {
+
+namespace {
+
+struct Builder {
+    Tree& t;
+    const double* x;
+    const double* y;
+    int rank, maxLevelArg;
+    std::vector<int> tmp;
+
+    int new_node(int level, int slot) {
+        t.parent.push_back(-1);
+        t.level.push_back(level);
+        t.slot.push_back(slot);
+        t.isLeaf.push_back(0);
+        t.isEmpty.push_back(0);
+        t.child.push_back({-1, -1, -1, -1});
+        t.ncx.push_back(0); t.ncy.push_back(0); t.nrx.push_back(0); t.nry.push_back(0);
+        t.begin.push_back(0); t.count.push_back(0);
+        return t.nn++;
+    }
+
+    // assignChildren (bbfmm.h:250-317); the children's point lists are a stable
+    // 4-way partition of the parent's range of `perm` (same order as push_back).
+    void assign(int id) {
+        if (t.count[id] == 0) {
+            t.isLeaf[id] = 1;
+            t.isEmpty[id] = 1;
+            return;
+        }
+        if (t.count[id] <= rank || t.level[id] == maxLevelArg) {
+            t.isLeaf[id] = 1;
+            t.maxLevel = std::max(t.maxLevel, t.level[id]);
+            return;
+        }
+        for (int i = 0; i < 4; ++i) {
+            int c = new_node(t.level[id] + 1, i);
+            t.child[id][i] = c;
+            t.parent[c] = id;
+            t.ncx[c] = t.ncx[id] + ((i & 1) - 0.5) * t.nrx[id];
+            t.ncy[c] = t.ncy[id] + (((i >> 1) & 1) - 0.5) * t.nry[id];
+            t.nrx[c] = t.nrx[id] * 0.5;
+            t.nry[c] = t.nry[id] * 0.5;
+        }
+        const int64_t b = t.begin[id], n = t.count[id];
+        const double cx = t.ncx[id], cy = t.ncy[id];
+        int64_t cnt[4] = {0, 0, 0, 0};
+        for (int64_t k = b; k < b + n; ++k) {
+            int idx = t.perm[k];
+            int y_bit = y[idx] < cy ? 0 : 1;
+            int x_bit = x[idx] < cx ? 0 : 1;
+            cnt[2 * y_bit + x_bit]++;
+        }
+        int64_t off[4];
+        off[0] = b;
+        for (int i = 1; i < 4; ++i) off[i] = off[i - 1] + cnt[i - 1];
+        for (int i = 0; i < 4; ++i) {
+            t.begin[t.child[id][i]] = off[i];
+            t.count[t.child[id][i]] = cnt[i];
+        }
+        for (int64_t k = b; k < b + n; ++k) {
+            int idx = t.perm[k];
+            int y_bit = y[idx] < cy ? 0 : 1;
+            int x_bit = x[idx] < cx ? 0 : 1;
+            tmp[off[2 * y_bit + x_bit]++] = idx;
+        }
+        std::copy(tmp.begin() + b, tmp.begin() + b + n, t.perm.begin() + b);
+        for (int i = 0; i < 4; ++i) assign(t.child[id][i]);
+    }
+};
+
+// findNode (bbfmm.h:416-429)
+inline int find_node(const Tree& t, double px, double py) {
+    int id = 0;
+    for (;;) {
+        if (std::fabs(t.ncx[id] - px) < kEps && std::fabs(t.ncy[id] - py) < kEps) return id;
+        if (t.isLeaf[id]) return id;
+        int x_bit = t.ncx[id] > px ? 0 : 1;
+        int y_bit = t.ncy[id] > py ? 0 : 1;
+        id = t.child[id][2 * y_bit + x_bit];
+    }
+}
+
+// isAdjacent (bbfmm.h:431-447)
+inline bool adjacent(const Tree& t, int a, int b) {
+    double diff_x = std::fabs(t.ncx[a] - t.ncx[b]), diff_y = std::fabs(t.ncy[a] - t.ncy[b]);
+    double r_x = std::fabs(t.nrx[a] + t.nrx[b]), r_y = std::fabs(t.nry[a] + t.nry[b]);
+    bool rdx = r_x >= diff_x - kEps;
+    bool rdy = r_y >= diff_y - kEps;
+    bool x_adj = (std::fabs(diff_x - r_x) < kEps) && rdy;
+    bool y_adj = (std::fabs(diff_y - r_y) < kEps) && rdx;
+    return x_adj || y_adj;
+}
+
+inline void set_insert(std::vector<int>& v, int x) {
+    auto it = std::lower_bound(v.begin(), v.end(), x);
+    if (it == v.end() || *it != x) v.insert(it, x);
+}
+
+// buildNode (bbfmm.h:334-413)
+void build_node(const Tree& t, int id, double minx, double miny, double maxx, double maxy, std::vector<int>& U,
+                std::vector<int>& V, std::vector<int>& W, std::vector<int>& X, std::vector<int>& queue) {
+    U.clear(); V.clear(); W.clear(); X.clear();
+    if (t.parent[id] != -1) {
+        int p = t.parent[id];
+        double dx = t.nrx[id], dy = t.nry[id];
+        double xs = t.ncx[p] - dx, ys = t.ncy[p] - dy;
+        for (int x_id = -2; x_id < 4; x_id++)
+            for (int y_id = -2; y_id < 4; y_id++) {
+                double curx = xs + 2 * x_id * dx;
+                double cury = ys + 2 * y_id * dy;
+                bool le = (curx <= maxx + kEps) && (cury <= maxy + kEps);
+                bool ge = (curx >= minx - kEps) && (cury >= miny - kEps);
+                bool eq = std::fabs(curx - t.ncx[id]) < kEps && std::fabs(cury - t.ncy[id]) < kEps;
+                if (!(le && ge && !eq)) continue;
+                int cur = find_node(t, curx, cury);
+                bool adj = adjacent(t, id, cur);
+                if (t.level[cur] < t.level[id]) {
+                    if (adj) {
+                        if (t.isLeaf[cur]) set_insert(U, cur);
+                    } else {
+                        set_insert(X, cur);
+                    }
+                }
+                if (t.level[cur] == t.level[id]) {
+                    if (!adj) {
+                        set_insert(V, cur);
+                    } else if (t.isLeaf[id]) {
+                        queue.clear();
+                        queue.push_back(cur);
+                        for (size_t h = 0; h < queue.size(); ++h) {
+                            int f = queue[h];
+                            if (!adjacent(t, f, id)) {
+                                set_insert(W, f);
+                            } else if (t.isLeaf[f]) {
+                                set_insert(U, f);
+                            } else {
+                                for (int i = 0; i < 4; ++i) queue.push_back(t.child[f][i]);
+                            }
+                        }
+                    }
+                }
+            }
+    }
+    if (t.isLeaf[id]) set_insert(U, id);
+}
+
+}  // namespace
+
+void Tree::build(const double* x, const double* y, int64_t n, int rank, int maxLevelArg, int nthreads) {
+    if (n <= 0) throw std::invalid_argument("tree needs at least one point");
+    *this = Tree();
+    // getCenterRadius (bbfmm.h:231-248)
+    double x_max = x[0], x_min = x[0], y_max = y[0], y_min = y[0];
+    for (int64_t i = 0; i < n; ++i) {
+        x_max = std::max(x_max, x[i]); y_max = std::max(y_max, y[i]);
+        x_min = std::min(x_min, x[i]); y_min = std::min(y_min, y[i]);
+    }
+    cx = (x_max + x_min) / 2.0;
+    cy = (y_max + y_min) / 2.0;
+    rx = (x_max - x_min) / 2.0;
+    ry = (y_max - y_min) / 2.0;
+    perm.resize(n);
+    for (int64_t i = 0; i < n; ++i) perm[i] = (int)i;
+    Builder b{*this, x, y, rank, maxLevelArg, std::vector<int>(n)};
+    int root = b.new_node(0, 0);
+    ncx[root] = cx; ncy[root] = cy; nrx[root] = rx; nry[root] = ry;
+    begin[root] = 0; count[root] = n;
+    b.assign(root);
+
+    // lists, in parallel over nodes
+    std::vector<std::vector<int>> L[4];
+    for (auto& l : L) l.resize(nn);
+    const double minx = cx - rx, miny = cy - ry, maxx = cx + rx, maxy = cy + ry;
+    std::atomic<int> next{0};
+    auto worker = [&]() {
+        std::vector<int> q;
+        for (;;) {
+            int s = next.fetch_add(256);
+            if (s >= nn) break;
+            int e = std::min(nn, s + 256);
+            for (int id = s; id < e; ++id) build_node(*this, id, minx, miny, maxx, maxy, L[0][id], L[1][id], L[2][id], L[3][id], q);
+        }
+    };
+    int nt = std::max(1, std::min(nthreads, 64));
+    std::vector<std::thread> th;
+    for (int i = 1; i < nt; ++i) th.emplace_back(worker);
+    worker();
+    for (auto& h : th) h.join();
+    std::vector<int64_t>* ptrs[4] = {&uPtr, &vPtr, &wPtr, &xPtr};
+    std::vector<int>* idxs[4] = {&uIdx, &vIdx, &wIdx, &xIdx};
+    for (int k = 0; k < 4; ++k) {
+        ptrs[k]->assign(nn + 1, 0);
+        for (int i = 0; i < nn; ++i) (*ptrs[k])[i + 1] = (*ptrs[k])[i] + (int64_t)L[k][i].size();
+        idxs[k]->resize((*ptrs[k])[nn]);
+        for (int i = 0; i < nn; ++i) std::copy(L[k][i].begin(), L[k][i].end(), idxs[k]->begin() + (*ptrs[k])[i]);
+    }
+}
+
+void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
+    (void)np;
+    if (nranks_ < 1 || rank_ < 0 || rank_ >= nranks_) throw std::invalid_argument("bad shard rank/nranks");
+    *this = Plan();
+    rank = rank_;
+    nranks = nranks_;
+    const int64_t N = t.count[0];
+    // ---- ownership: contiguous runs of a subtree frontier (DFS order == tree order)
+    if (nranks == 1) {
+        ownBegin = 0;
+        ownEnd = N;
+    } else {
+        int Lc = 0;
+        std::vector<int> frontier;
+        for (;;) {
+            frontier.clear();
+            for (int i = 0; i < t.nn; ++i)
+                if (t.level[i] == Lc || (t.level[i] < Lc && t.isLeaf[i])) frontier.push_back(i);
+            if ((int)frontier.size() >= 16 * nranks || Lc >= t.maxLevel) break;
+            ++Lc;
+        }
+        std::sort(frontier.begin(), frontier.end(), [&](int a, int b) {
+            return t.begin[a] != t.begin[b] ? t.begin[a] < t.begin[b] : t.count[a] < t.count[b];
+        });
+        // balance by point count; boundaries fall on frontier-node starts
+        std::vector<int64_t> cuts(nranks + 1, N);
+        cuts[0] = 0;
+        int r = 1;
+        for (int f : frontier) {
+            while (r < nranks && t.begin[f] + t.count[f] / 2 >= (N * r) / nranks) {
+                cuts[r] = t.begin[f];
+                ++r;
+            }
+        }
+        for (; r < nranks; ++r) cuts[r] = N;
+        for (int k = 1; k <= nranks; ++k) cuts[k] = std::max(cuts[k], cuts[k - 1]);
+        ownBegin = cuts[rank];
+        ownEnd = cuts[rank + 1];
+    }
+    auto intersects = [&](int n) { return t.begin[n] < ownEnd && t.begin[n] + t.count[n] > ownBegin; };
+    // ---- up pass (global): P2M leaves and M2M levels
+    m2mLevels.assign(t.maxLevel + 1, {});
+    l2lLevels.assign(t.maxLevel + 1, {});
+    for (int i = 0; i < t.nn; ++i) {
+        if (t.isEmpty[i]) continue;
+        if (t.isLeaf[i]) p2mLeaves.push_back(i);
+        else m2mLevels[t.level[i]].push_back(i);
+    }
+    // ---- M2L over V then X (bbfmm.h:1051-1065), active non-empty targets
+    m2lPtr.push_back(0);
+    for (int i = 0; i < t.nn; ++i) {
+        if (t.isEmpty[i] || t.parent[i] == -1 || !intersects(i)) continue;
+        m2lTgt.push_back(i);
+        for (int64_t k = t.vPtr[i]; k < t.vPtr[i + 1]; ++k)
+            if (!t.isEmpty[t.vIdx[k]]) m2lSrc.push_back(t.vIdx[k]);
+        for (int64_t k = t.xPtr[i]; k < t.xPtr[i + 1]; ++k)
+            if (!t.isEmpty[t.xIdx[k]]) m2lSrc.push_back(t.xIdx[k]);
+        m2lPtr.push_back((int64_t)m2lSrc.size());
+        if (t.level[i] >= 2) l2lLevels[t.level[i]].push_back(i);
+    }
+    pairsM2L = (int64_t)m2lSrc.size();
+    // ---- near field over U then W (bbfmm.h:1081-1099), owned non-empty leaves
+    nearPtr.push_back(0);
+    for (int i = 0; i < t.nn; ++i) {
+        if (!t.isLeaf[i] || t.isEmpty[i] || !intersects(i)) continue;
+        if (t.begin[i] < ownBegin || t.begin[i] + t.count[i] > ownEnd)
+            throw std::logic_error("shard boundary splits a leaf");
+        leaves.push_back(i);
+        nearKOff.push_back(nearKTotal);
+        int64_t S = 0;
+        for (int64_t k = t.uPtr[i]; k < t.uPtr[i + 1]; ++k)
+            if (!t.isEmpty[t.uIdx[k]]) { nearSrc.push_back(t.uIdx[k]); S += t.count[t.uIdx[k]]; }
+        for (int64_t k = t.wPtr[i]; k < t.wPtr[i + 1]; ++k)
+            if (!t.isEmpty[t.wIdx[k]]) { nearSrc.push_back(t.wIdx[k]); S += t.count[t.wIdx[k]]; }
+        nearPtr.push_back((int64_t)nearSrc.size());
+        nearKTotal += S * t.count[i];
+    }
+    pairsNear = nearKTotal;
+}
+
+}  // namespace aniso

@@ -1,0 +1,67 @@
+// kernels.hpp -- device-side parameter block and kernel declarations.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace aniso {
+
+constexpr int kNP = 4;          // Chebyshev order per dimension (np); rank = 16
+constexpr int kRank = kNP * kNP;
+constexpr int kMaxD = 6;        // quadRule supported on the GPU path
+
+// Small read-only tables shared by all kernels of one operator (lives in HBM,
+// served from L1/L2: a few KB).
+struct Params {
+    int sz, d, d2, nsq;
+    double dx;
+    double gx[kMaxD], gw[kMaxD];            // volume Gauss rule (line integral)
+    double cheb[kNP];                       // -cos((i+1/2) pi / np)
+    double tnode[kNP * kNP];                // T_l(c_i) at [i + l*np]
+    double R[4][kRank * kRank];             // M2M / L2L transfer, col-major
+    double interp[kMaxD * kMaxD * kMaxD * kMaxD];  // d2 x d2 col-major
+    double sqrtW[kMaxD * kMaxD];
+    double coefScale[kMaxD * kMaxD];        // 1 / legendreNorms
+    double legB[kMaxD * kMaxD * kMaxD];     // Taylor-shifted Legendre coefficients
+};
+
+enum StageMask : int {
+    kStageFar = 1,      // M2L + L2L + L2P (both kernels)
+    kStageNear = 2,     // U/W near field (both kernels)
+    kStageStencil = 4,  // nearRemoval + refineAddOn
+    kStageSing = 8,     // singularAddOn
+    kStageAll = 15,
+};
+
+void launch_prepare(int64_t N, const int* perm, const double* charge, const double* w, double* fT, double* fO,
+                    hipStream_t s);
+void launch_p2m(int nl, const int* leaves, const int64_t* begin, const int64_t* count, const double* ncx,
+                const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
+                const double* fT, const Params* P, double* mult, hipStream_t s);
+void launch_m2m(int n, const int* nodes, const int4* child, const int64_t* count, const Params* P, double* mult,
+                hipStream_t s);
+void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* src, const double* K, const double* mult,
+                double* local, hipStream_t s);
+void launch_l2l(int n, const int* nodes, const int* parent, const int* slot, const Params* P, double* local,
+                hipStream_t s);
+void launch_near_l2p(int nl, const int* leaves, const int64_t* nearPtr, const int* nearSrc, const int64_t* nearKOff,
+                     const double* K, const int64_t* begin, const int64_t* count, const double* ncx,
+                     const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
+                     const double* fT, const double* local, const int* perm, const Params* P, int maxS, int flags,
+                     double* out, hipStream_t s);
+void launch_corr(int d, int64_t b, int64_t e, const int* perm, const double* charge, const double* fO, const double* C,
+                 const double* mu, const Params* P, int flags, double scale, double* out, hipStream_t s);
+void launch_cache_m2l(int64_t npairs, const int* pairTgt, const int* src, const double* ncx, const double* ncy,
+                      const double* nrx, const double* nry, const double* stcoef, const Params* P, int mode,
+                      double* K, hipStream_t s);
+void launch_cache_near(int nl, const int* leaves, const int64_t* nearPtr, const int* nearSrc, const int64_t* nearKOff,
+                       const int64_t* begin, const int64_t* count, const double* pxT, const double* pyT,
+                       const double* stcoef, const Params* P, int mode, int maxSrc, double* K, hipStream_t s);
+void launch_permute(int64_t N, const int* perm, const double* orig, double* tree, hipStream_t s);
+
+// host-callable device helpers used by tests through the C ABI
+void launch_line_integrals(int n, const double* seg, const double* stcoef, const Params* P, double* out,
+                           hipStream_t s);
+
+}  // namespace aniso
