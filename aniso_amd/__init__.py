@@ -31,6 +31,13 @@ def lib():
     """Load the C ABI library (raises if it has not been built)."""
     global _lib
     if _lib is None:
+        # PyTorch-ROCm ships its own libamdhip64.so.7; load it first so that this
+        # library binds to the same HIP runtime (same SONAME) instead of a second
+        # copy from /opt/rocm -- two runtimes in one process cannot share a GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise AnisoError(-1, f"{LIB_PATH} not built; run `make -C aniso_amd/csrc`")
         L = ctypes.CDLL(LIB_PATH)
