@@ -67,6 +67,8 @@ def lib():
             "aniso_set_timing": [P, I],
             "aniso_stage_times": [P, fp],
             "aniso_line_integrals": [P, dp, I, dp],
+            "aniso_forward_dev": [P, P, P, P],
+            "aniso_gmres": [P, dp, dp, I, I, D, dp, I, ip, dp],
             "aniso_last_error": [ctypes.c_char_p, ctypes.c_size_t],
         }
         for name, args in sig.items():
@@ -185,6 +187,27 @@ class Aniso:
             _check(lib().aniso_mapping_stages_dev(self.address, ctypes.c_void_p(charge.data_ptr()), int(id_), int(mask),
                                                   ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(s)))
         return out
+
+    def forward_dev(self, u, out, stream=None):
+        """main.cpp forwardOperator on device tensors: out = u - K_0(sigma_s .* u)."""
+        import torch
+
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_forward_dev(self.address, ctypes.c_void_p(u.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                       ctypes.c_void_p(s)))
+        return out
+
+    def gmres(self, q, m=80, maxit=400, tol=1e-12, x0=None):
+        """main.cpp:121-141 on the device: returns (iters, x, residual history, final residual)."""
+        q = _f64(q, self.N, "q")
+        x = np.zeros(self.N) if x0 is None else _f64(x0, self.N, "x0").copy()
+        hist = np.zeros(maxit + 2)
+        it = ctypes.c_int()
+        fr = ctypes.c_double()
+        _check(lib().aniso_gmres(self.address, _dp(q), _dp(x), int(m), int(maxit), float(tol), _dp(hist), len(hist),
+                                 ctypes.byref(it), ctypes.byref(fr)))
+        n = abs(it.value) + 1 if it.value != 0 else 1
+        return it.value, x, hist[:n], fr.value
 
     def set_shard(self, rank, nranks):
         _check(lib().aniso_set_shard(self.address, int(rank), int(nranks)))

@@ -74,8 +74,8 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
 Operator::~Operator() {
     if (device >= 0) {
         (void)hipSetDevice(device);
-        for (auto& e : ev)
-            if (e) (void)hipEventDestroy(e);
+        for (auto& set : evPool)
+            for (auto& e : set) (void)hipEventDestroy(e);
         if (own) (void)hipStreamDestroy(own);
     }
 }
@@ -104,7 +104,6 @@ void Operator::ensureDevice() {
     }
     HIP_CHECK(hipGetDevice(&device));
     HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
-    for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
     // tree-order coordinates
     std::vector<double> pxT(geo.N), pyT(geo.N);
     for (int64_t k = 0; k < geo.N; ++k) {
@@ -184,6 +183,8 @@ void Operator::ensureDevice() {
     dOut.alloc(geo.N * sizeof(double));
     dFT.alloc(geo.N * sizeof(double));
     dFO.alloc(geo.N * sizeof(double));
+    dTmp.alloc(geo.N * sizeof(double));
+    dTmp2.alloc(geo.N * sizeof(double));
     dMult.alloc((size_t)tree.nn * kRank * sizeof(double));
     dLocal.alloc((size_t)tree.nn * kRank * sizeof(double));
     HIP_CHECK(hipMemset(dMult.p, 0, dMult.bytes));
@@ -244,6 +245,7 @@ void Operator::setCoeff(const double* ss, const double* st) {
         }
     }
     up(dStCoef, coef);
+    up(dSigmaS, sigma_s);
     for (auto& m : modes) m.ready = false;
     coeffSet = true;
 }
@@ -252,9 +254,9 @@ void Operator::setCoeff(const double* ss, const double* st) {
 // (merged operators, built on the GPU), refineAddOnCache + singularAddCache
 // (translation-invariant stencil tables, built on the host).
 void Operator::cache(int id) {
-    if (!coeffSet) throw std::runtime_error("cache called before setCoeff");
     if (id < 0 || id >= kernelSize)
         throw std::out_of_range("kernel id " + std::to_string(id) + " out of range [0, " + std::to_string(kernelSize) + ")");
+    if (!coeffSet) throw std::runtime_error("cache called before setCoeff");
     ensureDevice();
     ModeCache& mc = modes[id];
     mc.Knear.alloc((size_t)plan.nearKTotal * sizeof(double));
@@ -277,6 +279,8 @@ void Operator::cache(int id) {
 }
 
 void Operator::mappingHost(const double* charge, int id, double* out) {
+    if (id < 0 || id >= kernelSize) throw std::out_of_range("kernel id out of range");
+    if (!modes[id].ready) throw std::runtime_error("mapping on kernel id " + std::to_string(id) + " before cache(" + std::to_string(id) + ")");
     ensureDevice();
     HIP_CHECK(hipMemcpyAsync(dCharge.p, charge, geo.N * sizeof(double), hipMemcpyHostToDevice, own));
     if (plan.nranks > 1) HIP_CHECK(hipMemsetAsync(dOut.p, 0, dOut.bytes, own));
@@ -294,7 +298,16 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
     const ModeCache& mc = modes[id];
     const Params* P = dParams.as<Params>();
     const bool tm = timeStages;
-    if (tm) HIP_CHECK(hipEventRecord(ev[0], s));
+    hipEvent_t* ev = nullptr;
+    if (tm) {
+        if (evUsed == (int)evPool.size()) {
+            std::array<hipEvent_t, 7> set;
+            for (auto& e : set) HIP_CHECK(hipEventCreate(&e));
+            evPool.push_back(set);
+        }
+        ev = evPool[evUsed++].data();
+        HIP_CHECK(hipEventRecord(ev[0], s));
+    }
     HIP_CHECK(hipMemsetAsync(dLocal.p, 0, dLocal.bytes, s));
     launch_prepare(geo.N, dPerm.as<int>(), charge, dW.as<double>(), dFT.as<double>(), dFO.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[1], s));
@@ -323,19 +336,34 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
     if (tm) HIP_CHECK(hipEventRecord(ev[5], s));
     launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), charge, dFO.as<double>(), mc.C.as<double>(),
                 mc.mu.as<double>(), P, mask, M_1_PI / 2.0, out, s);
-    if (tm) {
-        HIP_CHECK(hipEventRecord(ev[6], s));
-        HIP_CHECK(hipEventSynchronize(ev[6]));
-        float t[6];
-        for (int i = 0; i < 6; ++i) HIP_CHECK(hipEventElapsedTime(&t[i], ev[i], ev[i + 1]));
-        lastTimes.prep = t[0];
-        lastTimes.up = t[1];
-        lastTimes.m2l = t[2];
-        lastTimes.down = t[3];
-        lastTimes.near = t[4];
-        lastTimes.corr = t[5];
-        lastTimes.total = t[0] + t[1] + t[2] + t[3] + t[4] + t[5];
-    }
+    if (tm) HIP_CHECK(hipEventRecord(ev[6], s));
+}
+
+void Operator::setTiming(bool on) {
+    timeStages = on;
+    if (on) evUsed = 0;
+}
+
+StageTimes Operator::stageTimes() {
+    StageTimes r;
+    if (evUsed == 0) return r;
+    HIP_CHECK(hipEventSynchronize(evPool[evUsed - 1][6]));
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < evUsed; ++k)
+        for (int i = 0; i < 6; ++i) {
+            float t = 0;
+            HIP_CHECK(hipEventElapsedTime(&t, evPool[k][i], evPool[k][i + 1]));
+            acc[i] += t;
+        }
+    for (double& a : acc) a /= evUsed;
+    r.prep = (float)acc[0];
+    r.up = (float)acc[1];
+    r.m2l = (float)acc[2];
+    r.down = (float)acc[3];
+    r.near = (float)acc[4];
+    r.corr = (float)acc[5];
+    r.total = (float)(acc[0] + acc[1] + acc[2] + acc[3] + acc[4] + acc[5]);
+    return r;
 }
 
 void Operator::lineIntegrals(const double* seg, int n, double* out) {

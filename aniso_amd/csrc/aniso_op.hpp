@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <map>
 #include <memory>
 #include <string>
@@ -58,9 +59,17 @@ public:
     // sharded apply: writes only owned targets of out (original order), others untouched
     void permuteToTree(const double* orig, double* tree, hipStream_t s);
     void lineIntegrals(const double* seg, int n, double* out);
+    // callers of the hot path (main.cpp:125-141)
+    void forwardDev(const double* u, double* out, hipStream_t s);
+    int gmresHost(const double* q, double* x, int m, int maxit, double tol, double* hist, int maxhist,
+                  double* finalResid);
+    hipStream_t stream() const { return own; }
     bool modeCached(int id) const { return id >= 0 && id < kernelSize && modes[id].ready; }
     int kernelSize = 0;
-    StageTimes lastTimes;
+    // stage timing with HIP events recorded in-stream (no host sync per apply);
+    // stageTimes() averages every apply recorded since setTiming(true)
+    void setTiming(bool on);
+    StageTimes stageTimes();
     bool timeStages = false;
 
     Geometry geo;
@@ -81,7 +90,8 @@ private:
     void uploadPlan();
     int device = -1;
     hipStream_t own = nullptr;
-    hipEvent_t ev[8] = {};
+    std::vector<std::array<hipEvent_t, 7>> evPool;
+    int evUsed = 0;
     int maxNearS = 0;
     // geometry / tree on device
     DevBuf dPxT, dPyT, dPerm, dW, dNcx, dNcy, dNrx, dNry, dBegin, dCount, dParent, dSlot, dChild, dIsLeaf;
@@ -89,7 +99,7 @@ private:
     std::vector<DevBuf> dM2M, dL2L;
     std::vector<int> m2mCount, l2lCount;
     DevBuf dParams, dStCoef;
-    DevBuf dCharge, dOut, dFT, dFO, dMult, dLocal;
+    DevBuf dCharge, dOut, dFT, dFO, dMult, dLocal, dSigmaS, dTmp, dTmp2;
     std::vector<ModeCache> modes;
 };
 

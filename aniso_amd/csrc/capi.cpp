@@ -163,6 +163,28 @@ int aniso_mapping_batched(aniso_handle h, const double* Q, int k, int id, double
     });
 }
 
+int aniso_forward_dev(aniso_handle h, const double* u, double* out, void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(u);
+        CHECK_PTR(out);
+        auto& op = get(h);
+        if (!op.modeCached(0)) throw std::runtime_error("forward operator before cache(0)");
+        op.forwardDev(u, out, (hipStream_t)stream);
+    });
+}
+
+int aniso_gmres(aniso_handle h, const double* q, double* x, int m, int maxit, double tol, double* hist, int maxhist,
+                int* iters, double* final_resid) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(q);
+        CHECK_PTR(x);
+        int j = get(h).gmresHost(q, x, m, maxit, tol, hist, hist ? maxhist : 0, final_resid);
+        if (iters) *iters = j;
+    });
+}
+
 int aniso_set_shard(aniso_handle h, int rank, int nranks) {
     CHECK_HANDLE(h);
     return guarded([&] { get(h).setShard(rank, nranks); });
@@ -265,14 +287,14 @@ int aniso_stats(aniso_handle h, int64_t* s) {
 
 int aniso_set_timing(aniso_handle h, int on) {
     CHECK_HANDLE(h);
-    return guarded([&] { get(h).timeStages = on != 0; });
+    return guarded([&] { get(h).setTiming(on != 0); });
 }
 
 int aniso_stage_times(aniso_handle h, float* t) {
     CHECK_HANDLE(h);
     return guarded([&] {
         CHECK_PTR(t);
-        auto& s = get(h).lastTimes;
+        auto s = get(h).stageTimes();
         t[0] = s.prep; t[1] = s.up; t[2] = s.m2l; t[3] = s.down; t[4] = s.near; t[5] = s.corr; t[6] = s.total;
     });
 }

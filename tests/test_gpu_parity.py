@@ -1,0 +1,253 @@
+"""Parity of the HIP path (through the C ABI) against the CPU oracle, the
+reference's recorded known answers, and size-independent properties.
+
+Tolerance (BASELINE.json north_star: "<= 1e-10 relative error"): relative L2 error
+<= 1e-10 of every full apply; per-stage errors are measured against the norm of
+the full output (a stage can be ~0, e.g. odd modes' singular term at d=1).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import gaussian_charge, main_coeffs, rough_coeffs
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KA = json.load(open(os.path.join(ROOT, "tests", "golden", "survey_known_answers.json")))
+TOL = 1e-10
+
+
+def _torch():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+def _pair(sz, d, ks, ns, ml=20, coeffs="main", seed=0):
+    import aniso_amd
+    from oracle.oracle_py import Oracle
+
+    a = aniso_amd.Aniso(sz, d, ks, 0.8, ns, 4, ml)
+    o = Oracle(sz, d, ks, 0.8, ns, 4, ml)
+    xy = a.getNodes()
+    ss, st = main_coeffs(xy) if coeffs == "main" else rough_coeffs(xy, seed)
+    a.setCoeff(ss, st)
+    o.setCoeff(ss, st)
+    return a, o, xy
+
+
+CASES = [
+    # sz, d, ks, ns, maxLevel, coeffs, modes
+    (16, 3, 1, 8, 20, "main", [0]),          # config 1 geometry (data.cfg parameters)
+    (8, 1, 5, 10, 20, "main", range(9)),     # aniso.m parameters, all 9 Fourier modes
+    (12, 2, 2, 8, 20, "rough", [0, 1, 2]),
+    (20, 3, 2, 8, 20, "rough", [0, 2]),
+    (11, 3, 1, 6, 20, "rough", [0]),         # odd sz: non-power-of-two tree with W/X lists
+    (24, 1, 3, 10, 2, "rough", [0, 3]),      # maxLevel-limited: 64-point leaves
+    (8, 2, 1, 8, 0, "main", [0]),            # maxLevel 0: one 256-point leaf, near field only
+    (1, 3, 1, 8, 20, "main", [0]),           # single square: the root is the only leaf
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"sz{c[0]}d{c[1]}ks{c[2]}ml{c[4]}{c[5]}")
+def test_mapping_matches_oracle(case):
+    sz, d, ks, ns, ml, coeffs, modes = case
+    a, o, xy = _pair(sz, d, ks, ns, ml, coeffs, seed=sz)
+    rng = np.random.default_rng(sz * 31 + d)
+    for q in (rng.uniform(-1, 1, a.N), gaussian_charge(xy)):
+        for m in modes:
+            a.cache(m)
+            o.cache(m)
+            out = a.mapping(q, m)
+            ref = o.mapping(q, m)
+            assert _rel(out, ref) <= TOL, (case, m, _rel(out, ref))
+
+
+@pytest.mark.parametrize("case", CASES[:4], ids=lambda c: f"sz{c[0]}d{c[1]}ks{c[2]}")
+def test_stages_match_oracle(case):
+    import aniso_amd
+
+    torch = _torch()
+    sz, d, ks, ns, ml, coeffs, modes = case
+    a, o, xy = _pair(sz, d, ks, ns, ml, coeffs, seed=1)
+    q = np.random.default_rng(5).uniform(-1, 1, a.N)
+    qd = torch.tensor(q, device="cuda")
+    s = 1.0 / (2 * np.pi)
+    for m in modes:
+        a.cache(m)
+        o.cache(m)
+        st = o.mapping_stages(q, m)
+        ref_total = st[5]
+        for mask, ref in ((aniso_amd.STAGE_FAR | aniso_amd.STAGE_NEAR, (st[0] + st[1]) * s),
+                          (aniso_amd.STAGE_STENCIL, (st[2] + st[3]) * s),
+                          (aniso_amd.STAGE_SING, st[4] * s)):
+            od = torch.zeros(a.N, dtype=torch.float64, device="cuda")
+            a.mapping_dev(qd, m, od, mask=mask)
+            torch.cuda.synchronize()
+            err = np.linalg.norm(od.cpu().numpy() - ref) / np.linalg.norm(ref_total)
+            assert err <= TOL, (case, m, mask, err)
+
+
+@pytest.mark.parametrize("name", ["probe256_d1", "probe1M_d3"])
+def test_reference_known_answers(name):
+    """Full-size pins: outputs the survey recorded from the reference itself."""
+    import aniso_amd
+
+    c = [x for x in KA["applies"] if x["name"] == name][0]
+    a = aniso_amd.Aniso(c["sz"], c["d"], c["ks"], c["g"], c["ns"], c["np"], c["maxLevel"])
+    xy = a.getNodes()
+    a.setCoeff(*main_coeffs(xy))
+    a.cache(c["mode"])
+    out = a.mapping(gaussian_charge(xy), c["mode"])
+    assert abs(np.linalg.norm(out) - c["out_norm2"]) <= TOL * c["out_norm2"]
+    assert abs(out[0] - c["out0"]) <= TOL * abs(c["out0"])
+    assert abs(out[len(out) // 2] - c["outHalf"]) <= 1e-9 * abs(c["outHalf"])
+
+
+def test_tree_counts_match_reference_at_full_size():
+    import aniso_amd
+
+    for c in KA["trees"]:
+        a = aniso_amd.Aniso(c["sz"], c["d"], 1, 0.5, 8, c["np"], c["maxLevel"])
+        s = a.stats()
+        assert s["tree_nodes"] == c["nodes"] and s["near_entries"] == c["nearPairs"]
+        assert s["m2l_entries"] == c["M2Lpairs"], c["name"]
+
+
+def test_line_integrals_match_oracle():
+    a, o, xy = _pair(17, 3, 1, 8, 20, "rough", seed=9)
+    rng = np.random.default_rng(11)
+    seg = rng.uniform(0.001, 0.999, (4000, 4))
+    seg[:500, 2] = seg[:500, 0]          # vertical segments
+    seg[500:1000, 3] = seg[500:1000, 1]  # horizontal segments
+    seg[1000:1100, 2:] = seg[1000:1100, :2] + 1e-3 * rng.uniform(-1, 1, (100, 2))  # short
+    k = np.arange(1, 16) / 17.0          # through grid corners
+    seg[1100:1115] = np.stack([k * 0 + 0.01, k * 0 + 0.01, k, k], 1)
+    got = a.line_integrals(seg)
+    ref = np.array([o.line_integral(*s) for s in seg])
+    assert np.max(np.abs(got - ref) / np.maximum(1.0, np.abs(ref))) <= 1e-12
+
+
+def test_linearity_and_determinism_at_config3_size():
+    """Size-independent properties at BASELINE's 1M-point geometry (config 3)."""
+    torch = _torch()
+    import aniso_amd
+
+    a = aniso_amd.Aniso(1024, 1, 1, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    a.setCoeff(*main_coeffs(xy))
+    a.cache(0)
+    rng = np.random.default_rng(1)
+    q1 = torch.tensor(rng.uniform(-1, 1, a.N), device="cuda")
+    q2 = torch.tensor(gaussian_charge(xy), device="cuda")
+    o1, o2, o3, o4 = (torch.zeros_like(q1) for _ in range(4))
+    a.mapping_dev(q1, 0, o1)
+    a.mapping_dev(q2, 0, o2)
+    a.mapping_dev(2.5 * q1 - 0.75 * q2, 0, o3)
+    a.mapping_dev(q1, 0, o4)
+    torch.cuda.synchronize()
+    lin = 2.5 * o1 - 0.75 * o2
+    assert float(torch.linalg.norm(o3 - lin) / torch.linalg.norm(lin)) <= 1e-13
+    assert torch.equal(o1, o4)  # bitwise deterministic
+    # positive kernel: a positive charge gives a positive potential
+    assert float(o2.min()) > 0
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_sharded_apply_composes_to_full(nranks):
+    torch = _torch()
+    import aniso_amd
+    from aniso_amd import dist as adist
+
+    sz, d, ks = 40, 2, 2
+    full = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, 20)
+    xy = full.getNodes()
+    coef = rough_coeffs(xy, 4)
+    full.setCoeff(*coef)
+    full.cache(1)
+    q = torch.tensor(np.random.default_rng(2).uniform(-1, 1, full.N), device="cuda")
+    ref = torch.zeros_like(q)
+    full.mapping_dev(q, 1, ref)
+    ranges = adist.shard_ranges(full, nranks)
+    perm = torch.tensor(full.tree_perm(), device="cuda", dtype=torch.int64)
+    L = adist.pad_len(ranges)
+    gathered = torch.zeros(nranks, L, dtype=torch.float64, device="cuda")
+    for r in range(nranks):
+        sh = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, 20)
+        sh.set_shard(r, nranks)
+        sh.setCoeff(*coef)
+        sh.cache(1)
+        out = torch.zeros_like(q)
+        sh.mapping_dev(q, 1, out)
+        gathered[r] = adist.local_slice(out, perm, ranges[r], L)
+    torch.cuda.synchronize()
+    got = adist.assemble_from_gathered(gathered, ranges, perm)
+    assert float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref)) <= 1e-14
+
+
+def test_batched_and_device_variants_agree():
+    torch = _torch()
+    a, o, xy = _pair(10, 2, 1, 8, 20, "rough", seed=3)
+    a.cache(0)
+    Q = np.random.default_rng(4).uniform(-1, 1, (a.N, 3))
+    B = a.mapping_batched(Q, 0)
+    for j in range(3):
+        assert np.array_equal(B[:, j], a.mapping(Q[:, j], 0))
+    qd = torch.tensor(Q[:, 0], device="cuda")
+    od = torch.zeros_like(qd)
+    a.mapping_dev(qd, 0, od)
+    torch.cuda.synchronize()
+    assert np.array_equal(od.cpu().numpy(), B[:, 0])
+
+
+def test_forward_operator_and_gmres_match_reference():
+    """main.cpp's GMRES on the device: same iteration count as the reference
+    (29 for the literal data.cfg) and the same solution as the oracle's GMRES."""
+    torch = _torch()
+    import aniso_amd
+    from oracle.oracle_py import Oracle
+
+    c = KA["gmres"][0]
+    a = aniso_amd.Aniso(c["sz"], c["d"], c["ks"], c["g"], c["ns"], c["np"], c["maxLevel"])
+    xy = a.getNodes()
+    ss, st = main_coeffs(xy)
+    a.setCoeff(ss, st)
+    a.cache(0)
+    q = gaussian_charge(xy)
+    # forward operator u - K0(sigma_s u)
+    u = torch.tensor(np.random.default_rng(0).uniform(-1, 1, a.N), device="cuda")
+    f = torch.zeros_like(u)
+    a.forward_dev(u, f)
+    k = a.mapping(u.cpu().numpy() * ss, 0)
+    torch.cuda.synchronize()
+    assert np.allclose(f.cpu().numpy(), u.cpu().numpy() - k, rtol=0, atol=1e-13 * np.abs(k).max())
+    j, x, hist, fr = a.gmres(q, c["m"], c["maxit"], c["tol"])
+    assert j == c["iterations"], (j, hist)
+    assert fr < c["tol"]
+    o = Oracle(c["sz"], c["d"], c["ks"], c["g"], c["ns"], c["np"], c["maxLevel"])
+    o.setCoeff(ss, st)
+    o.cache(0)
+    jo, xo, ho, fro = o.gmres_main(q, c["m"], c["maxit"], c["tol"])
+    assert jo == j
+    assert _rel(x, xo) <= 1e-10
+    assert np.allclose(hist, ho[: len(hist)], rtol=1e-6, atol=0)
+
+
+def test_uncached_mode_fails_loudly():
+    import aniso_amd
+
+    a = aniso_amd.Aniso(6, 1, 2, 0.8, 8, 4, 20)
+    xy = a.getNodes()
+    a.setCoeff(*main_coeffs(xy))
+    a.cache(0)
+    with pytest.raises(aniso_amd.AnisoError) as e:
+        a.mapping(np.ones(a.N), 2)
+    assert e.value.code == 3

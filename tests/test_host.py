@@ -1,0 +1,120 @@
+"""Host-side product logic on CPU: the C ABI library loads and exports every
+symbol of include/aniso_mi355x.h; geometry and the quadtree / interaction lists
+are bit-identical to the oracle's restatement of bbfmm::tree; argument / state
+errors are reported like the reference's MEX errors; no CPU fallback exists."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import aniso_amd
+from oracle.oracle_py import Oracle, OTree
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    names = aniso_amd.exported_symbols()
+    assert len(names) >= 25
+    L = aniso_amd.lib()
+    for n in names:
+        assert hasattr(L, n), n
+    out = subprocess.run(["nm", "-D", "--defined-only", aniso_amd.LIB_PATH], capture_output=True, text=True).stdout
+    for n in names:
+        assert f" T {n}" in out, n
+    assert "gfx950" in aniso_amd.version()
+
+
+def test_library_contains_gfx950_code_object():
+    blob = open(aniso_amd.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"k_m2l" in blob and b"k_near_l2p" in blob
+
+
+@pytest.mark.parametrize("sz,d,ns", [(1, 1, 8), (3, 2, 8), (16, 3, 8), (13, 3, 10)])
+def test_geometry_matches_oracle_bit_exact(sz, d, ns):
+    a = aniso_amd.Aniso(sz, d, 1, 0.5, ns, 4, 20)
+    o = Oracle(sz, d, 1, 0.5, ns, 4, 20)
+    assert a.N == o.N == sz * sz * d * d
+    assert np.array_equal(a.getNodes(), o.getNodes())
+    assert np.array_equal(a.getWeights(), o.weights())
+    assert abs(a.getWeights().sum() - 1.0) < 1e-13
+
+
+@pytest.mark.parametrize("sz,d,ml", [(1, 1, 20), (2, 1, 20), (16, 3, 20), (120, 3, 5), (7, 3, 20), (37, 2, 20),
+                                     (50, 1, 3), (8, 2, 0), (97, 1, 20)])
+def test_tree_and_lists_bit_exact_vs_oracle(sz, d, ml):
+    a = aniso_amd.Aniso(sz, d, 1, 0.5, 8, 4, ml)
+    xy = a.getNodes()
+    ot = OTree(xy[:, 0], xy[:, 1], 16, ml)
+    ints, geom = a.tree_nodes()
+    oi, og = ot.node_ints(), ot.node_geom()
+    assert ints.shape[0] == ot.nn
+    assert np.array_equal(ints[:, :10], oi[:, :10])
+    assert np.array_equal(geom, og)
+    for w in range(4):
+        ptr, idx = a.tree_list(w)
+        ol = ot.lists(w)
+        for i in range(ot.nn):
+            assert np.array_equal(idx[ptr[i]:ptr[i + 1]], ol[i]), (w, i)
+    perm = a.tree_perm()
+    assert np.array_equal(np.sort(perm), np.arange(a.N))
+    for i in range(ot.nn):
+        if ints[i, 7]:  # leaves: same point order as the reference's sourceIndex
+            assert np.array_equal(perm[ints[i, 10]:ints[i, 10] + ints[i, 9]], ot.sources(i))
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_shards_partition_targets_and_work(nranks):
+    a = aniso_amd.Aniso(64, 1, 1, 0.5, 8, 4, 20)
+    full = a.stats()
+    ranges, leaves, near = [], 0, 0
+    for r in range(nranks):
+        a.set_shard(r, nranks)
+        ranges.append(a.shard())
+        s = a.stats()
+        leaves += s["leaves"]
+        near += s["near_entries"]
+    assert ranges[0][0] == 0 and ranges[-1][1] == a.N
+    for (b0, e0), (b1, e1) in zip(ranges, ranges[1:]):
+        assert e0 == b1
+    sizes = [e - b for b, e in ranges]
+    assert max(sizes) <= 1.6 * a.N / nranks
+    assert leaves == full["leaves"] and near == full["near_entries"]
+
+
+def test_errors_are_reported_not_swallowed():
+    with pytest.raises(aniso_amd.AnisoError) as e:
+        aniso_amd.Aniso(16, 3, 1, 0.5, 8, 5, 20)  # np must be 4
+    assert e.value.code == 1
+    with pytest.raises(aniso_amd.AnisoError):
+        aniso_amd.Aniso(0, 3, 1, 0.5, 8, 4, 20)
+    with pytest.raises(aniso_amd.AnisoError):
+        aniso_amd.Aniso(4, 30, 1, 0.5, 8, 4, 20)  # quadrature degree not implemented
+    a = aniso_amd.Aniso(4, 1, 2, 0.5, 8, 4, 20)
+    with pytest.raises(aniso_amd.AnisoError) as e:
+        a.cache(3)  # kernel ids 0..2
+    assert e.value.code == 4
+    with pytest.raises(aniso_amd.AnisoError) as e:
+        a.cache(0)  # before setCoeff
+    assert e.value.code == 3
+    with pytest.raises(aniso_amd.AnisoError) as e:
+        a.mapping(np.zeros(a.N), 0)  # before cache
+    assert e.value.code == 3
+    with pytest.raises(aniso_amd.AnisoError):
+        a.mapping(np.zeros(a.N + 1), 0)
+    L = aniso_amd.lib()
+    assert L.aniso_cache(None, 0) == 5
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    a = aniso_amd.Aniso(4, 1, 1, 0.5, 8, 4, 20)
+    with pytest.raises(aniso_amd.AnisoError) as e:
+        a.setCoeff(np.ones(a.N), np.ones(a.N))  # needs the HIP device
+    assert e.value.code == 2
