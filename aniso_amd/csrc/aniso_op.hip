@@ -204,21 +204,18 @@ void Operator::uploadPlan() {
     for (size_t i = 0; i < plan.m2lTgt.size(); ++i)
         for (int64_t p = plan.m2lPtr[i]; p < plan.m2lPtr[i + 1]; ++p) pairTgt[p] = plan.m2lTgt[i];
     up(dM2LPairTgt, pairTgt);
-    up(dP2M, plan.p2mLeaves);
-    dM2M.clear();
-    dL2L.clear();
-    dM2M = std::vector<DevBuf>(plan.m2mLevels.size());
-    dL2L = std::vector<DevBuf>(plan.l2lLevels.size());
-    m2mCount.assign(plan.m2mLevels.size(), 0);
-    l2lCount.assign(plan.l2lLevels.size(), 0);
-    for (size_t L = 0; L < plan.m2mLevels.size(); ++L) {
-        up(dM2M[L], plan.m2mLevels[L]);
-        m2mCount[L] = (int)plan.m2mLevels[L].size();
-    }
-    for (size_t L = 0; L < plan.l2lLevels.size(); ++L) {
-        up(dL2L[L], plan.l2lLevels[L]);
-        l2lCount[L] = (int)plan.l2lLevels[L].size();
-    }
+    up(dUpDirect, plan.upDirect);
+    up(dTopNode, plan.topNode);
+    std::vector<int4> tc(plan.topChild.size());
+    for (size_t i = 0; i < tc.size(); ++i)
+        tc[i] = make_int4(plan.topChild[i][0], plan.topChild[i][1], plan.topChild[i][2], plan.topChild[i][3]);
+    up(dTopChild, tc);
+    up(dTopGroup, plan.topGroupStart);
+    if (plan.topNode.size() * kRank * sizeof(double) > 64 * 1024)
+        throw std::logic_error("up-pass top levels exceed one workgroup's LDS");
+    int depth = 0;
+    for (int i = 0; i < tree.nn; ++i) depth = std::max(depth, tree.level[i]);
+    if (depth >= kMaxDepth) throw std::invalid_argument("tree deeper than " + std::to_string(kMaxDepth) + " levels");
     maxNearS = 1;
     for (size_t li = 0; li < plan.leaves.size(); ++li) {
         int64_t S = 0;
@@ -308,31 +305,27 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
         ev = evPool[evUsed++].data();
         HIP_CHECK(hipEventRecord(ev[0], s));
     }
-    HIP_CHECK(hipMemsetAsync(dLocal.p, 0, dLocal.bytes, s));
     launch_prepare(geo.N, dPerm.as<int>(), charge, dW.as<double>(), dFT.as<double>(), dFO.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[1], s));
-    // up pass (global, every rank): P2M at leaves, then M2M bottom-up
-    launch_p2m((int)plan.p2mLeaves.size(), dP2M.as<int>(), dBegin.as<int64_t>(), dCount.as<int64_t>(),
-               dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(),
-               dPyT.as<double>(), dFT.as<double>(), P, dMult.as<double>(), s);
-    for (int L = (int)m2mCount.size() - 1; L >= 0; --L)
-        launch_m2m(m2mCount[L], dM2M[L].as<int>(), dChild.as<int4>(), dCount.as<int64_t>(), P, dMult.as<double>(), s);
+    // up pass (global, every rank): direct P2M below the cut, M2M above it
+    launch_up_direct((int)plan.upDirect.size(), dUpDirect.as<int>(), dBegin.as<int64_t>(), dCount.as<int64_t>(),
+                     dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(),
+                     dPyT.as<double>(), dFT.as<double>(), P, dMult.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[2], s));
+    launch_up_top((int)plan.topNode.size(), plan.topInternal, dTopNode.as<int>(), dTopChild.as<int4>(),
+                  (int)plan.topGroupStart.size() - 1, dTopGroup.as<int>(), P, dMult.as<double>(), s);
+    if (tm) HIP_CHECK(hipEventRecord(ev[3], s));
+    // M2L for every active node (writes its local; L2L is applied by the leaf walk)
     if (mask & kStageFar) {
         launch_m2l((int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LSrc.as<int>(),
                    mc.Km2l.as<double>(), dMult.as<double>(), dLocal.as<double>(), s);
-    }
-    if (tm) HIP_CHECK(hipEventRecord(ev[3], s));
-    if (mask & kStageFar) {
-        for (size_t L = 2; L < l2lCount.size(); ++L)
-            launch_l2l(l2lCount[L], dL2L[L].as<int>(), dParent.as<int>(), dSlot.as<int>(), P, dLocal.as<double>(), s);
     }
     if (tm) HIP_CHECK(hipEventRecord(ev[4], s));
     launch_near_l2p((int)plan.leaves.size(), dLeaves.as<int>(), dNearPtr.as<int64_t>(), dNearSrc.as<int>(),
                     dNearKOff.as<int64_t>(), mc.Knear.as<double>(), dBegin.as<int64_t>(), dCount.as<int64_t>(),
                     dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(),
-                    dPyT.as<double>(), dFT.as<double>(), dLocal.as<double>(), dPerm.as<int>(), P, maxNearS, mask,
-                    out, s);
+                    dPyT.as<double>(), dFT.as<double>(), dLocal.as<double>(), dParent.as<int>(), dSlot.as<int>(),
+                    dPerm.as<int>(), P, maxNearS, mask, out, s);
     if (tm) HIP_CHECK(hipEventRecord(ev[5], s));
     launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), charge, dFO.as<double>(), mc.C.as<double>(),
                 mc.mu.as<double>(), P, mask, M_1_PI / 2.0, out, s);
@@ -357,9 +350,9 @@ StageTimes Operator::stageTimes() {
         }
     for (double& a : acc) a /= evUsed;
     r.prep = (float)acc[0];
-    r.up = (float)acc[1];
-    r.m2l = (float)acc[2];
-    r.down = (float)acc[3];
+    r.upDirect = (float)acc[1];
+    r.upTop = (float)acc[2];
+    r.m2l = (float)acc[3];
     r.near = (float)acc[4];
     r.corr = (float)acc[5];
     r.total = (float)(acc[0] + acc[1] + acc[2] + acc[3] + acc[4] + acc[5]);

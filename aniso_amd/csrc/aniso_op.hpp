@@ -37,7 +37,7 @@ struct ModeCache {
 };
 
 struct StageTimes {
-    float prep = 0, up = 0, m2l = 0, down = 0, near = 0, corr = 0, total = 0;
+    float prep = 0, upDirect = 0, upTop = 0, m2l = 0, near = 0, corr = 0, total = 0;
 };
 
 class Operator {
@@ -95,9 +95,8 @@ private:
     int maxNearS = 0;
     // geometry / tree on device
     DevBuf dPxT, dPyT, dPerm, dW, dNcx, dNcy, dNrx, dNry, dBegin, dCount, dParent, dSlot, dChild, dIsLeaf;
-    DevBuf dLeaves, dNearPtr, dNearSrc, dNearKOff, dM2LTgt, dM2LPtr, dM2LSrc, dM2LPairTgt, dP2M;
-    std::vector<DevBuf> dM2M, dL2L;
-    std::vector<int> m2mCount, l2lCount;
+    DevBuf dLeaves, dNearPtr, dNearSrc, dNearKOff, dM2LTgt, dM2LPtr, dM2LSrc, dM2LPairTgt;
+    DevBuf dUpDirect, dTopNode, dTopChild, dTopGroup;
     DevBuf dParams, dStCoef;
     DevBuf dCharge, dOut, dFT, dFO, dMult, dLocal, dSigmaS, dTmp, dTmp2;
     std::vector<ModeCache> modes;

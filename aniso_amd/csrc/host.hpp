@@ -65,9 +65,14 @@ struct Plan {
     std::vector<int> m2lTgt;                   // active target nodes with M2L work
     std::vector<int64_t> m2lPtr;               // CSR over m2lTgt -> source nodes
     std::vector<int> m2lSrc;
-    std::vector<int> p2mLeaves;                // every non-empty leaf (up pass is global)
-    std::vector<std::vector<int>> m2mLevels;   // non-leaf nodes per level (global)
-    std::vector<std::vector<int>> l2lLevels;   // active non-empty nodes per level >= 2
+    // up pass (global on every rank): direct P2M for nodes at level >= upCut and
+    // for all leaves; M2M in one workgroup for the internal nodes above upCut.
+    int upCut = 0;
+    std::vector<int> upDirect;
+    std::vector<int> topNode;                  // slots: internal (deepest level first), then their children
+    std::vector<std::array<int, 4>> topChild;  // per internal slot: child slots (-1 = empty)
+    std::vector<int> topGroupStart;            // slot ranges of internal nodes per level
+    int topInternal = 0;
     int64_t pairsNear = 0, pairsM2L = 0;       // kernel entries per apply
 
     void build(const Tree& t, int np, int rank, int nranks);

@@ -248,14 +248,38 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         ownEnd = cuts[rank + 1];
     }
     auto intersects = [&](int n) { return t.begin[n] < ownEnd && t.begin[n] + t.count[n] > ownBegin; };
-    // ---- up pass (global): P2M leaves and M2M levels
-    m2mLevels.assign(t.maxLevel + 1, {});
-    l2lLevels.assign(t.maxLevel + 1, {});
+    // ---- up pass (global): direct P2M at level >= upCut and leaves; M2M above
+    upCut = std::min(4, t.maxLevel);
+    std::vector<std::vector<int>> internalByLevel(upCut + 1);
     for (int i = 0; i < t.nn; ++i) {
         if (t.isEmpty[i]) continue;
-        if (t.isLeaf[i]) p2mLeaves.push_back(i);
-        else m2mLevels[t.level[i]].push_back(i);
+        if (t.isLeaf[i] || t.level[i] >= upCut) upDirect.push_back(i);
+        else internalByLevel[t.level[i]].push_back(i);
     }
+    std::vector<int> slotOf(t.nn, -1);
+    topGroupStart.push_back(0);
+    for (int L = upCut - 1; L >= 0; --L) {
+        for (int i : internalByLevel[L]) {
+            slotOf[i] = (int)topNode.size();
+            topNode.push_back(i);
+        }
+        topGroupStart.push_back((int)topNode.size());
+    }
+    topInternal = (int)topNode.size();
+    for (int s = 0; s < topInternal; ++s)
+        for (int q = 0; q < 4; ++q) {
+            int c = t.child[topNode[s]][q];
+            if (c >= 0 && !t.isEmpty[c] && slotOf[c] < 0) {
+                slotOf[c] = (int)topNode.size();
+                topNode.push_back(c);
+            }
+        }
+    topChild.resize(topInternal);
+    for (int s = 0; s < topInternal; ++s)
+        for (int q = 0; q < 4; ++q) {
+            int c = t.child[topNode[s]][q];
+            topChild[s][q] = (c >= 0 && !t.isEmpty[c]) ? slotOf[c] : -1;
+        }
     // ---- M2L over V then X (bbfmm.h:1051-1065), active non-empty targets
     m2lPtr.push_back(0);
     for (int i = 0; i < t.nn; ++i) {
@@ -266,7 +290,6 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         for (int64_t k = t.xPtr[i]; k < t.xPtr[i + 1]; ++k)
             if (!t.isEmpty[t.xIdx[k]]) m2lSrc.push_back(t.xIdx[k]);
         m2lPtr.push_back((int64_t)m2lSrc.size());
-        if (t.level[i] >= 2) l2lLevels[t.level[i]].push_back(i);
     }
     pairsM2L = (int64_t)m2lSrc.size();
     // ---- near field over U then W (bbfmm.h:1081-1099), owned non-empty leaves
@@ -283,9 +306,9 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         for (int64_t k = t.wPtr[i]; k < t.wPtr[i + 1]; ++k)
             if (!t.isEmpty[t.wIdx[k]]) { nearSrc.push_back(t.wIdx[k]); S += t.count[t.wIdx[k]]; }
         nearPtr.push_back((int64_t)nearSrc.size());
-        nearKTotal += S * t.count[i];
+        nearKTotal += S * (t.count[i] + (t.count[i] & 1));  // rows padded to even: 16-B aligned columns
+        pairsNear += S * t.count[i];
     }
-    pairsNear = nearKTotal;
 }
 
 }  // namespace aniso

@@ -171,48 +171,96 @@ __global__ void k_prepare(int64_t N, const int* __restrict__ perm, const double*
     fO[k] = charge[k] * w[k];
 }
 
-// P2M: nodeCharge = R^T q, R(k, j*np+i) = Sx(k,i) Sy(k,j)  (bbfmm.h:832-844)
-__global__ void k_p2m(int nl, const int* __restrict__ leaves, const int64_t* __restrict__ begin,
-                      const int64_t* __restrict__ count, const double* __restrict__ ncx,
-                      const double* __restrict__ ncy, const double* __restrict__ nrx, const double* __restrict__ nry,
-                      const double* __restrict__ pxT, const double* __restrict__ pyT, const double* __restrict__ fT,
-                      const Params* __restrict__ P, double* __restrict__ mult) {
-    int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    int li = gid >> 4, p = gid & 15;
-    if (li >= nl) return;
-    int n = leaves[li];
-    int i = p & 3, j = p >> 2;
-    double cx = ncx[n], cy = ncy[n], rx = nrx[n], ry = nry[n];
-    int64_t b = begin[n], e = b + count[n];
-    double acc = 0.0;
-    for (int64_t k = b; k < e; ++k) {
+// Up pass, part 1: multipole of every node at level >= Lc (and of every leaf) by
+// direct P2M over the node's contiguous tree-order point range, one wave per node.
+// For a degree np-1 Chebyshev interpolant the reference's M2M translation of the
+// children's P2M equals the parent's P2M exactly (the parent's interpolation
+// polynomials are reproduced by the children's interpolants), so this is the
+// reference's upPass (bbfmm.h:825-861) up to rounding, without one launch per level.
+__global__ void __launch_bounds__(256) k_up_direct(int nn, const int* __restrict__ nodes,
+                                                   const int64_t* __restrict__ begin,
+                                                   const int64_t* __restrict__ count, const double* __restrict__ ncx,
+                                                   const double* __restrict__ ncy, const double* __restrict__ nrx,
+                                                   const double* __restrict__ nry, const double* __restrict__ pxT,
+                                                   const double* __restrict__ pyT, const double* __restrict__ fT,
+                                                   const Params* __restrict__ P, double* __restrict__ mult) {
+    const int wi = (blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+    const int lane = threadIdx.x & (kWave - 1);
+    if (wi >= nn) return;
+    const int n = nodes[wi];
+    const double cx = ncx[n], cy = ncy[n], irx = 1.0 / nrx[n], iry = 1.0 / nry[n];
+    const int64_t b = begin[n], e = b + count[n];
+    double acc[kRank];
+#pragma unroll
+    for (int p = 0; p < kRank; ++p) acc[p] = 0.0;
+    for (int64_t k = b + lane; k < e; k += kWave) {
         double Sx[kNP], Sy[kNP];
-        cheb_weights(P, (pxT[k] - cx) / rx, Sx);
-        cheb_weights(P, (pyT[k] - cy) / ry, Sy);
-        acc += Sx[i] * Sy[j] * fT[k];
+        cheb_weights(P, (pxT[k] - cx) * irx, Sx);
+        cheb_weights(P, (pyT[k] - cy) * iry, Sy);
+        const double f = fT[k];
+#pragma unroll
+        for (int j = 0; j < kNP; ++j) {
+            const double sf = Sy[j] * f;
+#pragma unroll
+            for (int i = 0; i < kNP; ++i) acc[j * kNP + i] += Sx[i] * sf;
+        }
     }
-    mult[(size_t)n * kRank + p] = acc;
+    // butterfly reduce-scatter of the 16 sums over 64 lanes (17 shuffles)
+#define ANISO_RS_STEP(NV, OFF, BIT)                               \
+    {                                                             \
+        const bool up = (lane >> (BIT)) & 1;                      \
+        _Pragma("unroll") for (int k = 0; k < (NV); ++k) {        \
+            double lo = acc[k], hi = acc[k + (NV)];               \
+            double keep = up ? hi : lo, send = up ? lo : hi;      \
+            acc[k] = keep + __shfl_xor(send, (OFF));              \
+        }                                                         \
+    }
+    ANISO_RS_STEP(8, 32, 5)
+    ANISO_RS_STEP(4, 16, 4)
+    ANISO_RS_STEP(2, 8, 3)
+    ANISO_RS_STEP(1, 4, 2)
+#undef ANISO_RS_STEP
+    double v = acc[0];
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    if ((lane & 3) == 0) {
+        const int p = (((lane >> 5) & 1) << 3) | (((lane >> 4) & 1) << 2) | (((lane >> 3) & 1) << 1) | ((lane >> 2) & 1);
+        mult[(size_t)n * kRank + p] = v;
+    }
 }
 
-// M2M: parent += R[slot]^T child for non-empty children  (bbfmm.h:855-859)
-__global__ void k_m2m(int nn, const int* __restrict__ nodes, const int4* __restrict__ child,
-                      const int64_t* __restrict__ count, const Params* __restrict__ P, double* __restrict__ mult) {
-    int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    int ni = gid >> 4, c = gid & 15;
-    if (ni >= nn) return;
-    int n = nodes[ni];
-    int4 ch = child[n];
-    int cs[4] = {ch.x, ch.y, ch.z, ch.w};
-    double acc = 0.0;
+// Up pass, part 2: M2M (bbfmm.h:855-859) for the few internal nodes above Lc, in
+// one workgroup, level by level in LDS.  Slots [0, nInternal) are internal nodes
+// ordered deepest level first (groups by levelStart); the rest are their
+// children computed by k_up_direct.
+__global__ void __launch_bounds__(256) k_up_top(int nslot, int nInternal, const int* __restrict__ slotNode,
+                                                const int4* __restrict__ slotChild, int ngroups,
+                                                const int* __restrict__ groupStart, const Params* __restrict__ P,
+                                                double* __restrict__ mult) {
+    extern __shared__ double sm[];
+    for (int i = threadIdx.x; i < nslot * kRank; i += blockDim.x)
+        sm[i] = (i / kRank) < nInternal ? 0.0 : mult[(size_t)slotNode[i / kRank] * kRank + (i % kRank)];
+    __syncthreads();
+    for (int gidx = 0; gidx < ngroups; ++gidx) {
+        for (int i = groupStart[gidx] * kRank + threadIdx.x; i < groupStart[gidx + 1] * kRank; i += blockDim.x) {
+            const int ls = i / kRank, c = i % kRank;
+            const int4 ch = slotChild[ls];
+            const int cs[4] = {ch.x, ch.y, ch.z, ch.w};
+            double acc = 0.0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (count[cs[i]] == 0) continue;
-        const double* cm = mult + (size_t)cs[i] * kRank;
-        const double* R = P->R[i] + (size_t)c * kRank;
+            for (int q = 0; q < 4; ++q) {
+                if (cs[q] < 0) continue;
+                const double* R = P->R[q] + (size_t)c * kRank;
+                const double* cm = sm + (size_t)cs[q] * kRank;
 #pragma unroll
-        for (int r = 0; r < kRank; ++r) acc += R[r] * cm[r];
+                for (int r = 0; r < kRank; ++r) acc += R[r] * cm[r];
+            }
+            sm[i] = acc;
+        }
+        __syncthreads();
     }
-    mult[(size_t)n * kRank + c] = acc;
+    for (int i = threadIdx.x; i < nInternal * kRank; i += blockDim.x)
+        mult[(size_t)slotNode[i / kRank] * kRank + (i % kRank)] = sm[i];
 }
 
 // M2L over the V then X lists with the cached merged 16x16 operators
@@ -254,21 +302,6 @@ __global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ t
     if (q == 0) local[(size_t)n * kRank + t] = acc;
 }
 
-// L2L: local += R[slot] * parent.local  (bbfmm.h:1070-1071)
-__global__ void k_l2l(int nn, const int* __restrict__ nodes, const int* __restrict__ parent,
-                      const int* __restrict__ slot, const Params* __restrict__ P, double* __restrict__ local) {
-    int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    int ni = gid >> 4, r = gid & 15;
-    if (ni >= nn) return;
-    int n = nodes[ni];
-    const double* pl = local + (size_t)parent[n] * kRank;
-    const double* R = P->R[slot[n]];
-    double acc = 0.0;
-#pragma unroll
-    for (int c = 0; c < kRank; ++c) acc += R[r + c * kRank] * pl[c];
-    local[(size_t)n * kRank + r] += acc;
-}
-
 // U/W near field + L2P for one target leaf per wave (bbfmm.h:1081-1113).  The
 // leaf's cached block is column-major nT x S (S = all U/W source points), read
 // as consecutive columns: lanes (t, column phase), t on the low lane bits.
@@ -278,8 +311,10 @@ __global__ void __launch_bounds__(256) k_near_l2p(
     const int64_t* __restrict__ count, const double* __restrict__ ncx, const double* __restrict__ ncy,
     const double* __restrict__ nrx, const double* __restrict__ nry, const double* __restrict__ pxT,
     const double* __restrict__ pyT, const double* __restrict__ fT, const double* __restrict__ local,
-    const int* __restrict__ perm, const Params* __restrict__ P, int maxS, int flags, double* __restrict__ out) {
+    const int* __restrict__ parent, const int* __restrict__ slot, const int* __restrict__ perm,
+    const Params* __restrict__ P, int maxS, int flags, double* __restrict__ out) {
     extern __shared__ double sh[];
+    __shared__ int chainS[4][kMaxDepth];
     const int wv = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
     const int li = blockIdx.x * (blockDim.x / kWave) + wv;
     const bool active = li < nl;
@@ -299,39 +334,88 @@ __global__ void __launch_bounds__(256) k_near_l2p(
             S += sc;
         }
     }
+    int depth = 0;
+    if (active && lane == 0) {
+        for (int a = n; parent[a] != -1 && depth < kMaxDepth; a = parent[a]) chainS[wv][depth++] = a;
+    }
     __syncthreads();
     if (!active) return;
-    const double* Kl = K + nearKOff[li];
-    const int nTp = nT <= 16 ? 16 : (nT <= 32 ? 32 : 64);
-    const int cps = kWave / nTp;
-    const int sph = lane / nTp;
-    for (int tc = 0; tc < nT; tc += kWave) {
-        const int t = tc + (lane & (nTp - 1));
-        double acc = 0.0;
-        if ((flags & kStageNear) && t < nT) {
-            int s = sph;
-            for (; s + cps < S; s += 2 * cps) {
-                double k0 = __builtin_nontemporal_load(Kl + (size_t)s * nT + t);
-                double k1 = __builtin_nontemporal_load(Kl + (size_t)(s + cps) * nT + t);
-                acc += k0 * fs[s] + k1 * fs[s + cps];
+    // L2L folded into the leaf (bbfmm.h:1070-1071): walk from the level-1 ancestor
+    // down to this leaf, local <- R[slot] local + M2L(node); lane p holds entry p&15.
+    double v = 0.0;
+    if (flags & kStageFar) {
+        depth = __shfl(depth, 0);
+        if (depth > 0) {
+            const int r = lane & (kRank - 1);
+            v = local[(size_t)chainS[wv][depth - 1] * kRank + r];
+            for (int k = depth - 2; k >= 0; --k) {
+                const int a = chainS[wv][k];
+                const double* R = P->R[slot[a]];
+                double acc = local[(size_t)a * kRank + r];
+#pragma unroll
+                for (int c = 0; c < kRank; ++c) acc += R[r + c * kRank] * __shfl(v, c);
+                v = acc;
             }
-            if (s < S) acc += __builtin_nontemporal_load(Kl + (size_t)s * nT + t) * fs[s];
         }
-        for (int off = nTp; off < kWave; off <<= 1) acc += __shfl_xor(acc, off);
-        if (sph == 0 && t < nT) {
-            if (flags & kStageFar) {
-                double Sx[kNP], Sy[kNP];
-                cheb_weights(P, (pxT[tb + t] - ncx[n]) / nrx[n], Sx);
-                cheb_weights(P, (pyT[tb + t] - ncy[n]) / nry[n], Sy);
-                const double* L = local + (size_t)n * kRank;
-                double l2p = 0.0;
+    }
+    double vv[kRank];
 #pragma unroll
-                for (int j = 0; j < kNP; ++j)
-#pragma unroll
-                    for (int i = 0; i < kNP; ++i) l2p += Sx[i] * Sy[j] * L[j * kNP + i];
-                acc += l2p;
+    for (int c = 0; c < kRank; ++c) vv[c] = __shfl(v, c);
+    // Block layout: column-major with the row count padded to even (nTs), so every
+    // lane reads 16 B (two targets of one source column); lanes = (row pair,
+    // column phase); 4 independent loads in flight per lane.
+    const double* Kl = K + nearKOff[li];
+    const int nTs = nT + (nT & 1);
+    const int rp = nTs >> 1;
+    int lpc = 1;
+    while (lpc < rp && lpc < kWave) lpc <<= 1;
+    const int cps = kWave / lpc;
+    const int cph = lane / lpc;
+    for (int rc = 0; rc < rp; rc += kWave) {
+        const int r = rc + (lane & (lpc - 1));
+        double a0 = 0.0, a1 = 0.0;
+        if ((flags & kStageNear) && r < rp) {
+            const dbl2* kc = reinterpret_cast<const dbl2*>(Kl) + r;
+            const int stride = rp;  // dbl2 elements per column
+            int s = cph;
+            for (; s + 3 * cps < S; s += 4 * cps) {
+                dbl2 k0 = __builtin_nontemporal_load(kc + (size_t)s * stride);
+                dbl2 k1 = __builtin_nontemporal_load(kc + (size_t)(s + cps) * stride);
+                dbl2 k2 = __builtin_nontemporal_load(kc + (size_t)(s + 2 * cps) * stride);
+                dbl2 k3 = __builtin_nontemporal_load(kc + (size_t)(s + 3 * cps) * stride);
+                double f0 = fs[s], f1 = fs[s + cps], f2 = fs[s + 2 * cps], f3 = fs[s + 3 * cps];
+                a0 += k0.x * f0 + k1.x * f1 + k2.x * f2 + k3.x * f3;
+                a1 += k0.y * f0 + k1.y * f1 + k2.y * f2 + k3.y * f3;
             }
-            out[perm[tb + t]] = acc;
+            for (; s < S; s += cps) {
+                dbl2 k0 = __builtin_nontemporal_load(kc + (size_t)s * stride);
+                a0 += k0.x * fs[s];
+                a1 += k0.y * fs[s];
+            }
+        }
+        for (int off = lpc; off < kWave; off <<= 1) {
+            a0 += __shfl_xor(a0, off);
+            a1 += __shfl_xor(a1, off);
+        }
+        if (cph == 0 && r < rp) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int t = 2 * r + h;
+                if (t >= nT) break;
+                double acc = h ? a1 : a0;
+                if (flags & kStageFar) {
+                    double Sx[kNP], Sy[kNP];
+                    cheb_weights(P, (pxT[tb + t] - ncx[n]) / nrx[n], Sx);
+                    cheb_weights(P, (pyT[tb + t] - ncy[n]) / nry[n], Sy);
+                    double l2p = 0.0;
+#pragma unroll
+                    for (int j = 0; j < kNP; ++j)
+#pragma unroll
+                        for (int i = 0; i < kNP; ++i) l2p += Sx[i] * Sy[j] * vv[j * kNP + i];
+                    acc += l2p;
+                }
+                out[perm[tb + t]] = acc;
+            }
         }
     }
 }
@@ -477,9 +561,14 @@ __global__ void __launch_bounds__(256) k_cache_near(int nl, const int* __restric
     __syncthreads();
     const int S = sOff[ns];
     double* Kl = K + nearKOff[li];
-    const int64_t total = (int64_t)nT * S;
+    const int nTs = nT + (nT & 1);  // rows padded to even (16-B loads in k_near_l2p)
+    const int64_t total = (int64_t)nTs * S;
     for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
-        int sc = (int)(e / nT), t = (int)(e - (int64_t)sc * nT);
+        int sc = (int)(e / nTs), t = (int)(e - (int64_t)sc * nTs);
+        if (t >= nT) {
+            Kl[e] = 0.0;
+            continue;
+        }
         int j = 0;
         while (sOff[j + 1] <= sc) ++j;
         int64_t sp = sBeg[j] + (sc - sOff[j]);
@@ -506,19 +595,20 @@ void launch_prepare(int64_t N, const int* perm, const double* charge, const doub
     HIP_LAUNCH_CHECK();
 }
 
-void launch_p2m(int nl, const int* leaves, const int64_t* begin, const int64_t* count, const double* ncx,
-                const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
-                const double* fT, const Params* P, double* mult, hipStream_t s) {
-    if (nl <= 0) return;
-    k_p2m<<<blocks_for((int64_t)nl * 16, 256), 256, 0, s>>>(nl, leaves, begin, count, ncx, ncy, nrx, nry, pxT, pyT,
-                                                            fT, P, mult);
+void launch_up_direct(int nn, const int* nodes, const int64_t* begin, const int64_t* count, const double* ncx,
+                      const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
+                      const double* fT, const Params* P, double* mult, hipStream_t s) {
+    if (nn <= 0) return;
+    k_up_direct<<<blocks_for((int64_t)nn * kWave, 256), 256, 0, s>>>(nn, nodes, begin, count, ncx, ncy, nrx, nry, pxT,
+                                                                    pyT, fT, P, mult);
     HIP_LAUNCH_CHECK();
 }
 
-void launch_m2m(int n, const int* nodes, const int4* child, const int64_t* count, const Params* P, double* mult,
-                hipStream_t s) {
-    if (n <= 0) return;
-    k_m2m<<<blocks_for((int64_t)n * 16, 256), 256, 0, s>>>(n, nodes, child, count, P, mult);
+void launch_up_top(int nslot, int nInternal, const int* slotNode, const int4* slotChild, int ngroups,
+                   const int* groupStart, const Params* P, double* mult, hipStream_t s) {
+    if (nInternal <= 0) return;
+    k_up_top<<<1, 256, (size_t)nslot * kRank * sizeof(double), s>>>(nslot, nInternal, slotNode, slotChild, ngroups,
+                                                                      groupStart, P, mult);
     HIP_LAUNCH_CHECK();
 }
 
@@ -529,24 +619,17 @@ void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* src, co
     HIP_LAUNCH_CHECK();
 }
 
-void launch_l2l(int n, const int* nodes, const int* parent, const int* slot, const Params* P, double* local,
-                hipStream_t s) {
-    if (n <= 0) return;
-    k_l2l<<<blocks_for((int64_t)n * 16, 256), 256, 0, s>>>(n, nodes, parent, slot, P, local);
-    HIP_LAUNCH_CHECK();
-}
-
 void launch_near_l2p(int nl, const int* leaves, const int64_t* nearPtr, const int* nearSrc, const int64_t* nearKOff,
                      const double* K, const int64_t* begin, const int64_t* count, const double* ncx,
                      const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
-                     const double* fT, const double* local, const int* perm, const Params* P, int maxS, int flags,
-                     double* out, hipStream_t s) {
+                     const double* fT, const double* local, const int* parent, const int* slot, const int* perm,
+                     const Params* P, int maxS, int flags, double* out, hipStream_t s) {
     if (nl <= 0) return;
     int wpb = maxS * 8 * 4 <= 48 * 1024 ? 4 : 1;
     size_t shm = (size_t)wpb * (maxS > 0 ? maxS : 1) * sizeof(double);
     k_near_l2p<<<blocks_for(nl, wpb), wpb * kWave, shm, s>>>(nl, leaves, nearPtr, nearSrc, nearKOff, K, begin, count,
-                                                            ncx, ncy, nrx, nry, pxT, pyT, fT, local, perm, P,
-                                                            maxS > 0 ? maxS : 1, flags, out);
+                                                            ncx, ncy, nrx, nry, pxT, pyT, fT, local, parent, slot,
+                                                            perm, P, maxS > 0 ? maxS : 1, flags, out);
     HIP_LAUNCH_CHECK();
 }
 

@@ -54,6 +54,21 @@ def ref_pairs(sz, d, ns, s):
     return 2 * s["near_entries"] + 2 * s["m2l_entries"] + p_rem + p_r + p_s
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/rNN_pmc_summary.json, made by tools/profile_round.sh + tools/pmc_summary.py
+    on this same bench command; FETCH_SIZE doubled per the gfx950 correction)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
+    if not files:
+        return None, None
+    k = json.load(open(files[-1]))["kernels"].get(kernel)
+    if not k:
+        return None, None
+    return int(k["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(args, gpu_check):
     """Oracle (oracle/, a faithful CPU port of the reference apply incl. the per-apply
     tree rebuild) on a bounded sample; returns (baseline dict, rel err vs GPU)."""
@@ -179,9 +194,10 @@ def main():
     m2l_bytes = 8.0 * my_stats["m2l_entries"] + 2.0 * 128.0 * my_stats["m2l_targets"]
     m2l_ms = times["m2l"]
     achieved = m2l_bytes / (m2l_ms * 1e-3) / 1e9 if m2l_ms > 0 else 0.0
+    traffic, tsrc = pmc_traffic("aniso::k_m2l") if world == 1 and args.sz == 1024 and args.d == 1 else (None, None)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_m2l",
-                "kernel_ms": round(m2l_ms, 5), "algorithmic_bytes": int(m2l_bytes)}
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_m2l",
+                "kernel_ms": round(m2l_ms, 5), "algorithmic_bytes": int(m2l_bytes), "traffic_source": tsrc}
     line = {
         "metric": "GMRES matvec/s at 1M quadrature points (main.cpp forwardOperator, mode 0)",
         "value": round(value, 3),
