@@ -204,6 +204,16 @@ void Operator::uploadPlan() {
     for (size_t i = 0; i < plan.m2lTgt.size(); ++i)
         for (int64_t p = plan.m2lPtr[i]; p < plan.m2lPtr[i + 1]; ++p) pairTgt[p] = plan.m2lTgt[i];
     up(dM2LPairTgt, pairTgt);
+    auto to_int4 = [](const std::vector<std::array<int, 4>>& v) {
+        std::vector<int4> o(v.size());
+        for (size_t i = 0; i < v.size(); ++i) o[i] = make_int4(v[i][0], v[i][1], v[i][2], v[i][3]);
+        return o;
+    };
+    up(dLeafInfo, to_int4(plan.leafInfo));
+    up(dNearPtsPtr, plan.nearPtsPtr);
+    up(dNearPts, plan.nearPts);
+    up(dChainPtr, plan.leafChainPtr);
+    up(dChain, plan.leafChain);
     up(dUpDirect, plan.upDirect);
     up(dTopNode, plan.topNode);
     std::vector<int4> tc(plan.topChild.size());
@@ -308,7 +318,7 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
     launch_prepare(geo.N, dPerm.as<int>(), charge, dW.as<double>(), dFT.as<double>(), dFO.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[1], s));
     // up pass (global, every rank): direct P2M below the cut, M2M above it
-    launch_up_direct((int)plan.upDirect.size(), dUpDirect.as<int>(), dBegin.as<int64_t>(), dCount.as<int64_t>(),
+    launch_up_direct((int)plan.upDirect.size(), plan.upBig, dUpDirect.as<int>(), dBegin.as<int64_t>(), dCount.as<int64_t>(),
                      dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(),
                      dPyT.as<double>(), dFT.as<double>(), P, dMult.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[2], s));
@@ -321,11 +331,13 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
                    mc.Km2l.as<double>(), dMult.as<double>(), dLocal.as<double>(), s);
     }
     if (tm) HIP_CHECK(hipEventRecord(ev[4], s));
-    launch_near_l2p((int)plan.leaves.size(), dLeaves.as<int>(), dNearPtr.as<int64_t>(), dNearSrc.as<int>(),
-                    dNearKOff.as<int64_t>(), mc.Knear.as<double>(), dBegin.as<int64_t>(), dCount.as<int64_t>(),
-                    dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(),
-                    dPyT.as<double>(), dFT.as<double>(), dLocal.as<double>(), dParent.as<int>(), dSlot.as<int>(),
-                    dPerm.as<int>(), P, maxNearS, mask, out, s);
+    launch_near((int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(),
+                dNearKOff.as<int64_t>(), mc.Knear.as<double>(), dFT.as<double>(), dPerm.as<int>(), maxNearS, mask, out,
+                s);
+    if (mask & kStageFar)
+        launch_leaf_far((int)plan.leaves.size(), dLeafInfo.as<int4>(), dChainPtr.as<int>(), dChain.as<int>(),
+                        dSlot.as<int>(), dLocal.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
+                        dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dPerm.as<int>(), P, out, s);
     if (tm) HIP_CHECK(hipEventRecord(ev[5], s));
     launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), charge, dFO.as<double>(), mc.C.as<double>(),
                 mc.mu.as<double>(), P, mask, M_1_PI / 2.0, out, s);

@@ -96,7 +96,7 @@ private:
     // geometry / tree on device
     DevBuf dPxT, dPyT, dPerm, dW, dNcx, dNcy, dNrx, dNry, dBegin, dCount, dParent, dSlot, dChild, dIsLeaf;
     DevBuf dLeaves, dNearPtr, dNearSrc, dNearKOff, dM2LTgt, dM2LPtr, dM2LSrc, dM2LPairTgt;
-    DevBuf dUpDirect, dTopNode, dTopChild, dTopGroup;
+    DevBuf dUpDirect, dTopNode, dTopChild, dTopGroup, dLeafInfo, dNearPtsPtr, dNearPts, dChainPtr, dChain;
     DevBuf dParams, dStCoef;
     DevBuf dCharge, dOut, dFT, dFO, dMult, dLocal, dSigmaS, dTmp, dTmp2;
     std::vector<ModeCache> modes;

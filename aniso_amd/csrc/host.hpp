@@ -13,6 +13,7 @@
 namespace aniso {
 
 constexpr double kEps = 1e-12;  // bbfmm/utils.h:46
+constexpr int kUpBig = 256;     // up-pass nodes with more points get a whole workgroup
 
 // Geometry::Geometry (Geometry.cpp:10-114) + the singular Duffy rule
 // (KernelFactory.cpp:15-16, 863-986).
@@ -61,6 +62,11 @@ struct Plan {
     std::vector<int64_t> nearPtr;              // CSR over leaves -> source nodes
     std::vector<int> nearSrc;
     std::vector<int64_t> nearKOff;             // per leaf: offset of its K block (doubles)
+    std::vector<std::array<int, 4>> leafInfo;  // per leaf: node, begin, count, S (source points)
+    std::vector<int> leafChainPtr, leafChain;  // per leaf: ancestors level 1 .. leaf (top-down)
+    std::vector<int64_t> nearPtsPtr;           // per leaf: its S source points (tree positions)
+    std::vector<int> nearPts;
+    int upBig = 0;                             // upDirect[0, upBig) have > kUpBig points
     int64_t nearKTotal = 0;
     std::vector<int> m2lTgt;                   // active target nodes with M2L work
     std::vector<int64_t> m2lPtr;               // CSR over m2lTgt -> source nodes

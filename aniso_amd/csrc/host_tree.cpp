@@ -251,11 +251,14 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     // ---- up pass (global): direct P2M at level >= upCut and leaves; M2M above
     upCut = std::min(4, t.maxLevel);
     std::vector<std::vector<int>> internalByLevel(upCut + 1);
+    std::vector<int> small;
     for (int i = 0; i < t.nn; ++i) {
         if (t.isEmpty[i]) continue;
-        if (t.isLeaf[i] || t.level[i] >= upCut) upDirect.push_back(i);
+        if (t.isLeaf[i] || t.level[i] >= upCut) (t.count[i] > kUpBig ? upDirect : small).push_back(i);
         else internalByLevel[t.level[i]].push_back(i);
     }
+    upBig = (int)upDirect.size();  // big nodes first: one 256-thread workgroup each
+    upDirect.insert(upDirect.end(), small.begin(), small.end());
     std::vector<int> slotOf(t.nn, -1);
     topGroupStart.push_back(0);
     for (int L = upCut - 1; L >= 0; --L) {
@@ -308,6 +311,24 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         nearPtr.push_back((int64_t)nearSrc.size());
         nearKTotal += S * (t.count[i] + (t.count[i] & 1));  // rows padded to even: 16-B aligned columns
         pairsNear += S * t.count[i];
+        if (S > (int64_t)1 << 30) throw std::invalid_argument("leaf neighbourhood too large");
+        leafInfo.push_back({i, (int)t.begin[i], (int)t.count[i], (int)S});
+    }
+    nearPtsPtr.push_back(0);
+    for (size_t li = 0; li < leaves.size(); ++li) {
+        for (int64_t j = nearPtr[li]; j < nearPtr[li + 1]; ++j) {
+            int s = nearSrc[j];
+            for (int64_t k = 0; k < t.count[s]; ++k) nearPts.push_back((int)(t.begin[s] + k));
+        }
+        nearPtsPtr.push_back((int64_t)nearPts.size());
+    }
+    leafChainPtr.push_back(0);
+    std::vector<int> up;
+    for (int n : leaves) {
+        up.clear();
+        for (int a = n; t.parent[a] != -1; a = t.parent[a]) up.push_back(a);
+        leafChain.insert(leafChain.end(), up.rbegin(), up.rend());
+        leafChainPtr.push_back((int)leafChain.size());
     }
 }
 

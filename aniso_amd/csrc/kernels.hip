@@ -177,35 +177,22 @@ __global__ void k_prepare(int64_t N, const int* __restrict__ perm, const double*
 // children's P2M equals the parent's P2M exactly (the parent's interpolation
 // polynomials are reproduced by the children's interpolants), so this is the
 // reference's upPass (bbfmm.h:825-861) up to rounding, without one launch per level.
-__global__ void __launch_bounds__(256) k_up_direct(int nn, const int* __restrict__ nodes,
-                                                   const int64_t* __restrict__ begin,
-                                                   const int64_t* __restrict__ count, const double* __restrict__ ncx,
-                                                   const double* __restrict__ ncy, const double* __restrict__ nrx,
-                                                   const double* __restrict__ nry, const double* __restrict__ pxT,
-                                                   const double* __restrict__ pyT, const double* __restrict__ fT,
-                                                   const Params* __restrict__ P, double* __restrict__ mult) {
-    const int wi = (blockIdx.x * blockDim.x + threadIdx.x) / kWave;
-    const int lane = threadIdx.x & (kWave - 1);
-    if (wi >= nn) return;
-    const int n = nodes[wi];
-    const double cx = ncx[n], cy = ncy[n], irx = 1.0 / nrx[n], iry = 1.0 / nry[n];
-    const int64_t b = begin[n], e = b + count[n];
-    double acc[kRank];
+__device__ __forceinline__ void p2m_point(const Params* __restrict__ P, double cx, double cy, double irx, double iry,
+                                          double x, double y, double f, double* acc) {
+    double Sx[kNP], Sy[kNP];
+    cheb_weights(P, (x - cx) * irx, Sx);
+    cheb_weights(P, (y - cy) * iry, Sy);
 #pragma unroll
-    for (int p = 0; p < kRank; ++p) acc[p] = 0.0;
-    for (int64_t k = b + lane; k < e; k += kWave) {
-        double Sx[kNP], Sy[kNP];
-        cheb_weights(P, (pxT[k] - cx) * irx, Sx);
-        cheb_weights(P, (pyT[k] - cy) * iry, Sy);
-        const double f = fT[k];
+    for (int j = 0; j < kNP; ++j) {
+        const double sf = Sy[j] * f;
 #pragma unroll
-        for (int j = 0; j < kNP; ++j) {
-            const double sf = Sy[j] * f;
-#pragma unroll
-            for (int i = 0; i < kNP; ++i) acc[j * kNP + i] += Sx[i] * sf;
-        }
+        for (int i = 0; i < kNP; ++i) acc[j * kNP + i] += Sx[i] * sf;
     }
-    // butterfly reduce-scatter of the 16 sums over 64 lanes (17 shuffles)
+}
+
+// Butterfly reduce-scatter of 16 per-lane sums over a wave (17 shuffles); lanes
+// with (lane & 3) == 0 return the total for entry p = rs_entry(lane).
+__device__ __forceinline__ double reduce_scatter16(double* acc, int lane) {
 #define ANISO_RS_STEP(NV, OFF, BIT)                               \
     {                                                             \
         const bool up = (lane >> (BIT)) & 1;                      \
@@ -223,10 +210,58 @@ __global__ void __launch_bounds__(256) k_up_direct(int nn, const int* __restrict
     double v = acc[0];
     v += __shfl_xor(v, 1);
     v += __shfl_xor(v, 2);
-    if ((lane & 3) == 0) {
-        const int p = (((lane >> 5) & 1) << 3) | (((lane >> 4) & 1) << 2) | (((lane >> 3) & 1) << 1) | ((lane >> 2) & 1);
-        mult[(size_t)n * kRank + p] = v;
+    return v;
+}
+
+__device__ __forceinline__ int rs_entry(int lane) {
+    return (((lane >> 5) & 1) << 3) | (((lane >> 4) & 1) << 2) | (((lane >> 3) & 1) << 1) | ((lane >> 2) & 1);
+}
+
+// Up pass, part 1.  Blocks [0, nBig) take one big node each with 256 threads;
+// the remaining blocks take four small nodes each (one per wave).  Loads are
+// issued four points deep per thread.
+__global__ void __launch_bounds__(256) k_up_direct(int nn, int nBig, const int* __restrict__ nodes,
+                                                   const int64_t* __restrict__ begin,
+                                                   const int64_t* __restrict__ count, const double* __restrict__ ncx,
+                                                   const double* __restrict__ ncy, const double* __restrict__ nrx,
+                                                   const double* __restrict__ nry, const double* __restrict__ pxT,
+                                                   const double* __restrict__ pyT, const double* __restrict__ fT,
+                                                   const Params* __restrict__ P, double* __restrict__ mult) {
+    __shared__ double red[4][kRank];
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const bool big = (int)blockIdx.x < nBig;
+    const int wi = big ? (int)blockIdx.x : nBig + ((int)blockIdx.x - nBig) * 4 + wv;
+    if (!big && wi >= nn) return;
+    const int n = nodes[wi];
+    const double cx = ncx[n], cy = ncy[n], irx = 1.0 / nrx[n], iry = 1.0 / nry[n];
+    const int64_t b = begin[n], e = b + count[n];
+    const int stride = big ? (int)blockDim.x : kWave;
+    double acc[kRank];
+#pragma unroll
+    for (int p = 0; p < kRank; ++p) acc[p] = 0.0;
+    int64_t k = b + (big ? threadIdx.x : lane);
+    for (; k + 3 * stride < e; k += 4 * stride) {
+        double x[4], y[4], f[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            x[u] = pxT[k + u * stride];
+            y[u] = pyT[k + u * stride];
+            f[u] = fT[k + u * stride];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) p2m_point(P, cx, cy, irx, iry, x[u], y[u], f[u], acc);
     }
+    for (; k < e; k += stride) p2m_point(P, cx, cy, irx, iry, pxT[k], pyT[k], fT[k], acc);
+    const double v = reduce_scatter16(acc, lane);
+    if (!big) {
+        if ((lane & 3) == 0) mult[(size_t)n * kRank + rs_entry(lane)] = v;
+        return;
+    }
+    if ((lane & 3) == 0) red[wv][rs_entry(lane)] = v;
+    __syncthreads();
+    if (threadIdx.x < kRank)
+        mult[(size_t)n * kRank + threadIdx.x] =
+            red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
 // Up pass, part 2: M2M (bbfmm.h:855-859) for the few internal nodes above Lc, in
@@ -302,69 +337,54 @@ __global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ t
     if (q == 0) local[(size_t)n * kRank + t] = acc;
 }
 
-// U/W near field + L2P for one target leaf per wave (bbfmm.h:1081-1113).  The
-// leaf's cached block is column-major nT x S (S = all U/W source points), read
-// as consecutive columns: lanes (t, column phase), t on the low lane bits.
-__global__ void __launch_bounds__(256) k_near_l2p(
-    int nl, const int* __restrict__ leaves, const int64_t* __restrict__ nearPtr, const int* __restrict__ nearSrc,
-    const int64_t* __restrict__ nearKOff, const double* __restrict__ K, const int64_t* __restrict__ begin,
-    const int64_t* __restrict__ count, const double* __restrict__ ncx, const double* __restrict__ ncy,
-    const double* __restrict__ nrx, const double* __restrict__ nry, const double* __restrict__ pxT,
-    const double* __restrict__ pyT, const double* __restrict__ fT, const double* __restrict__ local,
-    const int* __restrict__ parent, const int* __restrict__ slot, const int* __restrict__ perm,
-    const Params* __restrict__ P, int maxS, int flags, double* __restrict__ out) {
+// U/W near field for one target leaf per wave (bbfmm.h:1081-1099, 1111-1113).
+// All per-leaf indexing comes from host-built descriptors loaded lane-parallel,
+// so a wave pays ~3 memory round trips before it starts streaming its block:
+//   leafInfo[li] = (node, begin, count, S), nearPts = the S source tree positions
+//   leafChain    = the leaf's ancestors from level 1 down to the leaf itself.
+// The block is column-major nTs x S (rows padded to even nTs): each lane reads
+// 16 B = two targets of one source column; lanes = (row pair, column phase),
+// 4 independent loads in flight per lane.
+__global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ leafInfo,
+                                              const int64_t* __restrict__ nearPtsPtr, const int* __restrict__ nearPts,
+                                              const int64_t* __restrict__ nearKOff, const double* __restrict__ K,
+                                              const double* __restrict__ fT, const int* __restrict__ perm, int maxS,
+                                              int flags, double* __restrict__ out) {
     extern __shared__ double sh[];
-    __shared__ int chainS[4][kMaxDepth];
     const int wv = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
     const int li = blockIdx.x * (blockDim.x / kWave) + wv;
     const bool active = li < nl;
     double* fs = sh + (size_t)wv * maxS;
-    int n = 0, nT = 0, S = 0;
-    int64_t tb = 0;
+    int4 info = make_int4(0, 0, 0, 0);
+    int64_t koff = 0;
     if (active) {
-        n = leaves[li];
-        nT = (int)count[n];
-        tb = begin[n];
-        // stage the source charges of all U/W members (each a contiguous tree range)
-        for (int64_t j = nearPtr[li]; j < nearPtr[li + 1]; ++j) {
-            int s = nearSrc[j];
-            int64_t sb = begin[s];
-            int sc = (int)count[s];
-            for (int k = lane; k < sc; k += kWave) fs[S + k] = fT[sb + k];
-            S += sc;
-        }
-    }
-    int depth = 0;
-    if (active && lane == 0) {
-        for (int a = n; parent[a] != -1 && depth < kMaxDepth; a = parent[a]) chainS[wv][depth++] = a;
-    }
-    __syncthreads();
-    if (!active) return;
-    // L2L folded into the leaf (bbfmm.h:1070-1071): walk from the level-1 ancestor
-    // down to this leaf, local <- R[slot] local + M2L(node); lane p holds entry p&15.
-    double v = 0.0;
-    if (flags & kStageFar) {
-        depth = __shfl(depth, 0);
-        if (depth > 0) {
-            const int r = lane & (kRank - 1);
-            v = local[(size_t)chainS[wv][depth - 1] * kRank + r];
-            for (int k = depth - 2; k >= 0; --k) {
-                const int a = chainS[wv][k];
-                const double* R = P->R[slot[a]];
-                double acc = local[(size_t)a * kRank + r];
+        info = leafInfo[li];
+        const int64_t pb = nearPtsPtr[li];
+        koff = nearKOff[li];
+        // stage the S source charges (lane-parallel gather, 4 loads in flight per lane)
+        const int S = info.w;
+        for (int s0 = 0; s0 < S; s0 += 4 * kWave) {
+            int ix[4];
+            double fv[4];
 #pragma unroll
-                for (int c = 0; c < kRank; ++c) acc += R[r + c * kRank] * __shfl(v, c);
-                v = acc;
+            for (int u = 0; u < 4; ++u) {
+                const int sidx = s0 + u * kWave + lane;
+                ix[u] = sidx < S ? nearPts[pb + sidx] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) fv[u] = ix[u] >= 0 ? fT[ix[u]] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int sidx = s0 + u * kWave + lane;
+                if (sidx < S) fs[sidx] = fv[u];
             }
         }
     }
-    double vv[kRank];
-#pragma unroll
-    for (int c = 0; c < kRank; ++c) vv[c] = __shfl(v, c);
-    // Block layout: column-major with the row count padded to even (nTs), so every
-    // lane reads 16 B (two targets of one source column); lanes = (row pair,
-    // column phase); 4 independent loads in flight per lane.
-    const double* Kl = K + nearKOff[li];
+    __syncthreads();
+    if (!active) return;
+    const int nT = info.z, S = info.w;
+    const int64_t tb = info.y;
+    const double* Kl = K + koff;
     const int nTs = nT + (nT & 1);
     const int rp = nTs >> 1;
     int lpc = 1;
@@ -402,21 +422,76 @@ __global__ void __launch_bounds__(256) k_near_l2p(
             for (int h = 0; h < 2; ++h) {
                 const int t = 2 * r + h;
                 if (t >= nT) break;
-                double acc = h ? a1 : a0;
-                if (flags & kStageFar) {
-                    double Sx[kNP], Sy[kNP];
-                    cheb_weights(P, (pxT[tb + t] - ncx[n]) / nrx[n], Sx);
-                    cheb_weights(P, (pyT[tb + t] - ncy[n]) / nry[n], Sy);
-                    double l2p = 0.0;
-#pragma unroll
-                    for (int j = 0; j < kNP; ++j)
-#pragma unroll
-                        for (int i = 0; i < kNP; ++i) l2p += Sx[i] * Sy[j] * vv[j * kNP + i];
-                    acc += l2p;
-                }
-                out[perm[tb + t]] = acc;
+                out[perm[tb + t]] = h ? a1 : a0;
             }
         }
+    }
+}
+
+// L2L + L2P per leaf (bbfmm.h:1070-1071, 1104), after k_near.  Sixteen lanes per
+// leaf (four leaves per wave): lane r holds entry r of the running local; the
+// walk goes from the level-1 ancestor down to the leaf, local <- R[slot] local +
+// M2L(node), with the ancestors' M2L locals prefetched in registers and the four
+// transfer matrices staged in LDS.  Then out[target] += L * local.
+__global__ void __launch_bounds__(256) k_leaf_far(int nl, const int4* __restrict__ leafInfo,
+                                                  const int* __restrict__ chainPtr, const int* __restrict__ chain,
+                                                  const int* __restrict__ slot, const double* __restrict__ local,
+                                                  const double* __restrict__ ncx, const double* __restrict__ ncy,
+                                                  const double* __restrict__ nrx, const double* __restrict__ nry,
+                                                  const double* __restrict__ pxT, const double* __restrict__ pyT,
+                                                  const int* __restrict__ perm, const Params* __restrict__ P,
+                                                  double* __restrict__ out) {
+    __shared__ double Rs[4][kRank * kRank];
+    for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) Rs[i / (kRank * kRank)][i % (kRank * kRank)] = P->R[i / (kRank * kRank)][i % (kRank * kRank)];
+    __syncthreads();
+    const int li = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int r = threadIdx.x & (kRank - 1);
+    if (li >= nl) return;
+    const int4 info = leafInfo[li];
+    const int cb = chainPtr[li], depth = chainPtr[li + 1] - cb;
+    if (depth == 0) return;  // the root itself is the leaf: no far field
+    const int myNode = r < depth ? chain[cb + r] : 0;
+    double m[kPrefetchDepth];
+#pragma unroll
+    for (int k = 0; k < kPrefetchDepth; ++k) {
+        const int a = __shfl(myNode, k, kRank);
+        m[k] = (k < depth) ? local[(size_t)a * kRank + r] : 0.0;
+    }
+    double v = m[0];
+#pragma unroll
+    for (int k = 1; k < kPrefetchDepth; ++k) {
+        if (k < depth) {
+            const double* R = Rs[slot[__shfl(myNode, k, kRank)]];
+            double acc = m[k];
+#pragma unroll
+            for (int c = 0; c < kRank; ++c) acc += R[r + c * kRank] * __shfl(v, c, kRank);
+            v = acc;
+        }
+    }
+    for (int k = kPrefetchDepth; k < depth; ++k) {  // trees deeper than the prefetch window
+        const int a = chain[cb + k];
+        const double* R = Rs[slot[a]];
+        double acc = local[(size_t)a * kRank + r];
+#pragma unroll
+        for (int c = 0; c < kRank; ++c) acc += R[r + c * kRank] * __shfl(v, c, kRank);
+        v = acc;
+    }
+    double vv[kRank];
+#pragma unroll
+    for (int c = 0; c < kRank; ++c) vv[c] = __shfl(v, c, kRank);
+    const int n = info.x, nT = info.z;
+    const int64_t tb = info.y;
+    const double cx = ncx[n], cy = ncy[n], rx = nrx[n], ry = nry[n];
+    for (int t = r; t < nT; t += kRank) {
+        double Sx[kNP], Sy[kNP];
+        cheb_weights(P, (pxT[tb + t] - cx) / rx, Sx);
+        cheb_weights(P, (pyT[tb + t] - cy) / ry, Sy);
+        double l2p = 0.0;
+#pragma unroll
+        for (int j = 0; j < kNP; ++j)
+#pragma unroll
+            for (int i = 0; i < kNP; ++i) l2p += Sx[i] * Sy[j] * vv[j * kNP + i];
+        out[perm[tb + t]] += l2p;
     }
 }
 
@@ -561,7 +636,7 @@ __global__ void __launch_bounds__(256) k_cache_near(int nl, const int* __restric
     __syncthreads();
     const int S = sOff[ns];
     double* Kl = K + nearKOff[li];
-    const int nTs = nT + (nT & 1);  // rows padded to even (16-B loads in k_near_l2p)
+    const int nTs = nT + (nT & 1);  // rows padded to even (16-B loads in k_near)
     const int64_t total = (int64_t)nTs * S;
     for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
         int sc = (int)(e / nTs), t = (int)(e - (int64_t)sc * nTs);
@@ -595,12 +670,12 @@ void launch_prepare(int64_t N, const int* perm, const double* charge, const doub
     HIP_LAUNCH_CHECK();
 }
 
-void launch_up_direct(int nn, const int* nodes, const int64_t* begin, const int64_t* count, const double* ncx,
+void launch_up_direct(int nn, int nBig, const int* nodes, const int64_t* begin, const int64_t* count, const double* ncx,
                       const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
                       const double* fT, const Params* P, double* mult, hipStream_t s) {
     if (nn <= 0) return;
-    k_up_direct<<<blocks_for((int64_t)nn * kWave, 256), 256, 0, s>>>(nn, nodes, begin, count, ncx, ncy, nrx, nry, pxT,
-                                                                    pyT, fT, P, mult);
+    const unsigned nb = (unsigned)nBig + blocks_for((int64_t)(nn - nBig), 4);
+    k_up_direct<<<nb, 256, 0, s>>>(nn, nBig, nodes, begin, count, ncx, ncy, nrx, nry, pxT, pyT, fT, P, mult);
     HIP_LAUNCH_CHECK();
 }
 
@@ -619,17 +694,23 @@ void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* src, co
     HIP_LAUNCH_CHECK();
 }
 
-void launch_near_l2p(int nl, const int* leaves, const int64_t* nearPtr, const int* nearSrc, const int64_t* nearKOff,
-                     const double* K, const int64_t* begin, const int64_t* count, const double* ncx,
-                     const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
-                     const double* fT, const double* local, const int* parent, const int* slot, const int* perm,
-                     const Params* P, int maxS, int flags, double* out, hipStream_t s) {
+void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts, const int64_t* nearKOff,
+                 const double* K, const double* fT, const int* perm, int maxS, int flags, double* out, hipStream_t s) {
     if (nl <= 0) return;
     int wpb = maxS * 8 * 4 <= 48 * 1024 ? 4 : 1;
     size_t shm = (size_t)wpb * (maxS > 0 ? maxS : 1) * sizeof(double);
-    k_near_l2p<<<blocks_for(nl, wpb), wpb * kWave, shm, s>>>(nl, leaves, nearPtr, nearSrc, nearKOff, K, begin, count,
-                                                            ncx, ncy, nrx, nry, pxT, pyT, fT, local, parent, slot,
-                                                            perm, P, maxS > 0 ? maxS : 1, flags, out);
+    k_near<<<blocks_for(nl, wpb), wpb * kWave, shm, s>>>(nl, leafInfo, nearPtsPtr, nearPts, nearKOff, K, fT, perm,
+                                                        maxS > 0 ? maxS : 1, flags, out);
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_leaf_far(int nl, const int4* leafInfo, const int* chainPtr, const int* chain, const int* slot,
+                     const double* local, const double* ncx, const double* ncy, const double* nrx, const double* nry,
+                     const double* pxT, const double* pyT, const int* perm, const Params* P, double* out,
+                     hipStream_t s) {
+    if (nl <= 0) return;
+    k_leaf_far<<<blocks_for((int64_t)nl * kRank, 256), 256, 0, s>>>(nl, leafInfo, chainPtr, chain, slot, local, ncx, ncy,
+                                                                   nrx, nry, pxT, pyT, perm, P, out);
     HIP_LAUNCH_CHECK();
 }
 
