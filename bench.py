@@ -116,6 +116,11 @@ def main():
     ap.add_argument("--max-level", type=int, default=20)
     ap.add_argument("--cpu-sz", type=int, default=256)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N>1 (gloo = CPU-staged rehearsal)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="all ranks on cuda:0 (rehearse the sharded path on a one-GPU box; use --backend gloo)")
+    ap.add_argument("--verify", action="store_true", help="check the sharded matvec against an unsharded operator")
     args = ap.parse_args()
 
     import torch
@@ -127,9 +132,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    dev = 0 if args.same_device else local
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
 
     op = aniso_amd.Aniso(args.sz, args.d, 5, 0.8, args.ns, 4, args.max_level)
     N = op.N
@@ -162,7 +171,12 @@ def main():
         op.mapping_dev(tmp, 0, app)
         b, e = ranges[rank]
         slice_buf[: e - b] = app[perm[b:e]]
-        dist.all_gather_into_tensor(gathered, slice_buf)
+        if args.backend == "nccl":
+            dist.all_gather_into_tensor(gathered, slice_buf)
+        else:  # gloo rehearsal: stage through host memory
+            parts = [torch.zeros(L, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(parts, slice_buf.cpu())
+            gathered.copy_(torch.stack(parts))
         adist.assemble_from_gathered(gathered, ranges, perm, out=app)
         torch.sub(x, app, out=y)
 
@@ -219,6 +233,20 @@ def main():
         "cache_build_s": round(t_cache, 3),
         "roofline": roofline,
     }
+    if args.verify:
+        # one matvec of a fixed vector through this (possibly sharded) path vs an
+        # unsharded operator on the same device
+        u = torch.tensor(gaussian(xy), device="cuda")
+        got = torch.zeros_like(u)
+        matvec(u, got)
+        ref_op = aniso_amd.Aniso(args.sz, args.d, 5, 0.8, args.ns, 4, args.max_level)
+        ref_op.setCoeff(ss, st)
+        ref_op.cache(0)
+        ref = torch.zeros_like(u)
+        ref_op.forward_dev(u, ref)
+        torch.cuda.synchronize()
+        line["verify_rel_err_vs_unsharded"] = float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref))
+        del ref_op
     if rank == 0 and world == 1 and not args.no_cpu:
         def gpu_check(sz, u, ref):
             a = aniso_amd.Aniso(sz, args.d, 1, 0.8, args.ns, 4, args.max_level)

@@ -252,3 +252,21 @@ def test_uncached_mode_fails_loudly():
     with pytest.raises(aniso_amd.AnisoError) as e:
         a.mapping(np.ones(a.N), 2)
     assert e.value.code == 3
+
+
+def test_bench_sharded_path_rehearsal_two_ranks():
+    """bench.py's N>1 matvec (subtree shards + all-gather) with two ranks sharing
+    the one GPU of the box and gloo collectives; checked against the unsharded op."""
+    import subprocess
+    import sys
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29533", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--sz", "128", "--backend", "gloo",
+           "--same-device", "--verify", "--no-cpu"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 2
+    assert res["verify_rel_err_vs_unsharded"] <= 1e-13

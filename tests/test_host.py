@@ -30,7 +30,8 @@ def test_library_exports_every_header_symbol():
 def test_library_contains_gfx950_code_object():
     blob = open(aniso_amd.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
-    assert b"k_m2l" in blob and b"k_near_l2p" in blob
+    for k in (b"k_m2l", b"k_near", b"k_leaf_far", b"k_up_direct", b"k_corr", b"k_cache_m2l"):
+        assert k in blob, k
 
 
 @pytest.mark.parametrize("sz,d,ns", [(1, 1, 8), (3, 2, 8), (16, 3, 8), (13, 3, 10)])
