@@ -202,8 +202,20 @@ void Operator::uploadPlan() {
     up(dM2LSrc, plan.m2lSrc);
     std::vector<int> pairTgt(plan.m2lSrc.size());
     for (size_t i = 0; i < plan.m2lTgt.size(); ++i)
-        for (int64_t p = plan.m2lPtr[i]; p < plan.m2lPtr[i + 1]; ++p) pairTgt[p] = plan.m2lTgt[i];
+        for (int64_t p = plan.m2lPtr[i]; p < plan.m2lPtr[i + 1]; ++p)  // ~target: canonical (column-major) block
+            pairTgt[p] = p < plan.m2lPtr[i] + plan.m2lNDir[i] ? plan.m2lTgt[i] : ~plan.m2lTgt[i];
     up(dM2LPairTgt, pairTgt);
+    up(dM2LNDir, plan.m2lNDir);
+    up(dM2LCanonBase, plan.m2lCanonBase);
+    up(dM2LInPtr, plan.m2lInPtr);
+    up(dM2LOutSlot, plan.m2lOutSlot);
+    dM2LPart.alloc((size_t)std::max(plan.m2lCanon, 1) * kRank * sizeof(double));
+    std::vector<int2> ns(plan.nearSym.size());
+    for (size_t i = 0; i < ns.size(); ++i) ns[i] = make_int2(plan.nearSym[i][0], plan.nearSym[i][1]);
+    up(dNearSym, ns);
+    up(dNearInPtr, plan.nearInPtr);
+    up(dNearInOff, plan.nearInOff);
+    dNearPart.alloc((size_t)std::max<int64_t>(plan.nearPartTotal, 1) * sizeof(double));
     auto to_int4 = [](const std::vector<std::array<int, 4>>& v) {
         std::vector<int4> o(v.size());
         for (size_t i = 0; i < v.size(); ++i) o[i] = make_int4(v[i][0], v[i][1], v[i][2], v[i][3]);
@@ -267,12 +279,12 @@ void Operator::cache(int id) {
     ensureDevice();
     ModeCache& mc = modes[id];
     mc.Knear.alloc((size_t)plan.nearKTotal * sizeof(double));
-    mc.Km2l.alloc((size_t)plan.pairsM2L * 256 * sizeof(double));
+    mc.Km2l.alloc((size_t)plan.storedM2L * 256 * sizeof(double));
     const Params* P = dParams.as<Params>();
     int maxSrc = 1;
     for (size_t li = 0; li < plan.leaves.size(); ++li)
         maxSrc = std::max<int>(maxSrc, (int)(plan.nearPtr[li + 1] - plan.nearPtr[li]));
-    launch_cache_m2l(plan.pairsM2L, dM2LPairTgt.as<int>(), dM2LSrc.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
+    launch_cache_m2l(plan.storedM2L,dM2LPairTgt.as<int>(), dM2LSrc.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
                      dNrx.as<double>(), dNry.as<double>(), dStCoef.as<double>(), P, id, mc.Km2l.as<double>(), own);
     launch_cache_near((int)plan.leaves.size(), dLeaves.as<int>(), dNearPtr.as<int64_t>(), dNearSrc.as<int>(),
                       dNearKOff.as<int64_t>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dPxT.as<double>(),
@@ -326,18 +338,26 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
                   (int)plan.topGroupStart.size() - 1, dTopGroup.as<int>(), P, dMult.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[3], s));
     // M2L for every active node (writes its local; L2L is applied by the leaf walk)
+    // K_{B<-A} = (-1)^m K_{A<-B}^T for the merged kernel; Id = m
+    const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
     if (mask & kStageFar) {
-        launch_m2l((int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LSrc.as<int>(),
-                   mc.Km2l.as<double>(), dMult.as<double>(), dLocal.as<double>(), s);
+        const int nt = (int)plan.m2lTgt.size();
+        launch_m2l(nt, dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(), dM2LCanonBase.as<int>(),
+                   dM2LOutSlot.as<int>(), dM2LSrc.as<int>(), mc.Km2l.as<double>(), dMult.as<double>(), sgn, dM2LPart.as<double>(),
+                   dLocal.as<double>(), s);
     }
-    if (tm) HIP_CHECK(hipEventRecord(ev[4], s));
+    if (tm) HIP_CHECK(hipEventRecord(ev[4], s));  // the m2l stage time is k_m2l alone (roofline kernel)
+    if ((mask & kStageFar) && plan.m2lCanon > 0)
+        launch_m2l_gather((int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LInPtr.as<int>(), dM2LPart.as<double>(),
+                          dLocal.as<double>(), s);
     launch_near((int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(),
-                dNearKOff.as<int64_t>(), mc.Knear.as<double>(), dFT.as<double>(), dPerm.as<int>(), maxNearS, mask, out,
-                s);
-    if (mask & kStageFar)
+                dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(), dFT.as<double>(), dPerm.as<int>(),
+                maxNearS, mask, sgn, dNearPart.as<double>(), out, s);
+    if ((mask & kStageFar) || ((mask & kStageNear) && plan.nearPartTotal > 0))
         launch_leaf_far((int)plan.leaves.size(), dLeafInfo.as<int4>(), dChainPtr.as<int>(), dChain.as<int>(),
                         dSlot.as<int>(), dLocal.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
-                        dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dPerm.as<int>(), P, out, s);
+                        dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dPerm.as<int>(), P,
+                        dNearInPtr.as<int>(), dNearInOff.as<int64_t>(), dNearPart.as<double>(), mask, out, s);
     if (tm) HIP_CHECK(hipEventRecord(ev[5], s));
     launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), charge, dFO.as<double>(), mc.C.as<double>(),
                 mc.mu.as<double>(), P, mask, M_1_PI / 2.0, out, s);

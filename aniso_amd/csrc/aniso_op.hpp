@@ -97,6 +97,8 @@ private:
     DevBuf dPxT, dPyT, dPerm, dW, dNcx, dNcy, dNrx, dNry, dBegin, dCount, dParent, dSlot, dChild, dIsLeaf;
     DevBuf dLeaves, dNearPtr, dNearSrc, dNearKOff, dM2LTgt, dM2LPtr, dM2LSrc, dM2LPairTgt;
     DevBuf dUpDirect, dTopNode, dTopChild, dTopGroup, dLeafInfo, dNearPtsPtr, dNearPts, dChainPtr, dChain;
+    DevBuf dM2LNDir, dM2LCanonBase, dM2LInPtr, dM2LOutSlot, dM2LPart;  // symmetric M2L
+    DevBuf dNearSym, dNearInPtr, dNearInOff, dNearPart;              // symmetric near field
     DevBuf dParams, dStCoef;
     DevBuf dCharge, dOut, dFT, dFO, dMult, dLocal, dSigmaS, dTmp, dTmp2;
     std::vector<ModeCache> modes;

@@ -282,6 +282,10 @@ int aniso_stats(aniso_handle h, int64_t* s) {
             if (op.tree.isLeaf[i]) mx = std::max<int64_t>(mx, op.tree.count[i]);
         s[6] = mx;
         s[7] = op.geo.N;
+        s[8] = op.plan.storedNear;
+        s[9] = op.plan.storedM2L;
+        s[10] = op.plan.m2lCanon;
+        s[11] = op.plan.nearPartTotal;
     });
 }
 

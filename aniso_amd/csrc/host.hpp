@@ -14,6 +14,7 @@ namespace aniso {
 
 constexpr double kEps = 1e-12;  // bbfmm/utils.h:46
 constexpr int kUpBig = 256;     // up-pass nodes with more points get a whole workgroup
+constexpr int kMaxCanon = 32;   // canonical (symmetric) M2L pairs per target: k_m2l's LDS staging
 
 // Geometry::Geometry (Geometry.cpp:10-114) + the singular Duffy rule
 // (KernelFactory.cpp:15-16, 863-986).
@@ -64,6 +65,17 @@ struct Plan {
     std::vector<int64_t> nearKOff;             // per leaf: offset of its K block (doubles)
     std::vector<std::array<int, 4>> leafInfo;  // per leaf: node, begin, count, S (source points)
     std::vector<int> leafChainPtr, leafChain;  // per leaf: ancestors level 1 .. leaf (top-down)
+    // symmetric storage: M2L targets' stored sources are
+    // [m2lNDir directed | canonical]; canonical pair c (= m2lCanonBase + j) sends
+    // its transposed product to partial slot m2lOutSlot[c]; slots are contiguous
+    // per receiver: [m2lInPtr[k], m2lInPtr[k+1]) for target m2lTgt[k].
+    bool symmetric = true;
+    std::vector<int> m2lNDir, m2lCanonBase, m2lInPtr, m2lOutSlot;
+    int m2lCanon = 0;
+    int64_t storedM2L = 0, storedNear = 0, nearPartTotal = 0;
+    std::vector<std::array<int, 2>> nearSym;   // per leaf: directed source points, partial base
+    std::vector<int> nearInPtr;                // per leaf: incoming partial ranges
+    std::vector<int64_t> nearInOff;
     std::vector<int64_t> nearPtsPtr;           // per leaf: its S source points (tree positions)
     std::vector<int> nearPts;
     int upBig = 0;                             // upDirect[0, upBig) have > kUpBig points

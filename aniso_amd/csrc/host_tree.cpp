@@ -2,6 +2,7 @@
 // (bbfmm.h:146-449), and the flattened per-shard work plan uploaded to HBM.
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cmath>
 #include <stdexcept>
 #include <thread>
@@ -283,36 +284,123 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
             int c = t.child[topNode[s]][q];
             topChild[s][q] = (c >= 0 && !t.isEmpty[c]) ? slotOf[c] : -1;
         }
-    // ---- M2L over V then X (bbfmm.h:1051-1065), active non-empty targets
+    // ---- M2L over V then X (bbfmm.h:1051-1065), active non-empty targets.
+    // V is a symmetric relation and K_{B<-A} = (-1)^m K_{A<-B}^T (tau is symmetric,
+    // g_m(-d) = (-1)^m g_m(d)), so when both ends are targets here only the block
+    // of the smaller id is stored (up to kMaxCanon per target, the rest directed):
+    // its owner also produces the transposed product into a partial slot; slots
+    // are numbered receiver-contiguously so k_m2l_gather reads one range per node.
+    const char* symEnv = std::getenv("ANISO_SYMMETRIC");
+    symmetric = !(symEnv && symEnv[0] == '0');
+    int maxCanon = kMaxCanon;  // ANISO_MAX_CANON: tuning/experiments only (<= kMaxCanon)
+    if (const char* mc = std::getenv("ANISO_MAX_CANON")) maxCanon = std::max(0, std::min(kMaxCanon, std::atoi(mc)));
+    std::vector<char> m2lActive(t.nn, 0);
+    for (int i = 0; i < t.nn; ++i) m2lActive[i] = !t.isEmpty[i] && t.parent[i] != -1 && intersects(i);
+    std::vector<std::vector<int>> inCanon(t.nn), inFrom(t.nn);  // per receiver: canonical ids, their senders
     m2lPtr.push_back(0);
+    int canon = 0;
+    std::vector<int> canonSrc;
     for (int i = 0; i < t.nn; ++i) {
-        if (t.isEmpty[i] || t.parent[i] == -1 || !intersects(i)) continue;
+        if (!m2lActive[i]) continue;
         m2lTgt.push_back(i);
-        for (int64_t k = t.vPtr[i]; k < t.vPtr[i + 1]; ++k)
-            if (!t.isEmpty[t.vIdx[k]]) m2lSrc.push_back(t.vIdx[k]);
+        canonSrc.clear();
+        for (int64_t k = t.vPtr[i]; k < t.vPtr[i + 1]; ++k) {
+            int b = t.vIdx[k];
+            if (t.isEmpty[b]) continue;
+            ++pairsM2L;
+            if (symmetric && m2lActive[b]) {
+                if (i < b && (int)canonSrc.size() < maxCanon) {
+                    canonSrc.push_back(b);
+                    continue;
+                }
+                if (i > b && std::find(inFrom[i].begin(), inFrom[i].end(), b) != inFrom[i].end())
+                    continue;  // arrives through b's transposed product
+            }
+            m2lSrc.push_back(b);
+        }
         for (int64_t k = t.xPtr[i]; k < t.xPtr[i + 1]; ++k)
-            if (!t.isEmpty[t.xIdx[k]]) m2lSrc.push_back(t.xIdx[k]);
+            if (!t.isEmpty[t.xIdx[k]]) {
+                m2lSrc.push_back(t.xIdx[k]);
+                ++pairsM2L;
+            }
+        m2lNDir.push_back((int)(m2lSrc.size() - m2lPtr.back()));
+        m2lCanonBase.push_back(canon);
+        for (int b : canonSrc) {
+            m2lSrc.push_back(b);
+            inCanon[b].push_back(canon++);
+            inFrom[b].push_back(i);
+        }
         m2lPtr.push_back((int64_t)m2lSrc.size());
     }
-    pairsM2L = (int64_t)m2lSrc.size();
-    // ---- near field over U then W (bbfmm.h:1081-1099), owned non-empty leaves
-    nearPtr.push_back(0);
+    m2lCanon = canon;
+    storedM2L = (int64_t)m2lSrc.size();
+    m2lOutSlot.assign(canon, -1);
+    m2lInPtr.push_back(0);
+    int slot = 0;
+    for (int i : m2lTgt) {
+        for (int c : inCanon[i]) m2lOutSlot[c] = slot++;
+        m2lInPtr.push_back(slot);
+    }
+    if (slot != canon) throw std::logic_error("symmetric M2L: canonical pair without an active receiver");
+    // ---- near field over U then W (bbfmm.h:1081-1099), owned non-empty leaves.
+    // U is symmetric as well: per leaf the stored sources are [directed | canonical]
+    // (self block, W members and unowned U members first; then the U members with a
+    // larger id); the transposed products land in a contiguous partial range.
+    std::vector<int> leafIdx(t.nn, -1);
     for (int i = 0; i < t.nn; ++i) {
         if (!t.isLeaf[i] || t.isEmpty[i] || !intersects(i)) continue;
         if (t.begin[i] < ownBegin || t.begin[i] + t.count[i] > ownEnd)
             throw std::logic_error("shard boundary splits a leaf");
+        leafIdx[i] = (int)leaves.size();
         leaves.push_back(i);
+    }
+    std::vector<std::vector<int64_t>> nearIn(leaves.size());
+    nearPtr.push_back(0);
+    int64_t partTotal = 0;
+    for (size_t li = 0; li < leaves.size(); ++li) {
+        const int i = leaves[li];
         nearKOff.push_back(nearKTotal);
-        int64_t S = 0;
-        for (int64_t k = t.uPtr[i]; k < t.uPtr[i + 1]; ++k)
-            if (!t.isEmpty[t.uIdx[k]]) { nearSrc.push_back(t.uIdx[k]); S += t.count[t.uIdx[k]]; }
-        for (int64_t k = t.wPtr[i]; k < t.wPtr[i + 1]; ++k)
-            if (!t.isEmpty[t.wIdx[k]]) { nearSrc.push_back(t.wIdx[k]); S += t.count[t.wIdx[k]]; }
+        int64_t S = 0, Sdir = 0;
+        canonSrc.clear();
+        for (int64_t k = t.uPtr[i]; k < t.uPtr[i + 1]; ++k) {
+            int b = t.uIdx[k];
+            if (t.isEmpty[b]) continue;
+            pairsNear += t.count[i] * t.count[b];
+            // k_near reduces a canonical column within one pass of <= 64 row pairs
+            if (symmetric && b != i && leafIdx[b] >= 0 && t.count[i] <= 128 && t.count[b] <= 128) {
+                if (i < b) canonSrc.push_back(b);
+                continue;
+            }
+            nearSrc.push_back(b);
+            S += t.count[b];
+        }
+        for (int64_t k = t.wPtr[i]; k < t.wPtr[i + 1]; ++k) {
+            int b = t.wIdx[k];
+            if (t.isEmpty[b]) continue;
+            pairsNear += t.count[i] * t.count[b];
+            nearSrc.push_back(b);
+            S += t.count[b];
+        }
+        Sdir = S;
+        const int64_t partBase = partTotal;
+        for (int b : canonSrc) {
+            nearSrc.push_back(b);
+            nearIn[leafIdx[b]].push_back(partTotal);
+            partTotal += t.count[b];
+            S += t.count[b];
+        }
         nearPtr.push_back((int64_t)nearSrc.size());
         nearKTotal += S * (t.count[i] + (t.count[i] & 1));  // rows padded to even: 16-B aligned columns
-        pairsNear += S * t.count[i];
-        if (S > (int64_t)1 << 30) throw std::invalid_argument("leaf neighbourhood too large");
+        storedNear += S * t.count[i];
+        if (S > (int64_t)1 << 30 || partTotal > (int64_t)1 << 31) throw std::invalid_argument("leaf neighbourhood too large");
         leafInfo.push_back({i, (int)t.begin[i], (int)t.count[i], (int)S});
+        nearSym.push_back({(int)Sdir, (int)partBase});
+    }
+    nearPartTotal = partTotal;
+    nearInPtr.push_back(0);
+    for (auto& v : nearIn) {
+        nearInOff.insert(nearInOff.end(), v.begin(), v.end());
+        nearInPtr.push_back((int)nearInOff.size());
     }
     nearPtsPtr.push_back(0);
     for (size_t li = 0; li < leaves.size(); ++li) {

@@ -14,6 +14,7 @@
 
 #include <cmath>
 
+#include "host.hpp"  // kMaxCanon
 #include "kernels.hpp"
 
 namespace aniso {
@@ -301,40 +302,170 @@ __global__ void __launch_bounds__(256) k_up_top(int nslot, int nInternal, const 
 // M2L over the V then X lists with the cached merged 16x16 operators
 // (bbfmm.h:1051-1065).  HBM-bound stream: one wave per target node, each pair's
 // 2 KB operator is read as 64 lanes x 32 contiguous bytes (two dwordx4 loads).
-// Lane l owns row t = l>>2 and columns 4(l&3)..4(l&3)+3.
+// Directed blocks are row-major K[t][s]: lane l owns row t = l>>2 and columns
+// 4(l&3)..4(l&3)+3.
+// Symmetric storage: the target's stored pairs are
+// [directed | canonical]; for a canonical pair (n, B) the same 2 KB block also
+// gives B's contribution sgn * K^T mult[n], written to partial slot
+// canonBase + j and gathered by k_m2l_gather.  Canonical blocks are stored
+// column-major (K[t][s] at s*16 + t): lane l owns column s = l>>2 and rows
+// 4(l&3)..4(l&3)+3, so the transposed product is 4 in-lane FMAs + a 4-lane
+// (quad) reduction per pair, and the forward product accumulates per lane across
+// pairs with one 16-lane reduction per target.
+// Lane-quad exchange through DPP quad_perm (no LDS round trip).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double quad_sum(double v) {
+    v += dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
+    return v;
+}
+
+// One 2 KB block as 64 lanes x 32 B: lane l reads doubles 4l .. 4l+3.  `ok`
+// is wave-uniform: a skipped block reads as zeros (the predicated tail of a
+// group costs no extra round trip).
+__device__ __forceinline__ void load_block(const double* __restrict__ K, int64_t p, int lane, bool ok, dbl2& x0,
+                                           dbl2& x1) {
+    x0 = dbl2{0.0, 0.0};
+    x1 = dbl2{0.0, 0.0};
+    if (ok) {
+        const dbl2* k = reinterpret_cast<const dbl2*>(K + (size_t)p * 256) + 2 * lane;
+        x0 = __builtin_nontemporal_load(k);
+        x1 = __builtin_nontemporal_load(k + 1);
+    }
+}
+
 __global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ tgt, const int64_t* __restrict__ ptr,
-                                             const int* __restrict__ src, const double* __restrict__ K,
-                                             const double* __restrict__ mult, double* __restrict__ local) {
-    int wave = (blockIdx.x * blockDim.x + threadIdx.x) / kWave;
-    int lane = threadIdx.x & (kWave - 1);
+                                             const int* __restrict__ nDir, const int* __restrict__ canonBase,
+                                             const int* __restrict__ outSlot, const int* __restrict__ src,
+                                             const double* __restrict__ K, const double* __restrict__ mult, double sgn,
+                                             double* __restrict__ partial, double* __restrict__ local) {
+    // wave-uniform indexing (readfirstlane): descriptors and source ids come
+    // through the scalar unit, so the stream's addresses never wait on a load
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) / kWave));
+    const int lane = threadIdx.x & (kWave - 1);
     if (wave >= ntgt) return;
-    int n = tgt[wave];
-    int t = lane >> 2, q = lane & 3;
-    int64_t p0 = ptr[wave], p1 = ptr[wave + 1];
-    double acc0 = 0.0, acc1 = 0.0;
-    int64_t p = p0;
-    for (; p + 1 < p1; p += 2) {
-        const dbl2* ka = reinterpret_cast<const dbl2*>(K + (size_t)p * 256 + t * 16 + q * 4);
-        const dbl2* kb = reinterpret_cast<const dbl2*>(K + (size_t)(p + 1) * 256 + t * 16 + q * 4);
-        dbl2 a0 = __builtin_nontemporal_load(ka), a1 = __builtin_nontemporal_load(ka + 1);
-        dbl2 b0 = __builtin_nontemporal_load(kb), b1 = __builtin_nontemporal_load(kb + 1);
-        const double2* ma = reinterpret_cast<const double2*>(mult + (size_t)src[p] * kRank + q * 4);
-        const double2* mb = reinterpret_cast<const double2*>(mult + (size_t)src[p + 1] * kRank + q * 4);
-        double2 ma0 = ma[0], ma1 = ma[1], mb0 = mb[0], mb1 = mb[1];
-        acc0 += a0.x * ma0.x + a0.y * ma0.y + a1.x * ma1.x + a1.y * ma1.y;
-        acc1 += b0.x * mb0.x + b0.y * mb0.y + b1.x * mb1.x + b1.y * mb1.y;
+    const int n = tgt[wave];
+    const int t = lane >> 2, q = lane & 3;
+    const int64_t p0 = ptr[wave], p1 = ptr[wave + 1], pd = p0 + nDir[wave];
+    const int nC = (int)(p1 - pd);  // canonical pairs, <= kMaxCanon (host plan)
+    // lane-parallel prefetch of the canonical sources and their partial slots
+    const int cSrc = lane < nC ? src[pd + lane] : 0;
+    const int cSlot = lane < nC ? outSlot[canonBase[wave] + lane] : 0;
+    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
+    // ---- directed pairs (row-major): lane owns row t, columns 4q .. 4q+3
+    for (int64_t c = p0; c < pd; c += kWave) {
+        const int cnt = (int)min<int64_t>(kWave, pd - c);
+        const int mySrc = lane < cnt ? src[c + lane] : 0;
+        for (int j = 0; j < cnt; j += 4) {
+            dbl2 a0, a1, b0, b1, c0, c1, d0, d1;
+            load_block(K, c + j, lane, true, a0, a1);
+            load_block(K, c + j + 1, lane, j + 1 < cnt, b0, b1);
+            load_block(K, c + j + 2, lane, j + 2 < cnt, c0, c1);
+            load_block(K, c + j + 3, lane, j + 3 < cnt, d0, d1);
+            // a skipped block's source id is a valid clamp; its block is zero
+            const double4 ma = *reinterpret_cast<const double4*>(mult + (size_t)__builtin_amdgcn_readlane(mySrc, j) * kRank + q * 4);
+            const double4 mb = *reinterpret_cast<const double4*>(mult + (size_t)__builtin_amdgcn_readlane(mySrc, min(j + 1, cnt - 1)) * kRank + q * 4);
+            const double4 mc = *reinterpret_cast<const double4*>(mult + (size_t)__builtin_amdgcn_readlane(mySrc, min(j + 2, cnt - 1)) * kRank + q * 4);
+            const double4 md = *reinterpret_cast<const double4*>(mult + (size_t)__builtin_amdgcn_readlane(mySrc, min(j + 3, cnt - 1)) * kRank + q * 4);
+            acc0 += a0.x * ma.x + a0.y * ma.y + a1.x * ma.z + a1.y * ma.w;
+            acc1 += b0.x * mb.x + b0.y * mb.y + b1.x * mb.z + b1.y * mb.w;
+            acc2 += c0.x * mc.x + c0.y * mc.y + c1.x * mc.z + c1.y * mc.w;
+            acc3 += d0.x * md.x + d0.y * md.y + d1.x * md.z + d1.y * md.w;
+        }
     }
-    if (p < p1) {
-        const dbl2* ka = reinterpret_cast<const dbl2*>(K + (size_t)p * 256 + t * 16 + q * 4);
-        dbl2 a0 = __builtin_nontemporal_load(ka), a1 = __builtin_nontemporal_load(ka + 1);
-        const double2* ma = reinterpret_cast<const double2*>(mult + (size_t)src[p] * kRank + q * 4);
-        double2 ma0 = ma[0], ma1 = ma[1];
-        acc0 += a0.x * ma0.x + a0.y * ma0.y + a1.x * ma1.x + a1.y * ma1.y;
+    double acc = (acc0 + acc1) + (acc2 + acc3);
+    // ---- canonical pairs (column-major): lane owns column s = t, rows 4q .. 4q+3
+    if (nC > 0) {
+        const double4 mn = *reinterpret_cast<const double4*>(mult + (size_t)n * kRank + q * 4);
+        const double m0 = sgn * mn.x, m1 = sgn * mn.y, m2 = sgn * mn.z, m3 = sgn * mn.w;
+        double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;  // forward rows 4q+j, this lane's column
+        // transposed products stay in registers (lane (s, q) keeps entry s of pair
+        // 4g + q) and are stored after the stream: on CDNA vmcnt also counts
+        // stores, so stores inside the loop would stall it
+        constexpr int kGroups = (kMaxCanon + 3) / 4;
+        double y[kGroups];
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g) {
+            y[g] = 0.0;
+            const int j = 4 * g;
+            if (j < nC) {
+                dbl2 a0, a1, b0, b1, e0, e1, f0, f1;
+                load_block(K, pd + j, lane, true, a0, a1);
+                load_block(K, pd + j + 1, lane, j + 1 < nC, b0, b1);
+                load_block(K, pd + j + 2, lane, j + 2 < nC, e0, e1);
+                load_block(K, pd + j + 3, lane, j + 3 < nC, f0, f1);
+                const double xa = mult[(size_t)__builtin_amdgcn_readlane(cSrc, j) * kRank + t];
+                const double xb = mult[(size_t)__builtin_amdgcn_readlane(cSrc, min(j + 1, nC - 1)) * kRank + t];
+                const double xe = mult[(size_t)__builtin_amdgcn_readlane(cSrc, min(j + 2, nC - 1)) * kRank + t];
+                const double xf = mult[(size_t)__builtin_amdgcn_readlane(cSrc, min(j + 3, nC - 1)) * kRank + t];
+                c0 += (a0.x * xa + b0.x * xb) + (e0.x * xe + f0.x * xf);
+                c1 += (a0.y * xa + b0.y * xb) + (e0.y * xe + f0.y * xf);
+                c2 += (a1.x * xa + b1.x * xb) + (e1.x * xe + f1.x * xf);
+                c3 += (a1.y * xa + b1.y * xb) + (e1.y * xe + f1.y * xf);
+                const double ya = quad_sum(a0.x * m0 + a0.y * m1 + a1.x * m2 + a1.y * m3);
+                const double yb = quad_sum(b0.x * m0 + b0.y * m1 + b1.x * m2 + b1.y * m3);
+                const double ye = quad_sum(e0.x * m0 + e0.y * m1 + e1.x * m2 + e1.y * m3);
+                const double yf = quad_sum(f0.x * m0 + f0.y * m1 + f1.x * m2 + f1.y * m3);
+                y[g] = q == 0 ? ya : q == 1 ? yb : q == 2 ? ye : yf;
+            }
+        }
+        // partial slots: lane (s, q) stores entry s of pair 4g + q (8 B lanes, 128 B
+        // per pair); slot ids shuffled with every lane active
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g) {
+            if (4 * g < nC) {
+                const int jj = 4 * g + q;
+                const int slot = __shfl(cSlot, jj);
+                if (jj < nC) partial[(size_t)slot * kRank + t] = y[g];
+            }
+        }
+        // forward rows: sum c_j over the 16 columns (lane bits 2..5), then row
+        // t = 4q' + j sits in entry j of the lanes with q == q' (e.g. lane q')
+#pragma unroll
+        for (int off = 4; off < kWave; off <<= 1) {
+            c0 += __shfl_xor(c0, off);
+            c1 += __shfl_xor(c1, off);
+            c2 += __shfl_xor(c2, off);
+            c3 += __shfl_xor(c3, off);
+        }
+        const int jr = t & 3;
+        const double v = jr == 0 ? c0 : jr == 1 ? c1 : jr == 2 ? c2 : c3;  // row 4q + jr
+        // lane (t, q) needs row t = 4(t>>2) + jr from a lane with q == t>>2
+        const double w = __shfl(v, 4 * t + (t >> 2));
+        if (q == 0) acc += w;
     }
-    double acc = acc0 + acc1;
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
+    acc = quad_sum(acc);
     if (q == 0) local[(size_t)n * kRank + t] = acc;
+}
+
+// local[B] += the transposed canonical-pair products addressed to B: one
+// contiguous slot range per target, summed in a fixed order (deterministic).
+// One thread per (target, entry).
+__global__ void k_m2l_gather(int ntgt, const int* __restrict__ tgt, const int* __restrict__ inPtr,
+                             const double* __restrict__ partial, double* __restrict__ local) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int w = gid >> 4, r = gid & 15;
+    if (w >= ntgt) return;
+    const int j0 = inPtr[w], j1 = inPtr[w + 1];
+    if (j0 == j1) return;
+    const double* pp = partial + (size_t)j0 * kRank + r;
+    const int n = j1 - j0;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int j = 0;
+    for (; j + 3 < n; j += 4) {
+        a0 += __builtin_nontemporal_load(pp + (size_t)j * kRank);
+        a1 += __builtin_nontemporal_load(pp + (size_t)(j + 1) * kRank);
+        a2 += __builtin_nontemporal_load(pp + (size_t)(j + 2) * kRank);
+        a3 += __builtin_nontemporal_load(pp + (size_t)(j + 3) * kRank);
+    }
+    for (; j < n; ++j) a0 += __builtin_nontemporal_load(pp + (size_t)j * kRank);
+    local[(size_t)tgt[w] * kRank + r] += (a0 + a1) + (a2 + a3);
 }
 
 // U/W near field for one target leaf per wave (bbfmm.h:1081-1099, 1111-1113).
@@ -347,9 +478,10 @@ __global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ t
 // 4 independent loads in flight per lane.
 __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ leafInfo,
                                               const int64_t* __restrict__ nearPtsPtr, const int* __restrict__ nearPts,
-                                              const int64_t* __restrict__ nearKOff, const double* __restrict__ K,
-                                              const double* __restrict__ fT, const int* __restrict__ perm, int maxS,
-                                              int flags, double* __restrict__ out) {
+                                              const int64_t* __restrict__ nearKOff, const int2* __restrict__ nearSym,
+                                              const double* __restrict__ K, const double* __restrict__ fT,
+                                              const int* __restrict__ perm, int maxS, int flags, double sgn,
+                                              double* __restrict__ partial, double* __restrict__ out) {
     extern __shared__ double sh[];
     const int wv = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
     const int li = blockIdx.x * (blockDim.x / kWave) + wv;
@@ -383,6 +515,8 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
     __syncthreads();
     if (!active) return;
     const int nT = info.z, S = info.w;
+    const int2 sym = nearSym[li];  // (directed source points Sdir, partial base)
+    const int Sdir = sym.x;
     const int64_t tb = info.y;
     const double* Kl = K + koff;
     const int nTs = nT + (nT & 1);
@@ -394,10 +528,37 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
     for (int rc = 0; rc < rp; rc += kWave) {
         const int r = rc + (lane & (lpc - 1));
         double a0 = 0.0, a1 = 0.0;
+        if ((flags & kStageNear) && S > Sdir) {
+            // canonical U pairs (host: only when rp <= 64): one read of each column
+            // gives this leaf's row sums and the other leaf's transposed product
+            // sgn * sum_t K[t][s] f[t], reduced over the column's lanes.
+            const dbl2* kc = reinterpret_cast<const dbl2*>(Kl) + r;
+            const double fa0 = (r < rp && 2 * r < nT) ? fT[tb + 2 * r] : 0.0;
+            const double fa1 = (r < rp && 2 * r + 1 < nT) ? fT[tb + 2 * r + 1] : 0.0;
+            const int ncol = S - Sdir;
+            for (int i0 = 0; i0 < ncol; i0 += cps) {
+                const int s = Sdir + i0 + cph;
+                const bool ok = (i0 + cph < ncol) && r < rp;
+                dbl2 k0 = ok ? __builtin_nontemporal_load(kc + (size_t)s * rp) : dbl2{0.0, 0.0};
+                const double fsv = ok ? fs[s] : 0.0;
+                a0 += k0.x * fsv;
+                a1 += k0.y * fsv;
+                double c = k0.x * fa0 + k0.y * fa1;
+                for (int off = 1; off < lpc; off <<= 1) c += __shfl_xor(c, off);
+                // column s's charge is consumed: its LDS word now holds the product
+                // (stores inside the stream would stall it: vmcnt counts stores)
+                if (ok && (lane & (lpc - 1)) == 0) fs[s] = sgn * c;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int i = lane; i < ncol; i += kWave) partial[(int64_t)sym.y + i] = fs[Sdir + i];
+        }
         if ((flags & kStageNear) && r < rp) {
             const dbl2* kc = reinterpret_cast<const dbl2*>(Kl) + r;
             const int stride = rp;  // dbl2 elements per column
             int s = cph;
+            const int S = Sdir;  // directed columns
             for (; s + 3 * cps < S; s += 4 * cps) {
                 dbl2 k0 = __builtin_nontemporal_load(kc + (size_t)s * stride);
                 dbl2 k1 = __builtin_nontemporal_load(kc + (size_t)(s + cps) * stride);
@@ -440,6 +601,9 @@ __global__ void __launch_bounds__(256) k_leaf_far(int nl, const int4* __restrict
                                                   const double* __restrict__ nrx, const double* __restrict__ nry,
                                                   const double* __restrict__ pxT, const double* __restrict__ pyT,
                                                   const int* __restrict__ perm, const Params* __restrict__ P,
+                                                  const int* __restrict__ nearInPtr,
+                                                  const int64_t* __restrict__ nearInOff,
+                                                  const double* __restrict__ nearPartial, int flags,
                                                   double* __restrict__ out) {
     __shared__ double Rs[4][kRank * kRank];
     for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) Rs[i / (kRank * kRank)][i % (kRank * kRank)] = P->R[i / (kRank * kRank)][i % (kRank * kRank)];
@@ -448,8 +612,19 @@ __global__ void __launch_bounds__(256) k_leaf_far(int nl, const int4* __restrict
     const int r = threadIdx.x & (kRank - 1);
     if (li >= nl) return;
     const int4 info = leafInfo[li];
+    const int n = info.x, nT = info.z;
+    const int64_t tb = info.y;
+    if (flags & kStageNear) {  // symmetric near field: transposed U-pair products addressed to this leaf
+        const int j0 = nearInPtr[li], j1 = nearInPtr[li + 1];
+        if (j0 < j1)
+            for (int t = r; t < nT; t += kRank) {
+                double acc = 0.0;
+                for (int j = j0; j < j1; ++j) acc += nearPartial[nearInOff[j] + t];
+                out[perm[tb + t]] += acc;
+            }
+    }
     const int cb = chainPtr[li], depth = chainPtr[li + 1] - cb;
-    if (depth == 0) return;  // the root itself is the leaf: no far field
+    if (!(flags & kStageFar) || depth == 0) return;  // the root itself is the leaf: no far field
     const int myNode = r < depth ? chain[cb + r] : 0;
     double m[kPrefetchDepth];
 #pragma unroll
@@ -479,8 +654,6 @@ __global__ void __launch_bounds__(256) k_leaf_far(int nl, const int4* __restrict
     double vv[kRank];
 #pragma unroll
     for (int c = 0; c < kRank; ++c) vv[c] = __shfl(v, c, kRank);
-    const int n = info.x, nT = info.z;
-    const int64_t tb = info.y;
     const double cx = ncx[n], cy = ncy[n], rx = nrx[n], ry = nry[n];
     for (int t = r; t < nT; t += kRank) {
         double Sx[kNP], Sy[kNP];
@@ -583,8 +756,10 @@ __global__ void k_permute(int64_t N, const int* __restrict__ perm, const double*
 
 // ----------------------------------------------------------------- cache build
 
-// downPassCache's M2L blocks (bbfmm.h:959-975, 782-804) for all (target, source)
-// pairs: entry e = pair*256 + t*16 + s, K[t][s] = kernel(cheb_s(src), cheb_t(tgt)).
+// downPassCache's M2L blocks (bbfmm.h:959-975, 782-804) for all stored (target,
+// source) pairs, K[t][s] = kernel(cheb_s(src), cheb_t(tgt)): directed blocks
+// row-major (pair*256 + t*16 + s), canonical blocks (pairTgt = ~target)
+// column-major (pair*256 + s*16 + t), the layouts k_m2l streams.
 __global__ void __launch_bounds__(256) k_cache_m2l(int64_t total, const int* __restrict__ pairTgt,
                                                    const int* __restrict__ src, const double* __restrict__ ncx,
                                                    const double* __restrict__ ncy, const double* __restrict__ nrx,
@@ -595,6 +770,12 @@ __global__ void __launch_bounds__(256) k_cache_m2l(int64_t total, const int* __r
     int64_t p = e >> 8;
     int t = (int)((e >> 4) & 15), s = (int)(e & 15);
     int tn = pairTgt[p], sn = src[p];
+    if (tn < 0) {  // canonical: column-major
+        tn = ~tn;
+        const int tmp = t;
+        t = s;
+        s = tmp;
+    }
     double bx = ncx[tn] + nrx[tn] * P->cheb[t & 3];
     double by = ncy[tn] + nry[tn] * P->cheb[t >> 2];
     double ax = ncx[sn] + nrx[sn] * P->cheb[s & 3];
@@ -687,30 +868,41 @@ void launch_up_top(int nslot, int nInternal, const int* slotNode, const int4* sl
     HIP_LAUNCH_CHECK();
 }
 
-void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* src, const double* K, const double* mult,
+void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
+                const int* outSlot, const int* src, const double* K, const double* mult, double sgn, double* partial,
                 double* local, hipStream_t s) {
     if (ntgt <= 0) return;
-    k_m2l<<<blocks_for((int64_t)ntgt * kWave, 256), 256, 0, s>>>(ntgt, tgt, ptr, src, K, mult, local);
+    k_m2l<<<blocks_for((int64_t)ntgt * kWave, 256), 256, 0, s>>>(ntgt, tgt, ptr, nDir, canonBase, outSlot, src, K, mult,
+                                                                sgn, partial, local);
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_m2l_gather(int ntgt, const int* tgt, const int* inPtr, const double* partial, double* local,
+                       hipStream_t s) {
+    if (ntgt <= 0) return;
+    k_m2l_gather<<<blocks_for((int64_t)ntgt * kRank, 256), 256, 0, s>>>(ntgt, tgt, inPtr, partial, local);
     HIP_LAUNCH_CHECK();
 }
 
 void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts, const int64_t* nearKOff,
-                 const double* K, const double* fT, const int* perm, int maxS, int flags, double* out, hipStream_t s) {
+                 const int2* nearSym, const double* K, const double* fT, const int* perm, int maxS, int flags,
+                 double sgn, double* partial, double* out, hipStream_t s) {
     if (nl <= 0) return;
     int wpb = maxS * 8 * 4 <= 48 * 1024 ? 4 : 1;
     size_t shm = (size_t)wpb * (maxS > 0 ? maxS : 1) * sizeof(double);
-    k_near<<<blocks_for(nl, wpb), wpb * kWave, shm, s>>>(nl, leafInfo, nearPtsPtr, nearPts, nearKOff, K, fT, perm,
-                                                        maxS > 0 ? maxS : 1, flags, out);
+    k_near<<<blocks_for(nl, wpb), wpb * kWave, shm, s>>>(nl, leafInfo, nearPtsPtr, nearPts, nearKOff, nearSym, K, fT,
+                                                        perm, maxS > 0 ? maxS : 1, flags, sgn, partial, out);
     HIP_LAUNCH_CHECK();
 }
 
 void launch_leaf_far(int nl, const int4* leafInfo, const int* chainPtr, const int* chain, const int* slot,
                      const double* local, const double* ncx, const double* ncy, const double* nrx, const double* nry,
-                     const double* pxT, const double* pyT, const int* perm, const Params* P, double* out,
-                     hipStream_t s) {
+                     const double* pxT, const double* pyT, const int* perm, const Params* P, const int* nearInPtr,
+                     const int64_t* nearInOff, const double* nearPartial, int flags, double* out, hipStream_t s) {
     if (nl <= 0) return;
     k_leaf_far<<<blocks_for((int64_t)nl * kRank, 256), 256, 0, s>>>(nl, leafInfo, chainPtr, chain, slot, local, ncx, ncy,
-                                                                   nrx, nry, pxT, pyT, perm, P, out);
+                                                                   nrx, nry, pxT, pyT, perm, P, nearInPtr, nearInOff,
+                                                                   nearPartial, flags, out);
     HIP_LAUNCH_CHECK();
 }
 

@@ -43,14 +43,18 @@ void launch_up_direct(int nn, int nBig, const int* nodes, const int64_t* begin, 
                       const double* fT, const Params* P, double* mult, hipStream_t s);
 void launch_up_top(int nslot, int nInternal, const int* slotNode, const int4* slotChild, int ngroups,
                    const int* groupStart, const Params* P, double* mult, hipStream_t s);
-void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* src, const double* K, const double* mult,
+void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
+                const int* outSlot, const int* src, const double* K, const double* mult, double sgn, double* partial,
                 double* local, hipStream_t s);
+void launch_m2l_gather(int ntgt, const int* tgt, const int* inPtr, const double* partial, double* local,
+                       hipStream_t s);
 void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts, const int64_t* nearKOff,
-                 const double* K, const double* fT, const int* perm, int maxS, int flags, double* out, hipStream_t s);
+                 const int2* nearSym, const double* K, const double* fT, const int* perm, int maxS, int flags,
+                 double sgn, double* partial, double* out, hipStream_t s);
 void launch_leaf_far(int nl, const int4* leafInfo, const int* chainPtr, const int* chain, const int* slot,
                      const double* local, const double* ncx, const double* ncy, const double* nrx, const double* nry,
-                     const double* pxT, const double* pyT, const int* perm, const Params* P, double* out,
-                     hipStream_t s);
+                     const double* pxT, const double* pyT, const int* perm, const Params* P, const int* nearInPtr,
+                     const int64_t* nearInOff, const double* nearPartial, int flags, double* out, hipStream_t s);
 void launch_corr(int d, int64_t b, int64_t e, const int* perm, const double* charge, const double* fO, const double* C,
                  const double* mu, const Params* P, int flags, double scale, double* out, hipStream_t s);
 void launch_cache_m2l(int64_t npairs, const int* pairTgt, const int* src, const double* ncx, const double* ncy,

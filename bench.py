@@ -204,8 +204,11 @@ def main():
     my_stats = op.stats()
     ms = 1e3 * elapsed / args.steps
     value = args.steps / elapsed
-    # dominant kernel: k_m2l (streams the merged 16x16 M2L operators)
-    m2l_bytes = 8.0 * my_stats["m2l_entries"] + 2.0 * 128.0 * my_stats["m2l_targets"]
+    # dominant kernel: k_m2l (streams the stored merged 16x16 M2L operators once:
+    # 2 KB per stored block, + multipole read and local write per target node, +
+    # one 128-B transposed partial per canonical pair)
+    m2l_bytes = (2048.0 * my_stats["stored_m2l"] + 2.0 * 128.0 * my_stats["m2l_targets"]
+                 + 128.0 * my_stats["m2l_canon"])
     m2l_ms = times["m2l"]
     achieved = m2l_bytes / (m2l_ms * 1e-3) / 1e9 if m2l_ms > 0 else 0.0
     traffic, tsrc = pmc_traffic("aniso::k_m2l") if world == 1 and args.sz == 1024 and args.d == 1 else (None, None)

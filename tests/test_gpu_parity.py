@@ -54,6 +54,7 @@ CASES = [
     (24, 1, 3, 10, 2, "rough", [0, 3]),      # maxLevel-limited: 64-point leaves
     (8, 2, 1, 8, 0, "main", [0]),            # maxLevel 0: one 256-point leaf, near field only
     (1, 3, 1, 8, 20, "main", [0]),           # single square: the root is the only leaf
+    (15, 3, 2, 8, 2, "rough", [0, 1]),       # ~127-point leaves: symmetric and directed U pairs mixed
 ]
 
 
@@ -270,3 +271,28 @@ def test_bench_sharded_path_rehearsal_two_ranks():
     res = json.loads(line)
     assert res["n_gpus"] == 2
     assert res["verify_rel_err_vs_unsharded"] <= 1e-13
+
+
+@pytest.mark.parametrize("sz,d,ks,ml", [(32, 1, 2, 20), (11, 3, 2, 20), (15, 3, 2, 2)])
+def test_symmetric_storage_matches_directed(sz, d, ks, ml, monkeypatch):
+    """Symmetric M2L / U-pair storage against the fully directed
+    plan (ANISO_SYMMETRIC=0) and the oracle, for even and odd modes."""
+    import aniso_amd
+
+    _torch()
+    a, o, xy = _pair(sz, d, ks, 8, ml, "rough", seed=3)
+    monkeypatch.setenv("ANISO_SYMMETRIC", "0")
+    b = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, ml)
+    monkeypatch.delenv("ANISO_SYMMETRIC")
+    b.setCoeff(*rough_coeffs(xy, 3))
+    sa, sb = a.stats(), b.stats()
+    assert sa["m2l_canon"] > 0 and sb["m2l_canon"] == 0 and sb["near_partial"] == 0
+    assert sa["stored_m2l"] < sb["stored_m2l"] and sa["stored_near"] < sb["stored_near"]
+    assert sa["m2l_pairs"] == sb["m2l_pairs"] and sa["near_entries"] == sb["near_entries"]
+    q = np.random.default_rng(5).uniform(-1, 1, a.N)
+    for m in range(2 * ks - 1):
+        for x in (a, b, o):
+            x.cache(m)
+        ya, yb, yo = a.mapping(q, m), b.mapping(q, m), o.mapping(q, m)
+        assert _rel(ya, yb) <= 1e-12, (m, _rel(ya, yb))
+        assert _rel(ya, yo) <= TOL and _rel(yb, yo) <= TOL
