@@ -256,7 +256,7 @@ class Aniso:
     def stage_times(self):
         t = (ctypes.c_float * 7)()
         _check(lib().aniso_stage_times(self.address, t))
-        return dict(zip(["prep", "up_direct", "up_top", "m2l", "near_l2l_l2p", "corr", "total"], list(t)))
+        return dict(zip(["prep", "up", "m2l", "near", "down", "corr", "total"], list(t)))
 
     def line_integrals(self, seg):
         seg = np.ascontiguousarray(np.asarray(seg, dtype=np.float64).reshape(-1, 4))

@@ -187,6 +187,7 @@ void Operator::ensureDevice() {
     dTmp2.alloc(geo.N * sizeof(double));
     dMult.alloc((size_t)tree.nn * kRank * sizeof(double));
     dLocal.alloc((size_t)tree.nn * kRank * sizeof(double));
+    dTotal.alloc((size_t)tree.nn * kRank * sizeof(double));
     HIP_CHECK(hipMemset(dMult.p, 0, dMult.bytes));
     HIP_CHECK(hipMemset(dLocal.p, 0, dLocal.bytes));
     uploadPlan();
@@ -224,20 +225,38 @@ void Operator::uploadPlan() {
     up(dLeafInfo, to_int4(plan.leafInfo));
     up(dNearPtsPtr, plan.nearPtsPtr);
     up(dNearPts, plan.nearPts);
-    up(dChainPtr, plan.leafChainPtr);
-    up(dChain, plan.leafChain);
-    up(dUpDirect, plan.upDirect);
-    up(dTopNode, plan.topNode);
-    std::vector<int4> tc(plan.topChild.size());
-    for (size_t i = 0; i < tc.size(); ++i)
-        tc[i] = make_int4(plan.topChild[i][0], plan.topChild[i][1], plan.topChild[i][2], plan.topChild[i][3]);
-    up(dTopChild, tc);
-    up(dTopGroup, plan.topGroupStart);
-    if (plan.topNode.size() * kRank * sizeof(double) > 64 * 1024)
-        throw std::logic_error("up-pass top levels exceed one workgroup's LDS");
-    int depth = 0;
-    for (int i = 0; i < tree.nn; ++i) depth = std::max(depth, tree.level[i]);
-    if (depth >= kMaxDepth) throw std::invalid_argument("tree deeper than " + std::to_string(kMaxDepth) + " levels");
+    up(dUpTaskPtr, plan.upTaskPtr);
+    up(dUpGrpPtr, plan.upGrpPtr);
+    up(dUpGrp, plan.upGrp);
+    up(dUpNode, plan.upNode);
+    up(dUpCode, to_int4(plan.upCode));
+    up(dDnTaskPtr, plan.dnTaskPtr);
+    up(dDnGrpPtr, plan.dnGrpPtr);
+    up(dDnGrp, plan.dnGrp);
+    up(dDnNode, to_int4(plan.dnNode));
+    up(dDnLeafPtr, plan.dnLeafPtr);
+    up(dDnLeafSlot, plan.dnLeafSlot);
+    up(dDnLeafIdx, plan.dnLeafIdx);
+    up(dDnLeafPts, plan.dnLeafPts);
+    up(dDnPtsRange, plan.dnPtsRange);
+    // per tier: points staged in LDS (tasks with more points read them from HBM)
+    constexpr int kPtsCapMax = 2048;
+    upTierCap.assign(plan.upTierTask.size(), 0);
+    for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k)
+        for (int task = plan.upTierTask[k]; task < plan.upTierTask[k + 1]; ++task) {
+            bool leaves = false;
+            for (int i = plan.upTaskPtr[task]; i < plan.upTaskPtr[task + 1]; ++i) leaves |= plan.upCode[i][0] == kLeafCode;
+            if (leaves)
+                upTierCap[k] = std::max<int>(upTierCap[k], (int)std::min<int64_t>(tree.count[plan.upNode[plan.upTaskPtr[task + 1] - 1]], kPtsCapMax));
+        }
+    dnTierCap.assign(plan.dnTierTask.size(), 0);
+    for (size_t k = 0; k + 1 < plan.dnTierTask.size(); ++k)
+        for (int task = plan.dnTierTask[k]; task < plan.dnTierTask[k + 1]; ++task)
+            dnTierCap[k] = std::max(dnTierCap[k], std::min(plan.dnPtsRange[task][1] - plan.dnPtsRange[task][0], kPtsCapMax));
+    // a task's expansions live in LDS (<= 4 levels: 85 nodes); a workgroup may use all 160 KiB
+    if (up_tier_lds(plan.upMaxTask, kPtsCapMax) > 160 * 1024 ||
+        down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, kPtsCapMax) > 160 * 1024)
+        throw std::logic_error("up/down pass task exceeds one workgroup's LDS");
     maxNearS = 1;
     for (size_t li = 0; li < plan.leaves.size(); ++li) {
         int64_t S = 0;
@@ -329,35 +348,39 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
     }
     launch_prepare(geo.N, dPerm.as<int>(), charge, dW.as<double>(), dFT.as<double>(), dFO.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[1], s));
-    // up pass (global, every rank): direct P2M below the cut, M2M above it
-    launch_up_direct((int)plan.upDirect.size(), plan.upBig, dUpDirect.as<int>(), dBegin.as<int64_t>(), dCount.as<int64_t>(),
-                     dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(),
-                     dPyT.as<double>(), dFT.as<double>(), P, dMult.as<double>(), s);
+    // up pass (global, every rank): tiers bottom-up
+    for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k)
+        launch_up_tier(plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask, upTierCap[k],
+                       dUpTaskPtr.as<int>(), dUpGrpPtr.as<int>(), dUpGrp.as<int>(), dUpNode.as<int>(),
+                       dUpCode.as<int4>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dNcx.as<double>(),
+                       dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(),
+                       dFT.as<double>(), P, dMult.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[2], s));
-    launch_up_top((int)plan.topNode.size(), plan.topInternal, dTopNode.as<int>(), dTopChild.as<int4>(),
-                  (int)plan.topGroupStart.size() - 1, dTopGroup.as<int>(), P, dMult.as<double>(), s);
-    if (tm) HIP_CHECK(hipEventRecord(ev[3], s));
-    // M2L for every active node (writes its local; L2L is applied by the leaf walk)
     // K_{B<-A} = (-1)^m K_{A<-B}^T for the merged kernel; Id = m
     const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
-    if (mask & kStageFar) {
-        const int nt = (int)plan.m2lTgt.size();
-        launch_m2l(nt, dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(), dM2LCanonBase.as<int>(),
-                   dM2LOutSlot.as<int>(), dM2LSrc.as<int>(), mc.Km2l.as<double>(), dMult.as<double>(), sgn, dM2LPart.as<double>(),
-                   dLocal.as<double>(), s);
-    }
-    if (tm) HIP_CHECK(hipEventRecord(ev[4], s));  // the m2l stage time is k_m2l alone (roofline kernel)
+    if (mask & kStageFar)
+        launch_m2l((int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(),
+                   dM2LCanonBase.as<int>(), dM2LOutSlot.as<int>(), dM2LSrc.as<int>(), mc.Km2l.as<double>(),
+                   dMult.as<double>(), sgn, dM2LPart.as<double>(), dLocal.as<double>(), s);
+    if (tm) HIP_CHECK(hipEventRecord(ev[3], s));
     if ((mask & kStageFar) && plan.m2lCanon > 0)
         launch_m2l_gather((int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LInPtr.as<int>(), dM2LPart.as<double>(),
                           dLocal.as<double>(), s);
     launch_near((int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(),
                 dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(), dFT.as<double>(), dPerm.as<int>(),
                 maxNearS, mask, sgn, dNearPart.as<double>(), out, s);
-    if ((mask & kStageFar) || ((mask & kStageNear) && plan.nearPartTotal > 0))
-        launch_leaf_far((int)plan.leaves.size(), dLeafInfo.as<int4>(), dChainPtr.as<int>(), dChain.as<int>(),
-                        dSlot.as<int>(), dLocal.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
-                        dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dPerm.as<int>(), P,
-                        dNearInPtr.as<int>(), dNearInOff.as<int64_t>(), dNearPart.as<double>(), mask, out, s);
+    if (tm) HIP_CHECK(hipEventRecord(ev[4], s));
+    // down pass (owned part): tiers top-down; L2L + M2L partial gather + L2P + near gather
+    if (mask & (kStageFar | kStageNear))
+        for (size_t k = 0; k + 1 < plan.dnTierTask.size(); ++k)
+            launch_down_tier(plan.dnTierTask[k + 1] - plan.dnTierTask[k], plan.dnTierTask[k], plan.dnMaxTask,
+                             plan.dnMaxLeaves, dnTierCap[k], dDnTaskPtr.as<int>(), dDnGrpPtr.as<int>(),
+                             dDnGrp.as<int>(), dDnNode.as<int4>(), dSlot.as<int>(), dLocal.as<double>(),
+                             dM2LPart.as<double>(), P, dTotal.as<double>(), dDnLeafPtr.as<int>(),
+                             dDnLeafSlot.as<int>(), dDnLeafIdx.as<int>(), dDnLeafPts.as<int>(), dDnPtsRange.as<int2>(),
+                             dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(),
+                             dPxT.as<double>(), dPyT.as<double>(), dPerm.as<int>(), dNearInPtr.as<int>(),
+                             dNearInOff.as<int64_t>(), dNearPart.as<double>(), mask, out, s);
     if (tm) HIP_CHECK(hipEventRecord(ev[5], s));
     launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), charge, dFO.as<double>(), mc.C.as<double>(),
                 mc.mu.as<double>(), P, mask, M_1_PI / 2.0, out, s);
@@ -382,10 +405,10 @@ StageTimes Operator::stageTimes() {
         }
     for (double& a : acc) a /= evUsed;
     r.prep = (float)acc[0];
-    r.upDirect = (float)acc[1];
-    r.upTop = (float)acc[2];
-    r.m2l = (float)acc[3];
-    r.near = (float)acc[4];
+    r.up = (float)acc[1];
+    r.m2l = (float)acc[2];
+    r.near = (float)acc[3];
+    r.down = (float)acc[4];
     r.corr = (float)acc[5];
     r.total = (float)(acc[0] + acc[1] + acc[2] + acc[3] + acc[4] + acc[5]);
     return r;

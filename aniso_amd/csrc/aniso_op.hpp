@@ -37,7 +37,7 @@ struct ModeCache {
 };
 
 struct StageTimes {
-    float prep = 0, upDirect = 0, upTop = 0, m2l = 0, near = 0, corr = 0, total = 0;
+    float prep = 0, up = 0, m2l = 0, near = 0, down = 0, corr = 0, total = 0;
 };
 
 class Operator {
@@ -93,14 +93,17 @@ private:
     std::vector<std::array<hipEvent_t, 7>> evPool;
     int evUsed = 0;
     int maxNearS = 0;
+    std::vector<int> upTierCap, dnTierCap;  // LDS point capacity per tier launch
     // geometry / tree on device
     DevBuf dPxT, dPyT, dPerm, dW, dNcx, dNcy, dNrx, dNry, dBegin, dCount, dParent, dSlot, dChild, dIsLeaf;
     DevBuf dLeaves, dNearPtr, dNearSrc, dNearKOff, dM2LTgt, dM2LPtr, dM2LSrc, dM2LPairTgt;
-    DevBuf dUpDirect, dTopNode, dTopChild, dTopGroup, dLeafInfo, dNearPtsPtr, dNearPts, dChainPtr, dChain;
+    DevBuf dUpTaskPtr, dUpGrpPtr, dUpGrp, dUpNode, dUpCode;                       // up-pass tiers
+    DevBuf dDnTaskPtr, dDnGrpPtr, dDnGrp, dDnNode, dDnLeafPtr, dDnLeafSlot, dDnLeafIdx, dDnLeafPts, dDnPtsRange;  // down
+    DevBuf dLeafInfo, dNearPtsPtr, dNearPts;
     DevBuf dM2LNDir, dM2LCanonBase, dM2LInPtr, dM2LOutSlot, dM2LPart;  // symmetric M2L
     DevBuf dNearSym, dNearInPtr, dNearInOff, dNearPart;              // symmetric near field
     DevBuf dParams, dStCoef;
-    DevBuf dCharge, dOut, dFT, dFO, dMult, dLocal, dSigmaS, dTmp, dTmp2;
+    DevBuf dCharge, dOut, dFT, dFO, dMult, dLocal, dTotal, dSigmaS, dTmp, dTmp2;
     std::vector<ModeCache> modes;
 };
 

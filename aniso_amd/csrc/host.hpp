@@ -13,7 +13,7 @@
 namespace aniso {
 
 constexpr double kEps = 1e-12;  // bbfmm/utils.h:46
-constexpr int kUpBig = 256;     // up-pass nodes with more points get a whole workgroup
+constexpr int kLeafCode = -2147483647 - 1;  // upCode of a leaf (P2M from its points)
 constexpr int kMaxCanon = 32;   // canonical (symmetric) M2L pairs per target: k_m2l's LDS staging
 
 // Geometry::Geometry (Geometry.cpp:10-114) + the singular Duffy rule
@@ -64,7 +64,6 @@ struct Plan {
     std::vector<int> nearSrc;
     std::vector<int64_t> nearKOff;             // per leaf: offset of its K block (doubles)
     std::vector<std::array<int, 4>> leafInfo;  // per leaf: node, begin, count, S (source points)
-    std::vector<int> leafChainPtr, leafChain;  // per leaf: ancestors level 1 .. leaf (top-down)
     // symmetric storage: M2L targets' stored sources are
     // [m2lNDir directed | canonical]; canonical pair c (= m2lCanonBase + j) sends
     // its transposed product to partial slot m2lOutSlot[c]; slots are contiguous
@@ -78,22 +77,35 @@ struct Plan {
     std::vector<int64_t> nearInOff;
     std::vector<int64_t> nearPtsPtr;           // per leaf: its S source points (tree positions)
     std::vector<int> nearPts;
-    int upBig = 0;                             // upDirect[0, upBig) have > kUpBig points
     int64_t nearKTotal = 0;
     std::vector<int> m2lTgt;                   // active target nodes with M2L work
     std::vector<int64_t> m2lPtr;               // CSR over m2lTgt -> source nodes
     std::vector<int> m2lSrc;
-    // up pass (global on every rank): direct P2M for nodes at level >= upCut and
-    // for all leaves; M2M in one workgroup for the internal nodes above upCut.
-    int upCut = 0;
-    std::vector<int> upDirect;
-    std::vector<int> topNode;                  // slots: internal (deepest level first), then their children
-    std::vector<std::array<int, 4>> topChild;  // per internal slot: child slots (-1 = empty)
-    std::vector<int> topGroupStart;            // slot ranges of internal nodes per level
-    int topInternal = 0;
+    // tiered up / down passes: tier k has root level
+    // tierRootLevel[k] and bottom level tierBottomLevel[k] (k = 0 is the deepest).
+    std::vector<int> tierRootLevel, tierBottomLevel;
+    // up (global on every rank; tiers bottom-up): task = subtree nodes, deepest
+    // level first; upCode per node: child LDS slots, -1 empty, -(id+2) a root of
+    // the tier below (read from HBM), kLeafCode for a leaf (P2M)
+    std::vector<int> upTierTask, upTaskPtr, upGrpPtr, upGrp, upNode;
+    std::vector<std::array<int, 4>> upCode;
+    int upMaxTask = 1;
+    int64_t upMaxPts = 0;  // points under a task root (staged in LDS when they fit)
+    // down (owned part; tiers top-down): dnNode = (node, parent code, child slot
+    // (R index), 0); leaves of each task in tree order (L2P + near gather)
+    std::vector<int> dnTierTask, dnTaskPtr, dnGrpPtr, dnGrp;
+    std::vector<std::array<int, 4>> dnNode;
+    std::vector<int> dnLeafPtr, dnLeafSlot, dnLeafIdx, dnLeafPts;  // leaves in tree order; dnLeafPts = begin
+    std::vector<std::array<int, 2>> dnPtsRange;                     // per task: owned point range
+    int dnMaxTask = 1, dnMaxLeaves = 1;
+    int64_t dnMaxPts = 0;
     int64_t pairsNear = 0, pairsM2L = 0;       // kernel entries per apply
 
     void build(const Tree& t, int np, int rank, int nranks);
+
+  private:
+    void buildUpTasks(const Tree& t);
+    void buildDownTasks(const Tree& t);
 };
 
 // Small per-mode tables for the correction stencil (nearRemoval + refineAddOn,

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <functional>
 #include <cmath>
 #include <stdexcept>
 #include <thread>
@@ -249,41 +250,26 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         ownEnd = cuts[rank + 1];
     }
     auto intersects = [&](int n) { return t.begin[n] < ownEnd && t.begin[n] + t.count[n] > ownBegin; };
-    // ---- up pass (global): direct P2M at level >= upCut and leaves; M2M above
-    upCut = std::min(4, t.maxLevel);
-    std::vector<std::vector<int>> internalByLevel(upCut + 1);
-    std::vector<int> small;
-    for (int i = 0; i < t.nn; ++i) {
-        if (t.isEmpty[i]) continue;
-        if (t.isLeaf[i] || t.level[i] >= upCut) (t.count[i] > kUpBig ? upDirect : small).push_back(i);
-        else internalByLevel[t.level[i]].push_back(i);
-    }
-    upBig = (int)upDirect.size();  // big nodes first: one 256-thread workgroup each
-    upDirect.insert(upDirect.end(), small.begin(), small.end());
-    std::vector<int> slotOf(t.nn, -1);
-    topGroupStart.push_back(0);
-    for (int L = upCut - 1; L >= 0; --L) {
-        for (int i : internalByLevel[L]) {
-            slotOf[i] = (int)topNode.size();
-            topNode.push_back(i);
-        }
-        topGroupStart.push_back((int)topNode.size());
-    }
-    topInternal = (int)topNode.size();
-    for (int s = 0; s < topInternal; ++s)
-        for (int q = 0; q < 4; ++q) {
-            int c = t.child[topNode[s]][q];
-            if (c >= 0 && !t.isEmpty[c] && slotOf[c] < 0) {
-                slotOf[c] = (int)topNode.size();
-                topNode.push_back(c);
+    // ---- tiers for the up / down passes (bbfmm.h:825-861 upPass, 1066-1106
+    // downPass): subtrees of at most 4 levels (the top one up to 5), each one
+    // workgroup with its nodes' expansions resident in LDS; roots of tier k-1
+    // sit one level below tier k's bottom and are exchanged through HBM.
+    {
+        // the root (level 0) never interacts: its multipole is never a source and
+        // its local is zero, so tiers cover levels 1 .. D (none for a lone leaf)
+        const int D = t.maxLevel;
+        tierRootLevel.clear();
+        tierBottomLevel.clear();
+        if (D >= 1) {
+            tierRootLevel.push_back(std::max(1, D - 3));
+            tierBottomLevel.push_back(D);
+            while (tierRootLevel.back() > 1) {
+                tierBottomLevel.push_back(tierRootLevel.back() - 1);
+                tierRootLevel.push_back(std::max(1, tierRootLevel.back() - 4));
             }
         }
-    topChild.resize(topInternal);
-    for (int s = 0; s < topInternal; ++s)
-        for (int q = 0; q < 4; ++q) {
-            int c = t.child[topNode[s]][q];
-            topChild[s][q] = (c >= 0 && !t.isEmpty[c]) ? slotOf[c] : -1;
-        }
+    }
+    buildUpTasks(t);
     // ---- M2L over V then X (bbfmm.h:1051-1065), active non-empty targets.
     // V is a symmetric relation and K_{B<-A} = (-1)^m K_{A<-B}^T (tau is symmetric,
     // g_m(-d) = (-1)^m g_m(d)), so when both ends are targets here only the block
@@ -410,14 +396,133 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         }
         nearPtsPtr.push_back((int64_t)nearPts.size());
     }
-    leafChainPtr.push_back(0);
-    std::vector<int> up;
-    for (int n : leaves) {
-        up.clear();
-        for (int a = n; t.parent[a] != -1; a = t.parent[a]) up.push_back(a);
-        leafChain.insert(leafChain.end(), up.rbegin(), up.rend());
-        leafChainPtr.push_back((int)leafChain.size());
+    buildDownTasks(t);
+}
+
+
+// Nodes of the subtree of `root` down to level `bottom`, level by level (keep()
+// filters nodes; children of leaves do not exist).
+static std::vector<std::vector<int>> task_levels(const Tree& t, int root, int bottom,
+                                                 const std::function<bool(int)>& keep) {
+    std::vector<std::vector<int>> lv{{root}};
+    while (t.level[lv.back()[0]] < bottom) {
+        std::vector<int> next;
+        for (int n : lv.back())
+            if (!t.isLeaf[n])
+                for (int q = 0; q < 4; ++q) {
+                    const int c = t.child[n][q];
+                    if (c >= 0 && keep(c)) next.push_back(c);
+                }
+        if (next.empty()) break;
+        lv.push_back(std::move(next));
     }
+    return lv;
+}
+
+void Plan::buildUpTasks(const Tree& t) {
+    std::vector<int> slotOf(t.nn, -1);
+    auto keep = [&](int n) { return !t.isEmpty[n]; };
+    upTierTask.assign(1, 0);
+    upTaskPtr.assign(1, 0);
+    upGrpPtr.assign(1, 0);
+    upGrp.clear();
+    upNode.clear();
+    upCode.clear();
+    upMaxTask = 1;
+    upMaxPts = 0;
+    for (size_t k = 0; k < tierRootLevel.size(); ++k) {  // bottom-up
+        for (int r = 0; r < t.nn; ++r) {
+            if (t.level[r] != tierRootLevel[k] || t.isEmpty[r]) continue;
+            auto lv = task_levels(t, r, tierBottomLevel[k], keep);
+            const int base = (int)upNode.size();
+            for (int L = (int)lv.size() - 1; L >= 0; --L) {  // deepest level first
+                upGrp.push_back((int)upNode.size());
+                for (int n : lv[L]) {
+                    slotOf[n] = (int)upNode.size() - base;
+                    upNode.push_back(n);
+                }
+            }
+            for (int i = base; i < (int)upNode.size(); ++i) {
+                const int n = upNode[i];
+                std::array<int, 4> c{kLeafCode, kLeafCode, kLeafCode, kLeafCode};
+                if (!t.isLeaf[n])
+                    for (int q = 0; q < 4; ++q) {
+                        const int ch = t.child[n][q];
+                        c[q] = (ch < 0 || t.isEmpty[ch]) ? -1
+                               : t.level[ch] <= tierBottomLevel[k] ? slotOf[ch]
+                                                                   : -(ch + 2);  // root of the tier below
+                    }
+                upCode.push_back(c);
+            }
+            upGrpPtr.push_back((int)upGrp.size());
+            upTaskPtr.push_back((int)upNode.size());
+            upMaxTask = std::max(upMaxTask, (int)upNode.size() - base);
+            upMaxPts = std::max<int64_t>(upMaxPts, t.count[r]);
+        }
+        upTierTask.push_back((int)upTaskPtr.size() - 1);
+    }
+    upGrp.push_back((int)upNode.size());  // sentinel: group g spans [upGrp[g], upGrp[g+1])
+}
+
+void Plan::buildDownTasks(const Tree& t) {
+    auto intersects = [&](int n) { return t.begin[n] < ownEnd && t.begin[n] + t.count[n] > ownBegin; };
+    auto keep = [&](int n) { return !t.isEmpty[n] && intersects(n); };
+    std::vector<int> slotOf(t.nn, -1), leafOf(t.nn, -1);
+    for (size_t i = 0; i < leaves.size(); ++i) leafOf[leaves[i]] = (int)i;
+    dnTierTask.assign(1, 0);
+    dnTaskPtr.assign(1, 0);
+    dnGrpPtr.assign(1, 0);
+    dnGrp.clear();
+    dnNode.clear();
+    dnLeafPtr.assign(1, 0);
+    dnLeafSlot.clear();
+    dnLeafIdx.clear();
+    dnLeafPts.clear();
+    dnPtsRange.clear();
+    dnMaxPts = 0;
+    dnMaxTask = 1;
+    dnMaxLeaves = 1;
+    for (int k = (int)tierRootLevel.size() - 1; k >= 0; --k) {  // top-down
+        for (int r = 0; r < t.nn; ++r) {
+            if (t.level[r] != tierRootLevel[k] || !keep(r)) continue;
+            auto lv = task_levels(t, r, tierBottomLevel[k], keep);
+            const int base = (int)dnNode.size();
+            for (auto& level : lv) {  // shallowest level first
+                dnGrp.push_back((int)dnNode.size());
+                for (int n : level) {
+                    slotOf[n] = (int)dnNode.size() - base;
+                    const int p = t.parent[n];  // the root's total is zero
+                    const int pc = (p < 0 || t.parent[p] < 0) ? -1 : n == r ? -(p + 2) : slotOf[p];
+                    dnNode.push_back({n, pc, t.slot[n], 0});
+                }
+            }
+            // owned leaves in tree order: they tile [ptsBegin, ptsEnd) contiguously
+            std::vector<int> lf;
+            for (int i = base; i < (int)dnNode.size(); ++i)
+                if (leafOf[dnNode[i][0]] >= 0) lf.push_back(i - base);
+            std::sort(lf.begin(), lf.end(), [&](int a, int b) { return t.begin[dnNode[base + a][0]] < t.begin[dnNode[base + b][0]]; });
+            int64_t pb = -1, pe = -1;
+            for (int sl : lf) {
+                const int n = dnNode[base + sl][0];
+                if (pe >= 0 && t.begin[n] != pe) throw std::logic_error("down task: owned leaves not contiguous");
+                if (pb < 0) pb = t.begin[n];
+                pe = t.begin[n] + t.count[n];
+                dnLeafSlot.push_back(sl);
+                dnLeafIdx.push_back(leafOf[n]);
+                dnLeafPts.push_back((int)t.begin[n]);
+            }
+            const int nl = (int)lf.size();
+            dnPtsRange.push_back({(int)std::max<int64_t>(pb, 0), (int)std::max<int64_t>(pe, 0)});
+            dnMaxPts = std::max<int64_t>(dnMaxPts, pe - pb);
+            dnLeafPtr.push_back((int)dnLeafSlot.size());
+            dnGrpPtr.push_back((int)dnGrp.size());
+            dnTaskPtr.push_back((int)dnNode.size());
+            dnMaxTask = std::max(dnMaxTask, (int)dnNode.size() - base);
+            dnMaxLeaves = std::max(dnMaxLeaves, nl);
+        }
+        dnTierTask.push_back((int)dnTaskPtr.size() - 1);
+    }
+    dnGrp.push_back((int)dnNode.size());
 }
 
 }  // namespace aniso

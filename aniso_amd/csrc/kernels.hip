@@ -60,6 +60,19 @@ __device__ __forceinline__ void cheb_weights(const Params* __restrict__ P, doubl
     }
 }
 
+// One Chebyshev interpolant weight S(s, c_i) (same arithmetic as cheb_weights).
+__device__ __forceinline__ double cheb_weight1(const Params* __restrict__ P, double s, int i) {
+    double T[kNP];
+    T[0] = 1.0;
+    T[1] = s;
+#pragma unroll
+    for (int l = 2; l < kNP; ++l) T[l] = 2.0 * s * T[l - 1] - T[l - 2];
+    double acc = 0.0;
+#pragma unroll
+    for (int l = 0; l < kNP; ++l) acc += T[l] * P->tnode[i + l * kNP];
+    return (2.0 * acc - 1.0) * (1.0 / kNP);
+}
+
 // integral_helper (KernelFactory.cpp:174-190): d-point Gauss rule on one piece
 // lying in one square; sigma_t's Legendre expansion is evaluated at GLOBAL
 // coordinates (reference quirk).  stcoef already carries 1/legendreNorms.
@@ -172,146 +185,115 @@ __global__ void k_prepare(int64_t N, const int* __restrict__ perm, const double*
     fO[k] = charge[k] * w[k];
 }
 
-// Up pass, part 1: multipole of every node at level >= Lc (and of every leaf) by
-// direct P2M over the node's contiguous tree-order point range, one wave per node.
-// For a degree np-1 Chebyshev interpolant the reference's M2M translation of the
-// children's P2M equals the parent's P2M exactly (the parent's interpolation
-// polynomials are reproduced by the children's interpolants), so this is the
-// reference's upPass (bbfmm.h:825-861) up to rounding, without one launch per level.
-__device__ __forceinline__ void p2m_point(const Params* __restrict__ P, double cx, double cy, double irx, double iry,
-                                          double x, double y, double f, double* acc) {
-    double Sx[kNP], Sy[kNP];
-    cheb_weights(P, (x - cx) * irx, Sx);
-    cheb_weights(P, (y - cy) * iry, Sy);
-#pragma unroll
-    for (int j = 0; j < kNP; ++j) {
-        const double sf = Sy[j] * f;
-#pragma unroll
-        for (int i = 0; i < kNP; ++i) acc[j * kNP + i] += Sx[i] * sf;
-    }
-}
-
-// Butterfly reduce-scatter of 16 per-lane sums over a wave (17 shuffles); lanes
-// with (lane & 3) == 0 return the total for entry p = rs_entry(lane).
-__device__ __forceinline__ double reduce_scatter16(double* acc, int lane) {
-#define ANISO_RS_STEP(NV, OFF, BIT)                               \
-    {                                                             \
-        const bool up = (lane >> (BIT)) & 1;                      \
-        _Pragma("unroll") for (int k = 0; k < (NV); ++k) {        \
-            double lo = acc[k], hi = acc[k + (NV)];               \
-            double keep = up ? hi : lo, send = up ? lo : hi;      \
-            acc[k] = keep + __shfl_xor(send, (OFF));              \
-        }                                                         \
-    }
-    ANISO_RS_STEP(8, 32, 5)
-    ANISO_RS_STEP(4, 16, 4)
-    ANISO_RS_STEP(2, 8, 3)
-    ANISO_RS_STEP(1, 4, 2)
-#undef ANISO_RS_STEP
-    double v = acc[0];
-    v += __shfl_xor(v, 1);
-    v += __shfl_xor(v, 2);
-    return v;
-}
-
-__device__ __forceinline__ int rs_entry(int lane) {
-    return (((lane >> 5) & 1) << 3) | (((lane >> 4) & 1) << 2) | (((lane >> 3) & 1) << 1) | ((lane >> 2) & 1);
-}
-
-// Up pass, part 1.  Blocks [0, nBig) take one big node each with 256 threads;
-// the remaining blocks take four small nodes each (one per wave).  Loads are
-// issued four points deep per thread.
-__global__ void __launch_bounds__(256) k_up_direct(int nn, int nBig, const int* __restrict__ nodes,
-                                                   const int64_t* __restrict__ begin,
-                                                   const int64_t* __restrict__ count, const double* __restrict__ ncx,
-                                                   const double* __restrict__ ncy, const double* __restrict__ nrx,
-                                                   const double* __restrict__ nry, const double* __restrict__ pxT,
-                                                   const double* __restrict__ pyT, const double* __restrict__ fT,
-                                                   const Params* __restrict__ P, double* __restrict__ mult) {
-    __shared__ double red[4][kRank];
-    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-    const bool big = (int)blockIdx.x < nBig;
-    const int wi = big ? (int)blockIdx.x : nBig + ((int)blockIdx.x - nBig) * 4 + wv;
-    if (!big && wi >= nn) return;
-    const int n = nodes[wi];
-    const double cx = ncx[n], cy = ncy[n], irx = 1.0 / nrx[n], iry = 1.0 / nry[n];
-    const int64_t b = begin[n], e = b + count[n];
-    const int stride = big ? (int)blockDim.x : kWave;
-    double acc[kRank];
-#pragma unroll
-    for (int p = 0; p < kRank; ++p) acc[p] = 0.0;
-    int64_t k = b + (big ? threadIdx.x : lane);
-    for (; k + 3 * stride < e; k += 4 * stride) {
-        double x[4], y[4], f[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            x[u] = pxT[k + u * stride];
-            y[u] = pyT[k + u * stride];
-            f[u] = fT[k + u * stride];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) p2m_point(P, cx, cy, irx, iry, x[u], y[u], f[u], acc);
-    }
-    for (; k < e; k += stride) p2m_point(P, cx, cy, irx, iry, pxT[k], pyT[k], fT[k], acc);
-    const double v = reduce_scatter16(acc, lane);
-    if (!big) {
-        if ((lane & 3) == 0) mult[(size_t)n * kRank + rs_entry(lane)] = v;
-        return;
-    }
-    if ((lane & 3) == 0) red[wv][rs_entry(lane)] = v;
-    __syncthreads();
-    if (threadIdx.x < kRank)
-        mult[(size_t)n * kRank + threadIdx.x] =
-            red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-}
-
-// Up pass, part 2: M2M (bbfmm.h:855-859) for the few internal nodes above Lc, in
-// one workgroup, level by level in LDS.  Slots [0, nInternal) are internal nodes
-// ordered deepest level first (groups by levelStart); the rest are their
-// children computed by k_up_direct.
-__global__ void __launch_bounds__(256) k_up_top(int nslot, int nInternal, const int* __restrict__ slotNode,
-                                                const int4* __restrict__ slotChild, int ngroups,
-                                                const int* __restrict__ groupStart, const Params* __restrict__ P,
-                                                double* __restrict__ mult) {
+// Up pass (bbfmm.h:825-861) as tiers of <= 4-level subtrees:
+// one workgroup per subtree keeps its nodes' multipoles in LDS, deepest level
+// first; a leaf's multipole is P2M over its contiguous tree-order points
+// (bbfmm.h:737-748), an internal node's is M2M of its children (bbfmm.h:855-859),
+// where a child below the tier is the root of a lower tier's task (read from HBM).
+// Phase 0 stages the transfer matrices, node boxes and the task's points in LDS
+// with one round of independent loads; the levels then run out of LDS.
+// One thread per (node, entry r), r = 4j + i:  M[r] = sum_p S(x_p, c_i) S(y_p, c_j) f_p.
+__global__ void __launch_bounds__(kTierThreads) k_up_tier(
+    int taskBase, int maxTask, int ptsCap, const int* __restrict__ taskPtr, const int* __restrict__ grpPtr,
+    const int* __restrict__ grp, const int* __restrict__ node, const int4* __restrict__ code,
+    const int64_t* __restrict__ begin, const int64_t* __restrict__ count, const double* __restrict__ ncx,
+    const double* __restrict__ ncy, const double* __restrict__ nrx, const double* __restrict__ nry,
+    const double* __restrict__ pxT, const double* __restrict__ pyT, const double* __restrict__ fT,
+    const Params* __restrict__ P, double* __restrict__ mult) {
     extern __shared__ double sm[];
-    for (int i = threadIdx.x; i < nslot * kRank; i += blockDim.x)
-        sm[i] = (i / kRank) < nInternal ? 0.0 : mult[(size_t)slotNode[i / kRank] * kRank + (i % kRank)];
+    int4* CD = reinterpret_cast<int4*>(sm);             // maxTask child codes
+    double* Rl = reinterpret_cast<double*>(CD + maxTask);  // 4 x 256 transfer matrices (transposed)
+    double* M = Rl + 4 * kRank * kRank;                 // maxTask x 16 multipoles
+    double* G = M + (size_t)maxTask * kRank;            // maxTask x 4: cx, cy, 1/rx, 1/ry
+    double* X = G + (size_t)maxTask * 4;                // ptsCap x (x, y, f)
+    double* Y = X + ptsCap;
+    double* F = Y + ptsCap;
+    int* LB = reinterpret_cast<int*>(F + ptsCap);       // maxTask: leaf point offset, count
+    int* LC = LB + maxTask;
+    const int task = taskBase + blockIdx.x;
+    const int n0 = taskPtr[task], n1 = taskPtr[task + 1], nt = n1 - n0;
+    const int root = node[n1 - 1];  // deepest level first: the root is last
+    const int64_t b0 = begin[root];
+    const int np = (int)count[root];
+    const bool staged = np <= ptsCap;
+    // M2M reads R[q][rr + 16 r] along rr: stage it transposed (r fastest) so the
+    // 16 lanes of one node hit 16 consecutive LDS words
+    for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) {
+        const int q = i >> 8, rr = (i >> 4) & 15, r = i & 15;
+        Rl[i] = P->R[q][rr + r * kRank];
+    }
+    for (int k = threadIdx.x; k < nt; k += blockDim.x) {
+        const int n = node[n0 + k];
+        G[4 * k] = ncx[n];
+        G[4 * k + 1] = ncy[n];
+        G[4 * k + 2] = 1.0 / nrx[n];
+        G[4 * k + 3] = 1.0 / nry[n];
+        LB[k] = (int)(begin[n] - b0);
+        LC[k] = (int)count[n];
+        CD[k] = code[n0 + k];
+    }
+    if (staged)
+        for (int p = threadIdx.x; p < np; p += blockDim.x) {
+            X[p] = pxT[b0 + p];
+            Y[p] = pyT[b0 + p];
+            F[p] = fT[b0 + p];
+        }
     __syncthreads();
-    for (int gidx = 0; gidx < ngroups; ++gidx) {
-        for (int i = groupStart[gidx] * kRank + threadIdx.x; i < groupStart[gidx + 1] * kRank; i += blockDim.x) {
-            const int ls = i / kRank, c = i % kRank;
-            const int4 ch = slotChild[ls];
-            const int cs[4] = {ch.x, ch.y, ch.z, ch.w};
+    const double* xs = staged ? X : pxT + b0;
+    const double* ys = staged ? Y : pyT + b0;
+    const double* fs = staged ? F : fT + b0;
+    for (int g = grpPtr[task]; g < grpPtr[task + 1]; ++g) {
+        const int s0 = grp[g] - n0, s1 = grp[g + 1] - n0;
+        for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
+            const int k = s0 + (it >> 4), r = it & (kRank - 1);
+            const int4 c = CD[k];
             double acc = 0.0;
+            if (c.x == kLeafCode) {
+                const double cx = G[4 * k], cy = G[4 * k + 1], irx = G[4 * k + 2], iry = G[4 * k + 3];
+                const int i = r & 3, j = r >> 2;
+                const int pb = LB[k], pe = pb + LC[k];
+                double a1 = 0.0;
+                int p = pb;
+                for (; p + 1 < pe; p += 2) {
+                    const double sx0 = cheb_weight1(P, (xs[p] - cx) * irx, i);
+                    const double sy0 = cheb_weight1(P, (ys[p] - cy) * iry, j);
+                    const double sx1 = cheb_weight1(P, (xs[p + 1] - cx) * irx, i);
+                    const double sy1 = cheb_weight1(P, (ys[p + 1] - cy) * iry, j);
+                    acc += sx0 * (sy0 * fs[p]);
+                    a1 += sx1 * (sy1 * fs[p + 1]);
+                }
+                if (p < pe) acc += cheb_weight1(P, (xs[p] - cx) * irx, i) * (cheb_weight1(P, (ys[p] - cy) * iry, j) * fs[p]);
+                acc += a1;
+            } else {
+                const int cs[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (cs[q] < 0) continue;
-                const double* R = P->R[q] + (size_t)c * kRank;
-                const double* cm = sm + (size_t)cs[q] * kRank;
+                for (int q = 0; q < 4; ++q) {
+                    if (cs[q] == -1) continue;
+                    const double* R = Rl + q * kRank * kRank + r;  // transposed: R[rr * 16 + r]
+                    double a = 0.0;
+                    if (cs[q] >= 0) {  // child in this task (LDS)
+                        const double* cm = M + (size_t)cs[q] * kRank;
 #pragma unroll
-                for (int r = 0; r < kRank; ++r) acc += R[r] * cm[r];
+                        for (int rr = 0; rr < kRank; ++rr) a += R[rr * kRank] * cm[rr];
+                    } else {  // root of the tier below (HBM)
+                        const double* cm = mult + (size_t)(-cs[q] - 2) * kRank;
+                        double v[kRank];
+#pragma unroll
+                        for (int rr = 0; rr < kRank; ++rr) v[rr] = cm[rr];
+#pragma unroll
+                        for (int rr = 0; rr < kRank; ++rr) a += R[rr * kRank] * v[rr];
+                    }
+                    acc += a;
+                }
             }
-            sm[i] = acc;
+            M[(size_t)k * kRank + r] = acc;
         }
         __syncthreads();
     }
-    for (int i = threadIdx.x; i < nInternal * kRank; i += blockDim.x)
-        mult[(size_t)slotNode[i / kRank] * kRank + (i % kRank)] = sm[i];
+    for (int it = threadIdx.x; it < nt * kRank; it += blockDim.x)
+        mult[(size_t)node[n0 + (it >> 4)] * kRank + (it & (kRank - 1))] = M[it];
 }
 
-// M2L over the V then X lists with the cached merged 16x16 operators
-// (bbfmm.h:1051-1065).  HBM-bound stream: one wave per target node, each pair's
-// 2 KB operator is read as 64 lanes x 32 contiguous bytes (two dwordx4 loads).
-// Directed blocks are row-major K[t][s]: lane l owns row t = l>>2 and columns
-// 4(l&3)..4(l&3)+3.
-// Symmetric storage: the target's stored pairs are
-// [directed | canonical]; for a canonical pair (n, B) the same 2 KB block also
-// gives B's contribution sgn * K^T mult[n], written to partial slot
-// canonBase + j and gathered by k_m2l_gather.  Canonical blocks are stored
-// column-major (K[t][s] at s*16 + t): lane l owns column s = l>>2 and rows
-// 4(l&3)..4(l&3)+3, so the transposed product is 4 in-lane FMAs + a 4-lane
-// (quad) reduction per pair, and the forward product accumulates per lane across
-// pairs with one 16-lane reduction per target.
 // Lane-quad exchange through DPP quad_perm (no LDS round trip).
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
@@ -446,9 +428,9 @@ __global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ t
 
 // local[B] += the transposed canonical-pair products addressed to B: one
 // contiguous slot range per target, summed in a fixed order (deterministic).
-// One thread per (target, entry).
-__global__ void k_m2l_gather(int ntgt, const int* __restrict__ tgt, const int* __restrict__ inPtr,
-                             const double* __restrict__ partial, double* __restrict__ local) {
+// One thread per (target, entry); 8 independent loads in flight per thread.
+__global__ void __launch_bounds__(256) k_m2l_gather(int ntgt, const int* __restrict__ tgt, const int* __restrict__ inPtr,
+                                                    const double* __restrict__ partial, double* __restrict__ local) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x;
     const int w = gid >> 4, r = gid & 15;
     if (w >= ntgt) return;
@@ -456,16 +438,16 @@ __global__ void k_m2l_gather(int ntgt, const int* __restrict__ tgt, const int* _
     if (j0 == j1) return;
     const double* pp = partial + (size_t)j0 * kRank + r;
     const int n = j1 - j0;
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int j = 0;
-    for (; j + 3 < n; j += 4) {
-        a0 += __builtin_nontemporal_load(pp + (size_t)j * kRank);
-        a1 += __builtin_nontemporal_load(pp + (size_t)(j + 1) * kRank);
-        a2 += __builtin_nontemporal_load(pp + (size_t)(j + 2) * kRank);
-        a3 += __builtin_nontemporal_load(pp + (size_t)(j + 3) * kRank);
+    for (; j + 7 < n; j += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] += __builtin_nontemporal_load(pp + (size_t)(j + u) * kRank);
     }
-    for (; j < n; ++j) a0 += __builtin_nontemporal_load(pp + (size_t)j * kRank);
-    local[(size_t)tgt[w] * kRank + r] += (a0 + a1) + (a2 + a3);
+#pragma unroll
+    for (int u = 0; u < 7; ++u)
+        if (j + u < n) a[u] += __builtin_nontemporal_load(pp + (size_t)(j + u) * kRank);
+    local[(size_t)tgt[w] * kRank + r] += ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
 // U/W near field for one target leaf per wave (bbfmm.h:1081-1099, 1111-1113).
@@ -589,82 +571,124 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
     }
 }
 
-// L2L + L2P per leaf (bbfmm.h:1070-1071, 1104), after k_near.  Sixteen lanes per
-// leaf (four leaves per wave): lane r holds entry r of the running local; the
-// walk goes from the level-1 ancestor down to the leaf, local <- R[slot] local +
-// M2L(node), with the ancestors' M2L locals prefetched in registers and the four
-// transfer matrices staged in LDS.  Then out[target] += L * local.
-__global__ void __launch_bounds__(256) k_leaf_far(int nl, const int4* __restrict__ leafInfo,
-                                                  const int* __restrict__ chainPtr, const int* __restrict__ chain,
-                                                  const int* __restrict__ slot, const double* __restrict__ local,
-                                                  const double* __restrict__ ncx, const double* __restrict__ ncy,
-                                                  const double* __restrict__ nrx, const double* __restrict__ nry,
-                                                  const double* __restrict__ pxT, const double* __restrict__ pyT,
-                                                  const int* __restrict__ perm, const Params* __restrict__ P,
-                                                  const int* __restrict__ nearInPtr,
-                                                  const int64_t* __restrict__ nearInOff,
-                                                  const double* __restrict__ nearPartial, int flags,
-                                                  double* __restrict__ out) {
-    __shared__ double Rs[4][kRank * kRank];
-    for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) Rs[i / (kRank * kRank)][i % (kRank * kRank)] = P->R[i / (kRank * kRank)][i % (kRank * kRank)];
-    __syncthreads();
-    const int li = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-    const int r = threadIdx.x & (kRank - 1);
-    if (li >= nl) return;
-    const int4 info = leafInfo[li];
-    const int n = info.x, nT = info.z;
-    const int64_t tb = info.y;
-    if (flags & kStageNear) {  // symmetric near field: transposed U-pair products addressed to this leaf
-        const int j0 = nearInPtr[li], j1 = nearInPtr[li + 1];
-        if (j0 < j1)
-            for (int t = r; t < nT; t += kRank) {
-                double acc = 0.0;
-                for (int j = j0; j < j1; ++j) acc += nearPartial[nearInOff[j] + t];
-                out[perm[tb + t]] += acc;
-            }
-    }
-    const int cb = chainPtr[li], depth = chainPtr[li + 1] - cb;
-    if (!(flags & kStageFar) || depth == 0) return;  // the root itself is the leaf: no far field
-    const int myNode = r < depth ? chain[cb + r] : 0;
-    double m[kPrefetchDepth];
-#pragma unroll
-    for (int k = 0; k < kPrefetchDepth; ++k) {
-        const int a = __shfl(myNode, k, kRank);
-        m[k] = (k < depth) ? local[(size_t)a * kRank + r] : 0.0;
-    }
-    double v = m[0];
-#pragma unroll
-    for (int k = 1; k < kPrefetchDepth; ++k) {
-        if (k < depth) {
-            const double* R = Rs[slot[__shfl(myNode, k, kRank)]];
-            double acc = m[k];
-#pragma unroll
-            for (int c = 0; c < kRank; ++c) acc += R[r + c * kRank] * __shfl(v, c, kRank);
-            v = acc;
+// Down pass (bbfmm.h:1066-1106) as tiers of <= 4-level subtrees, top-down, after
+// k_m2l, k_m2l_gather and k_near.  Per node: total = local (its M2L, transposed
+// partials included) + L2L of the parent's total
+// (bbfmm.h:1070-1071; the parent is in LDS, or in HBM for a task root).  Then per
+// owned leaf point: L2P (bbfmm.h:1104) + the gathered transposed U-pair products
+// of k_near, added to out.  dn = (node, parent code, child slot, 0).
+// Phase 0 issues every independent global load of the task at once (locals of
+// all nodes, the roots' parent totals, box geometry, points and
+// their output slots) into LDS; the levels and the points then run out of LDS.
+__global__ void __launch_bounds__(kTierThreads) k_down_tier(
+    int taskBase, int maxTask, int maxLeaves, int ptsCap, const int* __restrict__ taskPtr,
+    const int* __restrict__ grpPtr, const int* __restrict__ grp, const int4* __restrict__ dn,
+    const int* __restrict__ slot, const double* __restrict__ local, const double* __restrict__ m2lPart,
+    const Params* __restrict__ P, double* __restrict__ total, const int* __restrict__ leafPtr,
+    const int* __restrict__ leafSlot, const int* __restrict__ leafIdx, const int* __restrict__ leafBegin,
+    const int2* __restrict__ ptsRange, const double* __restrict__ ncx, const double* __restrict__ ncy,
+    const double* __restrict__ nrx, const double* __restrict__ nry, const double* __restrict__ pxT,
+    const double* __restrict__ pyT, const int* __restrict__ perm, const int* __restrict__ nearInPtr,
+    const int64_t* __restrict__ nearInOff, const double* __restrict__ nearPart, int flags, double* __restrict__ out) {
+    extern __shared__ double sm[];
+    int4* DN = reinterpret_cast<int4*>(sm);             // maxTask node records
+    double* Rl = reinterpret_cast<double*>(DN + maxTask);  // 4 x 256 transfer matrices
+    double* T = Rl + 4 * kRank * kRank;                 // maxTask x 16 totals
+    double* PT = T + (size_t)maxTask * kRank;           // 16: the task root's parent total
+    double* G = PT + kRank;                             // maxLeaves x 4: leaf cx, cy, 1/rx, 1/ry
+    double* X = G + (size_t)maxLeaves * 4;              // ptsCap x (x, y)
+    double* Y = X + ptsCap;
+    int* PM = reinterpret_cast<int*>(Y + ptsCap);       // ptsCap: perm (output index)
+    int* LB = PM + ptsCap;                              // maxLeaves + 1: leaf begins (tree positions)
+    int* LS = LB + maxLeaves + 1;                       // maxLeaves: leaf slot in the task
+    int* LI = LS + maxLeaves;                           // maxLeaves: plan leaf index
+    const int task = taskBase + blockIdx.x;
+    const int n0 = taskPtr[task], n1 = taskPtr[task + 1], nt = n1 - n0;
+    const int l0 = leafPtr[task], nl = leafPtr[task + 1] - l0;
+    const int2 pr = ptsRange[task];
+    const int npts = pr.y - pr.x;
+    const bool staged = npts <= ptsCap;
+    const bool far = flags & kStageFar;
+    // ---- phase 0: independent loads
+    if (far) {
+        for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) Rl[i] = (&P->R[0][0])[i];
+        for (int k = threadIdx.x; k < nt; k += blockDim.x) DN[k] = dn[n0 + k];
+        for (int it = threadIdx.x; it < nt * kRank; it += blockDim.x) {
+            const int k = it >> 4, r = it & (kRank - 1);
+            T[it] = local[(size_t)dn[n0 + k].x * kRank + r];
+        }
+        if (threadIdx.x < kRank) {
+            const int pc = dn[n0].y;
+            PT[threadIdx.x] = pc <= -2 ? total[(size_t)(-pc - 2) * kRank + threadIdx.x] : 0.0;
         }
     }
-    for (int k = kPrefetchDepth; k < depth; ++k) {  // trees deeper than the prefetch window
-        const int a = chain[cb + k];
-        const double* R = Rs[slot[a]];
-        double acc = local[(size_t)a * kRank + r];
-#pragma unroll
-        for (int c = 0; c < kRank; ++c) acc += R[r + c * kRank] * __shfl(v, c, kRank);
-        v = acc;
+    for (int e = threadIdx.x; e < nl; e += blockDim.x) {
+        LB[e] = leafBegin[l0 + e];
+        LS[e] = leafSlot[l0 + e];
+        LI[e] = leafIdx[l0 + e];
+        const int n = dn[n0 + leafSlot[l0 + e]].x;
+        G[4 * e] = ncx[n];
+        G[4 * e + 1] = ncy[n];
+        G[4 * e + 2] = 1.0 / nrx[n];
+        G[4 * e + 3] = 1.0 / nry[n];
     }
-    double vv[kRank];
+    if (threadIdx.x == 0) LB[nl] = pr.y;
+    if (staged)
+        for (int p = threadIdx.x; p < npts; p += blockDim.x) {
+            X[p] = pxT[pr.x + p];
+            Y[p] = pyT[pr.x + p];
+            PM[p] = perm[pr.x + p];
+        }
+    __syncthreads();
+    // ---- phase 1: L2L level by level (shallowest first), out of LDS
+    if (far) {
+        for (int g = grpPtr[task]; g < grpPtr[task + 1]; ++g) {
+            const int s0 = grp[g] - n0, s1 = grp[g + 1] - n0;
+            for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
+                const int k = s0 + (it >> 4), r = it & (kRank - 1);
+                const int4 d = DN[k];
+                if (d.y == -1) continue;
+                const double* pt = d.y >= 0 ? T + (size_t)d.y * kRank : PT;
+                const double* R = Rl + d.z * kRank * kRank;
+                double l2l = 0.0;
 #pragma unroll
-    for (int c = 0; c < kRank; ++c) vv[c] = __shfl(v, c, kRank);
-    const double cx = ncx[n], cy = ncy[n], rx = nrx[n], ry = nry[n];
-    for (int t = r; t < nT; t += kRank) {
-        double Sx[kNP], Sy[kNP];
-        cheb_weights(P, (pxT[tb + t] - cx) / rx, Sx);
-        cheb_weights(P, (pyT[tb + t] - cy) / ry, Sy);
-        double l2p = 0.0;
+                for (int c = 0; c < kRank; ++c) l2l += R[r + c * kRank] * pt[c];
+                T[(size_t)k * kRank + r] += l2l;
+            }
+            __syncthreads();
+        }
+        for (int it = threadIdx.x; it < nt * kRank; it += blockDim.x)
+            total[(size_t)DN[it >> 4].x * kRank + (it & (kRank - 1))] = T[it];
+    }
+    // ---- phase 2: owned points: L2P + near gather
+    for (int g = threadIdx.x; g < npts; g += blockDim.x) {
+        const int kpos = pr.x + g;
+        int lo = 0, hi = nl - 1;  // last leaf with LB <= kpos
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (LB[mid] <= kpos) lo = mid;
+            else hi = mid - 1;
+        }
+        const int t = kpos - LB[lo], li = LI[lo];
+        double v = 0.0;
+        if (flags & kStageNear) {
+            const int j0 = nearInPtr[li], j1 = nearInPtr[li + 1];
+            for (int j = j0; j < j1; ++j) v += nearPart[nearInOff[j] + t];
+        }
+        if (far) {
+            const double x = staged ? X[g] : pxT[kpos], y = staged ? Y[g] : pyT[kpos];
+            double Sx[kNP], Sy[kNP];
+            cheb_weights(P, (x - G[4 * lo]) * G[4 * lo + 2], Sx);
+            cheb_weights(P, (y - G[4 * lo + 1]) * G[4 * lo + 3], Sy);
+            const double* L = T + (size_t)LS[lo] * kRank;
+            double l2p = 0.0;
 #pragma unroll
-        for (int j = 0; j < kNP; ++j)
+            for (int j = 0; j < kNP; ++j)
 #pragma unroll
-            for (int i = 0; i < kNP; ++i) l2p += Sx[i] * Sy[j] * vv[j * kNP + i];
-        out[perm[tb + t]] += l2p;
+                for (int i = 0; i < kNP; ++i) l2p += Sx[i] * Sy[j] * L[j * kNP + i];
+            v += l2p;
+        }
+        out[staged ? PM[g] : perm[kpos]] += v;
     }
 }
 
@@ -851,20 +875,24 @@ void launch_prepare(int64_t N, const int* perm, const double* charge, const doub
     HIP_LAUNCH_CHECK();
 }
 
-void launch_up_direct(int nn, int nBig, const int* nodes, const int64_t* begin, const int64_t* count, const double* ncx,
-                      const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
-                      const double* fT, const Params* P, double* mult, hipStream_t s) {
-    if (nn <= 0) return;
-    const unsigned nb = (unsigned)nBig + blocks_for((int64_t)(nn - nBig), 4);
-    k_up_direct<<<nb, 256, 0, s>>>(nn, nBig, nodes, begin, count, ncx, ncy, nrx, nry, pxT, pyT, fT, P, mult);
-    HIP_LAUNCH_CHECK();
+size_t up_tier_lds(int maxTask, int ptsCap) {
+    return (size_t)(4 * kRank * kRank + maxTask * (kRank + 4) + 3 * ptsCap) * sizeof(double) +
+           (size_t)2 * maxTask * sizeof(int) + (size_t)maxTask * sizeof(int4);
 }
 
-void launch_up_top(int nslot, int nInternal, const int* slotNode, const int4* slotChild, int ngroups,
-                   const int* groupStart, const Params* P, double* mult, hipStream_t s) {
-    if (nInternal <= 0) return;
-    k_up_top<<<1, 256, (size_t)nslot * kRank * sizeof(double), s>>>(nslot, nInternal, slotNode, slotChild, ngroups,
-                                                                      groupStart, P, mult);
+size_t down_tier_lds(int maxTask, int maxLeaves, int ptsCap) {
+    return (size_t)(4 * kRank * kRank + maxTask * kRank + kRank + 4 * maxLeaves + 2 * ptsCap) * sizeof(double) +
+           (size_t)(ptsCap + 3 * maxLeaves + 4) * sizeof(int) + (size_t)maxTask * sizeof(int4);
+}
+
+void launch_up_tier(int ntask, int taskBase, int maxTask, int ptsCap, const int* taskPtr, const int* grpPtr,
+                    const int* grp, const int* node, const int4* code, const int64_t* begin, const int64_t* count,
+                    const double* ncx, const double* ncy, const double* nrx, const double* nry, const double* pxT,
+                    const double* pyT, const double* fT, const Params* P, double* mult, hipStream_t s) {
+    if (ntask <= 0) return;
+    k_up_tier<<<ntask, kTierThreads, up_tier_lds(maxTask, ptsCap), s>>>(
+        taskBase, maxTask, ptsCap, taskPtr, grpPtr, grp, node, code, begin, count, ncx, ncy, nrx, nry, pxT, pyT, fT,
+        P, mult);
     HIP_LAUNCH_CHECK();
 }
 
@@ -895,14 +923,18 @@ void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const 
     HIP_LAUNCH_CHECK();
 }
 
-void launch_leaf_far(int nl, const int4* leafInfo, const int* chainPtr, const int* chain, const int* slot,
-                     const double* local, const double* ncx, const double* ncy, const double* nrx, const double* nry,
-                     const double* pxT, const double* pyT, const int* perm, const Params* P, const int* nearInPtr,
-                     const int64_t* nearInOff, const double* nearPartial, int flags, double* out, hipStream_t s) {
-    if (nl <= 0) return;
-    k_leaf_far<<<blocks_for((int64_t)nl * kRank, 256), 256, 0, s>>>(nl, leafInfo, chainPtr, chain, slot, local, ncx, ncy,
-                                                                   nrx, nry, pxT, pyT, perm, P, nearInPtr, nearInOff,
-                                                                   nearPartial, flags, out);
+void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, int ptsCap, const int* taskPtr,
+                      const int* grpPtr, const int* grp, const int4* dn, const int* slot, const double* local,
+                      const double* m2lPart, const Params* P, double* total, const int* leafPtr, const int* leafSlot,
+                      const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
+                      const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
+                      const int* perm, const int* nearInPtr, const int64_t* nearInOff, const double* nearPart,
+                      int flags, double* out, hipStream_t s) {
+    if (ntask <= 0) return;
+    k_down_tier<<<ntask, kTierThreads, down_tier_lds(maxTask, maxLeaves, ptsCap), s>>>(
+        taskBase, maxTask, maxLeaves, ptsCap, taskPtr, grpPtr, grp, dn, slot, local, m2lPart, P, total, leafPtr,
+        leafSlot, leafIdx, leafBegin, ptsRange, ncx, ncy, nrx, nry, pxT, pyT, perm, nearInPtr, nearInOff, nearPart,
+        flags, out);
     HIP_LAUNCH_CHECK();
 }
 

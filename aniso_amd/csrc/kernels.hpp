@@ -10,8 +10,6 @@ namespace aniso {
 constexpr int kNP = 4;          // Chebyshev order per dimension (np); rank = 16
 constexpr int kRank = kNP * kNP;
 constexpr int kMaxD = 6;        // quadRule supported on the GPU path
-constexpr int kMaxDepth = 64;   // tree depth bound (lane-parallel chain load)
-constexpr int kPrefetchDepth = 12;  // ancestors whose locals are prefetched in registers
 
 // Small read-only tables shared by all kernels of one operator (lives in HBM,
 // served from L1/L2: a few KB).
@@ -38,11 +36,13 @@ enum StageMask : int {
 
 void launch_prepare(int64_t N, const int* perm, const double* charge, const double* w, double* fT, double* fO,
                     hipStream_t s);
-void launch_up_direct(int nn, int nBig, const int* nodes, const int64_t* begin, const int64_t* count, const double* ncx,
-                      const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
-                      const double* fT, const Params* P, double* mult, hipStream_t s);
-void launch_up_top(int nslot, int nInternal, const int* slotNode, const int4* slotChild, int ngroups,
-                   const int* groupStart, const Params* P, double* mult, hipStream_t s);
+constexpr int kTierThreads = 512;  // workgroup of the up / down pass tiers
+size_t up_tier_lds(int maxTask, int ptsCap);
+size_t down_tier_lds(int maxTask, int maxLeaves, int ptsCap);
+void launch_up_tier(int ntask, int taskBase, int maxTask, int ptsCap, const int* taskPtr, const int* grpPtr,
+                    const int* grp, const int* node, const int4* code, const int64_t* begin, const int64_t* count,
+                    const double* ncx, const double* ncy, const double* nrx, const double* nry, const double* pxT,
+                    const double* pyT, const double* fT, const Params* P, double* mult, hipStream_t s);
 void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
                 const int* outSlot, const int* src, const double* K, const double* mult, double sgn, double* partial,
                 double* local, hipStream_t s);
@@ -51,10 +51,13 @@ void launch_m2l_gather(int ntgt, const int* tgt, const int* inPtr, const double*
 void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts, const int64_t* nearKOff,
                  const int2* nearSym, const double* K, const double* fT, const int* perm, int maxS, int flags,
                  double sgn, double* partial, double* out, hipStream_t s);
-void launch_leaf_far(int nl, const int4* leafInfo, const int* chainPtr, const int* chain, const int* slot,
-                     const double* local, const double* ncx, const double* ncy, const double* nrx, const double* nry,
-                     const double* pxT, const double* pyT, const int* perm, const Params* P, const int* nearInPtr,
-                     const int64_t* nearInOff, const double* nearPartial, int flags, double* out, hipStream_t s);
+void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, int ptsCap, const int* taskPtr,
+                      const int* grpPtr, const int* grp, const int4* dn, const int* slot, const double* local,
+                      const double* m2lPart, const Params* P, double* total, const int* leafPtr, const int* leafSlot,
+                      const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
+                      const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
+                      const int* perm, const int* nearInPtr, const int64_t* nearInOff, const double* nearPart,
+                      int flags, double* out, hipStream_t s);
 void launch_corr(int d, int64_t b, int64_t e, const int* perm, const double* charge, const double* fO, const double* C,
                  const double* mu, const Params* P, int flags, double scale, double* out, hipStream_t s);
 void launch_cache_m2l(int64_t npairs, const int* pairTgt, const int* src, const double* ncx, const double* ncy,

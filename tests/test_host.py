@@ -30,7 +30,7 @@ def test_library_exports_every_header_symbol():
 def test_library_contains_gfx950_code_object():
     blob = open(aniso_amd.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
-    for k in (b"k_m2l", b"k_near", b"k_leaf_far", b"k_up_direct", b"k_corr", b"k_cache_m2l"):
+    for k in (b"k_m2l", b"k_near", b"k_down_tier", b"k_up_tier", b"k_corr", b"k_cache_m2l"):
         assert k in blob, k
 
 
