@@ -214,8 +214,9 @@ void Operator::uploadPlan() {
     std::vector<int2> ns(plan.nearSym.size());
     for (size_t i = 0; i < ns.size(); ++i) ns[i] = make_int2(plan.nearSym[i][0], plan.nearSym[i][1]);
     up(dNearSym, ns);
-    up(dNearInPtr, plan.nearInPtr);
-    up(dNearInOff, plan.nearInOff);
+    up(dDnLeafNear, plan.dnLeafNear);
+    up(dDnNearPtr, plan.dnNearPtr);
+    up(dDnNearOff, plan.dnNearOff);
     dNearPart.alloc((size_t)std::max<int64_t>(plan.nearPartTotal, 1) * sizeof(double));
     auto to_int4 = [](const std::vector<std::array<int, 4>>& v) {
         std::vector<int4> o(v.size());
@@ -255,7 +256,7 @@ void Operator::uploadPlan() {
             dnTierCap[k] = std::max(dnTierCap[k], std::min(plan.dnPtsRange[task][1] - plan.dnPtsRange[task][0], kPtsCapMax));
     // a task's expansions live in LDS (<= 4 levels: 85 nodes); a workgroup may use all 160 KiB
     if (up_tier_lds(plan.upMaxTask, kPtsCapMax) > 160 * 1024 ||
-        down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, kPtsCapMax) > 160 * 1024)
+        down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, kPtsCapMax, plan.dnMaxNear) > 160 * 1024)
         throw std::logic_error("up/down pass task exceeds one workgroup's LDS");
     maxNearS = 1;
     for (size_t li = 0; li < plan.leaves.size(); ++li) {
@@ -379,8 +380,9 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
                              dM2LPart.as<double>(), P, dTotal.as<double>(), dDnLeafPtr.as<int>(),
                              dDnLeafSlot.as<int>(), dDnLeafIdx.as<int>(), dDnLeafPts.as<int>(), dDnPtsRange.as<int2>(),
                              dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(),
-                             dPxT.as<double>(), dPyT.as<double>(), dPerm.as<int>(), dNearInPtr.as<int>(),
-                             dNearInOff.as<int64_t>(), dNearPart.as<double>(), mask, out, s);
+                             dPxT.as<double>(), dPyT.as<double>(), dPerm.as<int>(), dDnLeafNear.as<int2>(),
+                             dDnNearPtr.as<int>(), dDnNearOff.as<int>(), plan.dnMaxNear, dNearPart.as<double>(), mask,
+                             out, s);
     if (tm) HIP_CHECK(hipEventRecord(ev[5], s));
     launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), charge, dFO.as<double>(), mc.C.as<double>(),
                 mc.mu.as<double>(), P, mask, M_1_PI / 2.0, out, s);

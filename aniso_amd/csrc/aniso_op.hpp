@@ -101,7 +101,7 @@ private:
     DevBuf dDnTaskPtr, dDnGrpPtr, dDnGrp, dDnNode, dDnLeafPtr, dDnLeafSlot, dDnLeafIdx, dDnLeafPts, dDnPtsRange;  // down
     DevBuf dLeafInfo, dNearPtsPtr, dNearPts;
     DevBuf dM2LNDir, dM2LCanonBase, dM2LInPtr, dM2LOutSlot, dM2LPart;  // symmetric M2L
-    DevBuf dNearSym, dNearInPtr, dNearInOff, dNearPart;              // symmetric near field
+    DevBuf dNearSym, dNearPart, dDnLeafNear, dDnNearPtr, dDnNearOff;              // symmetric near field
     DevBuf dParams, dStCoef;
     DevBuf dCharge, dOut, dFT, dFO, dMult, dLocal, dTotal, dSigmaS, dTmp, dTmp2;
     std::vector<ModeCache> modes;

@@ -73,8 +73,7 @@ struct Plan {
     int m2lCanon = 0;
     int64_t storedM2L = 0, storedNear = 0, nearPartTotal = 0;
     std::vector<std::array<int, 2>> nearSym;   // per leaf: directed source points, partial base
-    std::vector<int> nearInPtr;                // per leaf: incoming partial ranges
-    std::vector<int64_t> nearInOff;
+    std::vector<int> nearInPtr, nearInOff;     // per leaf: offsets of the partial blocks addressed to it
     std::vector<int64_t> nearPtsPtr;           // per leaf: its S source points (tree positions)
     std::vector<int> nearPts;
     int64_t nearKTotal = 0;
@@ -97,6 +96,9 @@ struct Plan {
     std::vector<std::array<int, 4>> dnNode;
     std::vector<int> dnLeafPtr, dnLeafSlot, dnLeafIdx, dnLeafPts;  // leaves in tree order; dnLeafPts = begin
     std::vector<std::array<int, 2>> dnPtsRange;                     // per task: owned point range
+    std::vector<std::array<int, 2>> dnLeafNear;  // per leaf entry: (first, count) in its task's dnNearOff
+    std::vector<int> dnNearPtr, dnNearOff;       // per task: the near partial offsets of its leaves
+    int dnMaxNear = 1;
     int dnMaxTask = 1, dnMaxLeaves = 1;
     int64_t dnMaxPts = 0;
     int64_t pairsNear = 0, pairsM2L = 0;       // kernel entries per apply

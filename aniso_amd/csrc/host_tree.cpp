@@ -340,7 +340,7 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         leafIdx[i] = (int)leaves.size();
         leaves.push_back(i);
     }
-    std::vector<std::vector<int64_t>> nearIn(leaves.size());
+    std::vector<std::vector<int>> nearInRef(leaves.size());  // per receiver: partial offsets of its blocks
     nearPtr.push_back(0);
     int64_t partTotal = 0;
     for (size_t li = 0; li < leaves.size(); ++li) {
@@ -371,20 +371,22 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         const int64_t partBase = partTotal;
         for (int b : canonSrc) {
             nearSrc.push_back(b);
-            nearIn[leafIdx[b]].push_back(partTotal);
+            nearInRef[leafIdx[b]].push_back((int)partTotal);  // sender-contiguous partials
             partTotal += t.count[b];
             S += t.count[b];
         }
         nearPtr.push_back((int64_t)nearSrc.size());
         nearKTotal += S * (t.count[i] + (t.count[i] & 1));  // rows padded to even: 16-B aligned columns
         storedNear += S * t.count[i];
-        if (S > (int64_t)1 << 30 || partTotal > (int64_t)1 << 31) throw std::invalid_argument("leaf neighbourhood too large");
+        if (S > (int64_t)1 << 30 || partTotal > ((int64_t)1 << 31) - 1)
+            throw std::invalid_argument("leaf neighbourhood too large");
         leafInfo.push_back({i, (int)t.begin[i], (int)t.count[i], (int)S});
         nearSym.push_back({(int)Sdir, (int)partBase});
     }
     nearPartTotal = partTotal;
-    nearInPtr.push_back(0);
-    for (auto& v : nearIn) {
+    nearInPtr.assign(1, 0);
+    nearInOff.clear();
+    for (auto& v : nearInRef) {
         nearInOff.insert(nearInOff.end(), v.begin(), v.end());
         nearInPtr.push_back((int)nearInOff.size());
     }
@@ -478,6 +480,10 @@ void Plan::buildDownTasks(const Tree& t) {
     dnLeafSlot.clear();
     dnLeafIdx.clear();
     dnLeafPts.clear();
+    dnLeafNear.clear();
+    dnNearOff.clear();
+    dnNearPtr.assign(1, 0);
+    dnMaxNear = 1;
     dnPtsRange.clear();
     dnMaxPts = 0;
     dnMaxTask = 1;
@@ -496,6 +502,7 @@ void Plan::buildDownTasks(const Tree& t) {
                     dnNode.push_back({n, pc, t.slot[n], 0});
                 }
             }
+            const int nearBase = (int)dnNearOff.size();
             // owned leaves in tree order: they tile [ptsBegin, ptsEnd) contiguously
             std::vector<int> lf;
             for (int i = base; i < (int)dnNode.size(); ++i)
@@ -510,11 +517,16 @@ void Plan::buildDownTasks(const Tree& t) {
                 dnLeafSlot.push_back(sl);
                 dnLeafIdx.push_back(leafOf[n]);
                 dnLeafPts.push_back((int)t.begin[n]);
+                const int li = leafOf[n];
+                dnLeafNear.push_back({(int)dnNearOff.size() - nearBase, nearInPtr[li + 1] - nearInPtr[li]});
+                dnNearOff.insert(dnNearOff.end(), nearInOff.begin() + nearInPtr[li], nearInOff.begin() + nearInPtr[li + 1]);
             }
             const int nl = (int)lf.size();
             dnPtsRange.push_back({(int)std::max<int64_t>(pb, 0), (int)std::max<int64_t>(pe, 0)});
             dnMaxPts = std::max<int64_t>(dnMaxPts, pe - pb);
             dnLeafPtr.push_back((int)dnLeafSlot.size());
+            dnNearPtr.push_back((int)dnNearOff.size());
+            dnMaxNear = std::max(dnMaxNear, (int)dnNearOff.size() - nearBase);
             dnGrpPtr.push_back((int)dnGrp.size());
             dnTaskPtr.push_back((int)dnNode.size());
             dnMaxTask = std::max(dnMaxTask, (int)dnNode.size() - base);

@@ -242,29 +242,56 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
     const double* xs = staged ? X : pxT + b0;
     const double* ys = staged ? Y : pyT + b0;
     const double* fs = staged ? F : fT + b0;
+    // P2M of the task's leaves (bbfmm.h:737-748): 16 lanes per leaf, one point per
+    // lane per pass (its 16 products in registers), then a 16-lane reduce-scatter
+    // leaves lane l with entry l
+    {
+        const int gi = threadIdx.x >> 4, ln = threadIdx.x & 15, ngrp = blockDim.x >> 4;
+        for (int k = gi; k < nt; k += ngrp) {
+            if (CD[k].x != kLeafCode) continue;  // uniform over the 16 lanes
+            const double cx = G[4 * k], cy = G[4 * k + 1], irx = G[4 * k + 2], iry = G[4 * k + 3];
+            const int pe = LB[k] + LC[k];
+            double acc[kRank];
+#pragma unroll
+            for (int e = 0; e < kRank; ++e) acc[e] = 0.0;
+            for (int p = LB[k] + ln; p < pe; p += 16) {
+                double Sx[kNP], Sy[kNP];
+                cheb_weights(P, (xs[p] - cx) * irx, Sx);
+                cheb_weights(P, (ys[p] - cy) * iry, Sy);
+                const double f = fs[p];
+#pragma unroll
+                for (int j = 0; j < kNP; ++j) {
+                    const double sf = Sy[j] * f;
+#pragma unroll
+                    for (int i = 0; i < kNP; ++i) acc[j * kNP + i] += Sx[i] * sf;
+                }
+            }
+#define ANISO_RS16(NV, OFF)                                        \
+    {                                                              \
+        const bool hi = ln & (OFF);                                \
+        _Pragma("unroll") for (int e = 0; e < (NV); ++e) {         \
+            const double keep = hi ? acc[e + (NV)] : acc[e];       \
+            const double send = hi ? acc[e] : acc[e + (NV)];       \
+            acc[e] = keep + __shfl_xor(send, (OFF));               \
+        }                                                          \
+    }
+            ANISO_RS16(8, 8)
+            ANISO_RS16(4, 4)
+            ANISO_RS16(2, 2)
+            ANISO_RS16(1, 1)
+#undef ANISO_RS16
+            M[(size_t)k * kRank + ln] = acc[0];
+        }
+    }
+    __syncthreads();
     for (int g = grpPtr[task]; g < grpPtr[task + 1]; ++g) {
         const int s0 = grp[g] - n0, s1 = grp[g + 1] - n0;
         for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
             const int k = s0 + (it >> 4), r = it & (kRank - 1);
             const int4 c = CD[k];
             double acc = 0.0;
-            if (c.x == kLeafCode) {
-                const double cx = G[4 * k], cy = G[4 * k + 1], irx = G[4 * k + 2], iry = G[4 * k + 3];
-                const int i = r & 3, j = r >> 2;
-                const int pb = LB[k], pe = pb + LC[k];
-                double a1 = 0.0;
-                int p = pb;
-                for (; p + 1 < pe; p += 2) {
-                    const double sx0 = cheb_weight1(P, (xs[p] - cx) * irx, i);
-                    const double sy0 = cheb_weight1(P, (ys[p] - cy) * iry, j);
-                    const double sx1 = cheb_weight1(P, (xs[p + 1] - cx) * irx, i);
-                    const double sy1 = cheb_weight1(P, (ys[p + 1] - cy) * iry, j);
-                    acc += sx0 * (sy0 * fs[p]);
-                    a1 += sx1 * (sy1 * fs[p + 1]);
-                }
-                if (p < pe) acc += cheb_weight1(P, (xs[p] - cx) * irx, i) * (cheb_weight1(P, (ys[p] - cy) * iry, j) * fs[p]);
-                acc += a1;
-            } else {
+            if (c.x == kLeafCode) continue;  // P2M above
+            {
                 const int cs[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -518,23 +545,28 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
             const double fa0 = (r < rp && 2 * r < nT) ? fT[tb + 2 * r] : 0.0;
             const double fa1 = (r < rp && 2 * r + 1 < nT) ? fT[tb + 2 * r + 1] : 0.0;
             const int ncol = S - Sdir;
-            for (int i0 = 0; i0 < ncol; i0 += cps) {
-                const int s = Sdir + i0 + cph;
-                const bool ok = (i0 + cph < ncol) && r < rp;
-                dbl2 k0 = ok ? __builtin_nontemporal_load(kc + (size_t)s * rp) : dbl2{0.0, 0.0};
-                const double fsv = ok ? fs[s] : 0.0;
-                a0 += k0.x * fsv;
-                a1 += k0.y * fsv;
-                double c = k0.x * fa0 + k0.y * fa1;
-                for (int off = 1; off < lpc; off <<= 1) c += __shfl_xor(c, off);
-                // column s's charge is consumed: its LDS word now holds the product
-                // (stores inside the stream would stall it: vmcnt counts stores)
-                if (ok && (lane & (lpc - 1)) == 0) fs[s] = sgn * c;
+            for (int i0 = 0; i0 < ncol; i0 += 4 * cps) {  // 4 columns per lane in flight
+                dbl2 kk[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int s = Sdir + i0 + u * cps + cph;
+                    ok[u] = (i0 + u * cps + cph < ncol) && r < rp;
+                    kk[u] = ok[u] ? __builtin_nontemporal_load(kc + (size_t)s * rp) : dbl2{0.0, 0.0};
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int s = Sdir + i0 + u * cps + cph;
+                    const double fsv = ok[u] ? fs[s] : 0.0;
+                    a0 += kk[u].x * fsv;
+                    a1 += kk[u].y * fsv;
+                    double c = kk[u].x * fa0 + kk[u].y * fa1;
+                    for (int off = 1; off < lpc; off <<= 1) c += __shfl_xor(c, off);
+                    // column s's charge is consumed: its LDS word now holds the
+                    // product, stored after the stream (vmcnt also counts stores)
+                    if (ok[u] && (lane & (lpc - 1)) == 0) fs[s] = sgn * c;
+                }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int i = lane; i < ncol; i += kWave) partial[(int64_t)sym.y + i] = fs[Sdir + i];
         }
         if ((flags & kStageNear) && r < rp) {
             const dbl2* kc = reinterpret_cast<const dbl2*>(Kl) + r;
@@ -569,6 +601,12 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
             }
         }
     }
+    if ((flags & kStageNear) && S > Sdir) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int i = lane; i < S - Sdir; i += kWave) partial[(int64_t)sym.y + i] = fs[Sdir + i];
+    }
 }
 
 // Down pass (bbfmm.h:1066-1106) as tiers of <= 4-level subtrees, top-down, after
@@ -588,8 +626,9 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     const int* __restrict__ leafSlot, const int* __restrict__ leafIdx, const int* __restrict__ leafBegin,
     const int2* __restrict__ ptsRange, const double* __restrict__ ncx, const double* __restrict__ ncy,
     const double* __restrict__ nrx, const double* __restrict__ nry, const double* __restrict__ pxT,
-    const double* __restrict__ pyT, const int* __restrict__ perm, const int* __restrict__ nearInPtr,
-    const int64_t* __restrict__ nearInOff, const double* __restrict__ nearPart, int flags, double* __restrict__ out) {
+    const double* __restrict__ pyT, const int* __restrict__ perm, const int2* __restrict__ leafNear,
+    const int* __restrict__ nearPtr, const int* __restrict__ nearOff, int maxNear, const double* __restrict__ nearPart,
+    int flags, double* __restrict__ out) {
     extern __shared__ double sm[];
     int4* DN = reinterpret_cast<int4*>(sm);             // maxTask node records
     double* Rl = reinterpret_cast<double*>(DN + maxTask);  // 4 x 256 transfer matrices
@@ -601,7 +640,9 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     int* PM = reinterpret_cast<int*>(Y + ptsCap);       // ptsCap: perm (output index)
     int* LB = PM + ptsCap;                              // maxLeaves + 1: leaf begins (tree positions)
     int* LS = LB + maxLeaves + 1;                       // maxLeaves: leaf slot in the task
-    int* LI = LS + maxLeaves;                           // maxLeaves: plan leaf index
+    int* NB = LS + maxLeaves;                           // maxLeaves: first of the leaf's near offsets in NO
+    int* NC = NB + maxLeaves;                           // maxLeaves: their count
+    int* NO = NC + maxLeaves;                           // maxNear: partial offsets of the blocks addressed here
     const int task = taskBase + blockIdx.x;
     const int n0 = taskPtr[task], n1 = taskPtr[task + 1], nt = n1 - n0;
     const int l0 = leafPtr[task], nl = leafPtr[task + 1] - l0;
@@ -625,7 +666,9 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     for (int e = threadIdx.x; e < nl; e += blockDim.x) {
         LB[e] = leafBegin[l0 + e];
         LS[e] = leafSlot[l0 + e];
-        LI[e] = leafIdx[l0 + e];
+        const int2 ni = leafNear[l0 + e];
+        NB[e] = ni.x;
+        NC[e] = ni.y;
         const int n = dn[n0 + leafSlot[l0 + e]].x;
         G[4 * e] = ncx[n];
         G[4 * e + 1] = ncy[n];
@@ -633,6 +676,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
         G[4 * e + 3] = 1.0 / nry[n];
     }
     if (threadIdx.x == 0) LB[nl] = pr.y;
+    for (int j = nearPtr[task] + threadIdx.x; j < nearPtr[task + 1]; j += blockDim.x) NO[j - nearPtr[task]] = nearOff[j];
     if (staged)
         for (int p = threadIdx.x; p < npts; p += blockDim.x) {
             X[p] = pxT[pr.x + p];
@@ -669,11 +713,11 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             if (LB[mid] <= kpos) lo = mid;
             else hi = mid - 1;
         }
-        const int t = kpos - LB[lo], li = LI[lo];
+        const int t = kpos - LB[lo];
         double v = 0.0;
         if (flags & kStageNear) {
-            const int j0 = nearInPtr[li], j1 = nearInPtr[li + 1];
-            for (int j = j0; j < j1; ++j) v += nearPart[nearInOff[j] + t];
+            const int* no = NO + NB[lo];
+            for (int j = 0; j < NC[lo]; ++j) v += nearPart[(size_t)no[j] + t];
         }
         if (far) {
             const double x = staged ? X[g] : pxT[kpos], y = staged ? Y[g] : pyT[kpos];
@@ -880,9 +924,9 @@ size_t up_tier_lds(int maxTask, int ptsCap) {
            (size_t)2 * maxTask * sizeof(int) + (size_t)maxTask * sizeof(int4);
 }
 
-size_t down_tier_lds(int maxTask, int maxLeaves, int ptsCap) {
+size_t down_tier_lds(int maxTask, int maxLeaves, int ptsCap, int maxNear) {
     return (size_t)(4 * kRank * kRank + maxTask * kRank + kRank + 4 * maxLeaves + 2 * ptsCap) * sizeof(double) +
-           (size_t)(ptsCap + 3 * maxLeaves + 4) * sizeof(int) + (size_t)maxTask * sizeof(int4);
+           (size_t)(ptsCap + 4 * maxLeaves + 4 + maxNear) * sizeof(int) + (size_t)maxTask * sizeof(int4);
 }
 
 void launch_up_tier(int ntask, int taskBase, int maxTask, int ptsCap, const int* taskPtr, const int* grpPtr,
@@ -928,13 +972,13 @@ void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, int p
                       const double* m2lPart, const Params* P, double* total, const int* leafPtr, const int* leafSlot,
                       const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
                       const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
-                      const int* perm, const int* nearInPtr, const int64_t* nearInOff, const double* nearPart,
-                      int flags, double* out, hipStream_t s) {
+                      const int* perm, const int2* leafNear, const int* nearPtr, const int* nearOff, int maxNear,
+                      const double* nearPart, int flags, double* out, hipStream_t s) {
     if (ntask <= 0) return;
-    k_down_tier<<<ntask, kTierThreads, down_tier_lds(maxTask, maxLeaves, ptsCap), s>>>(
+    k_down_tier<<<ntask, kTierThreads, down_tier_lds(maxTask, maxLeaves, ptsCap, maxNear), s>>>(
         taskBase, maxTask, maxLeaves, ptsCap, taskPtr, grpPtr, grp, dn, slot, local, m2lPart, P, total, leafPtr,
-        leafSlot, leafIdx, leafBegin, ptsRange, ncx, ncy, nrx, nry, pxT, pyT, perm, nearInPtr, nearInOff, nearPart,
-        flags, out);
+        leafSlot, leafIdx, leafBegin, ptsRange, ncx, ncy, nrx, nry, pxT, pyT, perm, leafNear, nearPtr, nearOff, maxNear,
+        nearPart, flags, out);
     HIP_LAUNCH_CHECK();
 }
 

@@ -38,7 +38,7 @@ void launch_prepare(int64_t N, const int* perm, const double* charge, const doub
                     hipStream_t s);
 constexpr int kTierThreads = 512;  // workgroup of the up / down pass tiers
 size_t up_tier_lds(int maxTask, int ptsCap);
-size_t down_tier_lds(int maxTask, int maxLeaves, int ptsCap);
+size_t down_tier_lds(int maxTask, int maxLeaves, int ptsCap, int maxNear);
 void launch_up_tier(int ntask, int taskBase, int maxTask, int ptsCap, const int* taskPtr, const int* grpPtr,
                     const int* grp, const int* node, const int4* code, const int64_t* begin, const int64_t* count,
                     const double* ncx, const double* ncy, const double* nrx, const double* nry, const double* pxT,
@@ -56,8 +56,8 @@ void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, int p
                       const double* m2lPart, const Params* P, double* total, const int* leafPtr, const int* leafSlot,
                       const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
                       const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
-                      const int* perm, const int* nearInPtr, const int64_t* nearInOff, const double* nearPart,
-                      int flags, double* out, hipStream_t s);
+                      const int* perm, const int2* leafNear, const int* nearPtr, const int* nearOff, int maxNear,
+                      const double* nearPart, int flags, double* out, hipStream_t s);
 void launch_corr(int d, int64_t b, int64_t e, const int* perm, const double* charge, const double* fO, const double* C,
                  const double* mu, const Params* P, int flags, double scale, double* out, hipStream_t s);
 void launch_cache_m2l(int64_t npairs, const int* pairTgt, const int* src, const double* ncx, const double* ncy,
