@@ -7,6 +7,7 @@
 //   mapping*    <- 'mapping'   one apply, all stages on the GPU
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
@@ -240,23 +241,8 @@ void Operator::uploadPlan() {
     up(dDnLeafIdx, plan.dnLeafIdx);
     up(dDnLeafPts, plan.dnLeafPts);
     up(dDnPtsRange, plan.dnPtsRange);
-    // per tier: points staged in LDS (tasks with more points read them from HBM)
-    constexpr int kPtsCapMax = 2048;
-    upTierCap.assign(plan.upTierTask.size(), 0);
-    for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k)
-        for (int task = plan.upTierTask[k]; task < plan.upTierTask[k + 1]; ++task) {
-            bool leaves = false;
-            for (int i = plan.upTaskPtr[task]; i < plan.upTaskPtr[task + 1]; ++i) leaves |= plan.upCode[i][0] == kLeafCode;
-            if (leaves)
-                upTierCap[k] = std::max<int>(upTierCap[k], (int)std::min<int64_t>(tree.count[plan.upNode[plan.upTaskPtr[task + 1] - 1]], kPtsCapMax));
-        }
-    dnTierCap.assign(plan.dnTierTask.size(), 0);
-    for (size_t k = 0; k + 1 < plan.dnTierTask.size(); ++k)
-        for (int task = plan.dnTierTask[k]; task < plan.dnTierTask[k + 1]; ++task)
-            dnTierCap[k] = std::max(dnTierCap[k], std::min(plan.dnPtsRange[task][1] - plan.dnPtsRange[task][0], kPtsCapMax));
     // a task's expansions live in LDS (<= 4 levels: 85 nodes); a workgroup may use all 160 KiB
-    if (up_tier_lds(plan.upMaxTask, kPtsCapMax) > 160 * 1024 ||
-        down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, kPtsCapMax, plan.dnMaxNear) > 160 * 1024)
+    if (up_tier_lds(plan.upMaxTask) > 160 * 1024 || down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, plan.dnMaxNear) > 160 * 1024)
         throw std::logic_error("up/down pass task exceeds one workgroup's LDS");
     maxNearS = 1;
     for (size_t li = 0; li < plan.leaves.size(); ++li) {
@@ -351,7 +337,7 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
     if (tm) HIP_CHECK(hipEventRecord(ev[1], s));
     // up pass (global, every rank): tiers bottom-up
     for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k)
-        launch_up_tier(plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask, upTierCap[k],
+        launch_up_tier(plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask,
                        dUpTaskPtr.as<int>(), dUpGrpPtr.as<int>(), dUpGrp.as<int>(), dUpNode.as<int>(),
                        dUpCode.as<int4>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dNcx.as<double>(),
                        dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(),
@@ -375,7 +361,7 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
     if (mask & (kStageFar | kStageNear))
         for (size_t k = 0; k + 1 < plan.dnTierTask.size(); ++k)
             launch_down_tier(plan.dnTierTask[k + 1] - plan.dnTierTask[k], plan.dnTierTask[k], plan.dnMaxTask,
-                             plan.dnMaxLeaves, dnTierCap[k], dDnTaskPtr.as<int>(), dDnGrpPtr.as<int>(),
+                             plan.dnMaxLeaves, dDnTaskPtr.as<int>(), dDnGrpPtr.as<int>(),
                              dDnGrp.as<int>(), dDnNode.as<int4>(), dSlot.as<int>(), dLocal.as<double>(),
                              dM2LPart.as<double>(), P, dTotal.as<double>(), dDnLeafPtr.as<int>(),
                              dDnLeafSlot.as<int>(), dDnLeafIdx.as<int>(), dDnLeafPts.as<int>(), dDnPtsRange.as<int2>(),

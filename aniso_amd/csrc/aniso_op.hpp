@@ -93,7 +93,6 @@ private:
     std::vector<std::array<hipEvent_t, 7>> evPool;
     int evUsed = 0;
     int maxNearS = 0;
-    std::vector<int> upTierCap, dnTierCap;  // LDS point capacity per tier launch
     // geometry / tree on device
     DevBuf dPxT, dPyT, dPerm, dW, dNcx, dNcy, dNrx, dNry, dBegin, dCount, dParent, dSlot, dChild, dIsLeaf;
     DevBuf dLeaves, dNearPtr, dNearSrc, dNearKOff, dM2LTgt, dM2LPtr, dM2LSrc, dM2LPairTgt;

@@ -89,7 +89,6 @@ struct Plan {
     std::vector<int> upTierTask, upTaskPtr, upGrpPtr, upGrp, upNode;
     std::vector<std::array<int, 4>> upCode;
     int upMaxTask = 1;
-    int64_t upMaxPts = 0;  // points under a task root (staged in LDS when they fit)
     // down (owned part; tiers top-down): dnNode = (node, parent code, child slot
     // (R index), 0); leaves of each task in tree order (L2P + near gather)
     std::vector<int> dnTierTask, dnTaskPtr, dnGrpPtr, dnGrp;
@@ -100,7 +99,6 @@ struct Plan {
     std::vector<int> dnNearPtr, dnNearOff;       // per task: the near partial offsets of its leaves
     int dnMaxNear = 1;
     int dnMaxTask = 1, dnMaxLeaves = 1;
-    int64_t dnMaxPts = 0;
     int64_t pairsNear = 0, pairsM2L = 0;       // kernel entries per apply
 
     void build(const Tree& t, int np, int rank, int nranks);

@@ -431,7 +431,6 @@ void Plan::buildUpTasks(const Tree& t) {
     upNode.clear();
     upCode.clear();
     upMaxTask = 1;
-    upMaxPts = 0;
     for (size_t k = 0; k < tierRootLevel.size(); ++k) {  // bottom-up
         for (int r = 0; r < t.nn; ++r) {
             if (t.level[r] != tierRootLevel[k] || t.isEmpty[r]) continue;
@@ -459,7 +458,6 @@ void Plan::buildUpTasks(const Tree& t) {
             upGrpPtr.push_back((int)upGrp.size());
             upTaskPtr.push_back((int)upNode.size());
             upMaxTask = std::max(upMaxTask, (int)upNode.size() - base);
-            upMaxPts = std::max<int64_t>(upMaxPts, t.count[r]);
         }
         upTierTask.push_back((int)upTaskPtr.size() - 1);
     }
@@ -485,7 +483,6 @@ void Plan::buildDownTasks(const Tree& t) {
     dnNearPtr.assign(1, 0);
     dnMaxNear = 1;
     dnPtsRange.clear();
-    dnMaxPts = 0;
     dnMaxTask = 1;
     dnMaxLeaves = 1;
     for (int k = (int)tierRootLevel.size() - 1; k >= 0; --k) {  // top-down
@@ -523,7 +520,6 @@ void Plan::buildDownTasks(const Tree& t) {
             }
             const int nl = (int)lf.size();
             dnPtsRange.push_back({(int)std::max<int64_t>(pb, 0), (int)std::max<int64_t>(pe, 0)});
-            dnMaxPts = std::max<int64_t>(dnMaxPts, pe - pb);
             dnLeafPtr.push_back((int)dnLeafSlot.size());
             dnNearPtr.push_back((int)dnNearOff.size());
             dnMaxNear = std::max(dnMaxNear, (int)dnNearOff.size() - nearBase);

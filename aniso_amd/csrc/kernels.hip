@@ -190,11 +190,11 @@ __global__ void k_prepare(int64_t N, const int* __restrict__ perm, const double*
 // first; a leaf's multipole is P2M over its contiguous tree-order points
 // (bbfmm.h:737-748), an internal node's is M2M of its children (bbfmm.h:855-859),
 // where a child below the tier is the root of a lower tier's task (read from HBM).
-// Phase 0 stages the transfer matrices, node boxes and the task's points in LDS
-// with one round of independent loads; the levels then run out of LDS.
+// Phase 0 stages the transfer matrices, node boxes and child codes in LDS with
+// one round of independent loads; the levels then run out of LDS.
 // One thread per (node, entry r), r = 4j + i:  M[r] = sum_p S(x_p, c_i) S(y_p, c_j) f_p.
 __global__ void __launch_bounds__(kTierThreads) k_up_tier(
-    int taskBase, int maxTask, int ptsCap, const int* __restrict__ taskPtr, const int* __restrict__ grpPtr,
+    int taskBase, int maxTask, const int* __restrict__ taskPtr, const int* __restrict__ grpPtr,
     const int* __restrict__ grp, const int* __restrict__ node, const int4* __restrict__ code,
     const int64_t* __restrict__ begin, const int64_t* __restrict__ count, const double* __restrict__ ncx,
     const double* __restrict__ ncy, const double* __restrict__ nrx, const double* __restrict__ nry,
@@ -205,17 +205,12 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
     double* Rl = reinterpret_cast<double*>(CD + maxTask);  // 4 x 256 transfer matrices (transposed)
     double* M = Rl + 4 * kRank * kRank;                 // maxTask x 16 multipoles
     double* G = M + (size_t)maxTask * kRank;            // maxTask x 4: cx, cy, 1/rx, 1/ry
-    double* X = G + (size_t)maxTask * 4;                // ptsCap x (x, y, f)
-    double* Y = X + ptsCap;
-    double* F = Y + ptsCap;
-    int* LB = reinterpret_cast<int*>(F + ptsCap);       // maxTask: leaf point offset, count
+    int* LB = reinterpret_cast<int*>(G + (size_t)maxTask * 4);  // maxTask: leaf point offset, count
     int* LC = LB + maxTask;
     const int task = taskBase + blockIdx.x;
     const int n0 = taskPtr[task], n1 = taskPtr[task + 1], nt = n1 - n0;
     const int root = node[n1 - 1];  // deepest level first: the root is last
     const int64_t b0 = begin[root];
-    const int np = (int)count[root];
-    const bool staged = np <= ptsCap;
     // M2M reads R[q][rr + 16 r] along rr: stage it transposed (r fastest) so the
     // 16 lanes of one node hit 16 consecutive LDS words
     for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) {
@@ -232,16 +227,11 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
         LC[k] = (int)count[n];
         CD[k] = code[n0 + k];
     }
-    if (staged)
-        for (int p = threadIdx.x; p < np; p += blockDim.x) {
-            X[p] = pxT[b0 + p];
-            Y[p] = pyT[b0 + p];
-            F[p] = fT[b0 + p];
-        }
     __syncthreads();
-    const double* xs = staged ? X : pxT + b0;
-    const double* ys = staged ? Y : pyT + b0;
-    const double* fs = staged ? F : fT + b0;
+    // each point is read once (lane per point, coalesced): no LDS staging
+    const double* xs = pxT + b0;
+    const double* ys = pyT + b0;
+    const double* fs = fT + b0;
     // P2M of the task's leaves (bbfmm.h:737-748): 16 lanes per leaf, one point per
     // lane per pass (its 16 products in registers), then a 16-lane reduce-scatter
     // leaves lane l with entry l
@@ -619,7 +609,7 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
 // all nodes, the roots' parent totals, box geometry, points and
 // their output slots) into LDS; the levels and the points then run out of LDS.
 __global__ void __launch_bounds__(kTierThreads) k_down_tier(
-    int taskBase, int maxTask, int maxLeaves, int ptsCap, const int* __restrict__ taskPtr,
+    int taskBase, int maxTask, int maxLeaves, const int* __restrict__ taskPtr,
     const int* __restrict__ grpPtr, const int* __restrict__ grp, const int4* __restrict__ dn,
     const int* __restrict__ slot, const double* __restrict__ local, const double* __restrict__ m2lPart,
     const Params* __restrict__ P, double* __restrict__ total, const int* __restrict__ leafPtr,
@@ -635,10 +625,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     double* T = Rl + 4 * kRank * kRank;                 // maxTask x 16 totals
     double* PT = T + (size_t)maxTask * kRank;           // 16: the task root's parent total
     double* G = PT + kRank;                             // maxLeaves x 4: leaf cx, cy, 1/rx, 1/ry
-    double* X = G + (size_t)maxLeaves * 4;              // ptsCap x (x, y)
-    double* Y = X + ptsCap;
-    int* PM = reinterpret_cast<int*>(Y + ptsCap);       // ptsCap: perm (output index)
-    int* LB = PM + ptsCap;                              // maxLeaves + 1: leaf begins (tree positions)
+    int* LB = reinterpret_cast<int*>(G + (size_t)maxLeaves * 4);  // maxLeaves + 1: leaf begins (tree positions)
     int* LS = LB + maxLeaves + 1;                       // maxLeaves: leaf slot in the task
     int* NB = LS + maxLeaves;                           // maxLeaves: first of the leaf's near offsets in NO
     int* NC = NB + maxLeaves;                           // maxLeaves: their count
@@ -648,7 +635,6 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     const int l0 = leafPtr[task], nl = leafPtr[task + 1] - l0;
     const int2 pr = ptsRange[task];
     const int npts = pr.y - pr.x;
-    const bool staged = npts <= ptsCap;
     const bool far = flags & kStageFar;
     // ---- phase 0: independent loads
     if (far) {
@@ -677,12 +663,6 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     }
     if (threadIdx.x == 0) LB[nl] = pr.y;
     for (int j = nearPtr[task] + threadIdx.x; j < nearPtr[task + 1]; j += blockDim.x) NO[j - nearPtr[task]] = nearOff[j];
-    if (staged)
-        for (int p = threadIdx.x; p < npts; p += blockDim.x) {
-            X[p] = pxT[pr.x + p];
-            Y[p] = pyT[pr.x + p];
-            PM[p] = perm[pr.x + p];
-        }
     __syncthreads();
     // ---- phase 1: L2L level by level (shallowest first), out of LDS
     if (far) {
@@ -720,7 +700,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             for (int j = 0; j < NC[lo]; ++j) v += nearPart[(size_t)no[j] + t];
         }
         if (far) {
-            const double x = staged ? X[g] : pxT[kpos], y = staged ? Y[g] : pyT[kpos];
+            const double x = pxT[kpos], y = pyT[kpos];
             double Sx[kNP], Sy[kNP];
             cheb_weights(P, (x - G[4 * lo]) * G[4 * lo + 2], Sx);
             cheb_weights(P, (y - G[4 * lo + 1]) * G[4 * lo + 3], Sy);
@@ -732,7 +712,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
                 for (int i = 0; i < kNP; ++i) l2p += Sx[i] * Sy[j] * L[j * kNP + i];
             v += l2p;
         }
-        out[staged ? PM[g] : perm[kpos]] += v;
+        out[perm[kpos]] += v;
     }
 }
 
@@ -919,23 +899,23 @@ void launch_prepare(int64_t N, const int* perm, const double* charge, const doub
     HIP_LAUNCH_CHECK();
 }
 
-size_t up_tier_lds(int maxTask, int ptsCap) {
-    return (size_t)(4 * kRank * kRank + maxTask * (kRank + 4) + 3 * ptsCap) * sizeof(double) +
-           (size_t)2 * maxTask * sizeof(int) + (size_t)maxTask * sizeof(int4);
+size_t up_tier_lds(int maxTask) {
+    return (size_t)(4 * kRank * kRank + maxTask * (kRank + 4)) * sizeof(double) + (size_t)2 * maxTask * sizeof(int) +
+           (size_t)maxTask * sizeof(int4);
 }
 
-size_t down_tier_lds(int maxTask, int maxLeaves, int ptsCap, int maxNear) {
-    return (size_t)(4 * kRank * kRank + maxTask * kRank + kRank + 4 * maxLeaves + 2 * ptsCap) * sizeof(double) +
-           (size_t)(ptsCap + 4 * maxLeaves + 4 + maxNear) * sizeof(int) + (size_t)maxTask * sizeof(int4);
+size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear) {
+    return (size_t)(4 * kRank * kRank + maxTask * kRank + kRank + 4 * maxLeaves) * sizeof(double) +
+           (size_t)(4 * maxLeaves + 4 + maxNear) * sizeof(int) + (size_t)maxTask * sizeof(int4);
 }
 
-void launch_up_tier(int ntask, int taskBase, int maxTask, int ptsCap, const int* taskPtr, const int* grpPtr,
+void launch_up_tier(int ntask, int taskBase, int maxTask, const int* taskPtr, const int* grpPtr,
                     const int* grp, const int* node, const int4* code, const int64_t* begin, const int64_t* count,
                     const double* ncx, const double* ncy, const double* nrx, const double* nry, const double* pxT,
                     const double* pyT, const double* fT, const Params* P, double* mult, hipStream_t s) {
     if (ntask <= 0) return;
-    k_up_tier<<<ntask, kTierThreads, up_tier_lds(maxTask, ptsCap), s>>>(
-        taskBase, maxTask, ptsCap, taskPtr, grpPtr, grp, node, code, begin, count, ncx, ncy, nrx, nry, pxT, pyT, fT,
+    k_up_tier<<<ntask, kTierThreads, up_tier_lds(maxTask), s>>>(
+        taskBase, maxTask, taskPtr, grpPtr, grp, node, code, begin, count, ncx, ncy, nrx, nry, pxT, pyT, fT,
         P, mult);
     HIP_LAUNCH_CHECK();
 }
@@ -967,7 +947,7 @@ void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const 
     HIP_LAUNCH_CHECK();
 }
 
-void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, int ptsCap, const int* taskPtr,
+void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const int* taskPtr,
                       const int* grpPtr, const int* grp, const int4* dn, const int* slot, const double* local,
                       const double* m2lPart, const Params* P, double* total, const int* leafPtr, const int* leafSlot,
                       const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
@@ -975,8 +955,8 @@ void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, int p
                       const int* perm, const int2* leafNear, const int* nearPtr, const int* nearOff, int maxNear,
                       const double* nearPart, int flags, double* out, hipStream_t s) {
     if (ntask <= 0) return;
-    k_down_tier<<<ntask, kTierThreads, down_tier_lds(maxTask, maxLeaves, ptsCap, maxNear), s>>>(
-        taskBase, maxTask, maxLeaves, ptsCap, taskPtr, grpPtr, grp, dn, slot, local, m2lPart, P, total, leafPtr,
+    k_down_tier<<<ntask, kTierThreads, down_tier_lds(maxTask, maxLeaves, maxNear), s>>>(
+        taskBase, maxTask, maxLeaves, taskPtr, grpPtr, grp, dn, slot, local, m2lPart, P, total, leafPtr,
         leafSlot, leafIdx, leafBegin, ptsRange, ncx, ncy, nrx, nry, pxT, pyT, perm, leafNear, nearPtr, nearOff, maxNear,
         nearPart, flags, out);
     HIP_LAUNCH_CHECK();

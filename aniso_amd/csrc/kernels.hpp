@@ -37,9 +37,9 @@ enum StageMask : int {
 void launch_prepare(int64_t N, const int* perm, const double* charge, const double* w, double* fT, double* fO,
                     hipStream_t s);
 constexpr int kTierThreads = 512;  // workgroup of the up / down pass tiers
-size_t up_tier_lds(int maxTask, int ptsCap);
-size_t down_tier_lds(int maxTask, int maxLeaves, int ptsCap, int maxNear);
-void launch_up_tier(int ntask, int taskBase, int maxTask, int ptsCap, const int* taskPtr, const int* grpPtr,
+size_t up_tier_lds(int maxTask);
+size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear);
+void launch_up_tier(int ntask, int taskBase, int maxTask, const int* taskPtr, const int* grpPtr,
                     const int* grp, const int* node, const int4* code, const int64_t* begin, const int64_t* count,
                     const double* ncx, const double* ncy, const double* nrx, const double* nry, const double* pxT,
                     const double* pyT, const double* fT, const Params* P, double* mult, hipStream_t s);
@@ -51,7 +51,7 @@ void launch_m2l_gather(int ntgt, const int* tgt, const int* inPtr, const double*
 void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts, const int64_t* nearKOff,
                  const int2* nearSym, const double* K, const double* fT, const int* perm, int maxS, int flags,
                  double sgn, double* partial, double* out, hipStream_t s);
-void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, int ptsCap, const int* taskPtr,
+void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const int* taskPtr,
                       const int* grpPtr, const int* grp, const int4* dn, const int* slot, const double* local,
                       const double* m2lPart, const Params* P, double* total, const int* leafPtr, const int* leafSlot,
                       const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
