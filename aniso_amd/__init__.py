@@ -254,9 +254,9 @@ class Aniso:
         _check(lib().aniso_set_timing(self.address, int(bool(on))))
 
     def stage_times(self):
-        t = (ctypes.c_float * 7)()
+        t = (ctypes.c_float * 8)()
         _check(lib().aniso_stage_times(self.address, t))
-        return dict(zip(["prep", "up", "m2l", "near", "down", "corr", "total"], list(t)))
+        return dict(zip(["prep", "up", "m2l", "gather", "near", "down", "corr", "total"], list(t)))
 
     def line_integrals(self, seg):
         seg = np.ascontiguousarray(np.asarray(seg, dtype=np.float64).reshape(-1, 4))

@@ -78,6 +78,9 @@ Operator::~Operator() {
         for (auto& set : evPool)
             for (auto& e : set) (void)hipEventDestroy(e);
         if (own) (void)hipStreamDestroy(own);
+        if (aux) (void)hipStreamDestroy(aux);
+        if (evFork) (void)hipEventDestroy(evFork);
+        if (evJoin) (void)hipEventDestroy(evJoin);
     }
 }
 
@@ -105,6 +108,10 @@ void Operator::ensureDevice() {
     }
     HIP_CHECK(hipGetDevice(&device));
     HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&evFork, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
+    if (const char* e = std::getenv("ANISO_OVERLAP")) overlap = e[0] == '1';
     // tree-order coordinates
     std::vector<double> pxT(geo.N), pyT(geo.N);
     for (int64_t k = 0; k < geo.N; ++k) {
@@ -326,7 +333,7 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
     hipEvent_t* ev = nullptr;
     if (tm) {
         if (evUsed == (int)evPool.size()) {
-            std::array<hipEvent_t, 7> set;
+            std::array<hipEvent_t, kStageEvents> set;
             for (auto& e : set) HIP_CHECK(hipEventCreate(&e));
             evPool.push_back(set);
         }
@@ -335,6 +342,26 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
     }
     launch_prepare(geo.N, dPerm.as<int>(), charge, dW.as<double>(), dFT.as<double>(), dFO.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[1], s));
+    // The near field and the corrections need only the prepared charges: they run
+    // on the auxiliary stream, overlapping the latency-bound up pass and the M2L
+    // stream (both write `out`: near stores, corr adds; the down pass adds after
+    // the join).
+    hipStream_t sn = overlap ? aux : s;
+    if (overlap) {
+        HIP_CHECK(hipEventRecord(evFork, s));
+        HIP_CHECK(hipStreamWaitEvent(aux, evFork, 0));
+    }
+    // K_{B<-A} = (-1)^m K_{A<-B}^T for the merged kernel (DESIGN.md §3.6); Id = m
+    const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
+    if (tm) HIP_CHECK(hipEventRecord(ev[6], sn));
+    launch_near((int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(),
+                dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(), dFT.as<double>(), dPerm.as<int>(),
+                maxNearS, mask, sgn, M_1_PI / 2.0, dNearPart.as<double>(), out, sn);
+    if (tm) HIP_CHECK(hipEventRecord(ev[7], sn));
+    launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), charge, dFO.as<double>(), mc.C.as<double>(),
+                mc.mu.as<double>(), P, mask, M_1_PI / 2.0, out, sn);
+    if (tm) HIP_CHECK(hipEventRecord(ev[8], sn));
+    if (overlap) HIP_CHECK(hipEventRecord(evJoin, aux));
     // up pass (global, every rank): tiers bottom-up
     for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k)
         launch_up_tier(plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask,
@@ -343,8 +370,6 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
                        dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(),
                        dFT.as<double>(), P, dMult.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[2], s));
-    // K_{B<-A} = (-1)^m K_{A<-B}^T for the merged kernel (DESIGN.md §3.6); Id = m
-    const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
     if (mask & kStageFar)
         launch_m2l((int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(),
                    dM2LCanonBase.as<int>(), dM2LOutSlot.as<int>(), dM2LSrc.as<int>(), mc.Km2l.as<double>(),
@@ -353,11 +378,10 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
     if ((mask & kStageFar) && plan.m2lCanon > 0)
         launch_m2l_gather((int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LInPtr.as<int>(), dM2LPart.as<double>(),
                           dLocal.as<double>(), s);
-    launch_near((int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(),
-                dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(), dFT.as<double>(), dPerm.as<int>(),
-                maxNearS, mask, sgn, dNearPart.as<double>(), out, s);
     if (tm) HIP_CHECK(hipEventRecord(ev[4], s));
-    // down pass (owned part): tiers top-down; L2L + M2L partial gather + L2P + near gather
+    if (overlap) HIP_CHECK(hipStreamWaitEvent(s, evJoin, 0));
+    if (tm) HIP_CHECK(hipEventRecord(ev[9], s));
+    // down pass (owned part): tiers top-down; L2L + L2P + gathered transposed near products
     if (mask & (kStageFar | kStageNear))
         for (size_t k = 0; k + 1 < plan.dnTierTask.size(); ++k)
             launch_down_tier(plan.dnTierTask[k + 1] - plan.dnTierTask[k], plan.dnTierTask[k], plan.dnMaxTask,
@@ -368,11 +392,8 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
                              dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(),
                              dPxT.as<double>(), dPyT.as<double>(), dPerm.as<int>(), dDnLeafNear.as<int2>(),
                              dDnNearPtr.as<int>(), dDnNearOff.as<int>(), plan.dnMaxNear, dNearPart.as<double>(), mask,
-                             out, s);
+                             M_1_PI / 2.0, out, s);
     if (tm) HIP_CHECK(hipEventRecord(ev[5], s));
-    launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), charge, dFO.as<double>(), mc.C.as<double>(),
-                mc.mu.as<double>(), P, mask, M_1_PI / 2.0, out, s);
-    if (tm) HIP_CHECK(hipEventRecord(ev[6], s));
 }
 
 void Operator::setTiming(bool on) {
@@ -383,22 +404,33 @@ void Operator::setTiming(bool on) {
 StageTimes Operator::stageTimes() {
     StageTimes r;
     if (evUsed == 0) return r;
-    HIP_CHECK(hipEventSynchronize(evPool[evUsed - 1][6]));
-    double acc[6] = {0, 0, 0, 0, 0, 0};
-    for (int k = 0; k < evUsed; ++k)
-        for (int i = 0; i < 6; ++i) {
-            float t = 0;
-            HIP_CHECK(hipEventElapsedTime(&t, evPool[k][i], evPool[k][i + 1]));
-            acc[i] += t;
-        }
+    HIP_CHECK(hipEventSynchronize(evPool[evUsed - 1][5]));
+    auto el = [](hipEvent_t a, hipEvent_t b) {
+        float t = 0;
+        HIP_CHECK(hipEventElapsedTime(&t, a, b));
+        return (double)t;
+    };
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < evUsed; ++k) {
+        const auto& e = evPool[k];
+        acc[0] += el(e[0], e[1]);  // prep
+        acc[1] += el(overlap ? e[1] : e[8], e[2]);  // up (after near + corr when serialized)
+        acc[2] += el(e[2], e[3]);  // m2l
+        acc[3] += el(e[3], e[4]);  // gather
+        acc[4] += el(e[6], e[7]);  // near (auxiliary stream)
+        acc[5] += el(e[9], e[5]);  // down (after the join)
+        acc[6] += el(e[7], e[8]);  // corr (auxiliary stream)
+        acc[7] += el(e[0], e[5]);  // whole apply
+    }
     for (double& a : acc) a /= evUsed;
     r.prep = (float)acc[0];
     r.up = (float)acc[1];
     r.m2l = (float)acc[2];
-    r.near = (float)acc[3];
-    r.down = (float)acc[4];
-    r.corr = (float)acc[5];
-    r.total = (float)(acc[0] + acc[1] + acc[2] + acc[3] + acc[4] + acc[5]);
+    r.gather = (float)acc[3];
+    r.near = (float)acc[4];
+    r.down = (float)acc[5];
+    r.corr = (float)acc[6];
+    r.total = (float)acc[7];
     return r;
 }
 

@@ -37,7 +37,7 @@ struct ModeCache {
 };
 
 struct StageTimes {
-    float prep = 0, up = 0, m2l = 0, near = 0, down = 0, corr = 0, total = 0;
+    float prep = 0, up = 0, m2l = 0, gather = 0, near = 0, down = 0, corr = 0, total = 0;
 };
 
 class Operator {
@@ -90,7 +90,11 @@ private:
     void uploadPlan();
     int device = -1;
     hipStream_t own = nullptr;
-    std::vector<std::array<hipEvent_t, 7>> evPool;
+    hipStream_t aux = nullptr;        // near field + corrections overlap the far field
+    hipEvent_t evFork = nullptr, evJoin = nullptr;
+    bool overlap = false;  // ANISO_OVERLAP=1: near + corr on the auxiliary stream (no gain measured)
+    static constexpr int kStageEvents = 10;
+    std::vector<std::array<hipEvent_t, kStageEvents>> evPool;
     int evUsed = 0;
     int maxNearS = 0;
     // geometry / tree on device

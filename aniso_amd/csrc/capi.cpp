@@ -299,7 +299,8 @@ int aniso_stage_times(aniso_handle h, float* t) {
     return guarded([&] {
         CHECK_PTR(t);
         auto s = get(h).stageTimes();
-        t[0] = s.prep; t[1] = s.up; t[2] = s.m2l; t[3] = s.near; t[4] = s.down; t[5] = s.corr; t[6] = s.total;
+        t[0] = s.prep; t[1] = s.up; t[2] = s.m2l; t[3] = s.gather; t[4] = s.near; t[5] = s.down; t[6] = s.corr;
+        t[7] = s.total;
     });
 }
 

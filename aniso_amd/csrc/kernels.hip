@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
                                               const int64_t* __restrict__ nearKOff, const int2* __restrict__ nearSym,
                                               const double* __restrict__ K, const double* __restrict__ fT,
                                               const int* __restrict__ perm, int maxS, int flags, double sgn,
-                                              double* __restrict__ partial, double* __restrict__ out) {
+                                              double scale, double* __restrict__ partial, double* __restrict__ out) {
     extern __shared__ double sh[];
     const int wv = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
     const int li = blockIdx.x * (blockDim.x / kWave) + wv;
@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
             for (int h = 0; h < 2; ++h) {
                 const int t = 2 * r + h;
                 if (t >= nT) break;
-                out[perm[tb + t]] = h ? a1 : a0;
+                out[perm[tb + t]] = scale * (h ? a1 : a0);
             }
         }
     }
@@ -618,7 +618,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     const double* __restrict__ nrx, const double* __restrict__ nry, const double* __restrict__ pxT,
     const double* __restrict__ pyT, const int* __restrict__ perm, const int2* __restrict__ leafNear,
     const int* __restrict__ nearPtr, const int* __restrict__ nearOff, int maxNear, const double* __restrict__ nearPart,
-    int flags, double* __restrict__ out) {
+    int flags, double scale, double* __restrict__ out) {
     extern __shared__ double sm[];
     int4* DN = reinterpret_cast<int4*>(sm);             // maxTask node records
     double* Rl = reinterpret_cast<double*>(DN + maxTask);  // 4 x 256 transfer matrices
@@ -712,15 +712,16 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
                 for (int i = 0; i < kNP; ++i) l2p += Sx[i] * Sy[j] * L[j * kNP + i];
             v += l2p;
         }
-        out[perm[kpos]] += v;
+        out[perm[kpos]] += scale * v;
     }
 }
 
 // Corrections (nearRemoval + refineAddOnFast + singularAddFast,
 // KernelFactory.cpp:445-478, 662-709, 828-860) as a 3x3-square stencil with
 // per-mode translation-invariant d2 x 9 x d2 weights, plus the singular term
-// from Legendre coefficients of the target's own square (O(d^4) moments), then
-// the final 1/(2 pi) scale (AnisoWrapper.cpp:129-130).
+// from Legendre coefficients of the target's own square (O(d^4) moments).  Every
+// contribution carries the final 1/(2 pi) (AnisoWrapper.cpp:129-130): k_near
+// stores its scaled sum, k_corr and k_down_tier add theirs, in any order.
 template <int D>
 __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* __restrict__ perm,
                                               const double* __restrict__ charge, const double* __restrict__ fO,
@@ -793,7 +794,7 @@ __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* _
             }
         acc += sing;
     }
-    out[t] = (out[t] + acc) * scale;
+    out[t] += acc * scale;  // near and far are scaled by their own kernels
 }
 
 __global__ void k_permute(int64_t N, const int* __restrict__ perm, const double* __restrict__ orig,
@@ -938,12 +939,12 @@ void launch_m2l_gather(int ntgt, const int* tgt, const int* inPtr, const double*
 
 void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts, const int64_t* nearKOff,
                  const int2* nearSym, const double* K, const double* fT, const int* perm, int maxS, int flags,
-                 double sgn, double* partial, double* out, hipStream_t s) {
+                 double sgn, double scale, double* partial, double* out, hipStream_t s) {
     if (nl <= 0) return;
     int wpb = maxS * 8 * 4 <= 48 * 1024 ? 4 : 1;
     size_t shm = (size_t)wpb * (maxS > 0 ? maxS : 1) * sizeof(double);
     k_near<<<blocks_for(nl, wpb), wpb * kWave, shm, s>>>(nl, leafInfo, nearPtsPtr, nearPts, nearKOff, nearSym, K, fT,
-                                                        perm, maxS > 0 ? maxS : 1, flags, sgn, partial, out);
+                                                        perm, maxS > 0 ? maxS : 1, flags, sgn, scale, partial, out);
     HIP_LAUNCH_CHECK();
 }
 
@@ -953,12 +954,12 @@ void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const
                       const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
                       const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
                       const int* perm, const int2* leafNear, const int* nearPtr, const int* nearOff, int maxNear,
-                      const double* nearPart, int flags, double* out, hipStream_t s) {
+                      const double* nearPart, int flags, double scale, double* out, hipStream_t s) {
     if (ntask <= 0) return;
     k_down_tier<<<ntask, kTierThreads, down_tier_lds(maxTask, maxLeaves, maxNear), s>>>(
         taskBase, maxTask, maxLeaves, taskPtr, grpPtr, grp, dn, slot, local, m2lPart, P, total, leafPtr,
         leafSlot, leafIdx, leafBegin, ptsRange, ncx, ncy, nrx, nry, pxT, pyT, perm, leafNear, nearPtr, nearOff, maxNear,
-        nearPart, flags, out);
+        nearPart, flags, scale, out);
     HIP_LAUNCH_CHECK();
 }
 

@@ -50,14 +50,14 @@ void launch_m2l_gather(int ntgt, const int* tgt, const int* inPtr, const double*
                        hipStream_t s);
 void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts, const int64_t* nearKOff,
                  const int2* nearSym, const double* K, const double* fT, const int* perm, int maxS, int flags,
-                 double sgn, double* partial, double* out, hipStream_t s);
+                 double sgn, double scale, double* partial, double* out, hipStream_t s);
 void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const int* taskPtr,
                       const int* grpPtr, const int* grp, const int4* dn, const int* slot, const double* local,
                       const double* m2lPart, const Params* P, double* total, const int* leafPtr, const int* leafSlot,
                       const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
                       const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
                       const int* perm, const int2* leafNear, const int* nearPtr, const int* nearOff, int maxNear,
-                      const double* nearPart, int flags, double* out, hipStream_t s);
+                      const double* nearPart, int flags, double scale, double* out, hipStream_t s);
 void launch_corr(int d, int64_t b, int64_t e, const int* perm, const double* charge, const double* fO, const double* C,
                  const double* mu, const Params* P, int flags, double scale, double* out, hipStream_t s);
 void launch_cache_m2l(int64_t npairs, const int* pairTgt, const int* src, const double* ncx, const double* ncy,

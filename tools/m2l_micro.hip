@@ -98,8 +98,12 @@ __global__ void __launch_bounds__(256) k_can(int ntgt, const int64_t* __restrict
             for (int g = 0; g < kGroups; ++g) {
                 if (4 * g < nC) {
                     const int jj = 4 * g + q;
-                    const int slot = STORE != 2 ? __shfl(cSlot, jj) : canonBase[wave] + jj;
-                    if (jj < nC) {
+                    int slot = STORE != 2 ? __shfl(cSlot, jj) : canonBase[wave] + jj;
+                    if (STORE == 6) slot &= 1023;  // L2-resident footprint (128 KB)
+                    if (STORE == 7) slot &= (1 << 15) - 1;  // 4 MB
+                    if (STORE == 8) slot &= (1 << 18) - 1;  // 32 MB
+                    if (STORE == 9) slot &= (1 << 19) - 1;  // 64 MB
+                    if (jj < nC && (STORE != 5 || jj % 3 == 0)) {
                         if (STORE == 3)
                             __builtin_nontemporal_store(y[g], partial + (size_t)slot * kRank + t);
                         else if (STORE == 4)
@@ -128,6 +132,87 @@ __global__ void __launch_bounds__(256) k_can(int ntgt, const int64_t* __restrict
     }
     acc = quad_sum(acc);
     if (q == 0) local[(size_t)n * kRank + t] = acc;
+    }
+}
+
+// persistent waves; the partial stores of target i are issued after the first
+// operator loads of target i+1 so no wait on the loads waits on the stores
+__global__ void __launch_bounds__(256) k_can_pipe(int ntgt, const int64_t* __restrict__ ptr, const int* __restrict__ canonBase,
+                                                  const int* __restrict__ outSlot, const int* __restrict__ src,
+                                                  const double* __restrict__ K, const double* __restrict__ mult,
+                                                  double* __restrict__ partial, double* __restrict__ local) {
+    const int wave0 = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) / kWave));
+    const int lane = threadIdx.x & (kWave - 1);
+    const int nw = (int)(gridDim.x * blockDim.x / kWave);
+    const int t = lane >> 2, q = lane & 3;
+    constexpr int kGroups = (kMaxCanon + 3) / 4;
+    double yp[kGroups];
+    int slotp[kGroups];
+    int nCp = 0;
+    for (int wave = wave0; wave < ntgt + nw; wave += nw) {
+        const bool live = wave < ntgt;
+        const int n = wave;
+        const int64_t pd = live ? ptr[wave] : 0, p1 = live ? ptr[wave + 1] : 0;
+        const int nC = (int)(p1 - pd);
+        const int cSrc = lane < nC ? src[pd + lane] : 0;
+        const int cSlot = lane < nC ? outSlot[canonBase[live ? wave : 0] + lane] : 0;
+        // first group's loads
+        dbl2 a0, a1, b0, b1, e0, e1, f0, f1;
+        load_block(K, pd, lane, nC > 0, a0, a1);
+        load_block(K, pd + 1, lane, nC > 1, b0, b1);
+        load_block(K, pd + 2, lane, nC > 2, e0, e1);
+        load_block(K, pd + 3, lane, nC > 3, f0, f1);
+        // previous target's partials
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g) {
+            if (4 * g < nCp) {
+                const int jj = 4 * g + q;
+                if (jj < nCp) partial[(size_t)slotp[g] * kRank + t] = yp[g];
+            }
+        }
+        if (!live) break;
+        const double4 mn = *reinterpret_cast<const double4*>(mult + (size_t)n * kRank + q * 4);
+        const double m0 = mn.x, m1 = mn.y, m2 = mn.z, m3 = mn.w;
+        double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g) {
+            yp[g] = 0.0;
+            const int j = 4 * g;
+            if (j < nC) {
+                if (g > 0) {
+                    load_block(K, pd + j, lane, true, a0, a1);
+                    load_block(K, pd + j + 1, lane, j + 1 < nC, b0, b1);
+                    load_block(K, pd + j + 2, lane, j + 2 < nC, e0, e1);
+                    load_block(K, pd + j + 3, lane, j + 3 < nC, f0, f1);
+                }
+                const double xa = mult[(size_t)__builtin_amdgcn_readlane(cSrc, j) * kRank + t];
+                const double xb = mult[(size_t)__builtin_amdgcn_readlane(cSrc, min(j + 1, nC - 1)) * kRank + t];
+                const double xe = mult[(size_t)__builtin_amdgcn_readlane(cSrc, min(j + 2, nC - 1)) * kRank + t];
+                const double xf = mult[(size_t)__builtin_amdgcn_readlane(cSrc, min(j + 3, nC - 1)) * kRank + t];
+                c0 += (a0.x * xa + b0.x * xb) + (e0.x * xe + f0.x * xf);
+                c1 += (a0.y * xa + b0.y * xb) + (e0.y * xe + f0.y * xf);
+                c2 += (a1.x * xa + b1.x * xb) + (e1.x * xe + f1.x * xf);
+                c3 += (a1.y * xa + b1.y * xb) + (e1.y * xe + f1.y * xf);
+                const double ya = quad_sum(a0.x * m0 + a0.y * m1 + a1.x * m2 + a1.y * m3);
+                const double yb = quad_sum(b0.x * m0 + b0.y * m1 + b1.x * m2 + b1.y * m3);
+                const double ye = quad_sum(e0.x * m0 + e0.y * m1 + e1.x * m2 + e1.y * m3);
+                const double yf = quad_sum(f0.x * m0 + f0.y * m1 + f1.x * m2 + f1.y * m3);
+                yp[g] = q == 0 ? ya : q == 1 ? yb : q == 2 ? ye : yf;
+                slotp[g] = __shfl(cSlot, (4 * g + q) & 63);
+            }
+        }
+        nCp = nC;
+#pragma unroll
+        for (int off = 4; off < kWave; off <<= 1) {
+            c0 += __shfl_xor(c0, off);
+            c1 += __shfl_xor(c1, off);
+            c2 += __shfl_xor(c2, off);
+            c3 += __shfl_xor(c3, off);
+        }
+        const int jr = t & 3;
+        const double v = jr == 0 ? c0 : jr == 1 ? c1 : jr == 2 ? c2 : c3;
+        double acc = __shfl(v, 4 * t + (t >> 2));
+        if (q == 0) local[(size_t)n * kRank + t] = acc;
     }
 }
 
@@ -225,6 +310,16 @@ int main() {
             run("store=contig", k_can<2, 1, 0>);
             run("store=none", k_can<0, 1, 0>);
             run("no-transpose", k_can<0, 0, 0>);
+            run("store=1/3", k_can<5, 1, 0>);
+            run("store=l2", k_can<6, 1, 0>);
+            run("store=4MB", k_can<7, 1, 0>);
+            run("store=32MB", k_can<8, 1, 0>);
+            run("store=64MB", k_can<9, 1, 0>);
+            for (int wpc : std::initializer_list<int>{}) {
+                char nm[64];
+                std::snprintf(nm, sizeof nm, "pipe%d", wpc);
+                run(nm, k_can_pipe, 256 * wpc / 4);
+            }
             run("store=nt", k_can<3, 1, 0>);
             run("store=sys", k_can<4, 1, 0>);
             for (int wpc : std::initializer_list<int>{}) {
