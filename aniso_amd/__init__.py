@@ -68,6 +68,8 @@ def lib():
             "aniso_stage_times": [P, fp],
             "aniso_line_integrals": [P, dp, I, dp],
             "aniso_forward_dev": [P, P, P, P],
+            "aniso_mapping_tree_dev": [P, P, I, P, P],
+            "aniso_forward_tree_dev": [P, P, P, P],
             "aniso_gmres": [P, dp, dp, I, I, D, dp, I, ip, dp],
             "aniso_last_error": [ctypes.c_char_p, ctypes.c_size_t],
         }
@@ -196,6 +198,24 @@ class Aniso:
         _check(lib().aniso_forward_dev(self.address, ctypes.c_void_p(u.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                                        ctypes.c_void_p(s)))
         return out
+
+    def mapping_tree_dev(self, q_tree, id_, out_slice, stream=None):
+        """mapping on a tree-order device vector (all N) into the owned tree-order slice."""
+        import torch
+
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_mapping_tree_dev(self.address, ctypes.c_void_p(q_tree.data_ptr()), int(id_),
+                                            ctypes.c_void_p(out_slice.data_ptr()), ctypes.c_void_p(s)))
+        return out_slice
+
+    def forward_tree_dev(self, x_tree, y_slice, stream=None):
+        """forwardOperator in tree order: y_slice = (x - K_0(sigma_s .* x))[own slice], x tree-ordered."""
+        import torch
+
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_forward_tree_dev(self.address, ctypes.c_void_p(x_tree.data_ptr()),
+                                            ctypes.c_void_p(y_slice.data_ptr()), ctypes.c_void_p(s)))
+        return y_slice
 
     def gmres(self, q, m=80, maxit=400, tol=1e-12, x0=None):
         """main.cpp:121-141 on the device: returns (iters, x, residual history, final residual)."""

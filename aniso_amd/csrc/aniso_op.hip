@@ -122,6 +122,10 @@ void Operator::ensureDevice() {
     up(dPyT, pyT);
     up(dPerm, tree.perm);
     up(dW, geo.w);
+    std::vector<double> wT(geo.N);
+    for (int64_t k = 0; k < geo.N; ++k) wT[k] = geo.w[tree.perm[k]];
+    up(dWT, wT);
+    dChargeO.alloc(geo.N * sizeof(double));
     up(dNcx, tree.ncx);
     up(dNcy, tree.ncy);
     up(dNrx, tree.nrx);
@@ -193,6 +197,7 @@ void Operator::ensureDevice() {
     dFO.alloc(geo.N * sizeof(double));
     dTmp.alloc(geo.N * sizeof(double));
     dTmp2.alloc(geo.N * sizeof(double));
+    dTmpS.alloc(geo.N * sizeof(double));
     dMult.alloc((size_t)tree.nn * kRank * sizeof(double));
     dLocal.alloc((size_t)tree.nn * kRank * sizeof(double));
     dTotal.alloc((size_t)tree.nn * kRank * sizeof(double));
@@ -278,6 +283,9 @@ void Operator::setCoeff(const double* ss, const double* st) {
     }
     up(dStCoef, coef);
     up(dSigmaS, sigma_s);
+    std::vector<double> sT(geo.N);
+    for (int64_t k = 0; k < geo.N; ++k) sT[k] = sigma_s[tree.perm[k]];
+    up(dSigmaT, sT);
     for (auto& m : modes) m.ready = false;
     coeffSet = true;
 }
@@ -324,6 +332,25 @@ void Operator::mappingHost(const double* charge, int id, double* out) {
 // mapping (AnisoWrapper.cpp:92-136) on device pointers, enqueued on stream s.
 // Only owned targets of `out` are written when the operator is sharded.
 void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t s, int mask) {
+    apply(charge, false, nullptr, id, out, false, s, mask);
+}
+
+// mapping on a tree-order input (all N) into the owned tree-order slice
+// out[k - ownBegin], k in [ownBegin, ownEnd): no permutation gathers, and the
+// slices of the shards concatenate to the tree-order output.
+void Operator::mappingTreeDev(const double* qTree, int id, double* outSlice, hipStream_t s) {
+    apply(qTree, true, nullptr, id, outSlice, true, s, kStageAll);
+}
+
+// main.cpp forwardOperator (main.cpp:125-136) in tree order: y = x - K_0(sigma_s x)
+// on the owned slice, x tree-ordered (all N).
+void Operator::forwardTreeDev(const double* xTree, double* ySlice, hipStream_t s) {
+    apply(xTree, true, dSigmaT.as<double>(), 0, dTmpS.as<double>(), true, s, kStageAll);
+    launch_sub_slice(plan.ownEnd - plan.ownBegin, xTree + plan.ownBegin, dTmpS.as<double>(), ySlice, s);
+}
+
+void Operator::apply(const double* charge, bool treeIn, const double* sigT, int id, double* out, bool treeOut,
+                     hipStream_t s, int mask) {
     if (id < 0 || id >= kernelSize) throw std::out_of_range("kernel id out of range");
     if (!modes[id].ready) throw std::runtime_error("mapping on kernel id " + std::to_string(id) + " before cache(" + std::to_string(id) + ")");
     ensureDevice();
@@ -340,7 +367,14 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
         ev = evPool[evUsed++].data();
         HIP_CHECK(hipEventRecord(ev[0], s));
     }
-    launch_prepare(geo.N, dPerm.as<int>(), charge, dW.as<double>(), dFT.as<double>(), dFO.as<double>(), s);
+    if (treeIn)
+        launch_prepare_tree(geo.N, dPerm.as<int>(), charge, sigT, dWT.as<double>(), dW.as<double>(), dFT.as<double>(),
+                            dFO.as<double>(), dChargeO.as<double>(), s);
+    else
+        launch_prepare(geo.N, dPerm.as<int>(), charge, dW.as<double>(), dFT.as<double>(), dFO.as<double>(), s);
+    const double* chargeO = treeIn ? dChargeO.as<double>() : charge;  // original order, for the corrections
+    const int* operm = treeOut ? nullptr : dPerm.as<int>();
+    const int64_t obase = treeOut ? plan.ownBegin : 0;
     if (tm) HIP_CHECK(hipEventRecord(ev[1], s));
     // The near field and the corrections need only the prepared charges: they run
     // on the auxiliary stream, overlapping the latency-bound up pass and the M2L
@@ -355,11 +389,11 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
     const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
     if (tm) HIP_CHECK(hipEventRecord(ev[6], sn));
     launch_near((int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(),
-                dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(), dFT.as<double>(), dPerm.as<int>(),
+                dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(), dFT.as<double>(), operm, obase,
                 maxNearS, mask, sgn, M_1_PI / 2.0, dNearPart.as<double>(), out, sn);
     if (tm) HIP_CHECK(hipEventRecord(ev[7], sn));
-    launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), charge, dFO.as<double>(), mc.C.as<double>(),
-                mc.mu.as<double>(), P, mask, M_1_PI / 2.0, out, sn);
+    launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), chargeO, dFO.as<double>(), mc.C.as<double>(),
+                mc.mu.as<double>(), P, mask, M_1_PI / 2.0, treeOut, out, sn);
     if (tm) HIP_CHECK(hipEventRecord(ev[8], sn));
     if (overlap) HIP_CHECK(hipEventRecord(evJoin, aux));
     // up pass (global, every rank): tiers bottom-up
@@ -390,7 +424,7 @@ void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t
                              dM2LPart.as<double>(), P, dTotal.as<double>(), dDnLeafPtr.as<int>(),
                              dDnLeafSlot.as<int>(), dDnLeafIdx.as<int>(), dDnLeafPts.as<int>(), dDnPtsRange.as<int2>(),
                              dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(),
-                             dPxT.as<double>(), dPyT.as<double>(), dPerm.as<int>(), dDnLeafNear.as<int2>(),
+                             dPxT.as<double>(), dPyT.as<double>(), operm, obase, dDnLeafNear.as<int2>(),
                              dDnNearPtr.as<int>(), dDnNearOff.as<int>(), plan.dnMaxNear, dNearPart.as<double>(), mask,
                              M_1_PI / 2.0, out, s);
     if (tm) HIP_CHECK(hipEventRecord(ev[5], s));

@@ -52,6 +52,8 @@ public:
     void cache(int id);
     void mappingHost(const double* charge, int id, double* out);
     void mappingDev(const double* charge, int id, double* out, hipStream_t s, int stageMask = 0x3f);
+    void mappingTreeDev(const double* qTree, int id, double* outSlice, hipStream_t s);
+    void forwardTreeDev(const double* xTree, double* ySlice, hipStream_t s);
 
     // --- extensions
     void setShard(int rank, int nranks);
@@ -86,6 +88,9 @@ public:
     int maxNearSources() const { return maxNearS; }
 
 private:
+    void apply(const double* charge, bool treeIn, const double* sigT, int id, double* out, bool treeOut, hipStream_t s,
+               int mask);
+
     void ensureDevice();
     void uploadPlan();
     int device = -1;
@@ -107,6 +112,7 @@ private:
     DevBuf dNearSym, dNearPart, dDnLeafNear, dDnNearPtr, dDnNearOff;              // symmetric near field
     DevBuf dParams, dStCoef;
     DevBuf dCharge, dOut, dFT, dFO, dMult, dLocal, dTotal, dSigmaS, dTmp, dTmp2;
+    DevBuf dWT, dSigmaT, dChargeO, dTmpS;  // tree-order path
     std::vector<ModeCache> modes;
 };
 

@@ -174,6 +174,26 @@ int aniso_forward_dev(aniso_handle h, const double* u, double* out, void* stream
     });
 }
 
+int aniso_mapping_tree_dev(aniso_handle h, const double* q_tree, int id, double* out_slice, void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(q_tree);
+        CHECK_PTR(out_slice);
+        get(h).mappingTreeDev(q_tree, id, out_slice, (hipStream_t)stream);
+    });
+}
+
+int aniso_forward_tree_dev(aniso_handle h, const double* x_tree, double* y_slice, void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(x_tree);
+        CHECK_PTR(y_slice);
+        auto& op = get(h);
+        if (!op.modeCached(0)) throw std::runtime_error("forward operator before cache(0)");
+        op.forwardTreeDev(x_tree, y_slice, (hipStream_t)stream);
+    });
+}
+
 int aniso_gmres(aniso_handle h, const double* q, double* x, int m, int maxit, double tol, double* hist, int maxhist,
                 int* iters, double* final_resid) {
     CHECK_HANDLE(h);

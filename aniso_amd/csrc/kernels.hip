@@ -176,6 +176,34 @@ __device__ double pair_kernel(const Params* __restrict__ P, const double* __rest
 
 // ----------------------------------------------------------------- apply kernels
 
+// Output slot of tree position k: the original index perm[k] (original-order
+// output) or the owned tree-order slice k - obase (operm == nullptr).
+__device__ __forceinline__ int64_t out_index(const int* __restrict__ operm, int64_t obase, int64_t k) {
+    return operm ? (int64_t)operm[k] : k - obase;
+}
+
+// Tree-order input: c = x_tree[k] (times sigma_s[k] in tree order when given);
+// fT[k] = c w_T[k]; the corrections read the original-order fO and charge.
+__global__ void k_prepare_tree(int64_t N, const int* __restrict__ perm, const double* __restrict__ xT,
+                               const double* __restrict__ sigT, const double* __restrict__ wT,
+                               const double* __restrict__ w, double* __restrict__ fT, double* __restrict__ fO,
+                               double* __restrict__ chargeO) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N) return;
+    const double c = sigT ? xT[k] * sigT[k] : xT[k];
+    const int t = perm[k];
+    fT[k] = c * wT[k];
+    fO[t] = c * w[t];
+    chargeO[t] = c;
+}
+
+// y = x - a on the owned tree slice (forward operator u - K(sigma_s u), main.cpp:125-136)
+__global__ void k_sub_slice(int64_t n, const double* __restrict__ x, const double* __restrict__ a,
+                            double* __restrict__ y) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = x[i] - a[i];
+}
+
 __global__ void k_prepare(int64_t N, const int* __restrict__ perm, const double* __restrict__ charge,
                           const double* __restrict__ w, double* __restrict__ fT, double* __restrict__ fO) {
     int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -479,8 +507,9 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
                                               const int64_t* __restrict__ nearPtsPtr, const int* __restrict__ nearPts,
                                               const int64_t* __restrict__ nearKOff, const int2* __restrict__ nearSym,
                                               const double* __restrict__ K, const double* __restrict__ fT,
-                                              const int* __restrict__ perm, int maxS, int flags, double sgn,
-                                              double scale, double* __restrict__ partial, double* __restrict__ out) {
+                                              const int* __restrict__ operm, int64_t obase, int maxS, int flags,
+                                              double sgn, double scale, double* __restrict__ partial,
+                                              double* __restrict__ out) {
     extern __shared__ double sh[];
     const int wv = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
     const int li = blockIdx.x * (blockDim.x / kWave) + wv;
@@ -587,7 +616,7 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
             for (int h = 0; h < 2; ++h) {
                 const int t = 2 * r + h;
                 if (t >= nT) break;
-                out[perm[tb + t]] = scale * (h ? a1 : a0);
+                out[out_index(operm, obase, tb + t)] = scale * (h ? a1 : a0);
             }
         }
     }
@@ -616,7 +645,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     const int* __restrict__ leafSlot, const int* __restrict__ leafIdx, const int* __restrict__ leafBegin,
     const int2* __restrict__ ptsRange, const double* __restrict__ ncx, const double* __restrict__ ncy,
     const double* __restrict__ nrx, const double* __restrict__ nry, const double* __restrict__ pxT,
-    const double* __restrict__ pyT, const int* __restrict__ perm, const int2* __restrict__ leafNear,
+    const double* __restrict__ pyT, const int* __restrict__ operm, int64_t obase, const int2* __restrict__ leafNear,
     const int* __restrict__ nearPtr, const int* __restrict__ nearOff, int maxNear, const double* __restrict__ nearPart,
     int flags, double scale, double* __restrict__ out) {
     extern __shared__ double sm[];
@@ -712,7 +741,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
                 for (int i = 0; i < kNP; ++i) l2p += Sx[i] * Sy[j] * L[j * kNP + i];
             v += l2p;
         }
-        out[perm[kpos]] += scale * v;
+        out[out_index(operm, obase, kpos)] += scale * v;
     }
 }
 
@@ -727,7 +756,7 @@ __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* _
                                               const double* __restrict__ charge, const double* __restrict__ fO,
                                               const double* __restrict__ C, const double* __restrict__ mu,
                                               const Params* __restrict__ P, int flags, double scale,
-                                              double* __restrict__ out) {
+                                              bool treeOut, double* __restrict__ out) {
     constexpr int D2 = D * D;
     int64_t k = b + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= e) return;
@@ -794,7 +823,7 @@ __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* _
             }
         acc += sing;
     }
-    out[t] += acc * scale;  // near and far are scaled by their own kernels
+    out[treeOut ? k - b : (int64_t)t] += acc * scale;  // near and far are scaled by their own kernels
 }
 
 __global__ void k_permute(int64_t N, const int* __restrict__ perm, const double* __restrict__ orig,
@@ -938,13 +967,14 @@ void launch_m2l_gather(int ntgt, const int* tgt, const int* inPtr, const double*
 }
 
 void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts, const int64_t* nearKOff,
-                 const int2* nearSym, const double* K, const double* fT, const int* perm, int maxS, int flags,
-                 double sgn, double scale, double* partial, double* out, hipStream_t s) {
+                 const int2* nearSym, const double* K, const double* fT, const int* operm, int64_t obase, int maxS,
+                 int flags, double sgn, double scale, double* partial, double* out, hipStream_t s) {
     if (nl <= 0) return;
     int wpb = maxS * 8 * 4 <= 48 * 1024 ? 4 : 1;
     size_t shm = (size_t)wpb * (maxS > 0 ? maxS : 1) * sizeof(double);
     k_near<<<blocks_for(nl, wpb), wpb * kWave, shm, s>>>(nl, leafInfo, nearPtsPtr, nearPts, nearKOff, nearSym, K, fT,
-                                                        perm, maxS > 0 ? maxS : 1, flags, sgn, scale, partial, out);
+                                                        operm, obase, maxS > 0 ? maxS : 1, flags, sgn, scale,
+                                                        partial, out);
     HIP_LAUNCH_CHECK();
 }
 
@@ -953,27 +983,28 @@ void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const
                       const double* m2lPart, const Params* P, double* total, const int* leafPtr, const int* leafSlot,
                       const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
                       const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
-                      const int* perm, const int2* leafNear, const int* nearPtr, const int* nearOff, int maxNear,
-                      const double* nearPart, int flags, double scale, double* out, hipStream_t s) {
+                      const int* operm, int64_t obase, const int2* leafNear, const int* nearPtr, const int* nearOff,
+                      int maxNear, const double* nearPart, int flags, double scale, double* out, hipStream_t s) {
     if (ntask <= 0) return;
     k_down_tier<<<ntask, kTierThreads, down_tier_lds(maxTask, maxLeaves, maxNear), s>>>(
         taskBase, maxTask, maxLeaves, taskPtr, grpPtr, grp, dn, slot, local, m2lPart, P, total, leafPtr,
-        leafSlot, leafIdx, leafBegin, ptsRange, ncx, ncy, nrx, nry, pxT, pyT, perm, leafNear, nearPtr, nearOff, maxNear,
-        nearPart, flags, scale, out);
+        leafSlot, leafIdx, leafBegin, ptsRange, ncx, ncy, nrx, nry, pxT, pyT, operm, obase, leafNear, nearPtr, nearOff,
+        maxNear, nearPart, flags, scale, out);
     HIP_LAUNCH_CHECK();
 }
 
 void launch_corr(int d, int64_t b, int64_t e, const int* perm, const double* charge, const double* fO, const double* C,
-                 const double* mu, const Params* P, int flags, double scale, double* out, hipStream_t s) {
+                 const double* mu, const Params* P, int flags, double scale, bool treeOut, double* out,
+                 hipStream_t s) {
     if (e <= b) return;
     unsigned nb = blocks_for(e - b, 256);
     switch (d) {
-        case 1: k_corr<1><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, out); break;
-        case 2: k_corr<2><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, out); break;
-        case 3: k_corr<3><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, out); break;
-        case 4: k_corr<4><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, out); break;
-        case 5: k_corr<5><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, out); break;
-        case 6: k_corr<6><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, out); break;
+        case 1: k_corr<1><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
+        case 2: k_corr<2><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
+        case 3: k_corr<3><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
+        case 4: k_corr<4><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
+        case 5: k_corr<5><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
+        case 6: k_corr<6><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
         default: throw_hip(hipErrorInvalidValue, __FILE__, __LINE__);
     }
     HIP_LAUNCH_CHECK();
@@ -995,6 +1026,19 @@ void launch_cache_near(int nl, const int* leaves, const int64_t* nearPtr, const 
     size_t shm = (size_t)maxSrc * sizeof(int64_t) + (size_t)(maxSrc + 1) * sizeof(int);
     k_cache_near<<<nl, 256, shm, s>>>(nl, leaves, nearPtr, nearSrc, nearKOff, begin, count, pxT, pyT, stcoef, P, mode,
                                       maxSrc, K);
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_prepare_tree(int64_t N, const int* perm, const double* xT, const double* sigT, const double* wT,
+                         const double* w, double* fT, double* fO, double* chargeO, hipStream_t s) {
+    if (N <= 0) return;
+    k_prepare_tree<<<blocks_for(N, 256), 256, 0, s>>>(N, perm, xT, sigT, wT, w, fT, fO, chargeO);
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_sub_slice(int64_t n, const double* x, const double* a, double* y, hipStream_t s) {
+    if (n <= 0) return;
+    k_sub_slice<<<blocks_for(n, 256), 256, 0, s>>>(n, x, a, y);
     HIP_LAUNCH_CHECK();
 }
 

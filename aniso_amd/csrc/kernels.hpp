@@ -48,18 +48,25 @@ void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, c
                 double* local, hipStream_t s);
 void launch_m2l_gather(int ntgt, const int* tgt, const int* inPtr, const double* partial, double* local,
                        hipStream_t s);
+// Output index mode of k_near / k_down_tier / k_corr: operm = perm writes the
+// original-order vector out[perm[k]]; operm = nullptr writes the owned tree-order
+// slice out[k - obase].
 void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts, const int64_t* nearKOff,
-                 const int2* nearSym, const double* K, const double* fT, const int* perm, int maxS, int flags,
-                 double sgn, double scale, double* partial, double* out, hipStream_t s);
+                 const int2* nearSym, const double* K, const double* fT, const int* operm, int64_t obase, int maxS,
+                 int flags, double sgn, double scale, double* partial, double* out, hipStream_t s);
 void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const int* taskPtr,
                       const int* grpPtr, const int* grp, const int4* dn, const int* slot, const double* local,
                       const double* m2lPart, const Params* P, double* total, const int* leafPtr, const int* leafSlot,
                       const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
                       const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
-                      const int* perm, const int2* leafNear, const int* nearPtr, const int* nearOff, int maxNear,
-                      const double* nearPart, int flags, double scale, double* out, hipStream_t s);
+                      const int* operm, int64_t obase, const int2* leafNear, const int* nearPtr, const int* nearOff,
+                      int maxNear, const double* nearPart, int flags, double scale, double* out, hipStream_t s);
 void launch_corr(int d, int64_t b, int64_t e, const int* perm, const double* charge, const double* fO, const double* C,
-                 const double* mu, const Params* P, int flags, double scale, double* out, hipStream_t s);
+                 const double* mu, const Params* P, int flags, double scale, bool treeOut, double* out,
+                 hipStream_t s);
+void launch_prepare_tree(int64_t N, const int* perm, const double* xT, const double* sigT, const double* wT,
+                         const double* w, double* fT, double* fO, double* chargeO, hipStream_t s);
+void launch_sub_slice(int64_t n, const double* x, const double* a, double* y, hipStream_t s);
 void launch_cache_m2l(int64_t npairs, const int* pairTgt, const int* src, const double* ncx, const double* ncy,
                       const double* nrx, const double* nry, const double* stcoef, const Params* P, int mode,
                       double* K, hipStream_t s);

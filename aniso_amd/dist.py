@@ -4,8 +4,10 @@ One process per GPU.  Every rank holds the whole input vector (GMRES vectors are
 replicated), runs the cheap up pass redundantly, and computes the targets of its
 FMM-subtree shard only (aniso_set_shard): those targets form one contiguous range
 of the tree order.  The output is assembled with ONE all-gather of the tree-ordered
-shard slices (RCCL over xGMI on the GPU box, gloo on CPU) and a permutation back to
-the original node order.  No other collective is on the data path.
+shard slices (RCCL over xGMI on the GPU box, gloo on CPU).  With the vectors kept
+in tree order (aniso_forward_tree_dev) the assembly is a single index gather of
+the padded all-gather buffer (gather_index); with original-order vectors it is a
+permutation (assemble_from_gathered).  No other collective is on the data path.
 """
 import numpy as np
 
@@ -64,3 +66,9 @@ def local_slice(full_orig, perm, rng, L):
     buf = np.zeros(L, dtype=full_orig.dtype)
     buf[: e - b] = full_orig[perm[b:e]]
     return buf
+
+
+def gather_index(ranges, L):
+    """Positions in the flattened (nranks, L) all-gather buffer of tree positions
+    0 .. N-1: tree[k] = gathered.reshape(-1)[idx[k]]."""
+    return np.concatenate([r * L + np.arange(e - b, dtype=np.int64) for r, (b, e) in enumerate(ranges)])

@@ -6,7 +6,8 @@ points"): the configs[2] geometry (sz=1024, d=1, ns=10, np=4, maxLevel=20,
 N = 1,048,576), main.cpp's coefficient functions, and main.cpp's GMRES matvec
 forwardOperator u - K_0(sigma_s .* u) (main.cpp:125-136): one apply of mode 0 per
 matvec.  A "step" is one matvec; steps are chained (v <- A v) with every vector
-resident in HBM.  fp64 throughout.
+resident in HBM, kept in tree order (a fixed relabelling of the unknowns, so no
+permutation gathers on the data path).  fp64 throughout.
 
 N GPUs (torchrun, one process per GPU, RCCL): the target set is sharded by FMM
 subtree (strong scaling: total work fixed).  Each rank applies its shard; one
@@ -145,40 +146,38 @@ def main():
     xy = op.getNodes()
     ss, st = main_coeffs(xy)
     full_stats = op.stats()
+    perm = torch.tensor(op.tree_perm(), device="cuda", dtype=torch.int64)
     if world > 1:
         ranges = adist.shard_ranges(op, world)
         op.set_shard(rank, world)
-        perm = torch.tensor(op.tree_perm(), device="cuda", dtype=torch.int64)
         L = adist.pad_len(ranges)
         slice_buf = torch.zeros(L, dtype=torch.float64, device="cuda")
         gathered = torch.zeros(world, L, dtype=torch.float64, device="cuda")
+        gidx = torch.tensor(adist.gather_index(ranges, L), device="cuda")
+        b_own, e_own = ranges[rank]
     op.setCoeff(ss, st)
     t0 = time.time()
     op.cache(0)
     torch.cuda.synchronize()
     t_cache = time.time() - t0
-    sig_s = torch.tensor(ss, device="cuda")
-    v = torch.tensor(gaussian(xy), device="cuda")
+    # GMRES vectors live in tree order (a fixed relabelling of the unknowns): the
+    # forward operator then needs no permutation gathers, and the shards' output
+    # slices concatenate to the next iterate
+    v = torch.tensor(gaussian(xy), device="cuda")[perm].contiguous()
     w = torch.zeros_like(v)
-    tmp = torch.zeros_like(v)
-    app = torch.zeros_like(v)
 
     def matvec(x, y):
         if world == 1:
-            op.forward_dev(x, y)
+            op.forward_tree_dev(x, y)
             return
-        torch.mul(x, sig_s, out=tmp)
-        op.mapping_dev(tmp, 0, app)
-        b, e = ranges[rank]
-        slice_buf[: e - b] = app[perm[b:e]]
+        op.forward_tree_dev(x, slice_buf)  # writes the owned e_own - b_own entries
         if args.backend == "nccl":
             dist.all_gather_into_tensor(gathered, slice_buf)
         else:  # gloo rehearsal: stage through host memory
             parts = [torch.zeros(L, dtype=torch.float64) for _ in range(world)]
             dist.all_gather(parts, slice_buf.cpu())
             gathered.copy_(torch.stack(parts))
-        adist.assemble_from_gathered(gathered, ranges, perm, out=app)
-        torch.sub(x, app, out=y)
+        torch.index_select(gathered.view(-1), 0, gidx, out=y)
 
     for _ in range(args.warmup):
         matvec(v, w)
@@ -241,13 +240,14 @@ def main():
         # unsharded operator on the same device
         u = torch.tensor(gaussian(xy), device="cuda")
         got = torch.zeros_like(u)
-        matvec(u, got)
+        matvec(u[perm].contiguous(), got)  # tree order in and out
         ref_op = aniso_amd.Aniso(args.sz, args.d, 5, 0.8, args.ns, 4, args.max_level)
         ref_op.setCoeff(ss, st)
         ref_op.cache(0)
         ref = torch.zeros_like(u)
-        ref_op.forward_dev(u, ref)
+        ref_op.forward_dev(u, ref)  # original order, unsharded
         torch.cuda.synchronize()
+        ref = ref[perm]
         line["verify_rel_err_vs_unsharded"] = float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref))
         del ref_op
     if rank == 0 and world == 1 and not args.no_cpu:
