@@ -87,7 +87,7 @@ def cpu_baseline(args, gpu_check):
     u = q * ss
     o.mapping(u, 0)  # warm-up
     reps, t0 = 0, time.time()
-    while reps < 3 or (time.time() - t0 < 5.0 and reps < 20):
+    while reps < 3 or time.time() - t0 < args.cpu_seconds:
         ref = o.mapping(u, 0)
         reps += 1
     t_apply = (time.time() - t0) / reps
@@ -115,7 +115,8 @@ def main():
     ap.add_argument("--d", type=int, default=1)
     ap.add_argument("--ns", type=int, default=10)
     ap.add_argument("--max-level", type=int, default=20)
-    ap.add_argument("--cpu-sz", type=int, default=256)
+    ap.add_argument("--cpu-sz", type=int, default=512, help="CPU baseline sample size (sz; N = sz^2 d^2)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline timing budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N>1 (gloo = CPU-staged rehearsal)")
