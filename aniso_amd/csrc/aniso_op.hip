@@ -125,7 +125,9 @@ void Operator::ensureDevice() {
     std::vector<double> wT(geo.N);
     for (int64_t k = 0; k < geo.N; ++k) wT[k] = geo.w[tree.perm[k]];
     up(dWT, wT);
-    dChargeO.alloc(geo.N * sizeof(double));
+    std::vector<int> iperm(geo.N);
+    for (int64_t k = 0; k < geo.N; ++k) iperm[tree.perm[k]] = (int)k;
+    up(dIperm, iperm);
     up(dNcx, tree.ncx);
     up(dNcy, tree.ncy);
     up(dNrx, tree.nrx);
@@ -194,7 +196,7 @@ void Operator::ensureDevice() {
     dCharge.alloc(geo.N * sizeof(double));
     dOut.alloc(geo.N * sizeof(double));
     dFT.alloc(geo.N * sizeof(double));
-    dFO.alloc(geo.N * sizeof(double));
+    dCT.alloc(geo.N * sizeof(double));
     dTmp.alloc(geo.N * sizeof(double));
     dTmp2.alloc(geo.N * sizeof(double));
     dTmpS.alloc(geo.N * sizeof(double));
@@ -367,19 +369,24 @@ void Operator::apply(const double* charge, bool treeIn, const double* sigT, int 
         ev = evPool[evUsed++].data();
         HIP_CHECK(hipEventRecord(ev[0], s));
     }
-    if (treeIn)
-        launch_prepare_tree(geo.N, dPerm.as<int>(), charge, sigT, dWT.as<double>(), dW.as<double>(), dFT.as<double>(),
-                            dFO.as<double>(), dChargeO.as<double>(), s);
-    else
-        launch_prepare(geo.N, dPerm.as<int>(), charge, dW.as<double>(), dFT.as<double>(), dFO.as<double>(), s);
-    const double* chargeO = treeIn ? dChargeO.as<double>() : charge;  // original order, for the corrections
     const int* operm = treeOut ? nullptr : dPerm.as<int>();
     const int64_t obase = treeOut ? plan.ownBegin : 0;
+    // up pass (global, every rank): tiers bottom-up; its P2M also forms the weighted
+    // charges fT (tree order) the near field and the corrections read
+    if (plan.upTierTask.size() < 2)  // a lone leaf: no up pass
+        launch_prepare(geo.N, charge, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(),
+                       dCT.as<double>(), s);
+    for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k)
+        launch_up_tier(plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask,
+                       dUpTaskPtr.as<int>(), dUpGrpPtr.as<int>(), dUpGrp.as<int>(), dUpNode.as<int>(),
+                       dUpCode.as<int4>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dNcx.as<double>(),
+                       dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(),
+                       charge, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(),
+                       dCT.as<double>(), P, dMult.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[1], s));
-    // The near field and the corrections need only the prepared charges: they run
-    // on the auxiliary stream, overlapping the latency-bound up pass and the M2L
-    // stream (both write `out`: near stores, corr adds; the down pass adds after
-    // the join).
+    // The near field and the corrections need only the weighted charges; with
+    // ANISO_OVERLAP=1 they run on the auxiliary stream beside the M2L stream (both
+    // write `out`: near stores, corr adds; the down pass adds after the join).
     hipStream_t sn = overlap ? aux : s;
     if (overlap) {
         HIP_CHECK(hipEventRecord(evFork, s));
@@ -392,17 +399,11 @@ void Operator::apply(const double* charge, bool treeIn, const double* sigT, int 
                 dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(), dFT.as<double>(), operm, obase,
                 maxNearS, mask, sgn, M_1_PI / 2.0, dNearPart.as<double>(), out, sn);
     if (tm) HIP_CHECK(hipEventRecord(ev[7], sn));
-    launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), chargeO, dFO.as<double>(), mc.C.as<double>(),
+    launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(), dFT.as<double>(),
+                mc.C.as<double>(),
                 mc.mu.as<double>(), P, mask, M_1_PI / 2.0, treeOut, out, sn);
     if (tm) HIP_CHECK(hipEventRecord(ev[8], sn));
     if (overlap) HIP_CHECK(hipEventRecord(evJoin, aux));
-    // up pass (global, every rank): tiers bottom-up
-    for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k)
-        launch_up_tier(plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask,
-                       dUpTaskPtr.as<int>(), dUpGrpPtr.as<int>(), dUpGrp.as<int>(), dUpNode.as<int>(),
-                       dUpCode.as<int4>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dNcx.as<double>(),
-                       dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(),
-                       dFT.as<double>(), P, dMult.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[2], s));
     if (mask & kStageFar)
         launch_m2l((int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(),
@@ -447,8 +448,7 @@ StageTimes Operator::stageTimes() {
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int k = 0; k < evUsed; ++k) {
         const auto& e = evPool[k];
-        acc[0] += el(e[0], e[1]);  // prep
-        acc[1] += el(overlap ? e[1] : e[8], e[2]);  // up (after near + corr when serialized)
+        acc[1] += el(e[0], e[1]);  // up, with the weighted charges (acc[0], prep, is fused into it)
         acc[2] += el(e[2], e[3]);  // m2l
         acc[3] += el(e[3], e[4]);  // gather
         acc[4] += el(e[6], e[7]);  // near (auxiliary stream)

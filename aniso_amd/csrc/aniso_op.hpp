@@ -111,8 +111,8 @@ private:
     DevBuf dM2LNDir, dM2LCanonBase, dM2LInPtr, dM2LOutSlot, dM2LPart;  // symmetric M2L
     DevBuf dNearSym, dNearPart, dDnLeafNear, dDnNearPtr, dDnNearOff;              // symmetric near field
     DevBuf dParams, dStCoef;
-    DevBuf dCharge, dOut, dFT, dFO, dMult, dLocal, dTotal, dSigmaS, dTmp, dTmp2;
-    DevBuf dWT, dSigmaT, dChargeO, dTmpS;  // tree-order path
+    DevBuf dCharge, dOut, dFT, dCT, dMult, dLocal, dTotal, dSigmaS, dTmp, dTmp2;
+    DevBuf dWT, dSigmaT, dIperm, dTmpS;  // tree-order path
     std::vector<ModeCache> modes;
 };
 

@@ -182,19 +182,24 @@ __device__ __forceinline__ int64_t out_index(const int* __restrict__ operm, int6
     return operm ? (int64_t)operm[k] : k - obase;
 }
 
-// Tree-order input: c = x_tree[k] (times sigma_s[k] in tree order when given);
-// fT[k] = c w_T[k]; the corrections read the original-order fO and charge.
-__global__ void k_prepare_tree(int64_t N, const int* __restrict__ perm, const double* __restrict__ xT,
-                               const double* __restrict__ sigT, const double* __restrict__ wT,
-                               const double* __restrict__ w, double* __restrict__ fT, double* __restrict__ fO,
-                               double* __restrict__ chargeO) {
+// Weighted charges in tree order: c = x_tree[k] (treeIn) or charge[perm[k]], times
+// sigma_s in tree order when given; fT[k] = c w_T[k] (FMM and stencil charges),
+// cT[k] = c (singular term).  The up pass does this inside its P2M; this kernel
+// covers a tree without up-pass tiers (a lone leaf).
+__device__ __forceinline__ double input_charge(const double* __restrict__ xin, int treeIn, const int* __restrict__ perm,
+                                               const double* __restrict__ sigT, int64_t k) {
+    const double c = treeIn ? xin[k] : xin[perm[k]];
+    return sigT ? c * sigT[k] : c;
+}
+
+__global__ void k_prepare(int64_t N, const double* __restrict__ xin, int treeIn, const int* __restrict__ perm,
+                          const double* __restrict__ sigT, const double* __restrict__ wT, double* __restrict__ fT,
+                          double* __restrict__ cT) {
     int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= N) return;
-    const double c = sigT ? xT[k] * sigT[k] : xT[k];
-    const int t = perm[k];
+    const double c = input_charge(xin, treeIn, perm, sigT, k);
     fT[k] = c * wT[k];
-    fO[t] = c * w[t];
-    chargeO[t] = c;
+    cT[k] = c;
 }
 
 // y = x - a on the owned tree slice (forward operator u - K(sigma_s u), main.cpp:125-136)
@@ -204,14 +209,6 @@ __global__ void k_sub_slice(int64_t n, const double* __restrict__ x, const doubl
     if (i < n) y[i] = x[i] - a[i];
 }
 
-__global__ void k_prepare(int64_t N, const int* __restrict__ perm, const double* __restrict__ charge,
-                          const double* __restrict__ w, double* __restrict__ fT, double* __restrict__ fO) {
-    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= N) return;
-    int t = perm[k];
-    fT[k] = charge[t] * w[t];
-    fO[k] = charge[k] * w[k];
-}
 
 // Up pass (bbfmm.h:825-861) as tiers of <= 4-level subtrees:
 // one workgroup per subtree keeps its nodes' multipoles in LDS, deepest level
@@ -226,8 +223,9 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
     const int* __restrict__ grp, const int* __restrict__ node, const int4* __restrict__ code,
     const int64_t* __restrict__ begin, const int64_t* __restrict__ count, const double* __restrict__ ncx,
     const double* __restrict__ ncy, const double* __restrict__ nrx, const double* __restrict__ nry,
-    const double* __restrict__ pxT, const double* __restrict__ pyT, const double* __restrict__ fT,
-    const Params* __restrict__ P, double* __restrict__ mult) {
+    const double* __restrict__ pxT, const double* __restrict__ pyT, const double* __restrict__ xin, int treeIn,
+    const int* __restrict__ perm, const double* __restrict__ sigT, const double* __restrict__ wT,
+    double* __restrict__ fT, double* __restrict__ cT, const Params* __restrict__ P, double* __restrict__ mult) {
     extern __shared__ double sm[];
     int4* CD = reinterpret_cast<int4*>(sm);             // maxTask child codes
     double* Rl = reinterpret_cast<double*>(CD + maxTask);  // 4 x 256 transfer matrices (transposed)
@@ -257,12 +255,10 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
     }
     __syncthreads();
     // each point is read once (lane per point, coalesced): no LDS staging
-    const double* xs = pxT + b0;
-    const double* ys = pyT + b0;
-    const double* fs = fT + b0;
     // P2M of the task's leaves (bbfmm.h:737-748): 16 lanes per leaf, one point per
     // lane per pass (its 16 products in registers), then a 16-lane reduce-scatter
-    // leaves lane l with entry l
+    // leaves lane l with entry l.  The weighted charges are formed here from the
+    // apply's input (the reference's charge .* weights, AnisoWrapper.cpp:105-110).
     {
         const int gi = threadIdx.x >> 4, ln = threadIdx.x & 15, ngrp = blockDim.x >> 4;
         for (int k = gi; k < nt; k += ngrp) {
@@ -273,10 +269,14 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
 #pragma unroll
             for (int e = 0; e < kRank; ++e) acc[e] = 0.0;
             for (int p = LB[k] + ln; p < pe; p += 16) {
+                const int64_t kp = b0 + p;
+                const double c = input_charge(xin, treeIn, perm, sigT, kp);
+                const double f = c * wT[kp];
+                fT[kp] = f;  // for k_near and the corrections
+                cT[kp] = c;
                 double Sx[kNP], Sy[kNP];
-                cheb_weights(P, (xs[p] - cx) * irx, Sx);
-                cheb_weights(P, (ys[p] - cy) * iry, Sy);
-                const double f = fs[p];
+                cheb_weights(P, (pxT[kp] - cx) * irx, Sx);
+                cheb_weights(P, (pyT[kp] - cy) * iry, Sy);
 #pragma unroll
                 for (int j = 0; j < kNP; ++j) {
                     const double sf = Sy[j] * f;
@@ -753,7 +753,8 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
 // stores its scaled sum, k_corr and k_down_tier add theirs, in any order.
 template <int D>
 __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* __restrict__ perm,
-                                              const double* __restrict__ charge, const double* __restrict__ fO,
+                                              const int* __restrict__ iperm, const double* __restrict__ cT,
+                                              const double* __restrict__ fT,
                                               const double* __restrict__ C, const double* __restrict__ mu,
                                               const Params* __restrict__ P, int flags, double scale,
                                               bool treeOut, double* __restrict__ out) {
@@ -774,17 +775,17 @@ __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* _
                 if (j + dc < 0 || j + dc >= sz) continue;
                 const int q9 = (dr + 1) * 3 + (dc + 1);
                 const double* w = C + ((size_t)tq * 9 + q9) * D2;
-                const double* f = fO + (size_t)(sq + dr * sz + dc) * D2;
+                const int* it = iperm + (size_t)(sq + dr * sz + dc) * D2;  // the square's points, tree positions
 #pragma unroll
-                for (int c = 0; c < D2; ++c) acc += w[c] * f[c];
+                for (int c = 0; c < D2; ++c) acc += w[c] * fT[it[c]];
             }
         }
     }
     if (flags & kStageSing) {
-        const double* h = charge + (size_t)sq * D2;
+        const int* it = iperm + (size_t)sq * D2;
         double hw[D2];
 #pragma unroll
-        for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * h[c];
+        for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cT[it[c]];
         const double X = (0.5 + i) * P->dx, Y = (0.5 + j) * P->dx;
         double bx[D][D], by[D][D];
 #pragma unroll
@@ -922,10 +923,10 @@ __global__ void k_line_integrals(int n, const double* __restrict__ seg, const do
 
 static inline unsigned blocks_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
-void launch_prepare(int64_t N, const int* perm, const double* charge, const double* w, double* fT, double* fO,
-                    hipStream_t s) {
+void launch_prepare(int64_t N, const double* xin, int treeIn, const int* perm, const double* sigT, const double* wT,
+                    double* fT, double* cT, hipStream_t s) {
     if (N <= 0) return;
-    k_prepare<<<blocks_for(N, 256), 256, 0, s>>>(N, perm, charge, w, fT, fO);
+    k_prepare<<<blocks_for(N, 256), 256, 0, s>>>(N, xin, treeIn, perm, sigT, wT, fT, cT);
     HIP_LAUNCH_CHECK();
 }
 
@@ -942,11 +943,12 @@ size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear) {
 void launch_up_tier(int ntask, int taskBase, int maxTask, const int* taskPtr, const int* grpPtr,
                     const int* grp, const int* node, const int4* code, const int64_t* begin, const int64_t* count,
                     const double* ncx, const double* ncy, const double* nrx, const double* nry, const double* pxT,
-                    const double* pyT, const double* fT, const Params* P, double* mult, hipStream_t s) {
+                    const double* pyT, const double* xin, int treeIn, const int* perm, const double* sigT,
+                    const double* wT, double* fT, double* cT, const Params* P, double* mult, hipStream_t s) {
     if (ntask <= 0) return;
     k_up_tier<<<ntask, kTierThreads, up_tier_lds(maxTask), s>>>(
-        taskBase, maxTask, taskPtr, grpPtr, grp, node, code, begin, count, ncx, ncy, nrx, nry, pxT, pyT, fT,
-        P, mult);
+        taskBase, maxTask, taskPtr, grpPtr, grp, node, code, begin, count, ncx, ncy, nrx, nry, pxT, pyT, xin, treeIn,
+        perm, sigT, wT, fT, cT, P, mult);
     HIP_LAUNCH_CHECK();
 }
 
@@ -993,18 +995,19 @@ void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const
     HIP_LAUNCH_CHECK();
 }
 
-void launch_corr(int d, int64_t b, int64_t e, const int* perm, const double* charge, const double* fO, const double* C,
+void launch_corr(int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT, const double* fT,
+                 const double* C,
                  const double* mu, const Params* P, int flags, double scale, bool treeOut, double* out,
                  hipStream_t s) {
     if (e <= b) return;
     unsigned nb = blocks_for(e - b, 256);
     switch (d) {
-        case 1: k_corr<1><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
-        case 2: k_corr<2><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
-        case 3: k_corr<3><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
-        case 4: k_corr<4><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
-        case 5: k_corr<5><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
-        case 6: k_corr<6><<<nb, 256, 0, s>>>(b, e, perm, charge, fO, C, mu, P, flags, scale, treeOut, out); break;
+        case 1: k_corr<1><<<nb, 256, 0, s>>>(b, e, perm, iperm, cT, fT, C, mu, P, flags, scale, treeOut, out); break;
+        case 2: k_corr<2><<<nb, 256, 0, s>>>(b, e, perm, iperm, cT, fT, C, mu, P, flags, scale, treeOut, out); break;
+        case 3: k_corr<3><<<nb, 256, 0, s>>>(b, e, perm, iperm, cT, fT, C, mu, P, flags, scale, treeOut, out); break;
+        case 4: k_corr<4><<<nb, 256, 0, s>>>(b, e, perm, iperm, cT, fT, C, mu, P, flags, scale, treeOut, out); break;
+        case 5: k_corr<5><<<nb, 256, 0, s>>>(b, e, perm, iperm, cT, fT, C, mu, P, flags, scale, treeOut, out); break;
+        case 6: k_corr<6><<<nb, 256, 0, s>>>(b, e, perm, iperm, cT, fT, C, mu, P, flags, scale, treeOut, out); break;
         default: throw_hip(hipErrorInvalidValue, __FILE__, __LINE__);
     }
     HIP_LAUNCH_CHECK();
@@ -1029,12 +1032,6 @@ void launch_cache_near(int nl, const int* leaves, const int64_t* nearPtr, const 
     HIP_LAUNCH_CHECK();
 }
 
-void launch_prepare_tree(int64_t N, const int* perm, const double* xT, const double* sigT, const double* wT,
-                         const double* w, double* fT, double* fO, double* chargeO, hipStream_t s) {
-    if (N <= 0) return;
-    k_prepare_tree<<<blocks_for(N, 256), 256, 0, s>>>(N, perm, xT, sigT, wT, w, fT, fO, chargeO);
-    HIP_LAUNCH_CHECK();
-}
 
 void launch_sub_slice(int64_t n, const double* x, const double* a, double* y, hipStream_t s) {
     if (n <= 0) return;

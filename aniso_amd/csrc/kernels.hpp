@@ -34,15 +34,16 @@ enum StageMask : int {
     kStageAll = 15,
 };
 
-void launch_prepare(int64_t N, const int* perm, const double* charge, const double* w, double* fT, double* fO,
-                    hipStream_t s);
+void launch_prepare(int64_t N, const double* xin, int treeIn, const int* perm, const double* sigT, const double* wT,
+                    double* fT, double* cT, hipStream_t s);
 constexpr int kTierThreads = 512;  // workgroup of the up / down pass tiers
 size_t up_tier_lds(int maxTask);
 size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear);
 void launch_up_tier(int ntask, int taskBase, int maxTask, const int* taskPtr, const int* grpPtr,
                     const int* grp, const int* node, const int4* code, const int64_t* begin, const int64_t* count,
                     const double* ncx, const double* ncy, const double* nrx, const double* nry, const double* pxT,
-                    const double* pyT, const double* fT, const Params* P, double* mult, hipStream_t s);
+                    const double* pyT, const double* xin, int treeIn, const int* perm, const double* sigT,
+                    const double* wT, double* fT, double* cT, const Params* P, double* mult, hipStream_t s);
 void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
                 const int* outSlot, const int* src, const double* K, const double* mult, double sgn, double* partial,
                 double* local, hipStream_t s);
@@ -61,11 +62,10 @@ void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const
                       const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
                       const int* operm, int64_t obase, const int2* leafNear, const int* nearPtr, const int* nearOff,
                       int maxNear, const double* nearPart, int flags, double scale, double* out, hipStream_t s);
-void launch_corr(int d, int64_t b, int64_t e, const int* perm, const double* charge, const double* fO, const double* C,
+void launch_corr(int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT, const double* fT,
+                 const double* C,
                  const double* mu, const Params* P, int flags, double scale, bool treeOut, double* out,
                  hipStream_t s);
-void launch_prepare_tree(int64_t N, const int* perm, const double* xT, const double* sigT, const double* wT,
-                         const double* w, double* fT, double* fO, double* chargeO, hipStream_t s);
 void launch_sub_slice(int64_t n, const double* x, const double* a, double* y, hipStream_t s);
 void launch_cache_m2l(int64_t npairs, const int* pairTgt, const int* src, const double* ncx, const double* ncy,
                       const double* nrx, const double* nry, const double* stcoef, const Params* P, int mode,
