@@ -230,6 +230,8 @@ void Operator::uploadPlan() {
     for (size_t i = 0; i < ns.size(); ++i) ns[i] = make_int2(plan.nearSym[i][0], plan.nearSym[i][1]);
     up(dNearSym, ns);
     up(dDnLeafNear, plan.dnLeafNear);
+    up(dDnChainPtr, plan.dnChainPtr);
+    up(dDnChain, plan.dnChain);
     up(dDnNearPtr, plan.dnNearPtr);
     up(dDnNearOff, plan.dnNearOff);
     dNearPart.alloc((size_t)std::max<int64_t>(plan.nearPartTotal, 1) * sizeof(double));
@@ -256,7 +258,7 @@ void Operator::uploadPlan() {
     up(dDnLeafPts, plan.dnLeafPts);
     up(dDnPtsRange, plan.dnPtsRange);
     // a task's expansions live in LDS (<= 4 levels: 85 nodes); a workgroup may use all 160 KiB
-    if (up_tier_lds(plan.upMaxTask) > 160 * 1024 || down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, plan.dnMaxNear) > 160 * 1024)
+    if (up_tier_lds(plan.upMaxTask) > 160 * 1024 || down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, plan.dnMaxNear, plan.dnMaxChain) > 160 * 1024)
         throw std::logic_error("up/down pass task exceeds one workgroup's LDS");
     maxNearS = 1;
     for (size_t li = 0; li < plan.leaves.size(); ++li) {
@@ -426,8 +428,8 @@ void Operator::apply(const double* charge, bool treeIn, const double* sigT, int 
                              dDnLeafSlot.as<int>(), dDnLeafIdx.as<int>(), dDnLeafPts.as<int>(), dDnPtsRange.as<int2>(),
                              dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(),
                              dPxT.as<double>(), dPyT.as<double>(), operm, obase, dDnLeafNear.as<int2>(),
-                             dDnNearPtr.as<int>(), dDnNearOff.as<int>(), plan.dnMaxNear, dNearPart.as<double>(), mask,
-                             M_1_PI / 2.0, out, s);
+                             dDnNearPtr.as<int>(), dDnNearOff.as<int>(), plan.dnMaxNear, dNearPart.as<double>(),
+                             dDnChainPtr.as<int>(), dDnChain.as<int2>(), plan.dnMaxChain, mask, M_1_PI / 2.0, out, s);
     if (tm) HIP_CHECK(hipEventRecord(ev[5], s));
 }
 

@@ -109,7 +109,7 @@ private:
     DevBuf dDnTaskPtr, dDnGrpPtr, dDnGrp, dDnNode, dDnLeafPtr, dDnLeafSlot, dDnLeafIdx, dDnLeafPts, dDnPtsRange;  // down
     DevBuf dLeafInfo, dNearPtsPtr, dNearPts;
     DevBuf dM2LNDir, dM2LCanonBase, dM2LInPtr, dM2LOutSlot, dM2LPart;  // symmetric M2L
-    DevBuf dNearSym, dNearPart, dDnLeafNear, dDnNearPtr, dDnNearOff;              // symmetric near field
+    DevBuf dNearSym, dNearPart, dDnLeafNear, dDnNearPtr, dDnNearOff, dDnChainPtr, dDnChain;              // symmetric near field
     DevBuf dParams, dStCoef;
     DevBuf dCharge, dOut, dFT, dCT, dMult, dLocal, dTotal, dSigmaS, dTmp, dTmp2;
     DevBuf dWT, dSigmaT, dIperm, dTmpS;  // tree-order path

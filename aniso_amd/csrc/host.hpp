@@ -89,8 +89,9 @@ struct Plan {
     std::vector<int> upTierTask, upTaskPtr, upGrpPtr, upGrp, upNode;
     std::vector<std::array<int, 4>> upCode;
     int upMaxTask = 1;
-    // down (owned part; tiers top-down): dnNode = (node, parent code, child slot
-    // (R index), 0); leaves of each task in tree order (L2P + near gather)
+    // down (owned part): tasks with owned leaves, all tiers in one launch; dnNode =
+    // (node, parent code: LDS slot, -1 none/zero, -2 the task root (chain total);
+    // child slot (R index), 0); leaves of each task in tree order (L2P + near gather)
     std::vector<int> dnTierTask, dnTaskPtr, dnGrpPtr, dnGrp;
     std::vector<std::array<int, 4>> dnNode;
     std::vector<int> dnLeafPtr, dnLeafSlot, dnLeafIdx, dnLeafPts;  // leaves in tree order; dnLeafPts = begin
@@ -98,6 +99,9 @@ struct Plan {
     std::vector<std::array<int, 2>> dnLeafNear;  // per leaf entry: (first, count) in its task's dnNearOff
     std::vector<int> dnNearPtr, dnNearOff;       // per task: the near partial offsets of its leaves
     int dnMaxNear = 1;
+    std::vector<int> dnChainPtr;                 // per task: its root's ancestors below the tree root,
+    std::vector<std::array<int, 2>> dnChain;     // top-down (node, child slot): the parent total's L2L chain
+    int dnMaxChain = 1;
     int dnMaxTask = 1, dnMaxLeaves = 1;
     int64_t pairsNear = 0, pairsM2L = 0;       // kernel entries per apply
 

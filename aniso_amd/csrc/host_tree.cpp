@@ -485,20 +485,36 @@ void Plan::buildDownTasks(const Tree& t) {
     dnPtsRange.clear();
     dnMaxTask = 1;
     dnMaxLeaves = 1;
+    // Every task with owned leaves is independent: it rebuilds its root's parent
+    // total from the ancestors' locals (L2L chain from level 1; the root's total is
+    // zero), so the tasks of all tiers go in ONE launch and leafless tasks are dropped.
+    dnChainPtr.assign(1, 0);
+    dnChain.clear();
+    dnMaxChain = 1;
+    std::vector<int> anc;
     for (int k = (int)tierRootLevel.size() - 1; k >= 0; --k) {  // top-down
         for (int r = 0; r < t.nn; ++r) {
             if (t.level[r] != tierRootLevel[k] || !keep(r)) continue;
             auto lv = task_levels(t, r, tierBottomLevel[k], keep);
+            bool hasLeaf = false;
+            for (auto& level : lv)
+                for (int n : level) hasLeaf |= leafOf[n] >= 0;
+            if (!hasLeaf) continue;
             const int base = (int)dnNode.size();
             for (auto& level : lv) {  // shallowest level first
                 dnGrp.push_back((int)dnNode.size());
                 for (int n : level) {
                     slotOf[n] = (int)dnNode.size() - base;
                     const int p = t.parent[n];  // the root's total is zero
-                    const int pc = (p < 0 || t.parent[p] < 0) ? -1 : n == r ? -(p + 2) : slotOf[p];
+                    const int pc = (p < 0 || t.parent[p] < 0) ? -1 : n == r ? -2 : slotOf[p];
                     dnNode.push_back({n, pc, t.slot[n], 0});
                 }
             }
+            anc.clear();  // ancestors of r below the root, top-down
+            for (int a = t.parent[r]; a >= 0 && t.parent[a] >= 0; a = t.parent[a]) anc.push_back(a);
+            for (auto it = anc.rbegin(); it != anc.rend(); ++it) dnChain.push_back({*it, t.slot[*it]});
+            dnChainPtr.push_back((int)dnChain.size());
+            dnMaxChain = std::max(dnMaxChain, (int)anc.size());
             const int nearBase = (int)dnNearOff.size();
             // owned leaves in tree order: they tile [ptsBegin, ptsEnd) contiguously
             std::vector<int> lf;
@@ -528,8 +544,8 @@ void Plan::buildDownTasks(const Tree& t) {
             dnMaxTask = std::max(dnMaxTask, (int)dnNode.size() - base);
             dnMaxLeaves = std::max(dnMaxLeaves, nl);
         }
-        dnTierTask.push_back((int)dnTaskPtr.size() - 1);
     }
+    dnTierTask.push_back((int)dnTaskPtr.size() - 1);  // one launch
     dnGrp.push_back((int)dnNode.size());
 }
 

@@ -647,13 +647,15 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     const double* __restrict__ nrx, const double* __restrict__ nry, const double* __restrict__ pxT,
     const double* __restrict__ pyT, const int* __restrict__ operm, int64_t obase, const int2* __restrict__ leafNear,
     const int* __restrict__ nearPtr, const int* __restrict__ nearOff, int maxNear, const double* __restrict__ nearPart,
-    int flags, double scale, double* __restrict__ out) {
+    const int* __restrict__ chainPtr, const int2* __restrict__ chain, int maxChain, int flags, double scale,
+    double* __restrict__ out) {
     extern __shared__ double sm[];
     int4* DN = reinterpret_cast<int4*>(sm);             // maxTask node records
     double* Rl = reinterpret_cast<double*>(DN + maxTask);  // 4 x 256 transfer matrices
     double* T = Rl + 4 * kRank * kRank;                 // maxTask x 16 totals
     double* PT = T + (size_t)maxTask * kRank;           // 16: the task root's parent total
-    double* G = PT + kRank;                             // maxLeaves x 4: leaf cx, cy, 1/rx, 1/ry
+    double* CH = PT + kRank;                            // maxChain x 16: the ancestors' locals
+    double* G = CH + (size_t)maxChain * kRank;          // maxLeaves x 4: leaf cx, cy, 1/rx, 1/ry
     int* LB = reinterpret_cast<int*>(G + (size_t)maxLeaves * 4);  // maxLeaves + 1: leaf begins (tree positions)
     int* LS = LB + maxLeaves + 1;                       // maxLeaves: leaf slot in the task
     int* NB = LS + maxLeaves;                           // maxLeaves: first of the leaf's near offsets in NO
@@ -673,10 +675,9 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             const int k = it >> 4, r = it & (kRank - 1);
             T[it] = local[(size_t)dn[n0 + k].x * kRank + r];
         }
-        if (threadIdx.x < kRank) {
-            const int pc = dn[n0].y;
-            PT[threadIdx.x] = pc <= -2 ? total[(size_t)(-pc - 2) * kRank + threadIdx.x] : 0.0;
-        }
+        const int c0 = chainPtr[task], nc = chainPtr[task + 1] - c0;
+        for (int it = threadIdx.x; it < nc * kRank; it += blockDim.x)
+            CH[it] = local[(size_t)chain[c0 + (it >> 4)].x * kRank + (it & (kRank - 1))];
     }
     for (int e = threadIdx.x; e < nl; e += blockDim.x) {
         LB[e] = leafBegin[l0 + e];
@@ -693,15 +694,29 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     if (threadIdx.x == 0) LB[nl] = pr.y;
     for (int j = nearPtr[task] + threadIdx.x; j < nearPtr[task + 1]; j += blockDim.x) NO[j - nearPtr[task]] = nearOff[j];
     __syncthreads();
-    // ---- phase 1: L2L level by level (shallowest first), out of LDS
+    // ---- phase 1: the root's parent total by the L2L chain from level 1 (one
+    // 16-lane group; bbfmm.h:1070-1071 along the ancestors), then the task's levels
     if (far) {
+        if (threadIdx.x < kRank) {
+            const int r = threadIdx.x, c0 = chainPtr[task], nc = chainPtr[task + 1] - c0;
+            double v = nc > 0 ? CH[r] : 0.0;
+            for (int j = 1; j < nc; ++j) {
+                const double* R = Rl + chain[c0 + j].y * kRank * kRank;
+                double a = CH[j * kRank + r];
+#pragma unroll
+                for (int c = 0; c < kRank; ++c) a += R[r + c * kRank] * __shfl(v, c, kRank);
+                v = a;
+            }
+            PT[r] = v;
+        }
+        __syncthreads();
         for (int g = grpPtr[task]; g < grpPtr[task + 1]; ++g) {
             const int s0 = grp[g] - n0, s1 = grp[g + 1] - n0;
             for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
                 const int k = s0 + (it >> 4), r = it & (kRank - 1);
                 const int4 d = DN[k];
                 if (d.y == -1) continue;
-                const double* pt = d.y >= 0 ? T + (size_t)d.y * kRank : PT;
+                const double* pt = d.y >= 0 ? T + (size_t)d.y * kRank : PT;  // -2: the task root
                 const double* R = Rl + d.z * kRank * kRank;
                 double l2l = 0.0;
 #pragma unroll
@@ -710,8 +725,6 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             }
             __syncthreads();
         }
-        for (int it = threadIdx.x; it < nt * kRank; it += blockDim.x)
-            total[(size_t)DN[it >> 4].x * kRank + (it & (kRank - 1))] = T[it];
     }
     // ---- phase 2: owned points: L2P + near gather
     for (int g = threadIdx.x; g < npts; g += blockDim.x) {
@@ -935,8 +948,8 @@ size_t up_tier_lds(int maxTask) {
            (size_t)maxTask * sizeof(int4);
 }
 
-size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear) {
-    return (size_t)(4 * kRank * kRank + maxTask * kRank + kRank + 4 * maxLeaves) * sizeof(double) +
+size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain) {
+    return (size_t)(4 * kRank * kRank + maxTask * kRank + kRank + maxChain * kRank + 4 * maxLeaves) * sizeof(double) +
            (size_t)(4 * maxLeaves + 4 + maxNear) * sizeof(int) + (size_t)maxTask * sizeof(int4);
 }
 
@@ -986,12 +999,13 @@ void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const
                       const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
                       const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
                       const int* operm, int64_t obase, const int2* leafNear, const int* nearPtr, const int* nearOff,
-                      int maxNear, const double* nearPart, int flags, double scale, double* out, hipStream_t s) {
+                      int maxNear, const double* nearPart, const int* chainPtr, const int2* chain, int maxChain,
+                      int flags, double scale, double* out, hipStream_t s) {
     if (ntask <= 0) return;
-    k_down_tier<<<ntask, kTierThreads, down_tier_lds(maxTask, maxLeaves, maxNear), s>>>(
+    k_down_tier<<<ntask, kTierThreads, down_tier_lds(maxTask, maxLeaves, maxNear, maxChain), s>>>(
         taskBase, maxTask, maxLeaves, taskPtr, grpPtr, grp, dn, slot, local, m2lPart, P, total, leafPtr,
         leafSlot, leafIdx, leafBegin, ptsRange, ncx, ncy, nrx, nry, pxT, pyT, operm, obase, leafNear, nearPtr, nearOff,
-        maxNear, nearPart, flags, scale, out);
+        maxNear, nearPart, chainPtr, chain, maxChain, flags, scale, out);
     HIP_LAUNCH_CHECK();
 }
 

@@ -38,7 +38,7 @@ void launch_prepare(int64_t N, const double* xin, int treeIn, const int* perm, c
                     double* fT, double* cT, hipStream_t s);
 constexpr int kTierThreads = 512;  // workgroup of the up / down pass tiers
 size_t up_tier_lds(int maxTask);
-size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear);
+size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain);
 void launch_up_tier(int ntask, int taskBase, int maxTask, const int* taskPtr, const int* grpPtr,
                     const int* grp, const int* node, const int4* code, const int64_t* begin, const int64_t* count,
                     const double* ncx, const double* ncy, const double* nrx, const double* nry, const double* pxT,
@@ -61,7 +61,8 @@ void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const
                       const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
                       const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
                       const int* operm, int64_t obase, const int2* leafNear, const int* nearPtr, const int* nearOff,
-                      int maxNear, const double* nearPart, int flags, double scale, double* out, hipStream_t s);
+                      int maxNear, const double* nearPart, const int* chainPtr, const int2* chain, int maxChain,
+                      int flags, double scale, double* out, hipStream_t s);
 void launch_corr(int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT, const double* fT,
                  const double* C,
                  const double* mu, const Params* P, int flags, double scale, bool treeOut, double* out,
