@@ -208,6 +208,12 @@ void Operator::ensureDevice() {
     uploadPlan();
 }
 
+static std::vector<int4> to_int4(const std::vector<std::array<int, 4>>& v) {
+    std::vector<int4> o(v.size());
+    for (size_t i = 0; i < v.size(); ++i) o[i] = make_int4(v[i][0], v[i][1], v[i][2], v[i][3]);
+    return o;
+}
+
 void Operator::uploadPlan() {
     up(dLeaves, plan.leaves);
     up(dNearPtr, plan.nearPtr);
@@ -230,16 +236,14 @@ void Operator::uploadPlan() {
     for (size_t i = 0; i < ns.size(); ++i) ns[i] = make_int2(plan.nearSym[i][0], plan.nearSym[i][1]);
     up(dNearSym, ns);
     up(dDnLeafNear, plan.dnLeafNear);
+    up(dDnDesc, to_int4(plan.dnDesc));
+    up(dDnGrpFix, plan.dnGrpFix);
+    up(dDnLeafGeom, plan.dnLeafGeom);
     up(dDnChainPtr, plan.dnChainPtr);
     up(dDnChain, plan.dnChain);
     up(dDnNearPtr, plan.dnNearPtr);
     up(dDnNearOff, plan.dnNearOff);
     dNearPart.alloc((size_t)std::max<int64_t>(plan.nearPartTotal, 1) * sizeof(double));
-    auto to_int4 = [](const std::vector<std::array<int, 4>>& v) {
-        std::vector<int4> o(v.size());
-        for (size_t i = 0; i < v.size(); ++i) o[i] = make_int4(v[i][0], v[i][1], v[i][2], v[i][3]);
-        return o;
-    };
     up(dLeafInfo, to_int4(plan.leafInfo));
     up(dNearPtsPtr, plan.nearPtsPtr);
     up(dNearPts, plan.nearPts);
@@ -248,6 +252,10 @@ void Operator::uploadPlan() {
     up(dUpGrp, plan.upGrp);
     up(dUpNode, plan.upNode);
     up(dUpCode, to_int4(plan.upCode));
+    up(dUpDesc, to_int4(plan.upDesc));
+    up(dUpGrpFix, plan.upGrpFix);
+    up(dUpGeom, plan.upGeom);
+    up(dUpLeaf, plan.upLeaf);
     up(dDnTaskPtr, plan.dnTaskPtr);
     up(dDnGrpPtr, plan.dnGrpPtr);
     up(dDnGrp, plan.dnGrp);
@@ -380,10 +388,9 @@ void Operator::apply(const double* charge, bool treeIn, const double* sigT, int 
                        dCT.as<double>(), s);
     for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k)
         launch_up_tier(plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask,
-                       dUpTaskPtr.as<int>(), dUpGrpPtr.as<int>(), dUpGrp.as<int>(), dUpNode.as<int>(),
-                       dUpCode.as<int4>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dNcx.as<double>(),
-                       dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(),
-                       charge, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(),
+                       dUpDesc.as<int4>(), dUpGrpFix.as<int>(), dUpNode.as<int>(), dUpCode.as<int4>(),
+                       dUpGeom.as<double4>(), dUpLeaf.as<int2>(), dPxT.as<double>(), dPyT.as<double>(), charge,
+                       treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(),
                        dCT.as<double>(), P, dMult.as<double>(), s);
     if (tm) HIP_CHECK(hipEventRecord(ev[1], s));
     // The near field and the corrections need only the weighted charges; with
@@ -420,16 +427,11 @@ void Operator::apply(const double* charge, bool treeIn, const double* sigT, int 
     if (tm) HIP_CHECK(hipEventRecord(ev[9], s));
     // down pass (owned part): tiers top-down; L2L + L2P + gathered transposed near products
     if (mask & (kStageFar | kStageNear))
-        for (size_t k = 0; k + 1 < plan.dnTierTask.size(); ++k)
-            launch_down_tier(plan.dnTierTask[k + 1] - plan.dnTierTask[k], plan.dnTierTask[k], plan.dnMaxTask,
-                             plan.dnMaxLeaves, dDnTaskPtr.as<int>(), dDnGrpPtr.as<int>(),
-                             dDnGrp.as<int>(), dDnNode.as<int4>(), dSlot.as<int>(), dLocal.as<double>(),
-                             dM2LPart.as<double>(), P, dTotal.as<double>(), dDnLeafPtr.as<int>(),
-                             dDnLeafSlot.as<int>(), dDnLeafIdx.as<int>(), dDnLeafPts.as<int>(), dDnPtsRange.as<int2>(),
-                             dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(),
-                             dPxT.as<double>(), dPyT.as<double>(), operm, obase, dDnLeafNear.as<int2>(),
-                             dDnNearPtr.as<int>(), dDnNearOff.as<int>(), plan.dnMaxNear, dNearPart.as<double>(),
-                             dDnChainPtr.as<int>(), dDnChain.as<int2>(), plan.dnMaxChain, mask, M_1_PI / 2.0, out, s);
+        launch_down_tier((int)plan.dnDesc.size() / 3, plan.dnMaxTask, plan.dnMaxLeaves, dDnDesc.as<int4>(),
+                         dDnGrpFix.as<int>(), dDnNode.as<int4>(), dLocal.as<double>(), P, dDnLeafSlot.as<int>(),
+                         dDnLeafPts.as<int>(), dDnLeafNear.as<int2>(), dDnLeafGeom.as<double4>(), dPxT.as<double>(),
+                         dPyT.as<double>(), operm, obase, dDnNearOff.as<int>(), plan.dnMaxNear,
+                         dNearPart.as<double>(), dDnChain.as<int2>(), plan.dnMaxChain, mask, M_1_PI / 2.0, out, s);
     if (tm) HIP_CHECK(hipEventRecord(ev[5], s));
 }
 

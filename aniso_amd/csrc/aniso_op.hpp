@@ -105,8 +105,8 @@ private:
     // geometry / tree on device
     DevBuf dPxT, dPyT, dPerm, dW, dNcx, dNcy, dNrx, dNry, dBegin, dCount, dParent, dSlot, dChild, dIsLeaf;
     DevBuf dLeaves, dNearPtr, dNearSrc, dNearKOff, dM2LTgt, dM2LPtr, dM2LSrc, dM2LPairTgt;
-    DevBuf dUpTaskPtr, dUpGrpPtr, dUpGrp, dUpNode, dUpCode;                       // up-pass tiers
-    DevBuf dDnTaskPtr, dDnGrpPtr, dDnGrp, dDnNode, dDnLeafPtr, dDnLeafSlot, dDnLeafIdx, dDnLeafPts, dDnPtsRange;  // down
+    DevBuf dUpTaskPtr, dUpGrpPtr, dUpGrp, dUpNode, dUpCode, dUpDesc, dUpGrpFix, dUpGeom, dUpLeaf;                       // up-pass tiers
+    DevBuf dDnTaskPtr, dDnGrpPtr, dDnGrp, dDnNode, dDnLeafPtr, dDnLeafSlot, dDnLeafIdx, dDnLeafPts, dDnPtsRange, dDnDesc, dDnGrpFix, dDnLeafGeom;  // down
     DevBuf dLeafInfo, dNearPtsPtr, dNearPts;
     DevBuf dM2LNDir, dM2LCanonBase, dM2LInPtr, dM2LOutSlot, dM2LPart;  // symmetric M2L
     DevBuf dNearSym, dNearPart, dDnLeafNear, dDnNearPtr, dDnNearOff, dDnChainPtr, dDnChain;              // symmetric near field

@@ -14,6 +14,7 @@ namespace aniso {
 
 constexpr double kEps = 1e-12;  // bbfmm/utils.h:46
 constexpr int kLeafCode = -2147483647 - 1;  // upCode of a leaf (P2M from its points)
+constexpr int kTaskLevels = 7;  // levels per up/down task record (tasks span <= 4)
 constexpr int kMaxCanon = 32;   // canonical (symmetric) M2L pairs per target: k_m2l's LDS staging
 
 // Geometry::Geometry (Geometry.cpp:10-114) + the singular Duffy rule
@@ -89,6 +90,13 @@ struct Plan {
     std::vector<int> upTierTask, upTaskPtr, upGrpPtr, upGrp, upNode;
     std::vector<std::array<int, 4>> upCode;
     int upMaxTask = 1;
+    // the same, as records the kernel loads in one round: per task (first node,
+    // nodes, first point, levels) + kTaskLevels+1 level starts; per node the box
+    // (cx, cy, 1/rx, 1/ry) and the point range relative to the task's first point
+    std::vector<std::array<int, 4>> upDesc;
+    std::vector<int> upGrpFix;
+    std::vector<std::array<double, 4>> upGeom;
+    std::vector<std::array<int, 2>> upLeaf;
     // down (owned part): tasks with owned leaves, all tiers in one launch; dnNode =
     // (node, parent code: LDS slot, -1 none/zero, -2 the task root (chain total);
     // child slot (R index), 0); leaves of each task in tree order (L2P + near gather)
@@ -102,6 +110,11 @@ struct Plan {
     std::vector<int> dnChainPtr;                 // per task: its root's ancestors below the tree root,
     std::vector<std::array<int, 2>> dnChain;     // top-down (node, child slot): the parent total's L2L chain
     int dnMaxChain = 1;
+    // per task three int4 records (nodes, leaves / owned points, chain / near
+    // offsets, levels) + kTaskLevels+1 level starts; per leaf entry its box
+    std::vector<std::array<int, 4>> dnDesc;
+    std::vector<int> dnGrpFix;
+    std::vector<std::array<double, 4>> dnLeafGeom;
     int dnMaxTask = 1, dnMaxLeaves = 1;
     int64_t pairsNear = 0, pairsM2L = 0;       // kernel entries per apply
 

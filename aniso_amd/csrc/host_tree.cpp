@@ -430,6 +430,10 @@ void Plan::buildUpTasks(const Tree& t) {
     upGrp.clear();
     upNode.clear();
     upCode.clear();
+    upDesc.clear();
+    upGrpFix.clear();
+    upGeom.clear();
+    upLeaf.clear();
     upMaxTask = 1;
     for (size_t k = 0; k < tierRootLevel.size(); ++k) {  // bottom-up
         for (int r = 0; r < t.nn; ++r) {
@@ -454,6 +458,20 @@ void Plan::buildUpTasks(const Tree& t) {
                                                                    : -(ch + 2);  // root of the tier below
                     }
                 upCode.push_back(c);
+            }
+            // per-task record and per-node records (one round of independent loads)
+            const int nt = (int)upNode.size() - base, ng = (int)lv.size();
+            if (ng > kTaskLevels) throw std::logic_error("up task deeper than its record");
+            const int64_t b0 = t.begin[r];
+            upDesc.push_back({base, nt, (int)b0, ng});
+            std::array<int, kTaskLevels + 1> gs{};
+            for (int g = 0; g < ng; ++g) gs[g] = upGrp[upGrp.size() - ng + g] - base;
+            gs[ng] = nt;
+            upGrpFix.insert(upGrpFix.end(), gs.begin(), gs.end());
+            for (int i = base; i < (int)upNode.size(); ++i) {
+                const int n = upNode[i];
+                upGeom.push_back({t.ncx[n], t.ncy[n], 1.0 / t.nrx[n], 1.0 / t.nry[n]});
+                upLeaf.push_back({(int)(t.begin[n] - b0), (int)t.count[n]});
             }
             upGrpPtr.push_back((int)upGrp.size());
             upTaskPtr.push_back((int)upNode.size());
@@ -483,6 +501,9 @@ void Plan::buildDownTasks(const Tree& t) {
     dnNearPtr.assign(1, 0);
     dnMaxNear = 1;
     dnPtsRange.clear();
+    dnDesc.clear();
+    dnGrpFix.clear();
+    dnLeafGeom.clear();
     dnMaxTask = 1;
     dnMaxLeaves = 1;
     // Every task with owned leaves is independent: it rebuilds its root's parent
@@ -535,6 +556,21 @@ void Plan::buildDownTasks(const Tree& t) {
                 dnNearOff.insert(dnNearOff.end(), nearInOff.begin() + nearInPtr[li], nearInOff.begin() + nearInPtr[li + 1]);
             }
             const int nl = (int)lf.size();
+            for (int sl : lf) {
+                const int n = dnNode[base + sl][0];
+                dnLeafGeom.push_back({t.ncx[n], t.ncy[n], 1.0 / t.nrx[n], 1.0 / t.nry[n]});
+            }
+            const int ng = (int)lv.size();
+            if (ng > kTaskLevels) throw std::logic_error("down task deeper than its record");
+            const int nt = (int)dnNode.size() - base;
+            dnDesc.push_back({base, nt, (int)dnLeafSlot.size() - nl, nl});
+            dnDesc.push_back({(int)std::max<int64_t>(pb, 0), (int)std::max<int64_t>(pe, 0),
+                              dnChainPtr[dnChainPtr.size() - 2], (int)anc.size()});
+            dnDesc.push_back({nearBase, (int)dnNearOff.size() - nearBase, ng, 0});
+            std::array<int, kTaskLevels + 1> gs{};
+            for (int g = 0; g < ng; ++g) gs[g] = dnGrp[dnGrp.size() - ng + g] - base;
+            gs[ng] = nt;
+            dnGrpFix.insert(dnGrpFix.end(), gs.begin(), gs.end());
             dnPtsRange.push_back({(int)std::max<int64_t>(pb, 0), (int)std::max<int64_t>(pe, 0)});
             dnLeafPtr.push_back((int)dnLeafSlot.size());
             dnNearPtr.push_back((int)dnNearOff.size());

@@ -219,24 +219,25 @@ __global__ void k_sub_slice(int64_t n, const double* __restrict__ x, const doubl
 // one round of independent loads; the levels then run out of LDS.
 // One thread per (node, entry r), r = 4j + i:  M[r] = sum_p S(x_p, c_i) S(y_p, c_j) f_p.
 __global__ void __launch_bounds__(kTierThreads) k_up_tier(
-    int taskBase, int maxTask, const int* __restrict__ taskPtr, const int* __restrict__ grpPtr,
-    const int* __restrict__ grp, const int* __restrict__ node, const int4* __restrict__ code,
-    const int64_t* __restrict__ begin, const int64_t* __restrict__ count, const double* __restrict__ ncx,
-    const double* __restrict__ ncy, const double* __restrict__ nrx, const double* __restrict__ nry,
-    const double* __restrict__ pxT, const double* __restrict__ pyT, const double* __restrict__ xin, int treeIn,
-    const int* __restrict__ perm, const double* __restrict__ sigT, const double* __restrict__ wT,
-    double* __restrict__ fT, double* __restrict__ cT, const Params* __restrict__ P, double* __restrict__ mult) {
+    int taskBase, int maxTask, const int4* __restrict__ desc, const int* __restrict__ grpFix,
+    const int* __restrict__ node, const int4* __restrict__ code, const double4* __restrict__ geom,
+    const int2* __restrict__ leafRange, const double* __restrict__ pxT, const double* __restrict__ pyT,
+    const double* __restrict__ xin, int treeIn, const int* __restrict__ perm, const double* __restrict__ sigT,
+    const double* __restrict__ wT, double* __restrict__ fT, double* __restrict__ cT, const Params* __restrict__ P,
+    double* __restrict__ mult) {
     extern __shared__ double sm[];
     int4* CD = reinterpret_cast<int4*>(sm);             // maxTask child codes
     double* Rl = reinterpret_cast<double*>(CD + maxTask);  // 4 x 256 transfer matrices (transposed)
     double* M = Rl + 4 * kRank * kRank;                 // maxTask x 16 multipoles
     double* G = M + (size_t)maxTask * kRank;            // maxTask x 4: cx, cy, 1/rx, 1/ry
-    int* LB = reinterpret_cast<int*>(G + (size_t)maxTask * 4);  // maxTask: leaf point offset, count
+    int* LB = reinterpret_cast<int*>(G + (size_t)maxTask * 4);  // maxTask: leaf point offset, count, node
     int* LC = LB + maxTask;
+    int* ND = LC + maxTask;
     const int task = taskBase + blockIdx.x;
-    const int n0 = taskPtr[task], n1 = taskPtr[task + 1], nt = n1 - n0;
-    const int root = node[n1 - 1];  // deepest level first: the root is last
-    const int64_t b0 = begin[root];
+    const int4 d = desc[task];  // first node, nodes, first point, levels
+    const int n0 = d.x, nt = d.y, ngrp = d.w;
+    const int64_t b0 = d.z;
+    const int* gs = grpFix + (size_t)task * (kTaskLevels + 1);
     // M2M reads R[q][rr + 16 r] along rr: stage it transposed (r fastest) so the
     // 16 lanes of one node hit 16 consecutive LDS words
     for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) {
@@ -244,14 +245,16 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
         Rl[i] = P->R[q][rr + r * kRank];
     }
     for (int k = threadIdx.x; k < nt; k += blockDim.x) {
-        const int n = node[n0 + k];
-        G[4 * k] = ncx[n];
-        G[4 * k + 1] = ncy[n];
-        G[4 * k + 2] = 1.0 / nrx[n];
-        G[4 * k + 3] = 1.0 / nry[n];
-        LB[k] = (int)(begin[n] - b0);
-        LC[k] = (int)count[n];
+        const double4 g = geom[n0 + k];
+        G[4 * k] = g.x;
+        G[4 * k + 1] = g.y;
+        G[4 * k + 2] = g.z;
+        G[4 * k + 3] = g.w;
+        const int2 lr = leafRange[n0 + k];
+        LB[k] = lr.x;
+        LC[k] = lr.y;
         CD[k] = code[n0 + k];
+        ND[k] = node[n0 + k];
     }
     __syncthreads();
     // each point is read once (lane per point, coalesced): no LDS staging
@@ -302,8 +305,8 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
         }
     }
     __syncthreads();
-    for (int g = grpPtr[task]; g < grpPtr[task + 1]; ++g) {
-        const int s0 = grp[g] - n0, s1 = grp[g + 1] - n0;
+    for (int g = 0; g < ngrp; ++g) {
+        const int s0 = gs[g], s1 = gs[g + 1];
         for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
             const int k = s0 + (it >> 4), r = it & (kRank - 1);
             const int4 c = CD[k];
@@ -336,7 +339,7 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
         __syncthreads();
     }
     for (int it = threadIdx.x; it < nt * kRank; it += blockDim.x)
-        mult[(size_t)node[n0 + (it >> 4)] * kRank + (it & (kRank - 1))] = M[it];
+        mult[(size_t)ND[it >> 4] * kRank + (it & (kRank - 1))] = M[it];
 }
 
 // Lane-quad exchange through DPP quad_perm (no LDS round trip).
@@ -638,16 +641,12 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
 // all nodes, the roots' parent totals, box geometry, points and
 // their output slots) into LDS; the levels and the points then run out of LDS.
 __global__ void __launch_bounds__(kTierThreads) k_down_tier(
-    int taskBase, int maxTask, int maxLeaves, const int* __restrict__ taskPtr,
-    const int* __restrict__ grpPtr, const int* __restrict__ grp, const int4* __restrict__ dn,
-    const int* __restrict__ slot, const double* __restrict__ local, const double* __restrict__ m2lPart,
-    const Params* __restrict__ P, double* __restrict__ total, const int* __restrict__ leafPtr,
-    const int* __restrict__ leafSlot, const int* __restrict__ leafIdx, const int* __restrict__ leafBegin,
-    const int2* __restrict__ ptsRange, const double* __restrict__ ncx, const double* __restrict__ ncy,
-    const double* __restrict__ nrx, const double* __restrict__ nry, const double* __restrict__ pxT,
-    const double* __restrict__ pyT, const int* __restrict__ operm, int64_t obase, const int2* __restrict__ leafNear,
-    const int* __restrict__ nearPtr, const int* __restrict__ nearOff, int maxNear, const double* __restrict__ nearPart,
-    const int* __restrict__ chainPtr, const int2* __restrict__ chain, int maxChain, int flags, double scale,
+    int maxTask, int maxLeaves, const int4* __restrict__ desc, const int* __restrict__ grpFix,
+    const int4* __restrict__ dn, const double* __restrict__ local, const Params* __restrict__ P,
+    const int* __restrict__ leafSlot, const int* __restrict__ leafBegin, const int2* __restrict__ leafNear,
+    const double4* __restrict__ leafGeom, const double* __restrict__ pxT, const double* __restrict__ pyT,
+    const int* __restrict__ operm, int64_t obase, const int* __restrict__ nearOff, int maxNear,
+    const double* __restrict__ nearPart, const int2* __restrict__ chain, int maxChain, int flags, double scale,
     double* __restrict__ out) {
     extern __shared__ double sm[];
     int4* DN = reinterpret_cast<int4*>(sm);             // maxTask node records
@@ -661,11 +660,15 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     int* NB = LS + maxLeaves;                           // maxLeaves: first of the leaf's near offsets in NO
     int* NC = NB + maxLeaves;                           // maxLeaves: their count
     int* NO = NC + maxLeaves;                           // maxNear: partial offsets of the blocks addressed here
-    const int task = taskBase + blockIdx.x;
-    const int n0 = taskPtr[task], n1 = taskPtr[task + 1], nt = n1 - n0;
-    const int l0 = leafPtr[task], nl = leafPtr[task + 1] - l0;
-    const int2 pr = ptsRange[task];
-    const int npts = pr.y - pr.x;
+    const int task = blockIdx.x;
+    // task record: (first node, nodes, first leaf entry, leaves), (owned points begin,
+    // end, first chain entry, chain length), (first near offset, count, levels, 0)
+    const int4 d0 = desc[3 * task], d1 = desc[3 * task + 1], d2 = desc[3 * task + 2];
+    const int n0 = d0.x, nt = d0.y, l0 = d0.z, nl = d0.w;
+    const int2 pr = make_int2(d1.x, d1.y);
+    const int c0 = d1.z, nc = d1.w;
+    const int npts = pr.y - pr.x, ngrp = d2.z;
+    const int* gs = grpFix + (size_t)task * (kTaskLevels + 1);
     const bool far = flags & kStageFar;
     // ---- phase 0: independent loads
     if (far) {
@@ -675,7 +678,6 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             const int k = it >> 4, r = it & (kRank - 1);
             T[it] = local[(size_t)dn[n0 + k].x * kRank + r];
         }
-        const int c0 = chainPtr[task], nc = chainPtr[task + 1] - c0;
         for (int it = threadIdx.x; it < nc * kRank; it += blockDim.x)
             CH[it] = local[(size_t)chain[c0 + (it >> 4)].x * kRank + (it & (kRank - 1))];
     }
@@ -685,20 +687,20 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
         const int2 ni = leafNear[l0 + e];
         NB[e] = ni.x;
         NC[e] = ni.y;
-        const int n = dn[n0 + leafSlot[l0 + e]].x;
-        G[4 * e] = ncx[n];
-        G[4 * e + 1] = ncy[n];
-        G[4 * e + 2] = 1.0 / nrx[n];
-        G[4 * e + 3] = 1.0 / nry[n];
+        const double4 g = leafGeom[l0 + e];
+        G[4 * e] = g.x;
+        G[4 * e + 1] = g.y;
+        G[4 * e + 2] = g.z;
+        G[4 * e + 3] = g.w;
     }
     if (threadIdx.x == 0) LB[nl] = pr.y;
-    for (int j = nearPtr[task] + threadIdx.x; j < nearPtr[task + 1]; j += blockDim.x) NO[j - nearPtr[task]] = nearOff[j];
+    for (int j = threadIdx.x; j < d2.y; j += blockDim.x) NO[j] = nearOff[d2.x + j];
     __syncthreads();
     // ---- phase 1: the root's parent total by the L2L chain from level 1 (one
     // 16-lane group; bbfmm.h:1070-1071 along the ancestors), then the task's levels
     if (far) {
         if (threadIdx.x < kRank) {
-            const int r = threadIdx.x, c0 = chainPtr[task], nc = chainPtr[task + 1] - c0;
+            const int r = threadIdx.x;
             double v = nc > 0 ? CH[r] : 0.0;
             for (int j = 1; j < nc; ++j) {
                 const double* R = Rl + chain[c0 + j].y * kRank * kRank;
@@ -710,8 +712,8 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             PT[r] = v;
         }
         __syncthreads();
-        for (int g = grpPtr[task]; g < grpPtr[task + 1]; ++g) {
-            const int s0 = grp[g] - n0, s1 = grp[g + 1] - n0;
+        for (int g = 0; g < ngrp; ++g) {
+            const int s0 = gs[g], s1 = gs[g + 1];
             for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
                 const int k = s0 + (it >> 4), r = it & (kRank - 1);
                 const int4 d = DN[k];
@@ -944,7 +946,7 @@ void launch_prepare(int64_t N, const double* xin, int treeIn, const int* perm, c
 }
 
 size_t up_tier_lds(int maxTask) {
-    return (size_t)(4 * kRank * kRank + maxTask * (kRank + 4)) * sizeof(double) + (size_t)2 * maxTask * sizeof(int) +
+    return (size_t)(4 * kRank * kRank + maxTask * (kRank + 4)) * sizeof(double) + (size_t)3 * maxTask * sizeof(int) +
            (size_t)maxTask * sizeof(int4);
 }
 
@@ -953,15 +955,14 @@ size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain) {
            (size_t)(4 * maxLeaves + 4 + maxNear) * sizeof(int) + (size_t)maxTask * sizeof(int4);
 }
 
-void launch_up_tier(int ntask, int taskBase, int maxTask, const int* taskPtr, const int* grpPtr,
-                    const int* grp, const int* node, const int4* code, const int64_t* begin, const int64_t* count,
-                    const double* ncx, const double* ncy, const double* nrx, const double* nry, const double* pxT,
-                    const double* pyT, const double* xin, int treeIn, const int* perm, const double* sigT,
-                    const double* wT, double* fT, double* cT, const Params* P, double* mult, hipStream_t s) {
+void launch_up_tier(int ntask, int taskBase, int maxTask, const int4* desc, const int* grpFix, const int* node,
+                    const int4* code, const double4* geom, const int2* leafRange, const double* pxT, const double* pyT,
+                    const double* xin, int treeIn, const int* perm, const double* sigT, const double* wT, double* fT,
+                    double* cT, const Params* P, double* mult, hipStream_t s) {
     if (ntask <= 0) return;
-    k_up_tier<<<ntask, kTierThreads, up_tier_lds(maxTask), s>>>(
-        taskBase, maxTask, taskPtr, grpPtr, grp, node, code, begin, count, ncx, ncy, nrx, nry, pxT, pyT, xin, treeIn,
-        perm, sigT, wT, fT, cT, P, mult);
+    k_up_tier<<<ntask, kTierThreads, up_tier_lds(maxTask), s>>>(taskBase, maxTask, desc, grpFix, node, code, geom,
+                                                               leafRange, pxT, pyT, xin, treeIn, perm, sigT, wT, fT,
+                                                               cT, P, mult);
     HIP_LAUNCH_CHECK();
 }
 
@@ -993,19 +994,15 @@ void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const 
     HIP_LAUNCH_CHECK();
 }
 
-void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const int* taskPtr,
-                      const int* grpPtr, const int* grp, const int4* dn, const int* slot, const double* local,
-                      const double* m2lPart, const Params* P, double* total, const int* leafPtr, const int* leafSlot,
-                      const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
-                      const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
-                      const int* operm, int64_t obase, const int2* leafNear, const int* nearPtr, const int* nearOff,
-                      int maxNear, const double* nearPart, const int* chainPtr, const int2* chain, int maxChain,
-                      int flags, double scale, double* out, hipStream_t s) {
+void launch_down_tier(int ntask, int maxTask, int maxLeaves, const int4* desc, const int* grpFix, const int4* dn,
+                      const double* local, const Params* P, const int* leafSlot, const int* leafBegin,
+                      const int2* leafNear, const double4* leafGeom, const double* pxT, const double* pyT,
+                      const int* operm, int64_t obase, const int* nearOff, int maxNear, const double* nearPart,
+                      const int2* chain, int maxChain, int flags, double scale, double* out, hipStream_t s) {
     if (ntask <= 0) return;
     k_down_tier<<<ntask, kTierThreads, down_tier_lds(maxTask, maxLeaves, maxNear, maxChain), s>>>(
-        taskBase, maxTask, maxLeaves, taskPtr, grpPtr, grp, dn, slot, local, m2lPart, P, total, leafPtr,
-        leafSlot, leafIdx, leafBegin, ptsRange, ncx, ncy, nrx, nry, pxT, pyT, operm, obase, leafNear, nearPtr, nearOff,
-        maxNear, nearPart, chainPtr, chain, maxChain, flags, scale, out);
+        maxTask, maxLeaves, desc, grpFix, dn, local, P, leafSlot, leafBegin, leafNear, leafGeom, pxT, pyT, operm,
+        obase, nearOff, maxNear, nearPart, chain, maxChain, flags, scale, out);
     HIP_LAUNCH_CHECK();
 }
 

@@ -39,11 +39,10 @@ void launch_prepare(int64_t N, const double* xin, int treeIn, const int* perm, c
 constexpr int kTierThreads = 512;  // workgroup of the up / down pass tiers
 size_t up_tier_lds(int maxTask);
 size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain);
-void launch_up_tier(int ntask, int taskBase, int maxTask, const int* taskPtr, const int* grpPtr,
-                    const int* grp, const int* node, const int4* code, const int64_t* begin, const int64_t* count,
-                    const double* ncx, const double* ncy, const double* nrx, const double* nry, const double* pxT,
-                    const double* pyT, const double* xin, int treeIn, const int* perm, const double* sigT,
-                    const double* wT, double* fT, double* cT, const Params* P, double* mult, hipStream_t s);
+void launch_up_tier(int ntask, int taskBase, int maxTask, const int4* desc, const int* grpFix, const int* node,
+                    const int4* code, const double4* geom, const int2* leafRange, const double* pxT, const double* pyT,
+                    const double* xin, int treeIn, const int* perm, const double* sigT, const double* wT, double* fT,
+                    double* cT, const Params* P, double* mult, hipStream_t s);
 void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
                 const int* outSlot, const int* src, const double* K, const double* mult, double sgn, double* partial,
                 double* local, hipStream_t s);
@@ -55,14 +54,11 @@ void launch_m2l_gather(int ntgt, const int* tgt, const int* inPtr, const double*
 void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts, const int64_t* nearKOff,
                  const int2* nearSym, const double* K, const double* fT, const int* operm, int64_t obase, int maxS,
                  int flags, double sgn, double scale, double* partial, double* out, hipStream_t s);
-void launch_down_tier(int ntask, int taskBase, int maxTask, int maxLeaves, const int* taskPtr,
-                      const int* grpPtr, const int* grp, const int4* dn, const int* slot, const double* local,
-                      const double* m2lPart, const Params* P, double* total, const int* leafPtr, const int* leafSlot,
-                      const int* leafIdx, const int* leafBegin, const int2* ptsRange, const double* ncx,
-                      const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
-                      const int* operm, int64_t obase, const int2* leafNear, const int* nearPtr, const int* nearOff,
-                      int maxNear, const double* nearPart, const int* chainPtr, const int2* chain, int maxChain,
-                      int flags, double scale, double* out, hipStream_t s);
+void launch_down_tier(int ntask, int maxTask, int maxLeaves, const int4* desc, const int* grpFix, const int4* dn,
+                      const double* local, const Params* P, const int* leafSlot, const int* leafBegin,
+                      const int2* leafNear, const double4* leafGeom, const double* pxT, const double* pyT,
+                      const int* operm, int64_t obase, const int* nearOff, int maxNear, const double* nearPart,
+                      const int2* chain, int maxChain, int flags, double scale, double* out, hipStream_t s);
 void launch_corr(int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT, const double* fT,
                  const double* C,
                  const double* mu, const Params* P, int flags, double scale, bool treeOut, double* out,
