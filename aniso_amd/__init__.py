@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libaniso_mi355x.so")
+LIB_PATH = os.environ.get("ANISO_LIB") or os.path.join(_HERE, "libaniso_mi355x.so")  # ANISO_LIB: dev builds
 _lib = None
 
 STAGE_FAR, STAGE_NEAR, STAGE_STENCIL, STAGE_SING, STAGE_ALL = 1, 2, 4, 8, 15

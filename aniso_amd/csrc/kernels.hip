@@ -176,6 +176,22 @@ __device__ double pair_kernel(const Params* __restrict__ P, const double* __rest
 
 // ----------------------------------------------------------------- apply kernels
 
+#ifdef ANISO_PROBE  // development build only (make probe): phase stamps of workgroup 0..kProbeWG-1
+constexpr int kProbeWG = 2048;
+__device__ unsigned long long g_probe[2][kProbeWG][8];
+#define ANISO_STAMP(K, W, I)                                                     \
+    do {                                                                          \
+        if (threadIdx.x == 0 && (W) < kProbeWG) g_probe[K][W][I] = wall_clock64(); \
+    } while (0)
+extern "C" int aniso_probe_read(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_probe), sizeof(g_probe));
+}
+#else
+#define ANISO_STAMP(K, W, I) \
+    do {                  \
+    } while (0)
+#endif
+
 // Output slot of tree position k: the original index perm[k] (original-order
 // output) or the owned tree-order slice k - obase (operm == nullptr).
 __device__ __forceinline__ int64_t out_index(const int* __restrict__ operm, int64_t obase, int64_t k) {
@@ -218,7 +234,7 @@ __global__ void k_sub_slice(int64_t n, const double* __restrict__ x, const doubl
 // Phase 0 stages the transfer matrices, node boxes and child codes in LDS with
 // one round of independent loads; the levels then run out of LDS.
 // One thread per (node, entry r), r = 4j + i:  M[r] = sum_p S(x_p, c_i) S(y_p, c_j) f_p.
-__global__ void __launch_bounds__(kTierThreads) k_up_tier(
+__global__ void __launch_bounds__(kUpThreads) k_up_tier(
     int taskBase, int maxTask, const int4* __restrict__ desc, const int* __restrict__ grpFix,
     const int* __restrict__ node, const int4* __restrict__ code, const double4* __restrict__ geom,
     const int2* __restrict__ leafRange, const double* __restrict__ pxT, const double* __restrict__ pyT,
@@ -234,6 +250,7 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
     int* LC = LB + maxTask;
     int* ND = LC + maxTask;
     const int task = taskBase + blockIdx.x;
+    ANISO_STAMP(0, task, 0);
     const int4 d = desc[task];  // first node, nodes, first point, levels
     const int n0 = d.x, nt = d.y, ngrp = d.w;
     const int64_t b0 = d.z;
@@ -257,6 +274,7 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
         ND[k] = node[n0 + k];
     }
     __syncthreads();
+    ANISO_STAMP(0, task, 1);
     // each point is read once (lane per point, coalesced): no LDS staging
     // P2M of the task's leaves (bbfmm.h:737-748): 16 lanes per leaf, one point per
     // lane per pass (its 16 products in registers), then a 16-lane reduce-scatter
@@ -305,6 +323,7 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
         }
     }
     __syncthreads();
+    ANISO_STAMP(0, task, 2);
     for (int g = 0; g < ngrp; ++g) {
         const int s0 = gs[g], s1 = gs[g + 1];
         for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
@@ -338,8 +357,10 @@ __global__ void __launch_bounds__(kTierThreads) k_up_tier(
         }
         __syncthreads();
     }
+    ANISO_STAMP(0, task, 3);
     for (int it = threadIdx.x; it < nt * kRank; it += blockDim.x)
         mult[(size_t)ND[it >> 4] * kRank + (it & (kRank - 1))] = M[it];
+    ANISO_STAMP(0, task, 4);
 }
 
 // Lane-quad exchange through DPP quad_perm (no LDS round trip).
@@ -661,6 +682,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     int* NC = NB + maxLeaves;                           // maxLeaves: their count
     int* NO = NC + maxLeaves;                           // maxNear: partial offsets of the blocks addressed here
     const int task = blockIdx.x;
+    ANISO_STAMP(1, task, 0);
     // task record: (first node, nodes, first leaf entry, leaves), (owned points begin,
     // end, first chain entry, chain length), (first near offset, count, levels, 0)
     const int4 d0 = desc[3 * task], d1 = desc[3 * task + 1], d2 = desc[3 * task + 2];
@@ -696,6 +718,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     if (threadIdx.x == 0) LB[nl] = pr.y;
     for (int j = threadIdx.x; j < d2.y; j += blockDim.x) NO[j] = nearOff[d2.x + j];
     __syncthreads();
+    ANISO_STAMP(1, task, 1);
     // ---- phase 1: the root's parent total by the L2L chain from level 1 (one
     // 16-lane group; bbfmm.h:1070-1071 along the ancestors), then the task's levels
     if (far) {
@@ -712,6 +735,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             PT[r] = v;
         }
         __syncthreads();
+        ANISO_STAMP(1, task, 2);
         for (int g = 0; g < ngrp; ++g) {
             const int s0 = gs[g], s1 = gs[g + 1];
             for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
@@ -728,6 +752,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             __syncthreads();
         }
     }
+    ANISO_STAMP(1, task, 3);
     // ---- phase 2: owned points: L2P + near gather
     for (int g = threadIdx.x; g < npts; g += blockDim.x) {
         const int kpos = pr.x + g;
@@ -758,6 +783,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
         }
         out[out_index(operm, obase, kpos)] += scale * v;
     }
+    ANISO_STAMP(1, task, 4);
 }
 
 // Corrections (nearRemoval + refineAddOnFast + singularAddFast,
@@ -960,7 +986,7 @@ void launch_up_tier(int ntask, int taskBase, int maxTask, const int4* desc, cons
                     const double* xin, int treeIn, const int* perm, const double* sigT, const double* wT, double* fT,
                     double* cT, const Params* P, double* mult, hipStream_t s) {
     if (ntask <= 0) return;
-    k_up_tier<<<ntask, kTierThreads, up_tier_lds(maxTask), s>>>(taskBase, maxTask, desc, grpFix, node, code, geom,
+    k_up_tier<<<ntask, kUpThreads, up_tier_lds(maxTask), s>>>(taskBase, maxTask, desc, grpFix, node, code, geom,
                                                                leafRange, pxT, pyT, xin, treeIn, perm, sigT, wT, fT,
                                                                cT, P, mult);
     HIP_LAUNCH_CHECK();

@@ -36,7 +36,10 @@ enum StageMask : int {
 
 void launch_prepare(int64_t N, const double* xin, int treeIn, const int* perm, const double* sigT, const double* wT,
                     double* fT, double* cT, hipStream_t s);
-constexpr int kTierThreads = 512;  // workgroup of the up / down pass tiers
+constexpr int kTierThreads = 256;  // workgroup of the down pass tasks
+// up pass tasks: 256 threads (P2M holds 16 products per lane, ~94 VGPRs = 5 waves
+// per SIMD), so four workgroups fit per CU and 1,024 tasks run in one round
+constexpr int kUpThreads = 256;
 size_t up_tier_lds(int maxTask);
 size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain);
 void launch_up_tier(int ntask, int taskBase, int maxTask, const int4* desc, const int* grpFix, const int* node,
