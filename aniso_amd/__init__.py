@@ -71,6 +71,9 @@ def lib():
             "aniso_mapping_tree_dev": [P, P, I, P, P],
             "aniso_forward_tree_dev": [P, P, P, P],
             "aniso_gmres": [P, dp, dp, I, I, D, dp, I, ip, dp],
+            "aniso_apply_block_dev": [P, I, P, I64, I, I, ip, dp, P, I64, I, P],
+            "aniso_block_op_dev": [P, I, P, I64, P, I64, I, P],
+            "aniso_block_mixes": [I, D, I, dp],
             "aniso_last_error": [ctypes.c_char_p, ctypes.c_size_t],
         }
         for name, args in sig.items():
@@ -217,6 +220,49 @@ class Aniso:
                                             ctypes.c_void_p(y_slice.data_ptr()), ctypes.c_void_p(s)))
         return y_slice
 
+    # ---- the block operator of aniso.m (aniso.m:121-157)
+    def apply_block_dev(self, x, ids, mixes, out, use_sigma=False, tree=False, stream=None):
+        """out[i] = sum_t sum_b mixes[t][i][b] mapping(sig .* x[b], ids[t]) on device tensors.
+
+        x: (nrhs, N) float64 CUDA tensor (rows may be strided); out: (nrhs, n_out)
+        with n_out = N (original order) or the owned slice length (tree=True);
+        mixes: (nterm, nrhs, nrhs) host array; use_sigma multiplies x by sigma_s.
+        """
+        import torch
+
+        ids = np.ascontiguousarray(np.asarray(ids, dtype=np.int32).reshape(-1))
+        nrhs = x.shape[0]
+        mixes = np.ascontiguousarray(np.asarray(mixes, dtype=np.float64).reshape(len(ids), nrhs, nrhs))
+        for t, nm in ((x, "x"), (out, "out")):
+            if not (t.is_cuda and t.dtype == torch.float64 and t.dim() == 2 and t.stride(1) == 1):
+                raise AnisoError(1, f"{nm} must be a 2-D float64 CUDA tensor with unit column stride")
+        if x.shape[1] != self.N or out.shape[0] != nrhs:
+            raise AnisoError(1, f"x must be (nrhs, {self.N}) and out (nrhs, n_out)")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_apply_block_dev(self.address, int(nrhs), ctypes.c_void_p(x.data_ptr()), int(x.stride(0)),
+                                           int(bool(use_sigma)), len(ids),
+                                           ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _dp(mixes),
+                                           ctypes.c_void_p(out.data_ptr()), int(out.stride(0)), int(bool(tree)),
+                                           ctypes.c_void_p(s)))
+        return out
+
+    def block_op_dev(self, which, x, out, tree=False, stream=None):
+        """aniso.m on ks stacked blocks: which = 0 forward, 1 mforward, 2 x - mforward(x).
+
+        x: (ks, N) device tensor (block b = u(b*n+1:(b+1)*n)); out: (ks, n_out)."""
+        import torch
+
+        for t, nm in ((x, "x"), (out, "out")):
+            if not (t.is_cuda and t.dtype == torch.float64 and t.dim() == 2 and t.stride(1) == 1):
+                raise AnisoError(1, f"{nm} must be a 2-D float64 CUDA tensor with unit column stride")
+        if x.shape[0] != self.ks or x.shape[1] != self.N or out.shape[0] != self.ks:
+            raise AnisoError(1, f"x must be ({self.ks}, {self.N}) and out ({self.ks}, n_out)")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_block_op_dev(self.address, int(which), ctypes.c_void_p(x.data_ptr()), int(x.stride(0)),
+                                        ctypes.c_void_p(out.data_ptr()), int(out.stride(0)), int(bool(tree)),
+                                        ctypes.c_void_p(s)))
+        return out
+
     def gmres(self, q, m=80, maxit=400, tol=1e-12, x0=None):
         """main.cpp:121-141 on the device: returns (iters, x, residual history, final residual)."""
         q = _f64(q, self.N, "q")
@@ -283,6 +329,13 @@ class Aniso:
         out = np.zeros(seg.shape[0])
         _check(lib().aniso_line_integrals(self.address, _dp(seg), seg.shape[0], _dp(out)))
         return out
+
+
+def block_mixes(nb, g, chi=True):
+    """The (2nb-1, nb, nb) mode mixes of aniso.m forward (chi=False) / mforward (chi=True)."""
+    m = np.zeros((2 * nb - 1) * nb * nb)
+    _check(lib().aniso_block_mixes(int(nb), float(g), int(bool(chi)), _dp(m)))
+    return m.reshape(2 * nb - 1, nb, nb)
 
 
 def version():

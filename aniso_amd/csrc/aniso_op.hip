@@ -75,12 +75,8 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
 Operator::~Operator() {
     if (device >= 0) {
         (void)hipSetDevice(device);
-        for (auto& set : evPool)
-            for (auto& e : set) (void)hipEventDestroy(e);
+        for (auto& e : evPool) (void)hipEventDestroy(e);
         if (own) (void)hipStreamDestroy(own);
-        if (aux) (void)hipStreamDestroy(aux);
-        if (evFork) (void)hipEventDestroy(evFork);
-        if (evJoin) (void)hipEventDestroy(evJoin);
     }
 }
 
@@ -108,10 +104,6 @@ void Operator::ensureDevice() {
     }
     HIP_CHECK(hipGetDevice(&device));
     HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
-    HIP_CHECK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
-    HIP_CHECK(hipEventCreateWithFlags(&evFork, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
-    if (const char* e = std::getenv("ANISO_OVERLAP")) overlap = e[0] == '1';
     // tree-order coordinates
     std::vector<double> pxT(geo.N), pyT(geo.N);
     for (int64_t k = 0; k < geo.N; ++k) {
@@ -195,17 +187,26 @@ void Operator::ensureDevice() {
     // work arrays
     dCharge.alloc(geo.N * sizeof(double));
     dOut.alloc(geo.N * sizeof(double));
-    dFT.alloc(geo.N * sizeof(double));
-    dCT.alloc(geo.N * sizeof(double));
     dTmp.alloc(geo.N * sizeof(double));
     dTmp2.alloc(geo.N * sizeof(double));
     dTmpS.alloc(geo.N * sizeof(double));
-    dMult.alloc((size_t)tree.nn * kRank * sizeof(double));
-    dLocal.alloc((size_t)tree.nn * kRank * sizeof(double));
-    dTotal.alloc((size_t)tree.nn * kRank * sizeof(double));
+    ensureWork(1);
+    uploadPlan();
+}
+
+// Per-right-hand-side work arrays, sized for the largest K used so far:
+// fT/cT [N][K], multipoles and locals [node][16][K], M2L and near partials.
+void Operator::ensureWork(int K) {
+    if (K <= workK) return;
+    workK = K;
+    dFT.alloc((size_t)geo.N * K * sizeof(double));
+    dCT.alloc((size_t)geo.N * K * sizeof(double));
+    dMult.alloc((size_t)tree.nn * kRank * K * sizeof(double));
+    dLocal.alloc((size_t)tree.nn * kRank * K * sizeof(double));
     HIP_CHECK(hipMemset(dMult.p, 0, dMult.bytes));
     HIP_CHECK(hipMemset(dLocal.p, 0, dLocal.bytes));
-    uploadPlan();
+    dM2LPart.alloc((size_t)std::max(plan.m2lCanon, 1) * kRank * K * sizeof(double));
+    dNearPart.alloc((size_t)std::max<int64_t>(plan.nearPartTotal, 1) * K * sizeof(double));
 }
 
 static std::vector<int4> to_int4(const std::vector<std::array<int, 4>>& v) {
@@ -231,7 +232,7 @@ void Operator::uploadPlan() {
     up(dM2LCanonBase, plan.m2lCanonBase);
     up(dM2LInPtr, plan.m2lInPtr);
     up(dM2LOutSlot, plan.m2lOutSlot);
-    dM2LPart.alloc((size_t)std::max(plan.m2lCanon, 1) * kRank * sizeof(double));
+    dM2LPart.alloc((size_t)std::max(plan.m2lCanon, 1) * kRank * workK * sizeof(double));
     std::vector<int2> ns(plan.nearSym.size());
     for (size_t i = 0; i < ns.size(); ++i) ns[i] = make_int2(plan.nearSym[i][0], plan.nearSym[i][1]);
     up(dNearSym, ns);
@@ -243,7 +244,7 @@ void Operator::uploadPlan() {
     up(dDnChain, plan.dnChain);
     up(dDnNearPtr, plan.dnNearPtr);
     up(dDnNearOff, plan.dnNearOff);
-    dNearPart.alloc((size_t)std::max<int64_t>(plan.nearPartTotal, 1) * sizeof(double));
+    dNearPart.alloc((size_t)std::max<int64_t>(plan.nearPartTotal, 1) * workK * sizeof(double));
     up(dLeafInfo, to_int4(plan.leafInfo));
     up(dNearPtsPtr, plan.nearPtsPtr);
     up(dNearPts, plan.nearPts);
@@ -266,7 +267,8 @@ void Operator::uploadPlan() {
     up(dDnLeafPts, plan.dnLeafPts);
     up(dDnPtsRange, plan.dnPtsRange);
     // a task's expansions live in LDS (<= 4 levels: 85 nodes); a workgroup may use all 160 KiB
-    if (up_tier_lds(plan.upMaxTask) > 160 * 1024 || down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, plan.dnMaxNear, plan.dnMaxChain) > 160 * 1024)
+    if (up_tier_lds(plan.upMaxTask, 1) > 160 * 1024 ||
+        down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, plan.dnMaxNear, plan.dnMaxChain, 1) > 160 * 1024)
         throw std::logic_error("up/down pass task exceeds one workgroup's LDS");
     maxNearS = 1;
     for (size_t li = 0; li < plan.leaves.size(); ++li) {
@@ -341,6 +343,29 @@ void Operator::mappingHost(const double* charge, int id, double* out) {
     HIP_CHECK(hipStreamSynchronize(own));
 }
 
+// k right-hand sides of one mode, up to 8 per batched apply (identity mix)
+void Operator::mappingBatchedHost(const double* Q, int k, int id, double* Out) {
+    if (k == 0) return;
+    ensureDevice();
+    const int64_t N = geo.N;
+    const int kb = std::min(k, 8);
+    DevBuf dq, dout;
+    dq.alloc((size_t)kb * N * sizeof(double));
+    dout.alloc((size_t)kb * N * sizeof(double));
+    for (int j0 = 0; j0 < k; j0 += kb) {
+        const int nb = std::min(kb, k - j0);
+        std::vector<double> eye((size_t)nb * nb, 0.0);
+        for (int i = 0; i < nb; ++i) eye[(size_t)i * nb + i] = 1.0;
+        HIP_CHECK(hipMemcpyAsync(dq.p, Q + (size_t)j0 * N, (size_t)nb * N * sizeof(double), hipMemcpyHostToDevice, own));
+        if (plan.nranks > 1) HIP_CHECK(hipMemsetAsync(dout.p, 0, dout.bytes, own));
+        applyBlock(nb, dq.as<double>(), N, false, nullptr, 1, &id, eye.data(), dout.as<double>(), N, false, own,
+                   kStageAll);
+        HIP_CHECK(hipMemcpyAsync(Out + (size_t)j0 * N, dout.p, (size_t)nb * N * sizeof(double), hipMemcpyDeviceToHost,
+                                 own));
+        HIP_CHECK(hipStreamSynchronize(own));
+    }
+}
+
 // mapping (AnisoWrapper.cpp:92-136) on device pointers, enqueued on stream s.
 // Only owned targets of `out` are written when the operator is sharded.
 void Operator::mappingDev(const double* charge, int id, double* out, hipStream_t s, int mask) {
@@ -358,109 +383,200 @@ void Operator::mappingTreeDev(const double* qTree, int id, double* outSlice, hip
 // on the owned slice, x tree-ordered (all N).
 void Operator::forwardTreeDev(const double* xTree, double* ySlice, hipStream_t s) {
     apply(xTree, true, dSigmaT.as<double>(), 0, dTmpS.as<double>(), true, s, kStageAll);
-    launch_sub_slice(plan.ownEnd - plan.ownBegin, xTree + plan.ownBegin, dTmpS.as<double>(), ySlice, s);
+    const int64_t n = plan.ownEnd - plan.ownBegin;
+    launch_sub_slice(n, 1, xTree + plan.ownBegin, n, dTmpS.as<double>(), n, ySlice, n, s);
 }
 
 void Operator::apply(const double* charge, bool treeIn, const double* sigT, int id, double* out, bool treeOut,
                      hipStream_t s, int mask) {
-    if (id < 0 || id >= kernelSize) throw std::out_of_range("kernel id out of range");
-    if (!modes[id].ready) throw std::runtime_error("mapping on kernel id " + std::to_string(id) + " before cache(" + std::to_string(id) + ")");
+    const double one = 1.0;
+    applyBlock(1, charge, geo.N, treeIn, sigT, 1, &id, &one, out, geo.N, treeOut, s, mask);
+}
+
+void Operator::applyBlockDev(int nrhs, const double* x, int64_t ldx, bool treeIn, bool useSigma, int nterm,
+                             const int* ids, const double* mixes, double* out, int64_t ldo, bool treeOut,
+                             hipStream_t s, int mask) {
+    if (useSigma && !coeffSet) throw std::runtime_error("block apply with sigma_s before setCoeff");
     ensureDevice();
-    const ModeCache& mc = modes[id];
+    applyBlock(nrhs, x, ldx, treeIn, useSigma ? dSigmaT.as<double>() : nullptr, nterm, ids, mixes, out, ldo, treeOut,
+               s, mask);
+}
+
+int Operator::mark(hipStream_t s) {
+    if (evUsed == (int)evPool.size()) {
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreate(&e));
+        evPool.push_back(e);
+    }
+    HIP_CHECK(hipEventRecord(evPool[evUsed], s));
+    return evUsed++;
+}
+
+// One batched apply: the up pass over the K base vectors, then per term t (mode
+// ids[t], mix mixes[t]) the near field, the corrections, the M2L stream and its
+// gather, each accumulating; then one down pass.  sigT (sigma_s in tree order, or
+// nullptr) multiplies the inputs at their tree positions.
+void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, const double* sigT, int nterm,
+                          const int* ids, const double* mixes, double* out, int64_t ldo, bool treeOut, hipStream_t s,
+                          int mask) {
+    if (K < 1 || K > 8) throw std::invalid_argument("block apply supports 1..8 right-hand sides, got " + std::to_string(K));
+    if (nterm < 1) throw std::invalid_argument("block apply needs at least one mode term");
+    for (int t = 0; t < nterm; ++t) {
+        if (ids[t] < 0 || ids[t] >= kernelSize) throw std::out_of_range("kernel id out of range");
+        if (!modes[ids[t]].ready)
+            throw std::runtime_error("mapping on kernel id " + std::to_string(ids[t]) + " before cache(" + std::to_string(ids[t]) + ")");
+    }
+    ensureDevice();
+    const int64_t nOut = treeOut ? plan.ownEnd - plan.ownBegin : geo.N;
+    if (!rhs_supported(K)) {  // pad with zero right-hand sides to the next compiled count
+        const int Kp = rhs_padded(K);
+        dPadIn.alloc((size_t)Kp * geo.N * sizeof(double));
+        dPadOut.alloc((size_t)Kp * geo.N * sizeof(double));
+        HIP_CHECK(hipMemsetAsync(dPadIn.p, 0, dPadIn.bytes, s));
+        HIP_CHECK(hipMemcpy2DAsync(dPadIn.p, geo.N * sizeof(double), x, ldx * sizeof(double), geo.N * sizeof(double), K,
+                                   hipMemcpyDeviceToDevice, s));
+        std::vector<double> mp((size_t)nterm * Kp * Kp, 0.0);
+        for (int t = 0; t < nterm; ++t)
+            for (int i = 0; i < K; ++i)
+                for (int b = 0; b < K; ++b) mp[((size_t)t * Kp + i) * Kp + b] = mixes[((size_t)t * K + i) * K + b];
+        applyBlock(Kp, dPadIn.as<double>(), geo.N, treeIn, sigT, nterm, ids, mp.data(), dPadOut.as<double>(), geo.N,
+                   treeOut, s, mask);
+        HIP_CHECK(hipMemcpy2DAsync(out, ldo * sizeof(double), dPadOut.p, geo.N * sizeof(double), nOut * sizeof(double),
+                                   K, hipMemcpyDeviceToDevice, s));
+        return;
+    }
+    if (K > 1 && (ldx < geo.N || ldo < nOut)) throw std::invalid_argument("block apply: leading dimension too small");
+    ensureWork(K);
+    if (up_tier_lds(plan.upMaxTask, K) > 160 * 1024 ||
+        down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, plan.dnMaxNear, plan.dnMaxChain, K) > 160 * 1024)
+        throw std::logic_error("up/down pass task exceeds one workgroup's LDS at " + std::to_string(K) + " right-hand sides");
     const Params* P = dParams.as<Params>();
     const bool tm = timeStages;
-    hipEvent_t* ev = nullptr;
-    if (tm) {
-        if (evUsed == (int)evPool.size()) {
-            std::array<hipEvent_t, kStageEvents> set;
-            for (auto& e : set) HIP_CHECK(hipEventCreate(&e));
-            evPool.push_back(set);
-        }
-        ev = evPool[evUsed++].data();
-        HIP_CHECK(hipEventRecord(ev[0], s));
-    }
+    auto span = [&](int stage, int a, int b) {
+        if (tm) spans.push_back({stage, a, b});
+    };
+    const int e0 = tm ? mark(s) : -1;
     const int* operm = treeOut ? nullptr : dPerm.as<int>();
     const int64_t obase = treeOut ? plan.ownBegin : 0;
+    const double scale = M_1_PI / 2.0;  // AnisoWrapper.cpp:129-130
     // up pass (global, every rank): tiers bottom-up; its P2M also forms the weighted
     // charges fT (tree order) the near field and the corrections read
     if (plan.upTierTask.size() < 2)  // a lone leaf: no up pass
-        launch_prepare(geo.N, charge, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(),
+        launch_prepare(K, geo.N, x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(),
                        dCT.as<double>(), s);
     for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k)
-        launch_up_tier(plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask,
+        launch_up_tier(K, plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask,
                        dUpDesc.as<int4>(), dUpGrpFix.as<int>(), dUpNode.as<int>(), dUpCode.as<int4>(),
-                       dUpGeom.as<double4>(), dUpLeaf.as<int2>(), dPxT.as<double>(), dPyT.as<double>(), charge,
-                       treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(),
-                       dCT.as<double>(), P, dMult.as<double>(), s);
-    if (tm) HIP_CHECK(hipEventRecord(ev[1], s));
-    // The near field and the corrections need only the weighted charges; with
-    // ANISO_OVERLAP=1 they run on the auxiliary stream beside the M2L stream (both
-    // write `out`: near stores, corr adds; the down pass adds after the join).
-    hipStream_t sn = overlap ? aux : s;
-    if (overlap) {
-        HIP_CHECK(hipEventRecord(evFork, s));
-        HIP_CHECK(hipStreamWaitEvent(aux, evFork, 0));
+                       dUpGeom.as<double4>(), dUpLeaf.as<int2>(), dPxT.as<double>(), dPyT.as<double>(), x, ldx,
+                       treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(), dCT.as<double>(), P,
+                       dMult.as<double>(), s);
+    int ep = tm ? mark(s) : -1;
+    span(1, e0, ep);
+    for (int t = 0; t < nterm; ++t) {
+        const int id = ids[t];
+        const ModeCache& mc = modes[id];
+        const double* mix = mixes + (size_t)t * K * K;
+        const int acc = t > 0 ? 1 : 0;
+        // K_{B<-A} = (-1)^m K_{A<-B}^T for the merged kernel; Id = m
+        const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
+        launch_near(K, (int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(),
+                    dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(), dFT.as<double>(), mix, operm,
+                    obase, ldo, maxNearS, mask, sgn, scale, acc, dNearPart.as<double>(), out, s);
+        int e = tm ? mark(s) : -1;
+        span(4, ep, e);
+        ep = e;
+        launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
+                    dFT.as<double>(), mix, mc.C.as<double>(), mc.mu.as<double>(), P, mask, scale, treeOut, ldo, out, s);
+        e = tm ? mark(s) : -1;
+        span(6, ep, e);
+        ep = e;
+        if (mask & kStageFar)
+            launch_m2l(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(),
+                       dM2LCanonBase.as<int>(), dM2LOutSlot.as<int>(), dM2LSrc.as<int>(), mc.Km2l.as<double>(),
+                       dMult.as<double>(), mix, sgn, acc, dM2LPart.as<double>(), dLocal.as<double>(), s);
+        e = tm ? mark(s) : -1;
+        span(2, ep, e);
+        ep = e;
+        if ((mask & kStageFar) && plan.m2lCanon > 0)
+            launch_m2l_gather(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LInPtr.as<int>(),
+                              dM2LPart.as<double>(), dLocal.as<double>(), s);
+        e = tm ? mark(s) : -1;
+        span(3, ep, e);
+        ep = e;
     }
-    // K_{B<-A} = (-1)^m K_{A<-B}^T for the merged kernel; Id = m
-    const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
-    if (tm) HIP_CHECK(hipEventRecord(ev[6], sn));
-    launch_near((int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(),
-                dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(), dFT.as<double>(), operm, obase,
-                maxNearS, mask, sgn, M_1_PI / 2.0, dNearPart.as<double>(), out, sn);
-    if (tm) HIP_CHECK(hipEventRecord(ev[7], sn));
-    launch_corr(geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(), dFT.as<double>(),
-                mc.C.as<double>(),
-                mc.mu.as<double>(), P, mask, M_1_PI / 2.0, treeOut, out, sn);
-    if (tm) HIP_CHECK(hipEventRecord(ev[8], sn));
-    if (overlap) HIP_CHECK(hipEventRecord(evJoin, aux));
-    if (tm) HIP_CHECK(hipEventRecord(ev[2], s));
-    if (mask & kStageFar)
-        launch_m2l((int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(),
-                   dM2LCanonBase.as<int>(), dM2LOutSlot.as<int>(), dM2LSrc.as<int>(), mc.Km2l.as<double>(),
-                   dMult.as<double>(), sgn, dM2LPart.as<double>(), dLocal.as<double>(), s);
-    if (tm) HIP_CHECK(hipEventRecord(ev[3], s));
-    if ((mask & kStageFar) && plan.m2lCanon > 0)
-        launch_m2l_gather((int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LInPtr.as<int>(), dM2LPart.as<double>(),
-                          dLocal.as<double>(), s);
-    if (tm) HIP_CHECK(hipEventRecord(ev[4], s));
-    if (overlap) HIP_CHECK(hipStreamWaitEvent(s, evJoin, 0));
-    if (tm) HIP_CHECK(hipEventRecord(ev[9], s));
-    // down pass (owned part): tiers top-down; L2L + L2P + gathered transposed near products
+    // down pass (owned part): L2L + L2P + gathered transposed near products, once
+    // for the sum over the terms (both are linear in the locals / partials)
     if (mask & (kStageFar | kStageNear))
-        launch_down_tier((int)plan.dnDesc.size() / 3, plan.dnMaxTask, plan.dnMaxLeaves, dDnDesc.as<int4>(),
+        launch_down_tier(K, (int)plan.dnDesc.size() / 3, plan.dnMaxTask, plan.dnMaxLeaves, dDnDesc.as<int4>(),
                          dDnGrpFix.as<int>(), dDnNode.as<int4>(), dLocal.as<double>(), P, dDnLeafSlot.as<int>(),
                          dDnLeafPts.as<int>(), dDnLeafNear.as<int2>(), dDnLeafGeom.as<double4>(), dPxT.as<double>(),
-                         dPyT.as<double>(), operm, obase, dDnNearOff.as<int>(), plan.dnMaxNear,
-                         dNearPart.as<double>(), dDnChain.as<int2>(), plan.dnMaxChain, mask, M_1_PI / 2.0, out, s);
-    if (tm) HIP_CHECK(hipEventRecord(ev[5], s));
+                         dPyT.as<double>(), operm, obase, ldo, dDnNearOff.as<int>(), plan.dnMaxNear,
+                         dNearPart.as<double>(), dDnChain.as<int2>(), plan.dnMaxChain, mask, scale, out, s);
+    if (tm) {
+        const int e = mark(s);
+        span(5, ep, e);
+        span(7, e0, e);
+        ++applies;
+    }
+}
+
+// aniso.m forward / mforward mixes (aniso.m:121-157).  Output block iid takes,
+// for every j in [-(nb-1), nb-1], mode m = |iid + j| of input block |j| with
+// weight chi_|j| (mforward; 1 for forward).  Per mode m the pairs (iid, b = |j|)
+// are j = m - iid and j = -m - iid (one j when m = 0).
+std::vector<double> Operator::blockMixes(int nb, double g, bool chi) {
+    if (nb < 1) throw std::invalid_argument("block count must be >= 1");
+    const int nm = 2 * nb - 1;
+    std::vector<double> mix((size_t)nm * nb * nb, 0.0);
+    const double gN = std::pow(g, nb);
+    for (int iid = 0; iid < nb; ++iid)
+        for (int j = -(nb - 1); j <= nb - 1; ++j) {
+            const int b = std::abs(j), m = std::abs(iid + j);
+            const double w = chi ? (std::pow(g, b) - gN) / (1.0 - gN) : 1.0;
+            mix[((size_t)m * nb + iid) * nb + b] += w;
+        }
+    return mix;
+}
+
+void Operator::blockOpDev(int which, const double* x, int64_t ldx, double* out, int64_t ldo, bool treeIo,
+                          hipStream_t s) {
+    if (which < 0 || which > 2) throw std::invalid_argument("block operator: which must be 0, 1 or 2");
+    const int nb = ks, nm = 2 * ks - 1;
+    const auto mix = blockMixes(nb, g, which != 0);
+    std::vector<int> ids(nm);
+    for (int m = 0; m < nm; ++m) ids[m] = m;
+    if (which < 2) {
+        applyBlockDev(nb, x, ldx, treeIo, which != 0, nm, ids.data(), mix.data(), out, ldo, treeIo, s);
+        return;
+    }
+    // x - mforward(x) on the owned targets (aniso.m:155)
+    const int64_t nOut = treeIo ? plan.ownEnd - plan.ownBegin : geo.N;
+    if (!treeIo && plan.nranks != 1) throw std::logic_error("block matvec in original order on a sharded handle: use tree order");
+    dBlk.alloc((size_t)nb * nOut * sizeof(double));
+    applyBlockDev(nb, x, ldx, treeIo, true, nm, ids.data(), mix.data(), dBlk.as<double>(), nOut, treeIo, s);
+    launch_sub_slice(nOut, nb, x + (treeIo ? plan.ownBegin : 0), ldx, dBlk.as<double>(), nOut, out, ldo, s);
 }
 
 void Operator::setTiming(bool on) {
     timeStages = on;
-    if (on) evUsed = 0;
+    if (on) {
+        evUsed = 0;
+        spans.clear();
+        applies = 0;
+    }
 }
 
 StageTimes Operator::stageTimes() {
     StageTimes r;
-    if (evUsed == 0) return r;
-    HIP_CHECK(hipEventSynchronize(evPool[evUsed - 1][5]));
-    auto el = [](hipEvent_t a, hipEvent_t b) {
-        float t = 0;
-        HIP_CHECK(hipEventElapsedTime(&t, a, b));
-        return (double)t;
-    };
+    if (applies == 0 || spans.empty()) return r;
+    HIP_CHECK(hipEventSynchronize(evPool[spans.back().b]));
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int k = 0; k < evUsed; ++k) {
-        const auto& e = evPool[k];
-        acc[1] += el(e[0], e[1]);  // up, with the weighted charges (acc[0], prep, is fused into it)
-        acc[2] += el(e[2], e[3]);  // m2l
-        acc[3] += el(e[3], e[4]);  // gather
-        acc[4] += el(e[6], e[7]);  // near (auxiliary stream)
-        acc[5] += el(e[9], e[5]);  // down (after the join)
-        acc[6] += el(e[7], e[8]);  // corr (auxiliary stream)
-        acc[7] += el(e[0], e[5]);  // whole apply
+    for (const Span& sp : spans) {
+        float t = 0;
+        HIP_CHECK(hipEventElapsedTime(&t, evPool[sp.a], evPool[sp.b]));
+        acc[sp.stage] += t;
     }
-    for (double& a : acc) a /= evUsed;
+    for (double& a : acc) a /= applies;
     r.prep = (float)acc[0];
     r.up = (float)acc[1];
     r.m2l = (float)acc[2];

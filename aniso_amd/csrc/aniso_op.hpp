@@ -51,9 +51,26 @@ public:
     void setCoeff(const double* sigma_s, const double* sigma_t);
     void cache(int id);
     void mappingHost(const double* charge, int id, double* out);
+    void mappingBatchedHost(const double* Q, int k, int id, double* Out);  // N x k column-major
     void mappingDev(const double* charge, int id, double* out, hipStream_t s, int stageMask = 0x3f);
     void mappingTreeDev(const double* qTree, int id, double* outSlice, hipStream_t s);
     void forwardTreeDev(const double* xTree, double* ySlice, hipStream_t s);
+
+    // --- block operator (aniso.m:121-157)
+    // out[i] = sum_t sum_b mixes[t][i][b] K_{ids[t]}(sig .* x[b]) for i, b < nrhs <= 8:
+    // one up pass over the nrhs base vectors, every mode's operators streamed once
+    // for all right-hand sides, one down pass.  x: nrhs vectors of all N points
+    // (stride ldx; original or tree order); out: original order (owned targets) or
+    // the owned tree-order slice (treeOut), stride ldo.  mixes: nterm x nrhs x nrhs.
+    void applyBlockDev(int nrhs, const double* x, int64_t ldx, bool treeIn, bool useSigma, int nterm, const int* ids,
+                       const double* mixes, double* out, int64_t ldo, bool treeOut, hipStream_t s,
+                       int mask = 15);
+    // aniso.m on nb = ks blocks of n = N points: which = 0 forward (the right-hand
+    // side, aniso.m:121-136), 1 mforward (aniso.m:138-157), 2 x - mforward(x) (the
+    // GMRES matvec, aniso.m:155); tree = tree-order input and owned-slice output.
+    void blockOpDev(int which, const double* x, int64_t ldx, double* out, int64_t ldo, bool tree, hipStream_t s);
+    // the (2 nb - 1) mode mixes of forward (chi = false) or mforward (chi = true)
+    static std::vector<double> blockMixes(int nb, double g, bool chi);
 
     // --- extensions
     void setShard(int rank, int nranks);
@@ -90,17 +107,24 @@ public:
 private:
     void apply(const double* charge, bool treeIn, const double* sigT, int id, double* out, bool treeOut, hipStream_t s,
                int mask);
+    void applyBlock(int K, const double* x, int64_t ldx, bool treeIn, const double* sigT, int nterm, const int* ids,
+                    const double* mixes, double* out, int64_t ldo, bool treeOut, hipStream_t s, int mask);
+    void ensureWork(int K);  // work arrays for K right-hand sides
+    int workK = 0;
 
     void ensureDevice();
     void uploadPlan();
     int device = -1;
     hipStream_t own = nullptr;
-    hipStream_t aux = nullptr;        // near field + corrections overlap the far field
-    hipEvent_t evFork = nullptr, evJoin = nullptr;
-    bool overlap = false;  // ANISO_OVERLAP=1: near + corr on the auxiliary stream (no gain measured)
-    static constexpr int kStageEvents = 10;
-    std::vector<std::array<hipEvent_t, kStageEvents>> evPool;
+    // stage timing: events recorded in-stream, (stage, start, end) spans per apply
+    std::vector<hipEvent_t> evPool;
     int evUsed = 0;
+    struct Span {
+        int stage, a, b;
+    };
+    std::vector<Span> spans;
+    int applies = 0;
+    int mark(hipStream_t s);
     int maxNearS = 0;
     // geometry / tree on device
     DevBuf dPxT, dPyT, dPerm, dW, dNcx, dNcy, dNrx, dNry, dBegin, dCount, dParent, dSlot, dChild, dIsLeaf;
@@ -111,8 +135,9 @@ private:
     DevBuf dM2LNDir, dM2LCanonBase, dM2LInPtr, dM2LOutSlot, dM2LPart;  // symmetric M2L
     DevBuf dNearSym, dNearPart, dDnLeafNear, dDnNearPtr, dDnNearOff, dDnChainPtr, dDnChain;              // symmetric near field
     DevBuf dParams, dStCoef;
-    DevBuf dCharge, dOut, dFT, dCT, dMult, dLocal, dTotal, dSigmaS, dTmp, dTmp2;
+    DevBuf dCharge, dOut, dFT, dCT, dMult, dLocal, dSigmaS, dTmp, dTmp2;
     DevBuf dWT, dSigmaT, dIperm, dTmpS;  // tree-order path
+    DevBuf dPadIn, dPadOut, dBlk;       // block operator: padded right-hand sides, x - mforward(x)
     std::vector<ModeCache> modes;
 };
 

@@ -1,0 +1,1024 @@
+// apply.hip -- the apply kernels (one mode-apply of the anisotropic RTE operator,
+// AnisoWrapper.cpp:92-136), for K right-hand sides at once.
+//
+// Reference behaviour (file:line under lowrank/aniso):
+//   up pass      bbfmm.h:825-861          (P2M leaf transfer, M2M)
+//   down pass    bbfmm.h:1041-1129        (M2L over V/X, L2L, U/W near, L2P)
+//   corrections  KernelFactory.cpp:445-478, 662-709, 828-860
+//   block caller aniso.m:139-157          (mforward: 9 modes x 5 blocks)
+//
+// Batching.  K right-hand sides share one read of every cached
+// operator.  The up pass computes the multipoles of K *base* vectors; each mode's
+// kernels apply a K x K mix to them on the fly (rhs i = sum_b mix[i][b] base b), so
+// the block operator of aniso.m streams each mode's operators once for all its
+// right-hand sides.  The far field is linear in the locals and L2L/L2P do not
+// depend on the mode, so locals and transposed near products accumulate over the
+// modes of a call and the down pass runs once.
+//
+// Layouts (K fastest): fT, cT [N][K] tree order; mult, local [node][16][K];
+// M2L partials [slot][16][K]; near partials [column][K]; outputs [K][ldo].
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <stdexcept>
+#include <string>
+
+#include "device_common.hpp"
+#include "host.hpp"
+
+namespace aniso {
+
+#ifdef ANISO_PROBE  // development build only (make probe): phase stamps of task 0..kProbeWG-1
+constexpr int kProbeWG = 2048;
+__device__ unsigned long long g_probe[2][kProbeWG][8];
+#define ANISO_STAMP(Q, W, I)                                                       \
+    do {                                                                            \
+        if (threadIdx.x == 0 && (W) < kProbeWG) g_probe[Q][W][I] = wall_clock64(); \
+    } while (0)
+extern "C" int aniso_probe_read(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_probe), sizeof(g_probe));
+}
+#else
+#define ANISO_STAMP(Q, W, I) \
+    do {                     \
+    } while (0)
+#endif
+
+template <int K>
+struct MixK {
+    double c[K][K];  // rhs i = sum_b c[i][b] * base b
+};
+
+template <int K>
+__device__ __forceinline__ void mix_apply(const MixK<K>& m, const double* base, double* v) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        double a = 0.0;
+#pragma unroll
+        for (int b = 0; b < K; ++b) a += m.c[i][b] * base[b];
+        v[i] = a;
+    }
+}
+
+// Output slot of tree position k: the original index perm[k] (original-order
+// output) or the owned tree-order slice k - obase (operm == nullptr).
+__device__ __forceinline__ int64_t out_index(const int* __restrict__ operm, int64_t obase, int64_t k) {
+    return operm ? (int64_t)operm[k] : k - obase;
+}
+
+// Base charge b of tree position k: x_tree[b][k] (treeIn) or x[b][perm[k]], times
+// sigma_s in tree order when given.
+__device__ __forceinline__ double input_charge(const double* __restrict__ xin, int64_t ldi, int b, int treeIn,
+                                               const int* __restrict__ perm, const double* __restrict__ sigT,
+                                               int64_t k) {
+    const double c = xin[(size_t)b * ldi + (treeIn ? k : (int64_t)perm[k])];
+    return sigT ? c * sigT[k] : c;
+}
+
+// fT[k][b] = c w_T[k] (FMM and stencil charges), cT[k][b] = c (singular term).
+// The up pass forms them inside its P2M; this kernel covers a tree without
+// up-pass tiers (a lone leaf).
+template <int K>
+__global__ void k_prepare(int64_t N, const double* __restrict__ xin, int64_t ldi, int treeIn,
+                          const int* __restrict__ perm, const double* __restrict__ sigT, const double* __restrict__ wT,
+                          double* __restrict__ fT, double* __restrict__ cT) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N) return;
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        const double c = input_charge(xin, ldi, b, treeIn, perm, sigT, k);
+        fT[k * K + b] = c * wT[k];
+        cT[k * K + b] = c;
+    }
+}
+
+// y[i] = x[i] - a[i] on the owned slice, for each right-hand side
+// (forwardOperator u - K(sigma_s u), main.cpp:125-136; aniso.m x - mforward(x)).
+__global__ void k_sub_slice(int64_t n, int nrhs, const double* __restrict__ x, int64_t ldx,
+                            const double* __restrict__ a, int64_t lda, double* __restrict__ y, int64_t ldy) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n * nrhs) return;
+    const int64_t r = i / n, j = i - r * n;
+    y[r * ldy + j] = x[r * ldx + j] - a[r * lda + j];
+}
+
+// ----------------------------------------------------------------- up pass
+
+// Up pass (bbfmm.h:825-861) as tiers of <= 4-level subtrees:
+// one workgroup per subtree keeps its nodes' multipoles in LDS, deepest level
+// first; a leaf's multipole is P2M over its contiguous tree-order points
+// (bbfmm.h:737-748), an internal node's is M2M of its children (bbfmm.h:855-859),
+// where a child below the tier is the root of a lower tier's task (read from HBM).
+// Phase 0 stages the transfer matrices, node boxes and child codes in LDS with
+// one round of independent loads; the levels then run out of LDS.
+template <int K>
+__global__ void __launch_bounds__(kUpThreads) k_up_tier(
+    int taskBase, int maxTask, const int4* __restrict__ desc, const int* __restrict__ grpFix,
+    const int* __restrict__ node, const int4* __restrict__ code, const double4* __restrict__ geom,
+    const int2* __restrict__ leafRange, const double* __restrict__ pxT, const double* __restrict__ pyT,
+    const double* __restrict__ xin, int64_t ldi, int treeIn, const int* __restrict__ perm,
+    const double* __restrict__ sigT, const double* __restrict__ wT, double* __restrict__ fT, double* __restrict__ cT,
+    const Params* __restrict__ P, double* __restrict__ mult) {
+    extern __shared__ double sm[];
+    int4* CD = reinterpret_cast<int4*>(sm);                // maxTask child codes
+    double* Rl = reinterpret_cast<double*>(CD + maxTask);  // 4 x 256 transfer matrices (transposed)
+    double* M = Rl + 4 * kRank * kRank;                    // maxTask x 16 x K multipoles
+    double* G = M + (size_t)maxTask * kRank * K;           // maxTask x 4: cx, cy, 1/rx, 1/ry
+    int* LB = reinterpret_cast<int*>(G + (size_t)maxTask * 4);  // maxTask: leaf point offset, count, node
+    int* LC = LB + maxTask;
+    int* ND = LC + maxTask;
+    const int task = taskBase + blockIdx.x;
+    ANISO_STAMP(0, task, 0);
+    const int4 d = desc[task];  // first node, nodes, first point, levels
+    const int n0 = d.x, nt = d.y, ngrp = d.w;
+    const int64_t b0 = d.z;
+    const int* gs = grpFix + (size_t)task * (kTaskLevels + 1);
+    // M2M reads R[q][rr + 16 r] along rr: stage it transposed (r fastest) so the
+    // 16 lanes of one node hit 16 consecutive LDS words
+    for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) {
+        const int q = i >> 8, rr = (i >> 4) & 15, r = i & 15;
+        Rl[i] = P->R[q][rr + r * kRank];
+    }
+    for (int k = threadIdx.x; k < nt; k += blockDim.x) {
+        const double4 g = geom[n0 + k];
+        G[4 * k] = g.x;
+        G[4 * k + 1] = g.y;
+        G[4 * k + 2] = g.z;
+        G[4 * k + 3] = g.w;
+        const int2 lr = leafRange[n0 + k];
+        LB[k] = lr.x;
+        LC[k] = lr.y;
+        CD[k] = code[n0 + k];
+        ND[k] = node[n0 + k];
+    }
+    __syncthreads();
+    ANISO_STAMP(0, task, 1);
+    // P2M of the task's leaves (bbfmm.h:737-748): 16 lanes per leaf, one point per
+    // lane per pass (its 16 products in registers), then a 16-lane reduce-scatter
+    // leaves lane l with entry l.  The weighted charges are formed here from the
+    // apply's input (the reference's charge .* weights, AnisoWrapper.cpp:105-110).
+    {
+        const int gi = threadIdx.x >> 4, ln = threadIdx.x & 15, ngr = blockDim.x >> 4;
+        for (int k = gi; k < nt; k += ngr) {
+            if (CD[k].x != kLeafCode) continue;  // uniform over the 16 lanes
+            const double cx = G[4 * k], cy = G[4 * k + 1], irx = G[4 * k + 2], iry = G[4 * k + 3];
+            const int pe = LB[k] + LC[k];
+#pragma unroll 1
+            for (int b = 0; b < K; ++b) {
+                double acc[kRank];
+#pragma unroll
+                for (int e = 0; e < kRank; ++e) acc[e] = 0.0;
+                for (int p = LB[k] + ln; p < pe; p += 16) {
+                    const int64_t kp = b0 + p;
+                    const double c = input_charge(xin, ldi, b, treeIn, perm, sigT, kp);
+                    const double f = c * wT[kp];
+                    fT[kp * K + b] = f;  // for k_near and the corrections
+                    cT[kp * K + b] = c;
+                    double Sx[kNP], Sy[kNP];
+                    cheb_weights(P, (pxT[kp] - cx) * irx, Sx);
+                    cheb_weights(P, (pyT[kp] - cy) * iry, Sy);
+#pragma unroll
+                    for (int j = 0; j < kNP; ++j) {
+                        const double sf = Sy[j] * f;
+#pragma unroll
+                        for (int i = 0; i < kNP; ++i) acc[j * kNP + i] += Sx[i] * sf;
+                    }
+                }
+#define ANISO_RS16(NV, OFF)                                        \
+    {                                                              \
+        const bool hi = ln & (OFF);                                \
+        _Pragma("unroll") for (int e = 0; e < (NV); ++e) {         \
+            const double keep = hi ? acc[e + (NV)] : acc[e];       \
+            const double send = hi ? acc[e] : acc[e + (NV)];       \
+            acc[e] = keep + __shfl_xor(send, (OFF));               \
+        }                                                          \
+    }
+                ANISO_RS16(8, 8)
+                ANISO_RS16(4, 4)
+                ANISO_RS16(2, 2)
+                ANISO_RS16(1, 1)
+#undef ANISO_RS16
+                M[((size_t)k * kRank + ln) * K + b] = acc[0];
+            }
+        }
+    }
+    __syncthreads();
+    ANISO_STAMP(0, task, 2);
+    for (int g = 0; g < ngrp; ++g) {
+        const int s0 = gs[g], s1 = gs[g + 1];
+        for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
+            const int k = s0 + (it >> 4), r = it & (kRank - 1);
+            const int4 c = CD[k];
+            if (c.x == kLeafCode) continue;  // P2M above
+            double acc[K];
+#pragma unroll
+            for (int b = 0; b < K; ++b) acc[b] = 0.0;
+            const int cs[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (cs[q] == -1) continue;
+                const double* R = Rl + q * kRank * kRank + r;  // transposed: R[rr * 16 + r]
+                if (cs[q] >= 0) {  // child in this task (LDS)
+                    const double* cm = M + (size_t)cs[q] * kRank * K;
+#pragma unroll
+                    for (int rr = 0; rr < kRank; ++rr)
+#pragma unroll
+                        for (int b = 0; b < K; ++b) acc[b] += R[rr * kRank] * cm[rr * K + b];
+                } else {  // root of the tier below (HBM)
+                    const double* cm = mult + (size_t)(-cs[q] - 2) * kRank * K;
+#pragma unroll
+                    for (int rr = 0; rr < kRank; ++rr)
+#pragma unroll
+                        for (int b = 0; b < K; ++b) acc[b] += R[rr * kRank] * cm[rr * K + b];
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < K; ++b) M[((size_t)k * kRank + r) * K + b] = acc[b];
+        }
+        __syncthreads();
+    }
+    ANISO_STAMP(0, task, 3);
+    for (int it = threadIdx.x; it < nt * kRank * K; it += blockDim.x)
+        mult[(size_t)ND[it / (kRank * K)] * kRank * K + it % (kRank * K)] = M[it];
+    ANISO_STAMP(0, task, 4);
+}
+
+// ----------------------------------------------------------------- M2L
+
+// M2L over the V then X lists with the cached merged 16x16 operators
+// (bbfmm.h:1051-1065).  HBM-bound stream: one wave per target node, each pair's
+// 2 KB operator is read as 64 lanes x 32 contiguous bytes (two dwordx4 loads).
+// Blocks are column-major (K[t][s] at s*16 + t): lane l owns column s = l>>2 and
+// rows 4(l&3)..4(l&3)+3.  Forward product: per lane partial sums over its column
+// for its 4 rows and every right-hand side, one 16-lane reduction per target.
+// Symmetric storage: the target's stored pairs are
+// [directed | canonical]; for a canonical pair (n, B) the same block also gives
+// B's contribution sgn * K^T mult[n] (4 in-lane FMAs + a DPP quad reduction per
+// right-hand side), stored to the receiver's partial slot and gathered by
+// k_m2l_gather.  Wave-uniform indexing (readfirstlane) keeps descriptors and
+// source ids on the scalar unit; PG blocks (PG x 2 KB) are in flight per wave.
+// Mixed entry s of a source multipole, every right-hand side.
+template <int K>
+__device__ __forceinline__ void m2l_source(const double* __restrict__ mult, const MixK<K>& mix, int srcId, int s,
+                                           double (&xm)[K]) {
+    double base[K];
+    const double* m = mult + ((size_t)srcId * kRank + s) * K;
+#pragma unroll
+    for (int b = 0; b < K; ++b) base[b] = m[b];
+    mix_apply(mix, base, xm);
+}
+
+// Forward contribution of G column-major blocks: lane (s, q) adds K[4q+j][s] x[s].
+template <int K, int G>
+__device__ __forceinline__ void m2l_forward(const dbl2 (&kb)[G][2], const double (&xm)[G][K], double (&c)[4][K]) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            c[0][i] += kb[g][0].x * xm[g][i];
+            c[1][i] += kb[g][0].y * xm[g][i];
+            c[2][i] += kb[g][1].x * xm[g][i];
+            c[3][i] += kb[g][1].y * xm[g][i];
+        }
+}
+
+template <int K, int PG>
+__global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ tgt, const int64_t* __restrict__ ptr,
+                                             const int* __restrict__ nDir, const int* __restrict__ canonBase,
+                                             const int* __restrict__ outSlot, const int* __restrict__ src,
+                                             const double* __restrict__ Kop, const double* __restrict__ mult,
+                                             MixK<K> mix, double sgn, int accum, double* __restrict__ partial,
+                                             double* __restrict__ local) {
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) / kWave));
+    const int lane = threadIdx.x & (kWave - 1);
+    if (wave >= ntgt) return;
+    const int n = tgt[wave];
+    const int s = lane >> 2, q = lane & 3;  // column s, rows 4q .. 4q+3
+    const int64_t p0 = ptr[wave], p1 = ptr[wave + 1], pd = p0 + nDir[wave];
+    const int nC = (int)(p1 - pd);  // canonical pairs, <= kMaxCanon (host plan)
+    const int cSrc = lane < nC ? src[pd + lane] : 0;
+    const int cSlot = lane < nC ? outSlot[canonBase[wave] + lane] : 0;
+    double c[4][K];  // forward: rows 4q+j, this lane's column, each right-hand side
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < K; ++i) c[j][i] = 0.0;
+    // ---- directed pairs, PG blocks in flight
+    for (int64_t cb = p0; cb < pd; cb += kWave) {
+        const int cnt = (int)min<int64_t>(kWave, pd - cb);
+        const int mySrc = lane < cnt ? src[cb + lane] : 0;
+        for (int j = 0; j < cnt; j += PG) {
+            dbl2 kb[PG][2];
+            double xm[PG][K];
+#pragma unroll
+            for (int g = 0; g < PG; ++g) load_block(Kop, cb + j + g, lane, j + g < cnt, kb[g][0], kb[g][1]);
+#pragma unroll
+            for (int g = 0; g < PG; ++g)  // a skipped block's source is a valid clamp; its block is zero
+                m2l_source<K>(mult, mix, __builtin_amdgcn_readlane(mySrc, min(j + g, cnt - 1)), s, xm[g]);
+            m2l_forward<K, PG>(kb, xm, c);
+        }
+    }
+    // ---- canonical pairs: both products from one read of the block, 4 in flight
+    if (nC > 0) {
+        double mn[4][K];  // the target's mixed multipole, rows 4q+j, times sgn
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            double base[K];
+#pragma unroll
+            for (int b = 0; b < K; ++b) base[b] = mult[((size_t)n * kRank + 4 * q + j) * K + b];
+            mix_apply(mix, base, mn[j]);
+#pragma unroll
+            for (int i = 0; i < K; ++i) mn[j][i] *= sgn;
+        }
+        // transposed products stay in registers (lane (s, q) keeps entry s of pair
+        // 4g + q, every right-hand side) and are stored after the stream: on CDNA
+        // vmcnt also counts stores, so stores inside the loop would stall it
+        constexpr int kGroups = (kMaxCanon + 3) / 4;
+        double y[kGroups][K];
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) y[g][i] = 0.0;
+            const int j = 4 * g;
+            if (j < nC) {
+                dbl2 kb[4][2];
+                double xm[4][K];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) load_block(Kop, pd + j + u, lane, j + u < nC, kb[u][0], kb[u][1]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    m2l_source<K>(mult, mix, __builtin_amdgcn_readlane(cSrc, min(j + u, nC - 1)), s, xm[u]);
+                m2l_forward<K, 4>(kb, xm, c);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        const double v = quad_sum(kb[u][0].x * mn[0][i] + kb[u][0].y * mn[1][i] +
+                                                  kb[u][1].x * mn[2][i] + kb[u][1].y * mn[3][i]);
+                        if (u == q) y[g][i] = v;
+                    }
+            }
+        }
+        // partial slots: lane (s, q) stores entry s of pair 4g + q (K contiguous
+        // doubles; 16 K contiguous per pair); slot ids shuffled with every lane active
+#pragma unroll
+        for (int g = 0; g < kGroups; ++g) {
+            if (4 * g < nC) {
+                const int jj = 4 * g + q;
+                const int slot = __shfl(cSlot, jj);
+                if (jj < nC) {
+                    double* dst = partial + ((size_t)slot * kRank + s) * K;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) dst[i] = y[g][i];
+                }
+            }
+        }
+    }
+    // ---- sum the forward partials over the 16 columns (lane bits 2..5); then row
+    // t = 4q' + j is entry j of the lanes with q == q' (e.g. lane 4t + (t>>2))
+#pragma unroll
+    for (int off = 4; off < kWave; off <<= 1)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < K; ++i) c[j][i] += __shfl_xor(c[j][i], off);
+    const int t = s;  // this lane writes row t (= its column index), right-hand sides i == q (mod 4)
+    const int jr = t & 3, srcLane = 4 * t + (t >> 2);
+    double* dst = local + ((size_t)n * kRank + t) * K;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const double sel = jr == 0 ? c[0][i] : jr == 1 ? c[1][i] : jr == 2 ? c[2][i] : c[3][i];
+        const double v = __shfl(sel, srcLane);
+        if ((i & 3) == q) dst[i] = accum ? dst[i] + v : v;
+    }
+}
+
+// local[B] += the transposed canonical-pair products addressed to B: one
+// contiguous slot range per target, summed in a fixed order (deterministic).
+// One thread per (target, entry, right-hand side); 8 loads in flight per thread.
+template <int K>
+__global__ void __launch_bounds__(256) k_m2l_gather(int ntgt, const int* __restrict__ tgt,
+                                                    const int* __restrict__ inPtr, const double* __restrict__ partial,
+                                                    double* __restrict__ local) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t w = gid / (kRank * K);
+    const int e = (int)(gid - w * (kRank * K));  // entry * K + rhs
+    if (w >= ntgt) return;
+    const int j0 = inPtr[w], j1 = inPtr[w + 1];
+    if (j0 == j1) return;
+    const double* pp = partial + (size_t)j0 * kRank * K + e;
+    const int n = j1 - j0;
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int j = 0;
+    for (; j + 7 < n; j += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] += __builtin_nontemporal_load(pp + (size_t)(j + u) * kRank * K);
+    }
+#pragma unroll
+    for (int u = 0; u < 7; ++u)
+        if (j + u < n) a[u] += __builtin_nontemporal_load(pp + (size_t)(j + u) * kRank * K);
+    local[(size_t)tgt[w] * kRank * K + e] += ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+// ----------------------------------------------------------------- near field
+
+// U/W near field for one target leaf per wave (bbfmm.h:1081-1099, 1111-1113).
+// All per-leaf indexing comes from host-built descriptors loaded lane-parallel:
+//   leafInfo[li] = (node, begin, count, S), nearPts = the S source tree positions.
+// The mixed source charges are staged in LDS ([S][K]).  The block is column-major
+// nTs x S (rows padded to even nTs): each lane reads 16 B = two targets of one
+// source column; lanes = (row pair, column phase), 4 independent loads in flight.
+// Canonical U pairs (host: both leaves <= 128 points): the same
+// column read also gives the other leaf's transposed product sgn * sum_t K[t][s]
+// f[t], reduced over the column's lanes, staged in LDS over the consumed charges
+// and stored after the stream.  accum: add to out and to the partials (later
+// modes of a block apply) instead of storing.
+template <int K>
+__global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ leafInfo,
+                                              const int64_t* __restrict__ nearPtsPtr, const int* __restrict__ nearPts,
+                                              const int64_t* __restrict__ nearKOff, const int2* __restrict__ nearSym,
+                                              const double* __restrict__ Kop, const double* __restrict__ fT,
+                                              MixK<K> mix, const int* __restrict__ operm, int64_t obase, int64_t ldo,
+                                              int maxS, int flags, double sgn, double scale, int accum,
+                                              double* __restrict__ partial, double* __restrict__ out) {
+    extern __shared__ double sh[];
+    const int wv = threadIdx.x / kWave, lane = threadIdx.x & (kWave - 1);
+    const int li = blockIdx.x * (blockDim.x / kWave) + wv;
+    const bool active = li < nl;
+    double* fs = sh + (size_t)wv * maxS * K;
+    int4 info = make_int4(0, 0, 0, 0);
+    int64_t koff = 0;
+    if (active) {
+        info = leafInfo[li];
+        const int64_t pb = nearPtsPtr[li];
+        koff = nearKOff[li];
+        // stage the S mixed source charges (lane-parallel gather, 4 points in flight per lane)
+        const int S = info.w;
+        for (int s0 = 0; s0 < S; s0 += 4 * kWave) {
+            int ix[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int sidx = s0 + u * kWave + lane;
+                ix[u] = sidx < S ? nearPts[pb + sidx] : -1;
+            }
+            double fv[4][K];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int b = 0; b < K; ++b) fv[u][b] = ix[u] >= 0 ? fT[(size_t)ix[u] * K + b] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int sidx = s0 + u * kWave + lane;
+                double v[K];
+                mix_apply(mix, fv[u], v);
+                if (sidx < S)
+#pragma unroll
+                    for (int i = 0; i < K; ++i) fs[(size_t)sidx * K + i] = v[i];
+            }
+        }
+    }
+    __syncthreads();
+    if (!active) return;
+    const int nT = info.z, S = info.w;
+    const int2 sym = nearSym[li];  // (directed source points Sdir, partial base)
+    const int Sdir = sym.x;
+    const int64_t tb = info.y;
+    const double* Kl = Kop + koff;
+    const int nTs = nT + (nT & 1);
+    const int rp = nTs >> 1;
+    int lpc = 1;
+    while (lpc < rp && lpc < kWave) lpc <<= 1;
+    const int cps = kWave / lpc;
+    const int cph = lane / lpc;
+    for (int rc = 0; rc < rp; rc += kWave) {
+        const int r = rc + (lane & (lpc - 1));
+        double a0[K], a1[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) a0[i] = a1[i] = 0.0;
+        if ((flags & kStageNear) && S > Sdir) {
+            const dbl2* kc = reinterpret_cast<const dbl2*>(Kl) + r;
+            double fa0[K], fa1[K];  // this leaf's mixed charges at rows 2r, 2r+1, times sgn
+            {
+                double b0[K], b1[K];
+#pragma unroll
+                for (int b = 0; b < K; ++b) {
+                    b0[b] = (r < rp && 2 * r < nT) ? fT[(size_t)(tb + 2 * r) * K + b] : 0.0;
+                    b1[b] = (r < rp && 2 * r + 1 < nT) ? fT[(size_t)(tb + 2 * r + 1) * K + b] : 0.0;
+                }
+                mix_apply(mix, b0, fa0);
+                mix_apply(mix, b1, fa1);
+            }
+            const int ncol = S - Sdir;
+            for (int i0 = 0; i0 < ncol; i0 += 4 * cps) {  // 4 columns per lane in flight
+                dbl2 kk[4];
+                bool ok[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int sc = Sdir + i0 + u * cps + cph;
+                    ok[u] = (i0 + u * cps + cph < ncol) && r < rp;
+                    kk[u] = ok[u] ? __builtin_nontemporal_load(kc + (size_t)sc * rp) : dbl2{0.0, 0.0};
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int sc = Sdir + i0 + u * cps + cph;
+                    double* fc = fs + (size_t)sc * K;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        const double fsv = ok[u] ? fc[i] : 0.0;
+                        a0[i] += kk[u].x * fsv;
+                        a1[i] += kk[u].y * fsv;
+                    }
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        double cc = kk[u].x * fa0[i] + kk[u].y * fa1[i];
+                        for (int off = 1; off < lpc; off <<= 1) cc += __shfl_xor(cc, off);
+                        // column sc's charges are consumed: its LDS words now hold the
+                        // product, stored after the stream (vmcnt also counts stores)
+                        if (ok[u] && (lane & (lpc - 1)) == 0) fc[i] = sgn * cc;
+                    }
+                }
+            }
+        }
+        if ((flags & kStageNear) && r < rp) {
+            const dbl2* kc = reinterpret_cast<const dbl2*>(Kl) + r;
+            int sc = cph;
+            for (; sc + 3 * cps < Sdir; sc += 4 * cps) {
+                dbl2 kk[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) kk[u] = __builtin_nontemporal_load(kc + (size_t)(sc + u * cps) * rp);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double* fc = fs + (size_t)(sc + u * cps) * K;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        a0[i] += kk[u].x * fc[i];
+                        a1[i] += kk[u].y * fc[i];
+                    }
+                }
+            }
+            for (; sc < Sdir; sc += cps) {
+                const dbl2 k0 = __builtin_nontemporal_load(kc + (size_t)sc * rp);
+                const double* fc = fs + (size_t)sc * K;
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    a0[i] += k0.x * fc[i];
+                    a1[i] += k0.y * fc[i];
+                }
+            }
+        }
+        for (int off = lpc; off < kWave; off <<= 1)
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                a0[i] += __shfl_xor(a0[i], off);
+                a1[i] += __shfl_xor(a1[i], off);
+            }
+        if (cph == 0 && r < rp) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int t = 2 * r + h;
+                if (t >= nT) break;
+                const int64_t o = out_index(operm, obase, tb + t);
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    const double v = scale * (h ? a1[i] : a0[i]);
+                    double* dst = out + (size_t)i * ldo + o;
+                    *dst = accum ? *dst + v : v;
+                }
+            }
+        }
+    }
+    if ((flags & kStageNear) && S > Sdir) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int nv = (S - Sdir) * K;
+        double* dst = partial + (size_t)sym.y * K;
+        for (int i = lane; i < nv; i += kWave) dst[i] = accum ? dst[i] + fs[(size_t)Sdir * K + i] : fs[(size_t)Sdir * K + i];
+    }
+}
+
+// ----------------------------------------------------------------- down pass
+
+// Down pass (bbfmm.h:1066-1106) over the owned subtree tasks, after k_m2l,
+// k_m2l_gather and k_near.  Every task rebuilds its root's parent total from the
+// ancestors' locals (L2L chain from level 1), so all tasks are independent.  Per
+// node: total = local (its M2L, transposed partials included) + L2L of the
+// parent's total (bbfmm.h:1070-1071).  Then per owned leaf point: L2P
+// (bbfmm.h:1104) + the gathered transposed U-pair products, added to out.
+// dn = (node, parent code: LDS slot, -1 none/zero, -2 the task root; child slot, 0).
+// Phase 0 issues every independent global load of the task at once (locals of
+// all nodes and chain ancestors, leaf boxes, near partial offsets) into LDS.
+template <int K>
+__global__ void __launch_bounds__(kTierThreads) k_down_tier(
+    int maxTask, int maxLeaves, const int4* __restrict__ desc, const int* __restrict__ grpFix,
+    const int4* __restrict__ dn, const double* __restrict__ local, const Params* __restrict__ P,
+    const int* __restrict__ leafSlot, const int* __restrict__ leafBegin, const int2* __restrict__ leafNear,
+    const double4* __restrict__ leafGeom, const double* __restrict__ pxT, const double* __restrict__ pyT,
+    const int* __restrict__ operm, int64_t obase, int64_t ldo, const int* __restrict__ nearOff, int maxNear,
+    const double* __restrict__ nearPart, const int2* __restrict__ chain, int maxChain, int flags, double scale,
+    double* __restrict__ out) {
+    constexpr int RK = kRank * K;
+    extern __shared__ double sm[];
+    int4* DN = reinterpret_cast<int4*>(sm);                // maxTask node records
+    double* Rl = reinterpret_cast<double*>(DN + maxTask);  // 4 x 256 transfer matrices
+    double* T = Rl + 4 * kRank * kRank;                    // maxTask x 16 x K totals
+    double* PT = T + (size_t)maxTask * RK;                 // 16 x K: the task root's parent total
+    double* CH = PT + RK;                                  // maxChain x 16 x K: the ancestors' locals
+    double* G = CH + (size_t)maxChain * RK;                // maxLeaves x 4: leaf cx, cy, 1/rx, 1/ry
+    int* LB = reinterpret_cast<int*>(G + (size_t)maxLeaves * 4);  // maxLeaves + 1: leaf begins
+    int* LS = LB + maxLeaves + 1;                          // maxLeaves: leaf slot in the task
+    int* NB = LS + maxLeaves;                              // maxLeaves: first of the leaf's near offsets in NO
+    int* NC = NB + maxLeaves;                              // maxLeaves: their count
+    int* NO = NC + maxLeaves;                              // maxNear: partial offsets addressed to this task
+    const int task = blockIdx.x;
+    ANISO_STAMP(1, task, 0);
+    // task record: (first node, nodes, first leaf entry, leaves), (owned points begin,
+    // end, first chain entry, chain length), (first near offset, count, levels, 0)
+    const int4 d0 = desc[3 * task], d1 = desc[3 * task + 1], d2 = desc[3 * task + 2];
+    const int n0 = d0.x, nt = d0.y, l0 = d0.z, nl = d0.w;
+    const int2 pr = make_int2(d1.x, d1.y);
+    const int c0 = d1.z, nc = d1.w;
+    const int npts = pr.y - pr.x, ngrp = d2.z;
+    const int* gs = grpFix + (size_t)task * (kTaskLevels + 1);
+    const bool far = flags & kStageFar;
+    // ---- phase 0: independent loads
+    if (far) {
+        for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) Rl[i] = (&P->R[0][0])[i];
+        for (int k = threadIdx.x; k < nt; k += blockDim.x) DN[k] = dn[n0 + k];
+        for (int it = threadIdx.x; it < nt * RK; it += blockDim.x)
+            T[it] = local[(size_t)dn[n0 + it / RK].x * RK + it % RK];
+        for (int it = threadIdx.x; it < nc * RK; it += blockDim.x)
+            CH[it] = local[(size_t)chain[c0 + it / RK].x * RK + it % RK];
+    }
+    for (int e = threadIdx.x; e < nl; e += blockDim.x) {
+        LB[e] = leafBegin[l0 + e];
+        LS[e] = leafSlot[l0 + e];
+        const int2 ni = leafNear[l0 + e];
+        NB[e] = ni.x;
+        NC[e] = ni.y;
+        const double4 g = leafGeom[l0 + e];
+        G[4 * e] = g.x;
+        G[4 * e + 1] = g.y;
+        G[4 * e + 2] = g.z;
+        G[4 * e + 3] = g.w;
+    }
+    if (threadIdx.x == 0) LB[nl] = pr.y;
+    for (int j = threadIdx.x; j < d2.y; j += blockDim.x) NO[j] = nearOff[d2.x + j];
+    __syncthreads();
+    ANISO_STAMP(1, task, 1);
+    // ---- phase 1: the root's parent total by the L2L chain from level 1
+    // (bbfmm.h:1070-1071 along the ancestors), then the task's levels
+    if (far) {
+        if constexpr (RK <= kWave) {  // one wave, lane (r, i) = r K + i; no barrier per step
+            if (threadIdx.x < kWave) {
+                const int r = threadIdx.x / K, i = threadIdx.x - (threadIdx.x / K) * K;
+                double v = (nc > 0 && threadIdx.x < RK) ? CH[threadIdx.x] : 0.0;
+                for (int jc = 1; jc < nc; ++jc) {
+                    const double* R = Rl + chain[c0 + jc].y * kRank * kRank;
+                    double a = threadIdx.x < RK ? CH[jc * RK + threadIdx.x] : 0.0;
+#pragma unroll
+                    for (int c = 0; c < kRank; ++c) a += R[(r & 15) + c * kRank] * __shfl(v, c * K + i);
+                    v = a;
+                }
+                if (threadIdx.x < RK) PT[threadIdx.x] = v;
+            }
+        } else {  // PT holds the running total; one thread per (entry, rhs), barriers per step
+            for (int it = threadIdx.x; it < RK; it += blockDim.x) PT[it] = nc > 0 ? CH[it] : 0.0;
+            __syncthreads();
+            for (int jc = 1; jc < nc; ++jc) {
+                const double* R = Rl + chain[c0 + jc].y * kRank * kRank;
+                const int r = threadIdx.x / K, i = threadIdx.x - (threadIdx.x / K) * K;
+                double a = 0.0;
+                if (threadIdx.x < RK) {
+                    a = CH[jc * RK + threadIdx.x];
+#pragma unroll
+                    for (int c = 0; c < kRank; ++c) a += R[r + c * kRank] * PT[c * K + i];
+                }
+                __syncthreads();
+                if (threadIdx.x < RK) PT[threadIdx.x] = a;
+                __syncthreads();
+            }
+        }
+        __syncthreads();
+        ANISO_STAMP(1, task, 2);
+        for (int g = 0; g < ngrp; ++g) {
+            const int s0 = gs[g], s1 = gs[g + 1];
+            for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
+                const int k = s0 + (it >> 4), r = it & (kRank - 1);
+                const int4 d = DN[k];
+                if (d.y == -1) continue;
+                const double* pt = d.y >= 0 ? T + (size_t)d.y * RK : PT;  // -2: the task root
+                const double* R = Rl + d.z * kRank * kRank;
+                double l2l[K];
+#pragma unroll
+                for (int i = 0; i < K; ++i) l2l[i] = 0.0;
+#pragma unroll
+                for (int c = 0; c < kRank; ++c) {
+                    const double rc = R[r + c * kRank];
+#pragma unroll
+                    for (int i = 0; i < K; ++i) l2l[i] += rc * pt[c * K + i];
+                }
+#pragma unroll
+                for (int i = 0; i < K; ++i) T[((size_t)k * kRank + r) * K + i] += l2l[i];
+            }
+            __syncthreads();
+        }
+    }
+    ANISO_STAMP(1, task, 3);
+    // ---- phase 2: owned points: L2P + near gather
+    for (int g = threadIdx.x; g < npts; g += blockDim.x) {
+        const int kpos = pr.x + g;
+        int lo = 0, hi = nl - 1;  // last leaf with LB <= kpos
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (LB[mid] <= kpos) lo = mid;
+            else hi = mid - 1;
+        }
+        const int t = kpos - LB[lo];
+        double v[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) v[i] = 0.0;
+        if (flags & kStageNear) {
+            const int* no = NO + NB[lo];
+            for (int j = 0; j < NC[lo]; ++j) {
+                const double* pp = nearPart + ((size_t)no[j] + t) * K;
+#pragma unroll
+                for (int i = 0; i < K; ++i) v[i] += pp[i];
+            }
+        }
+        if (far) {
+            const double x = pxT[kpos], y = pyT[kpos];
+            double Sx[kNP], Sy[kNP];
+            cheb_weights(P, (x - G[4 * lo]) * G[4 * lo + 2], Sx);
+            cheb_weights(P, (y - G[4 * lo + 1]) * G[4 * lo + 3], Sy);
+            const double* L = T + (size_t)LS[lo] * RK;
+            double l2p[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) l2p[i] = 0.0;
+#pragma unroll
+            for (int j = 0; j < kNP; ++j)
+#pragma unroll
+                for (int ii = 0; ii < kNP; ++ii) {
+                    const double w = Sx[ii] * Sy[j];
+#pragma unroll
+                    for (int i = 0; i < K; ++i) l2p[i] += w * L[(j * kNP + ii) * K + i];
+                }
+#pragma unroll
+            for (int i = 0; i < K; ++i) v[i] += l2p[i];
+        }
+        const int64_t o = out_index(operm, obase, kpos);
+#pragma unroll
+        for (int i = 0; i < K; ++i) out[(size_t)i * ldo + o] += scale * v[i];
+    }
+    ANISO_STAMP(1, task, 4);
+}
+
+// ----------------------------------------------------------------- corrections
+
+// Corrections (nearRemoval + refineAddOnFast + singularAddFast,
+// KernelFactory.cpp:445-478, 662-709, 828-860) as a 3x3-square stencil with
+// per-mode translation-invariant d2 x 9 x d2 weights, plus the singular term
+// from Legendre coefficients of the target's own square (O(d^4) moments).  Every
+// contribution carries the final 1/(2 pi) (AnisoWrapper.cpp:129-130): k_near
+// stores (or adds) its scaled sum, k_corr and k_down_tier add theirs.
+template <int D, int K>
+__global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* __restrict__ perm,
+                                              const int* __restrict__ iperm, const double* __restrict__ cT,
+                                              const double* __restrict__ fT, MixK<K> mix,
+                                              const double* __restrict__ C, const double* __restrict__ mu,
+                                              const Params* __restrict__ P, int flags, double scale, bool treeOut,
+                                              int64_t ldo, double* __restrict__ out) {
+    constexpr int D2 = D * D;
+    int64_t k = b + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= e) return;
+    const int t = perm[k];
+    const int sz = P->sz;
+    const int sq = t / D2, tq = t - sq * D2;
+    const int i = sq / sz, j = sq - i * sz;
+    double acc[K];
+#pragma unroll
+    for (int r = 0; r < K; ++r) acc[r] = 0.0;
+    if (flags & kStageStencil) {
+        double base[K];  // the stencil is linear: weight the base charges, mix once
+#pragma unroll
+        for (int r = 0; r < K; ++r) base[r] = 0.0;
+#pragma unroll
+        for (int dr = -1; dr <= 1; ++dr) {
+            if (i + dr < 0 || i + dr >= sz) continue;
+#pragma unroll
+            for (int dc = -1; dc <= 1; ++dc) {
+                if (j + dc < 0 || j + dc >= sz) continue;
+                const int q9 = (dr + 1) * 3 + (dc + 1);
+                const double* w = C + ((size_t)tq * 9 + q9) * D2;
+                const int* it = iperm + (size_t)(sq + dr * sz + dc) * D2;  // the square's points, tree positions
+#pragma unroll
+                for (int c = 0; c < D2; ++c) {
+                    const double* f = fT + (size_t)it[c] * K;
+#pragma unroll
+                    for (int r = 0; r < K; ++r) base[r] += w[c] * f[r];
+                }
+            }
+        }
+        mix_apply(mix, base, acc);
+    }
+    if (flags & kStageSing) {
+        const int* it = iperm + (size_t)sq * D2;
+        const double X = (0.5 + i) * P->dx, Y = (0.5 + j) * P->dx;
+        double bx[D][D], by[D][D];
+#pragma unroll
+        for (int n = 0; n < D; ++n)
+#pragma unroll
+            for (int a = 0; a < D; ++a) {
+                double sx = 0.0, sy = 0.0, px = 1.0, py = 1.0;
+#pragma unroll
+                for (int e2 = 0; e2 < D; ++e2) {
+                    double cb = P->legB[(n * D + a) * D + e2];
+                    sx += cb * px;
+                    sy += cb * py;
+                    px *= X;
+                    py *= Y;
+                }
+                bx[n][a] = sx;
+                by[n][a] = sy;
+            }
+        const double* m = mu + (size_t)tq * D * D;
+        double mom[D][D];  // the square's moments, shared by every right-hand side
+#pragma unroll
+        for (int n = 0; n < D; ++n)
+#pragma unroll
+            for (int kk = 0; kk < D; ++kk) {
+                double a2 = 0.0;
+#pragma unroll
+                for (int a = 0; a <= n; ++a)
+#pragma unroll
+                    for (int bb = 0; bb <= kk; ++bb) a2 += bx[n][a] * by[kk][bb] * m[a * D + bb];
+                mom[n][kk] = a2;
+            }
+        double base[K];  // the term is linear in the charges: per base charge, then mixed
+#pragma unroll 1
+        for (int r = 0; r < K; ++r) {
+            double hw[D2];
+#pragma unroll
+            for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cT[(size_t)it[c] * K + r];
+            double sg = 0.0;
+#pragma unroll
+            for (int n = 0; n < D; ++n)
+#pragma unroll
+                for (int kk = 0; kk < D; ++kk) {
+                    // Legendre coefficient c_{n,k} = (interpolate * (sqrtW .* h))_{nk} / norm_nk
+                    double cf = 0.0;
+#pragma unroll
+                    for (int q = 0; q < D2; ++q) cf += P->interp[(n * D + kk) + q * D2] * hw[q];
+                    sg += cf * P->coefScale[n * D + kk] * mom[n][kk];
+                }
+            base[r] = sg;
+        }
+        double sing[K];
+        mix_apply(mix, base, sing);
+#pragma unroll
+        for (int r = 0; r < K; ++r) acc[r] += sing[r];
+    }
+    const int64_t o = treeOut ? k - b : (int64_t)t;
+#pragma unroll
+    for (int r = 0; r < K; ++r) out[(size_t)r * ldo + o] += acc[r] * scale;
+}
+
+// ----------------------------------------------------------------- launchers
+
+template <int K>
+static MixK<K> make_mix(const double* m) {  // m: K x K row-major host array
+    MixK<K> x;
+    for (int i = 0; i < K; ++i)
+        for (int b = 0; b < K; ++b) x.c[i][b] = m[i * K + b];
+    return x;
+}
+
+#define ANISO_DISPATCH_K(k, CALL)                               \
+    switch (k) {                                                \
+        case 1: { constexpr int KK = 1; CALL; } break;          \
+        case 2: { constexpr int KK = 2; CALL; } break;          \
+        case 4: { constexpr int KK = 4; CALL; } break;          \
+        case 5: { constexpr int KK = 5; CALL; } break;          \
+        case 8: { constexpr int KK = 8; CALL; } break;          \
+        default: throw std::invalid_argument("unsupported right-hand-side count " + std::to_string(k)); \
+    }
+
+bool rhs_supported(int k) { return k == 1 || k == 2 || k == 4 || k == 5 || k == 8; }
+int rhs_padded(int k) {
+    for (int c : {1, 2, 4, 5, 8})
+        if (k <= c) return c;
+    return -1;
+}
+
+void launch_prepare(int K, int64_t N, const double* xin, int64_t ldi, int treeIn, const int* perm,
+                    const double* sigT, const double* wT, double* fT, double* cT, hipStream_t s) {
+    if (N <= 0) return;
+    ANISO_DISPATCH_K(K, (k_prepare<KK><<<blocks_for(N, 256), 256, 0, s>>>(N, xin, ldi, treeIn, perm, sigT, wT, fT, cT)));
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_sub_slice(int64_t n, int nrhs, const double* x, int64_t ldx, const double* a, int64_t lda, double* y,
+                      int64_t ldy, hipStream_t s) {
+    if (n <= 0 || nrhs <= 0) return;
+    k_sub_slice<<<blocks_for(n * nrhs, 256), 256, 0, s>>>(n, nrhs, x, ldx, a, lda, y, ldy);
+    HIP_LAUNCH_CHECK();
+}
+
+size_t up_tier_lds(int maxTask, int K) {
+    return (size_t)(4 * kRank * kRank + maxTask * (kRank * K + 4)) * sizeof(double) +
+           (size_t)3 * maxTask * sizeof(int) + (size_t)maxTask * sizeof(int4);
+}
+
+size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain, int K) {
+    return (size_t)(4 * kRank * kRank + (maxTask + 1 + maxChain) * kRank * K + 4 * maxLeaves) * sizeof(double) +
+           (size_t)(4 * maxLeaves + 4 + maxNear) * sizeof(int) + (size_t)maxTask * sizeof(int4);
+}
+
+void launch_up_tier(int K, int ntask, int taskBase, int maxTask, const int4* desc, const int* grpFix, const int* node,
+                    const int4* code, const double4* geom, const int2* leafRange, const double* pxT, const double* pyT,
+                    const double* xin, int64_t ldi, int treeIn, const int* perm, const double* sigT, const double* wT,
+                    double* fT, double* cT, const Params* P, double* mult, hipStream_t s) {
+    if (ntask <= 0) return;
+    const size_t shm = up_tier_lds(maxTask, K);
+    ANISO_DISPATCH_K(K, (k_up_tier<KK><<<ntask, kUpThreads, shm, s>>>(taskBase, maxTask, desc, grpFix, node, code, geom,
+                                                                      leafRange, pxT, pyT, xin, ldi, treeIn, perm, sigT,
+                                                                      wT, fT, cT, P, mult)));
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_m2l(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
+                const int* outSlot, const int* src, const double* Kop, const double* mult, const double* mix,
+                double sgn, int accum, double* partial, double* local, hipStream_t s) {
+    if (ntgt <= 0) return;
+    const unsigned nb = blocks_for((int64_t)ntgt * kWave, 256);
+    // blocks in flight per wave: 4 (8 KB) for one or two right-hand sides, 2 above
+    ANISO_DISPATCH_K(K, (k_m2l<KK, (KK <= 2 ? 4 : 2)><<<nb, 256, 0, s>>>(ntgt, tgt, ptr, nDir, canonBase, outSlot, src,
+                                                                          Kop, mult, make_mix<KK>(mix), sgn, accum,
+                                                                          partial, local)));
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_m2l_gather(int K, int ntgt, const int* tgt, const int* inPtr, const double* partial, double* local,
+                       hipStream_t s) {
+    if (ntgt <= 0) return;
+    const unsigned nb = blocks_for((int64_t)ntgt * kRank * K, 256);
+    ANISO_DISPATCH_K(K, (k_m2l_gather<KK><<<nb, 256, 0, s>>>(ntgt, tgt, inPtr, partial, local)));
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_near(int K, int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
+                 const int64_t* nearKOff, const int2* nearSym, const double* Kop, const double* fT, const double* mix,
+                 const int* operm, int64_t obase, int64_t ldo, int maxS, int flags, double sgn, double scale,
+                 int accum, double* partial, double* out, hipStream_t s) {
+    if (nl <= 0) return;
+    const int S = maxS > 0 ? maxS : 1;
+    const int wpb = (size_t)S * K * 8 * 4 <= 48 * 1024 ? 4 : 1;  // waves per block, LDS = waves x S x K doubles
+    const size_t shm = (size_t)wpb * S * K * sizeof(double);
+    if (shm > 160 * 1024) throw std::invalid_argument("near field: leaf neighbourhood too large for LDS");
+    ANISO_DISPATCH_K(K, (k_near<KK><<<blocks_for(nl, wpb), wpb * kWave, shm, s>>>(
+                            nl, leafInfo, nearPtsPtr, nearPts, nearKOff, nearSym, Kop, fT, make_mix<KK>(mix), operm,
+                            obase, ldo, S, flags, sgn, scale, accum, partial, out)));
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* desc, const int* grpFix,
+                      const int4* dn, const double* local, const Params* P, const int* leafSlot, const int* leafBegin,
+                      const int2* leafNear, const double4* leafGeom, const double* pxT, const double* pyT,
+                      const int* operm, int64_t obase, int64_t ldo, const int* nearOff, int maxNear,
+                      const double* nearPart, const int2* chain, int maxChain, int flags, double scale, double* out,
+                      hipStream_t s) {
+    if (ntask <= 0) return;
+    const size_t shm = down_tier_lds(maxTask, maxLeaves, maxNear, maxChain, K);
+    ANISO_DISPATCH_K(K, (k_down_tier<KK><<<ntask, kTierThreads, shm, s>>>(
+                            maxTask, maxLeaves, desc, grpFix, dn, local, P, leafSlot, leafBegin, leafNear, leafGeom,
+                            pxT, pyT, operm, obase, ldo, nearOff, maxNear, nearPart, chain, maxChain, flags, scale,
+                            out)));
+    HIP_LAUNCH_CHECK();
+}
+
+template <int D>
+static void corr_d(int K, unsigned nb, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT,
+                   const double* fT, const double* mix, const double* C, const double* mu, const Params* P, int flags,
+                   double scale, bool treeOut, int64_t ldo, double* out, hipStream_t s) {
+    ANISO_DISPATCH_K(K, (k_corr<D, KK><<<nb, 256, 0, s>>>(b, e, perm, iperm, cT, fT, make_mix<KK>(mix), C, mu, P,
+                                                          flags, scale, treeOut, ldo, out)));
+}
+
+void launch_corr(int K, int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT,
+                 const double* fT, const double* mix, const double* C, const double* mu, const Params* P, int flags,
+                 double scale, bool treeOut, int64_t ldo, double* out, hipStream_t s) {
+    if (e <= b) return;
+    const unsigned nb = blocks_for(e - b, 256);
+    switch (d) {
+        case 1: corr_d<1>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
+        case 2: corr_d<2>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
+        case 3: corr_d<3>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
+        case 4: corr_d<4>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
+        case 5: corr_d<5>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
+        case 6: corr_d<6>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
+        default: throw std::invalid_argument("quadRule out of range");
+    }
+    HIP_LAUNCH_CHECK();
+}
+
+}  // namespace aniso

@@ -159,7 +159,7 @@ int aniso_mapping_batched(aniso_handle h, const double* Q, int k, int id, double
         CHECK_PTR(Out);
         if (k < 0) throw std::invalid_argument("k must be >= 0");
         auto& op = get(h);
-        for (int j = 0; j < k; ++j) op.mappingHost(Q + (size_t)j * op.geo.N, id, Out + (size_t)j * op.geo.N);
+        op.mappingBatchedHost(Q, k, id, Out);
     });
 }
 
@@ -191,6 +191,37 @@ int aniso_forward_tree_dev(aniso_handle h, const double* x_tree, double* y_slice
         auto& op = get(h);
         if (!op.modeCached(0)) throw std::runtime_error("forward operator before cache(0)");
         op.forwardTreeDev(x_tree, y_slice, (hipStream_t)stream);
+    });
+}
+
+int aniso_apply_block_dev(aniso_handle h, int nrhs, const double* x, int64_t ldx, int use_sigma, int nterm,
+                          const int* ids, const double* mixes, double* out, int64_t ldo, int tree, void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(x);
+        CHECK_PTR(out);
+        CHECK_PTR(ids);
+        CHECK_PTR(mixes);
+        get(h).applyBlockDev(nrhs, x, ldx, tree != 0, use_sigma != 0, nterm, ids, mixes, out, ldo, tree != 0,
+                             (hipStream_t)stream);
+    });
+}
+
+int aniso_block_op_dev(aniso_handle h, int which, const double* x, int64_t ldx, double* out, int64_t ldo, int tree,
+                       void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(x);
+        CHECK_PTR(out);
+        get(h).blockOpDev(which, x, ldx, out, ldo, tree != 0, (hipStream_t)stream);
+    });
+}
+
+int aniso_block_mixes(int nb, double g, int chi, double* mixes) {
+    return guarded([&] {
+        CHECK_PTR(mixes);
+        const auto m = aniso::Operator::blockMixes(nb, g, chi != 0);
+        std::copy(m.begin(), m.end(), mixes);
     });
 }
 

@@ -1,0 +1,86 @@
+// device_common.hpp -- device helpers shared by the apply kernels (apply.hip) and
+// the cache-build kernels (kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.hpp"
+
+namespace aniso {
+
+[[noreturn]] void throw_hip(hipError_t e, const char* file, int line);
+
+#define HIP_LAUNCH_CHECK()                                                                  \
+    do {                                                                                    \
+        hipError_t e__ = hipGetLastError();                                                 \
+        if (e__ != hipSuccess) throw_hip(e__, __FILE__, __LINE__);                          \
+    } while (0)
+
+constexpr int kWave = 64;
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+static inline unsigned blocks_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+// Chebyshev interpolant S(s, c_i) = (-1 + 2 sum_l T_l(s) T_l(c_i)) / np  (bbfmm.h:635-656, 737-748)
+__device__ __forceinline__ void cheb_weights(const Params* __restrict__ P, double s, double* S) {
+    double T[kNP];
+    T[0] = 1.0;
+    T[1] = s;
+#pragma unroll
+    for (int l = 2; l < kNP; ++l) T[l] = 2.0 * s * T[l - 1] - T[l - 2];
+#pragma unroll
+    for (int i = 0; i < kNP; ++i) {
+        double acc = 0.0;
+#pragma unroll
+        for (int l = 0; l < kNP; ++l) acc += T[l] * P->tnode[i + l * kNP];
+        S[i] = (2.0 * acc - 1.0) * (1.0 / kNP);
+    }
+}
+
+// One Chebyshev interpolant weight S(s, c_i) (same arithmetic as cheb_weights).
+__device__ __forceinline__ double cheb_weight1(const Params* __restrict__ P, double s, int i) {
+    double T[kNP];
+    T[0] = 1.0;
+    T[1] = s;
+#pragma unroll
+    for (int l = 2; l < kNP; ++l) T[l] = 2.0 * s * T[l - 1] - T[l - 2];
+    double acc = 0.0;
+#pragma unroll
+    for (int l = 0; l < kNP; ++l) acc += T[l] * P->tnode[i + l * kNP];
+    return (2.0 * acc - 1.0) * (1.0 / kNP);
+}
+
+// Lane-quad exchange through DPP quad_perm (no LDS round trip).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double quad_sum(double v) {
+    v += dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
+    return v;
+}
+
+// One 2 KB block as 64 lanes x 32 B: lane l reads doubles 4l .. 4l+3.  `ok`
+// is wave-uniform: a skipped block reads as zeros (the predicated tail of a
+// group costs no extra round trip).
+__device__ __forceinline__ void load_block(const double* __restrict__ K, int64_t p, int lane, bool ok, dbl2& x0,
+                                           dbl2& x1) {
+    x0 = dbl2{0.0, 0.0};
+    x1 = dbl2{0.0, 0.0};
+    if (ok) {
+        const dbl2* k = reinterpret_cast<const dbl2*>(K + (size_t)p * 256) + 2 * lane;
+        x0 = __builtin_nontemporal_load(k);
+        x1 = __builtin_nontemporal_load(k + 1);
+    }
+}
+
+
+
+
+}  // namespace aniso

@@ -34,39 +34,53 @@ enum StageMask : int {
     kStageAll = 15,
 };
 
-void launch_prepare(int64_t N, const double* xin, int treeIn, const int* perm, const double* sigT, const double* wT,
-                    double* fT, double* cT, hipStream_t s);
 constexpr int kTierThreads = 256;  // workgroup of the down pass tasks
 // up pass tasks: 256 threads (P2M holds 16 products per lane, ~94 VGPRs = 5 waves
 // per SIMD), so four workgroups fit per CU and 1,024 tasks run in one round
 constexpr int kUpThreads = 256;
-size_t up_tier_lds(int maxTask);
-size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain);
-void launch_up_tier(int ntask, int taskBase, int maxTask, const int4* desc, const int* grpFix, const int* node,
+
+// ---- apply kernels (apply.hip), batched over K right-hand sides.
+// K is a runtime argument dispatched to compiled instances (rhs_supported); the
+// operator pads other counts with zero right-hand sides (rhs_padded).  Vectors are
+// [K][ld] (rhs-major); tree-order work arrays fT/cT are [N][K], expansions
+// [node][16][K].  `mix` is a K x K row-major matrix: the kernels of one mode
+// apply it to the base inputs on the fly (rhs i = sum_b mix[i][b] base b).
+bool rhs_supported(int k);
+int rhs_padded(int k);  // smallest supported count >= k, or -1
+void launch_prepare(int K, int64_t N, const double* xin, int64_t ldi, int treeIn, const int* perm,
+                    const double* sigT, const double* wT, double* fT, double* cT, hipStream_t s);
+size_t up_tier_lds(int maxTask, int K);
+size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain, int K);
+void launch_up_tier(int K, int ntask, int taskBase, int maxTask, const int4* desc, const int* grpFix, const int* node,
                     const int4* code, const double4* geom, const int2* leafRange, const double* pxT, const double* pyT,
-                    const double* xin, int treeIn, const int* perm, const double* sigT, const double* wT, double* fT,
-                    double* cT, const Params* P, double* mult, hipStream_t s);
-void launch_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
-                const int* outSlot, const int* src, const double* K, const double* mult, double sgn, double* partial,
-                double* local, hipStream_t s);
-void launch_m2l_gather(int ntgt, const int* tgt, const int* inPtr, const double* partial, double* local,
+                    const double* xin, int64_t ldi, int treeIn, const int* perm, const double* sigT, const double* wT,
+                    double* fT, double* cT, const Params* P, double* mult, hipStream_t s);
+// accum = 0 stores local, 1 adds to it (later modes of a block apply)
+void launch_m2l(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
+                const int* outSlot, const int* src, const double* Kop, const double* mult, const double* mix,
+                double sgn, int accum, double* partial, double* local, hipStream_t s);
+void launch_m2l_gather(int K, int ntgt, const int* tgt, const int* inPtr, const double* partial, double* local,
                        hipStream_t s);
 // Output index mode of k_near / k_down_tier / k_corr: operm = perm writes the
 // original-order vector out[perm[k]]; operm = nullptr writes the owned tree-order
-// slice out[k - obase].
-void launch_near(int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts, const int64_t* nearKOff,
-                 const int2* nearSym, const double* K, const double* fT, const int* operm, int64_t obase, int maxS,
-                 int flags, double sgn, double scale, double* partial, double* out, hipStream_t s);
-void launch_down_tier(int ntask, int maxTask, int maxLeaves, const int4* desc, const int* grpFix, const int4* dn,
-                      const double* local, const Params* P, const int* leafSlot, const int* leafBegin,
+// slice out[k - obase].  ldo = the stride between right-hand sides of out.
+void launch_near(int K, int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
+                 const int64_t* nearKOff, const int2* nearSym, const double* Kop, const double* fT, const double* mix,
+                 const int* operm, int64_t obase, int64_t ldo, int maxS, int flags, double sgn, double scale,
+                 int accum, double* partial, double* out, hipStream_t s);
+void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* desc, const int* grpFix,
+                      const int4* dn, const double* local, const Params* P, const int* leafSlot, const int* leafBegin,
                       const int2* leafNear, const double4* leafGeom, const double* pxT, const double* pyT,
-                      const int* operm, int64_t obase, const int* nearOff, int maxNear, const double* nearPart,
-                      const int2* chain, int maxChain, int flags, double scale, double* out, hipStream_t s);
-void launch_corr(int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT, const double* fT,
-                 const double* C,
-                 const double* mu, const Params* P, int flags, double scale, bool treeOut, double* out,
-                 hipStream_t s);
-void launch_sub_slice(int64_t n, const double* x, const double* a, double* y, hipStream_t s);
+                      const int* operm, int64_t obase, int64_t ldo, const int* nearOff, int maxNear,
+                      const double* nearPart, const int2* chain, int maxChain, int flags, double scale, double* out,
+                      hipStream_t s);
+void launch_corr(int K, int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT,
+                 const double* fT, const double* mix, const double* C, const double* mu, const Params* P, int flags,
+                 double scale, bool treeOut, int64_t ldo, double* out, hipStream_t s);
+void launch_sub_slice(int64_t n, int nrhs, const double* x, int64_t ldx, const double* a, int64_t lda, double* y,
+                      int64_t ldy, hipStream_t s);
+
+// ---- cache build and helpers (kernels.hip)
 void launch_cache_m2l(int64_t npairs, const int* pairTgt, const int* src, const double* ncx, const double* ncy,
                       const double* nrx, const double* nry, const double* stcoef, const Params* P, int mode,
                       double* K, hipStream_t s);

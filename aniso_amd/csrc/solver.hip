@@ -22,11 +22,6 @@ namespace aniso {
 
 constexpr int kRedBlocks = 512;
 
-__global__ void k_mul(int64_t n, const double* __restrict__ a, const double* __restrict__ b, double* __restrict__ c) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) c[i] = a[i] * b[i];
-}
-
 // y = alpha x + beta y
 __global__ void k_axpby(int64_t n, double alpha, const double* __restrict__ x, double beta, double* __restrict__ y) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -89,8 +84,7 @@ struct DeviceBlas {
 void Operator::forwardDev(const double* u, double* out, hipStream_t s) {
     if (plan.nranks != 1) throw std::logic_error("forward operator on a sharded handle: gather first");
     ensureDevice();
-    k_mul<<<nblk(geo.N), 256, 0, s>>>(geo.N, u, dSigmaS.as<double>(), dTmp.as<double>());
-    mappingDev(dTmp.as<double>(), 0, dTmp2.as<double>(), s, kStageAll);
+    apply(u, false, dSigmaT.as<double>(), 0, dTmp2.as<double>(), false, s, kStageAll);  // sigma_s .* u inside the up pass
     k_sub<<<nblk(geo.N), 256, 0, s>>>(geo.N, u, dTmp2.as<double>(), out);
 }
 

@@ -119,3 +119,19 @@ def test_no_cpu_fallback_without_gpu():
     with pytest.raises(aniso_amd.AnisoError) as e:
         a.setCoeff(np.ones(a.N), np.ones(a.N))  # needs the HIP device
     assert e.value.code == 2
+
+
+@pytest.mark.parametrize("nb,g", [(1, 0.8), (3, 0.5), (5, 0.8)])
+def test_block_mixes_follow_aniso_m(nb, g):
+    """aniso.m:121-157: output block iid gets chi_|j| K_{|iid+j|} u_|j| for every
+    j in [-(nb-1), nb-1]; the mixes regroup those terms by mode."""
+    for chi in (False, True):
+        got = aniso_amd.block_mixes(nb, g, chi)
+        ref = np.zeros((2 * nb - 1, nb, nb))
+        for i in range(-(nb - 1), 1):
+            iid = abs(i)
+            for j in range(-(nb - 1), nb):
+                b = abs(j)
+                w = (g ** b - g ** nb) / (1 - g ** nb) if chi else 1.0
+                ref[abs(i - j), iid, b] += w
+        assert np.array_equal(got, ref)
