@@ -66,6 +66,11 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     kernelSize = 2 * ks - 1;
     geo.build(sz, d, ns);
     tree.build(geo.px.data(), geo.py.data(), geo.N, np * np, maxLevel, host_threads());
+    // symmetric U storage pays for single right-hand sides; a block handle (ks > 1,
+    // the aniso.m operator) reads every near block directed.
+    // ANISO_NEAR_SYMMETRIC=0/1 overrides.
+    plan.nearSymmetric = ks == 1;
+    if (const char* e = std::getenv("ANISO_NEAR_SYMMETRIC")) plan.nearSymmetric = e[0] == '1';
     plan.build(tree, np, 0, 1);
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
@@ -199,8 +204,8 @@ void Operator::ensureDevice() {
 void Operator::ensureWork(int K) {
     if (K <= workK) return;
     workK = K;
-    dFT.alloc((size_t)geo.N * K * sizeof(double));
-    dCT.alloc((size_t)geo.N * K * sizeof(double));
+    dFT.alloc((size_t)geo.N * rhs_stride(K) * sizeof(double));
+    dCT.alloc((size_t)geo.N * rhs_stride(K) * sizeof(double));
     dMult.alloc((size_t)tree.nn * kRank * K * sizeof(double));
     dLocal.alloc((size_t)tree.nn * kRank * K * sizeof(double));
     HIP_CHECK(hipMemset(dMult.p, 0, dMult.bytes));
@@ -479,9 +484,15 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         const int acc = t > 0 ? 1 : 0;
         // K_{B<-A} = (-1)^m K_{A<-B}^T for the merged kernel; Id = m
         const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
-        launch_near(K, (int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(),
-                    dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(), dFT.as<double>(), mix, operm,
-                    obase, ldo, maxNearS, mask, sgn, scale, acc, dNearPart.as<double>(), out, s);
+        if (plan.nearPartTotal > 0)  // symmetric U storage: transposed products to partials
+            launch_near_sym(K, (int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
+                            dNearPts.as<int>(), dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(),
+                            dFT.as<double>(), mix, operm, obase, ldo, maxNearS, mask, sgn, scale, acc,
+                            dNearPart.as<double>(), out, s);
+        else
+            launch_near(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
+                        dNearPts.as<int>(), dNearKOff.as<int64_t>(), mc.Knear.as<double>(), dFT.as<double>(), mix, operm,
+                        obase, ldo, mask, scale, acc, out, s);
         int e = tm ? mark(s) : -1;
         span(4, ep, e);
         ep = e;

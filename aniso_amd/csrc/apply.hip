@@ -15,7 +15,7 @@
 // depend on the mode, so locals and transposed near products accumulate over the
 // modes of a call and the down pass runs once.
 //
-// Layouts (K fastest): fT, cT [N][K] tree order; mult, local [node][16][K];
+// Layouts (K fastest): fT, cT [N][KS] tree order (KS = K rounded up to even); mult, local [node][16][K];
 // M2L partials [slot][16][K]; near partials [column][K]; outputs [K][ldo].
 #include <hip/hip_runtime.h>
 
@@ -43,6 +43,11 @@ extern "C" int aniso_probe_read(unsigned long long* host) {
     do {                     \
     } while (0)
 #endif
+
+// Row stride of the tree-order charge arrays fT/cT [N][KS]: K rounded up to even
+// (K > 1) so a row is whole 16-B vectors.
+template <int K>
+constexpr int kStride = (K == 1 || K % 2 == 0) ? K : K + 1;
 
 template <int K>
 struct MixK {
@@ -87,8 +92,8 @@ __global__ void k_prepare(int64_t N, const double* __restrict__ xin, int64_t ldi
 #pragma unroll
     for (int b = 0; b < K; ++b) {
         const double c = input_charge(xin, ldi, b, treeIn, perm, sigT, k);
-        fT[k * K + b] = c * wT[k];
-        cT[k * K + b] = c;
+        fT[k * kStride<K> + b] = c * wT[k];
+        cT[k * kStride<K> + b] = c;
     }
 }
 
@@ -172,8 +177,8 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
                     const int64_t kp = b0 + p;
                     const double c = input_charge(xin, ldi, b, treeIn, perm, sigT, kp);
                     const double f = c * wT[kp];
-                    fT[kp * K + b] = f;  // for k_near and the corrections
-                    cT[kp * K + b] = c;
+                    fT[kp * kStride<K> + b] = f;  // for k_near and the corrections
+                    cT[kp * kStride<K> + b] = c;
                     double Sx[kNP], Sy[kNP];
                     cheb_weights(P, (pxT[kp] - cx) * irx, Sx);
                     cheb_weights(P, (pyT[kp] - cy) * iry, Sy);
@@ -250,22 +255,20 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
 // 2 KB operator is read as 64 lanes x 32 contiguous bytes (two dwordx4 loads).
 // Blocks are column-major (K[t][s] at s*16 + t): lane l owns column s = l>>2 and
 // rows 4(l&3)..4(l&3)+3.  Forward product: per lane partial sums over its column
-// for its 4 rows and every right-hand side, one 16-lane reduction per target.
+// for its 4 rows and every base vector, one 16-lane reduction and the mode's mix
+// per target.
 // Symmetric storage: the target's stored pairs are
 // [directed | canonical]; for a canonical pair (n, B) the same block also gives
 // B's contribution sgn * K^T mult[n] (4 in-lane FMAs + a DPP quad reduction per
 // right-hand side), stored to the receiver's partial slot and gathered by
 // k_m2l_gather.  Wave-uniform indexing (readfirstlane) keeps descriptors and
 // source ids on the scalar unit; PG blocks (PG x 2 KB) are in flight per wave.
-// Mixed entry s of a source multipole, every right-hand side.
+// Entry s of a source multipole (base vectors), every right-hand side.
 template <int K>
-__device__ __forceinline__ void m2l_source(const double* __restrict__ mult, const MixK<K>& mix, int srcId, int s,
-                                           double (&xm)[K]) {
-    double base[K];
+__device__ __forceinline__ void m2l_source(const double* __restrict__ mult, int srcId, int s, double (&xm)[K]) {
     const double* m = mult + ((size_t)srcId * kRank + s) * K;
 #pragma unroll
-    for (int b = 0; b < K; ++b) base[b] = m[b];
-    mix_apply(mix, base, xm);
+    for (int b = 0; b < K; ++b) xm[b] = m[b];
 }
 
 // Forward contribution of G column-major blocks: lane (s, q) adds K[4q+j][s] x[s].
@@ -314,7 +317,7 @@ __global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ t
             for (int g = 0; g < PG; ++g) load_block(Kop, cb + j + g, lane, j + g < cnt, kb[g][0], kb[g][1]);
 #pragma unroll
             for (int g = 0; g < PG; ++g)  // a skipped block's source is a valid clamp; its block is zero
-                m2l_source<K>(mult, mix, __builtin_amdgcn_readlane(mySrc, min(j + g, cnt - 1)), s, xm[g]);
+                m2l_source<K>(mult, __builtin_amdgcn_readlane(mySrc, min(j + g, cnt - 1)), s, xm[g]);
             m2l_forward<K, PG>(kb, xm, c);
         }
     }
@@ -347,7 +350,7 @@ __global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ t
                 for (int u = 0; u < 4; ++u) load_block(Kop, pd + j + u, lane, j + u < nC, kb[u][0], kb[u][1]);
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    m2l_source<K>(mult, mix, __builtin_amdgcn_readlane(cSrc, min(j + u, nC - 1)), s, xm[u]);
+                    m2l_source<K>(mult, __builtin_amdgcn_readlane(cSrc, min(j + u, nC - 1)), s, xm[u]);
                 m2l_forward<K, 4>(kb, xm, c);
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
@@ -382,14 +385,24 @@ __global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ t
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int i = 0; i < K; ++i) c[j][i] += __shfl_xor(c[j][i], off);
+    // The forward sums are over base multipoles: the mode's mix is applied once
+    // per target row here (linear), not per pair.
     const int t = s;  // this lane writes row t (= its column index), right-hand sides i == q (mod 4)
     const int jr = t & 3, srcLane = 4 * t + (t >> 2);
+    double v[K];
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+        const double sel = jr == 0 ? c[0][b] : jr == 1 ? c[1][b] : jr == 2 ? c[2][b] : c[3][b];
+        v[b] = __shfl(sel, srcLane);
+    }
     double* dst = local + ((size_t)n * kRank + t) * K;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        const double sel = jr == 0 ? c[0][i] : jr == 1 ? c[1][i] : jr == 2 ? c[2][i] : c[3][i];
-        const double v = __shfl(sel, srcLane);
-        if ((i & 3) == q) dst[i] = accum ? dst[i] + v : v;
+        if ((i & 3) != q) continue;
+        double w = 0.0;
+#pragma unroll
+        for (int b = 0; b < K; ++b) w += mix.c[i][b] * v[b];
+        dst[i] = accum ? dst[i] + w : w;
     }
 }
 
@@ -422,19 +435,31 @@ __global__ void __launch_bounds__(256) k_m2l_gather(int ntgt, const int* __restr
 
 // ----------------------------------------------------------------- near field
 
-// U/W near field for one target leaf per wave (bbfmm.h:1081-1099, 1111-1113).
-// All per-leaf indexing comes from host-built descriptors loaded lane-parallel:
+// Sum over the lpc lanes of a column group (lpc a power of two, wave-uniform):
+// DPP quad exchanges for the first two steps, swizzles above.
+__device__ __forceinline__ double group_sum(double v, int lpc) {
+    if (lpc >= 2) v += dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
+    if (lpc >= 4) v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
+    for (int off = 4; off < lpc; off <<= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// U/W near field with symmetric U storage, one target leaf per wave
+// (bbfmm.h:1081-1099, 1111-1113).  All per-leaf indexing comes from host-built descriptors loaded lane-parallel:
 //   leafInfo[li] = (node, begin, count, S), nearPts = the S source tree positions.
-// The mixed source charges are staged in LDS ([S][K]).  The block is column-major
-// nTs x S (rows padded to even nTs): each lane reads 16 B = two targets of one
-// source column; lanes = (row pair, column phase), 4 independent loads in flight.
-// Canonical U pairs (host: both leaves <= 128 points): the same
-// column read also gives the other leaf's transposed product sgn * sum_t K[t][s]
-// f[t], reduced over the column's lanes, staged in LDS over the consumed charges
-// and stored after the stream.  accum: add to out and to the partials (later
-// modes of a block apply) instead of storing.
+// The S base source charges are staged in LDS ([S][K], unmixed).  The block is
+// column-major nT4 x S (rows padded to a multiple of 4): lane (row quad rq,
+// column phase) reads 32 B = rows 4rq..4rq+3 of one column, two to four columns
+// in flight.  Forward: per-lane sums over its columns of the base charges, one
+// cross-lane reduction per leaf, then the mode's mix applied to the nT outputs
+// (linear: mixing the sums equals summing the mixed charges, at nT instead of S
+// mixes).  Canonical U pairs (host: both leaves <= 128 points):
+// the same column read also gives the other leaf's transposed product
+// sgn * sum_t K[t][s] f_mix[t], reduced over the column's lanes (DPP), staged in
+// LDS over the consumed charges and stored after the stream.  accum: add to out
+// and to the partials (later modes of a block apply) instead of storing.
 template <int K>
-__global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ leafInfo,
+__global__ void __launch_bounds__(256) k_near_sym(int nl, const int4* __restrict__ leafInfo,
                                               const int64_t* __restrict__ nearPtsPtr, const int* __restrict__ nearPts,
                                               const int64_t* __restrict__ nearKOff, const int2* __restrict__ nearSym,
                                               const double* __restrict__ Kop, const double* __restrict__ fT,
@@ -452,28 +477,20 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
         info = leafInfo[li];
         const int64_t pb = nearPtsPtr[li];
         koff = nearKOff[li];
-        // stage the S mixed source charges (lane-parallel gather, 4 points in flight per lane)
-        const int S = info.w;
-        for (int s0 = 0; s0 < S; s0 += 4 * kWave) {
-            int ix[4];
+        // stage the S x K base charges: lane-contiguous (source, rhs) entries (the
+        // points of one source leaf are contiguous in tree order), 4 in flight
+        const int SK = info.w * K;
+        for (int e0 = 0; e0 < SK; e0 += 4 * kWave) {
+            double fv[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int sidx = s0 + u * kWave + lane;
-                ix[u] = sidx < S ? nearPts[pb + sidx] : -1;
+                const int e = e0 + u * kWave + lane;
+                fv[u] = e < SK ? fT[(size_t)nearPts[pb + e / K] * kStride<K> + e % K] : 0.0;
             }
-            double fv[4][K];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int b = 0; b < K; ++b) fv[u][b] = ix[u] >= 0 ? fT[(size_t)ix[u] * K + b] : 0.0;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int sidx = s0 + u * kWave + lane;
-                double v[K];
-                mix_apply(mix, fv[u], v);
-                if (sidx < S)
-#pragma unroll
-                    for (int i = 0; i < K; ++i) fs[(size_t)sidx * K + i] = v[i];
+                const int e = e0 + u * kWave + lane;
+                if (e < SK) fs[e] = fv[u];
             }
         }
     }
@@ -483,117 +500,271 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
     const int2 sym = nearSym[li];  // (directed source points Sdir, partial base)
     const int Sdir = sym.x;
     const int64_t tb = info.y;
-    const double* Kl = Kop + koff;
-    const int nTs = nT + (nT & 1);
-    const int rp = nTs >> 1;
-    int lpc = 1;
-    while (lpc < rp && lpc < kWave) lpc <<= 1;
+    const int nq = (nT + 3) >> 2;  // row quads
+    const int cstr = 2 * nq;       // column stride in 16-B units
+    int lpc = 1;                   // lanes per column
+    while (lpc < nq && lpc < kWave) lpc <<= 1;
     const int cps = kWave / lpc;
     const int cph = lane / lpc;
-    for (int rc = 0; rc < rp; rc += kWave) {
-        const int r = rc + (lane & (lpc - 1));
-        double a0[K], a1[K];
+    const bool nearOn = flags & kStageNear;
+    for (int rc = 0; rc < nq; rc += kWave) {  // > 64 row quads: leaves over 256 points (directed only)
+        const int rq = rc + (lane & (lpc - 1));
+        const bool rowOk = rq < nq;
+        const dbl2* kc = reinterpret_cast<const dbl2*>(Kop + koff) + 2 * rq;
+        double a[4][K];  // forward: rows 4rq+j, base charges
 #pragma unroll
-        for (int i = 0; i < K; ++i) a0[i] = a1[i] = 0.0;
-        if ((flags & kStageNear) && S > Sdir) {
-            const dbl2* kc = reinterpret_cast<const dbl2*>(Kl) + r;
-            double fa0[K], fa1[K];  // this leaf's mixed charges at rows 2r, 2r+1, times sgn
-            {
-                double b0[K], b1[K];
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int b = 0; b < K; ++b) {
-                    b0[b] = (r < rp && 2 * r < nT) ? fT[(size_t)(tb + 2 * r) * K + b] : 0.0;
-                    b1[b] = (r < rp && 2 * r + 1 < nT) ? fT[(size_t)(tb + 2 * r + 1) * K + b] : 0.0;
-                }
-                mix_apply(mix, b0, fa0);
-                mix_apply(mix, b1, fa1);
+            for (int b = 0; b < K; ++b) a[j][b] = 0.0;
+        if (nearOn && S > Sdir) {
+            double fa[4][K];  // this leaf's mixed charges at rows 4rq+j, times sgn
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double bv[K];
+                const bool ok = rowOk && 4 * rq + j < nT;
+#pragma unroll
+                for (int b = 0; b < K; ++b) bv[b] = ok ? fT[(size_t)(tb + 4 * rq + j) * kStride<K> + b] : 0.0;
+                mix_apply(mix, bv, fa[j]);
+#pragma unroll
+                for (int i = 0; i < K; ++i) fa[j][i] *= sgn;
             }
             const int ncol = S - Sdir;
-            for (int i0 = 0; i0 < ncol; i0 += 4 * cps) {  // 4 columns per lane in flight
-                dbl2 kk[4];
-                bool ok[4];
+            for (int i0 = 0; i0 < ncol; i0 += 2 * cps) {  // 2 columns per lane in flight
+                dbl2 kk[2][2];
+                bool ok[2];
+                int sc[2];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int sc = Sdir + i0 + u * cps + cph;
-                    ok[u] = (i0 + u * cps + cph < ncol) && r < rp;
-                    kk[u] = ok[u] ? __builtin_nontemporal_load(kc + (size_t)sc * rp) : dbl2{0.0, 0.0};
+                for (int u = 0; u < 2; ++u) {
+                    const int c = i0 + u * cps + cph;
+                    ok[u] = c < ncol && rowOk;
+                    sc[u] = Sdir + min(c, ncol - 1);
+                    const dbl2* p = kc + (size_t)sc[u] * cstr;
+                    kk[u][0] = ok[u] ? __builtin_nontemporal_load(p) : dbl2{0.0, 0.0};
+                    kk[u][1] = ok[u] ? __builtin_nontemporal_load(p + 1) : dbl2{0.0, 0.0};
                 }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int sc = Sdir + i0 + u * cps + cph;
-                    double* fc = fs + (size_t)sc * K;
+                for (int u = 0; u < 2; ++u) {
+                    double* fc = fs + (size_t)sc[u] * K;
+                    const double k4[4] = {kk[u][0].x, kk[u][0].y, kk[u][1].x, kk[u][1].y};
 #pragma unroll
-                    for (int i = 0; i < K; ++i) {
-                        const double fsv = ok[u] ? fc[i] : 0.0;
-                        a0[i] += kk[u].x * fsv;
-                        a1[i] += kk[u].y * fsv;
-                    }
+                    for (int b = 0; b < K; ++b) {
+                        const double fv = fc[b];
 #pragma unroll
-                    for (int i = 0; i < K; ++i) {
-                        double cc = kk[u].x * fa0[i] + kk[u].y * fa1[i];
-                        for (int off = 1; off < lpc; off <<= 1) cc += __shfl_xor(cc, off);
-                        // column sc's charges are consumed: its LDS words now hold the
-                        // product, stored after the stream (vmcnt also counts stores)
-                        if (ok[u] && (lane & (lpc - 1)) == 0) fc[i] = sgn * cc;
+                        for (int j = 0; j < 4; ++j) a[j][b] += k4[j] * fv;
                     }
+                    double y[K];
+#pragma unroll
+                    for (int i = 0; i < K; ++i)
+                        y[i] = group_sum(k4[0] * fa[0][i] + k4[1] * fa[1][i] + k4[2] * fa[2][i] + k4[3] * fa[3][i],
+                                         lpc);
+                    // column sc's charges are consumed (every lane of the group has
+                    // read them above): its LDS words now hold the product, stored
+                    // after the stream (vmcnt also counts stores)
+                    if (ok[u] && (lane & (lpc - 1)) == 0)
+#pragma unroll
+                        for (int i = 0; i < K; ++i) fc[i] = y[i];
                 }
             }
         }
-        if ((flags & kStageNear) && r < rp) {
-            const dbl2* kc = reinterpret_cast<const dbl2*>(Kl) + r;
+        if (nearOn && rowOk) {
             int sc = cph;
             for (; sc + 3 * cps < Sdir; sc += 4 * cps) {
-                dbl2 kk[4];
+                dbl2 kk[4][2];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) kk[u] = __builtin_nontemporal_load(kc + (size_t)(sc + u * cps) * rp);
+                for (int u = 0; u < 4; ++u) {
+                    const dbl2* p = kc + (size_t)(sc + u * cps) * cstr;
+                    kk[u][0] = __builtin_nontemporal_load(p);
+                    kk[u][1] = __builtin_nontemporal_load(p + 1);
+                }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const double* fc = fs + (size_t)(sc + u * cps) * K;
 #pragma unroll
-                    for (int i = 0; i < K; ++i) {
-                        a0[i] += kk[u].x * fc[i];
-                        a1[i] += kk[u].y * fc[i];
+                    for (int b = 0; b < K; ++b) {
+                        const double fv = fc[b];
+                        a[0][b] += kk[u][0].x * fv;
+                        a[1][b] += kk[u][0].y * fv;
+                        a[2][b] += kk[u][1].x * fv;
+                        a[3][b] += kk[u][1].y * fv;
                     }
                 }
             }
             for (; sc < Sdir; sc += cps) {
-                const dbl2 k0 = __builtin_nontemporal_load(kc + (size_t)sc * rp);
+                const dbl2* p = kc + (size_t)sc * cstr;
+                const dbl2 k0 = __builtin_nontemporal_load(p), k1 = __builtin_nontemporal_load(p + 1);
                 const double* fc = fs + (size_t)sc * K;
 #pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    a0[i] += k0.x * fc[i];
-                    a1[i] += k0.y * fc[i];
+                for (int b = 0; b < K; ++b) {
+                    const double fv = fc[b];
+                    a[0][b] += k0.x * fv;
+                    a[1][b] += k0.y * fv;
+                    a[2][b] += k1.x * fv;
+                    a[3][b] += k1.y * fv;
                 }
             }
         }
+        // sum over the column phases (lane bits above the column group)
         for (int off = lpc; off < kWave; off <<= 1)
 #pragma unroll
-            for (int i = 0; i < K; ++i) {
-                a0[i] += __shfl_xor(a0[i], off);
-                a1[i] += __shfl_xor(a1[i], off);
-            }
-        if (cph == 0 && r < rp) {
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int t = 2 * r + h;
+                for (int b = 0; b < K; ++b) a[j][b] += __shfl_xor(a[j][b], off);
+        if (cph == 0 && rowOk) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int t = 4 * rq + j;
                 if (t >= nT) break;
                 const int64_t o = out_index(operm, obase, tb + t);
+                double v[K];
+                mix_apply(mix, a[j], v);
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
-                    const double v = scale * (h ? a1[i] : a0[i]);
                     double* dst = out + (size_t)i * ldo + o;
-                    *dst = accum ? *dst + v : v;
+                    *dst = accum ? *dst + scale * v[i] : scale * v[i];
                 }
             }
         }
     }
-    if ((flags & kStageNear) && S > Sdir) {
+    if (nearOn && S > Sdir) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int nv = (S - Sdir) * K;
         double* dst = partial + (size_t)sym.y * K;
-        for (int i = lane; i < nv; i += kWave) dst[i] = accum ? dst[i] + fs[(size_t)Sdir * K + i] : fs[(size_t)Sdir * K + i];
+        const double* src = fs + (size_t)Sdir * K;
+        for (int i = lane; i < nv; i += kWave) dst[i] = accum ? dst[i] + src[i] : src[i];
+    }
+}
+
+// Load the K charges of one tree position (row of fT / cT, stride kStride<K>).
+template <int K>
+__device__ __forceinline__ void load_charges(const double* __restrict__ p, double (&c)[K]) {
+    if constexpr (K == 1) {
+        c[0] = p[0];
+    } else {
+#pragma unroll
+        for (int v = 0; v < kStride<K> / 2; ++v) {
+            const dbl2 x = reinterpret_cast<const dbl2*>(p)[v];
+            c[2 * v] = x.x;
+            if (2 * v + 1 < K) c[2 * v + 1] = x.y;
+        }
+    }
+}
+
+// U/W near field, directed storage (every U/W block stored for its target; the
+// layout of block applies): G lanes per target leaf (G = 16 when
+// every leaf has <= 16 points, 4 leaves per wave; else 64).  The block is
+// column-major nT4 x S (rows padded to a multiple of 4); lane (row quad rq, column
+// phase) reads 32 B = rows 4rq..4rq+3 of a column and the column's K base charges
+// straight from fT (L1/L2: the lanes of a column share the line), U columns in
+// flight per lane.  Forward sums per lane over its columns, one reduction over the
+// column phases (DPP row rotations for G = 16), then the mode's mix at the nT
+// outputs.  No LDS, no partials.
+template <int K, int G, int U>
+__global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ leafInfo,
+                                              const int64_t* __restrict__ nearPtsPtr, const int* __restrict__ nearPts,
+                                              const int64_t* __restrict__ nearKOff, const double* __restrict__ Kop,
+                                              const double* __restrict__ fT, MixK<K> mix,
+                                              const int* __restrict__ operm, int64_t obase, int64_t ldo, int flags,
+                                              double scale, int accum, double* __restrict__ out) {
+    static_assert(G == 16 || G == 64, "leaf group of 16 or 64 lanes");
+    constexpr int KS = kStride<K>;
+    const int gl = threadIdx.x & (G - 1);
+    const int li = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
+    const bool active = li < nl;
+    int4 info = make_int4(0, 0, 0, 0);
+    int64_t pb = 0, koff = 0;
+    if (active) {
+        info = leafInfo[li];
+        pb = nearPtsPtr[li];
+        koff = nearKOff[li];
+    }
+    const int nT = info.z, S = (flags & kStageNear) ? info.w : 0;
+    const int64_t tb = info.y;
+    const int nq = (nT + 3) >> 2;  // row quads
+    const int cstr = 2 * nq;       // column stride in 16-B units
+    int lpc = 4;                   // lanes per column (G = 16: leaves <= 16 points, 4 quads)
+    if constexpr (G == 64) {
+        lpc = 1;
+        while (lpc < nq && lpc < kWave) lpc <<= 1;
+    }
+    const int cps = G / lpc, cph = gl / lpc;
+    for (int rc = 0; rc < nq || rc == 0; rc += G) {  // > 64 row quads: leaves over 256 points
+        const int rq = rc + (gl & (lpc - 1));
+        const bool rowOk = active && rq < nq;
+        const dbl2* kc = reinterpret_cast<const dbl2*>(Kop + koff) + 2 * rq;
+        double a[4][K];  // rows 4rq+j, base charges
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int b = 0; b < K; ++b) a[j][b] = 0.0;
+        if (rowOk) {
+            for (int c0 = cph; c0 < S; c0 += U * cps) {
+                int ix[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int sc = c0 + u * cps;
+                    ix[u] = nearPts[pb + min(sc, S - 1)];
+                }
+                dbl2 kk[U][2];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int sc = c0 + u * cps;
+                    const dbl2* p = kc + (size_t)min(sc, S - 1) * cstr;
+                    const bool ok = sc < S;
+                    kk[u][0] = ok ? __builtin_nontemporal_load(p) : dbl2{0.0, 0.0};
+                    kk[u][1] = ok ? __builtin_nontemporal_load(p + 1) : dbl2{0.0, 0.0};
+                }
+                double f[U][K];
+#pragma unroll
+                for (int u = 0; u < U; ++u) load_charges<K>(fT + (size_t)ix[u] * KS, f[u]);
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+#pragma unroll
+                    for (int b = 0; b < K; ++b) {
+                        a[0][b] += kk[u][0].x * f[u][b];
+                        a[1][b] += kk[u][0].y * f[u][b];
+                        a[2][b] += kk[u][1].x * f[u][b];
+                        a[3][b] += kk[u][1].y * f[u][b];
+                    }
+            }
+        }
+        // sum over the column phases: G = 16 -> lanes 4 and 8 apart in a 16-lane row
+        if constexpr (G == 16) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int b = 0; b < K; ++b) {
+                    double v = a[j][b];
+                    v += dpp_f64<0x124>(v);  // row_ror:4
+                    v += dpp_f64<0x128>(v);  // row_ror:8
+                    a[j][b] = v;
+                }
+        } else {
+            for (int off = lpc; off < kWave; off <<= 1)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int b = 0; b < K; ++b) a[j][b] += __shfl_xor(a[j][b], off);
+        }
+        // column phase p writes rows 4rq + p of its quad (G = 16: 4 phases = 4 rows)
+        if (rowOk) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int t = 4 * rq + j;
+                const bool mine = (G == 16) ? (cph == j) : (cph == 0);
+                if (!mine || t >= nT) continue;
+                const int64_t o = out_index(operm, obase, tb + t);
+                double v[K];
+                mix_apply(mix, a[j], v);
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    double* dst = out + (size_t)i * ldo + o;
+                    *dst = accum ? *dst + scale * v[i] : scale * v[i];
+                }
+            }
+        }
+        if constexpr (G == 16) break;
     }
 }
 
@@ -813,7 +984,7 @@ __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* _
                 const int* it = iperm + (size_t)(sq + dr * sz + dc) * D2;  // the square's points, tree positions
 #pragma unroll
                 for (int c = 0; c < D2; ++c) {
-                    const double* f = fT + (size_t)it[c] * K;
+                    const double* f = fT + (size_t)it[c] * kStride<K>;
 #pragma unroll
                     for (int r = 0; r < K; ++r) base[r] += w[c] * f[r];
                 }
@@ -859,7 +1030,7 @@ __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* _
         for (int r = 0; r < K; ++r) {
             double hw[D2];
 #pragma unroll
-            for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cT[(size_t)it[c] * K + r];
+            for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cT[(size_t)it[c] * kStride<K> + r];
             double sg = 0.0;
 #pragma unroll
             for (int n = 0; n < D; ++n)
@@ -904,6 +1075,7 @@ static MixK<K> make_mix(const double* m) {  // m: K x K row-major host array
     }
 
 bool rhs_supported(int k) { return k == 1 || k == 2 || k == 4 || k == 5 || k == 8; }
+int rhs_stride(int k) { return (k == 1 || k % 2 == 0) ? k : k + 1; }
 int rhs_padded(int k) {
     for (int c : {1, 2, 4, 5, 8})
         if (k <= c) return c;
@@ -966,18 +1138,34 @@ void launch_m2l_gather(int K, int ntgt, const int* tgt, const int* inPtr, const 
     HIP_LAUNCH_CHECK();
 }
 
-void launch_near(int K, int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
-                 const int64_t* nearKOff, const int2* nearSym, const double* Kop, const double* fT, const double* mix,
-                 const int* operm, int64_t obase, int64_t ldo, int maxS, int flags, double sgn, double scale,
-                 int accum, double* partial, double* out, hipStream_t s) {
+void launch_near_sym(int K, int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
+                     const int64_t* nearKOff, const int2* nearSym, const double* Kop, const double* fT,
+                     const double* mix, const int* operm, int64_t obase, int64_t ldo, int maxS, int flags, double sgn,
+                     double scale, int accum, double* partial, double* out, hipStream_t s) {
     if (nl <= 0) return;
     const int S = maxS > 0 ? maxS : 1;
     const int wpb = (size_t)S * K * 8 * 4 <= 48 * 1024 ? 4 : 1;  // waves per block, LDS = waves x S x K doubles
     const size_t shm = (size_t)wpb * S * K * sizeof(double);
     if (shm > 160 * 1024) throw std::invalid_argument("near field: leaf neighbourhood too large for LDS");
-    ANISO_DISPATCH_K(K, (k_near<KK><<<blocks_for(nl, wpb), wpb * kWave, shm, s>>>(
+    ANISO_DISPATCH_K(K, (k_near_sym<KK><<<blocks_for(nl, wpb), wpb * kWave, shm, s>>>(
                             nl, leafInfo, nearPtsPtr, nearPts, nearKOff, nearSym, Kop, fT, make_mix<KK>(mix), operm,
                             obase, ldo, S, flags, sgn, scale, accum, partial, out)));
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_near(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
+                 const int64_t* nearKOff, const double* Kop, const double* fT, const double* mix, const int* operm,
+                 int64_t obase, int64_t ldo, int flags, double scale, int accum, double* out, hipStream_t s) {
+    if (nl <= 0) return;
+    if (maxLeaf <= 16) {  // 4 leaves per wave
+        ANISO_DISPATCH_K(K, (k_near<KK, 16, 4><<<blocks_for((int64_t)nl * 16, 256), 256, 0, s>>>(
+                                nl, leafInfo, nearPtsPtr, nearPts, nearKOff, Kop, fT, make_mix<KK>(mix), operm, obase,
+                                ldo, flags, scale, accum, out)));
+    } else {
+        ANISO_DISPATCH_K(K, (k_near<KK, 64, 4><<<blocks_for((int64_t)nl * 64, 256), 256, 0, s>>>(
+                                nl, leafInfo, nearPtsPtr, nearPts, nearKOff, Kop, fT, make_mix<KK>(mix), operm, obase,
+                                ldo, flags, scale, accum, out)));
+    }
     HIP_LAUNCH_CHECK();
 }
 

@@ -70,6 +70,10 @@ struct Plan {
     // its transposed product to partial slot m2lOutSlot[c]; slots are contiguous
     // per receiver: [m2lInPtr[k], m2lInPtr[k+1]) for target m2lTgt[k].
     bool symmetric = true;
+    // input: symmetric U storage in the near field (worth it for single right-hand
+    // sides; block applies read every block directed)
+    bool nearSymmetric = true;
+    int nearMaxLeaf = 0;  // largest owned target leaf (points)
     std::vector<int> m2lNDir, m2lCanonBase, m2lInPtr, m2lOutSlot;
     int m2lCanon = 0;
     int64_t storedM2L = 0, storedNear = 0, nearPartTotal = 0;

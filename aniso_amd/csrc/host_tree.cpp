@@ -213,7 +213,9 @@ void Tree::build(const double* x, const double* y, int64_t n, int rank, int maxL
 void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     (void)np;
     if (nranks_ < 1 || rank_ < 0 || rank_ >= nranks_) throw std::invalid_argument("bad shard rank/nranks");
+    const bool symNear = nearSymmetric;
     *this = Plan();
+    nearSymmetric = symNear;
     rank = rank_;
     nranks = nranks_;
     const int64_t N = t.count[0];
@@ -352,8 +354,8 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
             int b = t.uIdx[k];
             if (t.isEmpty[b]) continue;
             pairsNear += t.count[i] * t.count[b];
-            // k_near reduces a canonical column within one pass of <= 64 row pairs
-            if (symmetric && b != i && leafIdx[b] >= 0 && t.count[i] <= 128 && t.count[b] <= 128) {
+            // k_near reduces a canonical column within one pass of <= 64 row quads
+            if (symmetric && nearSymmetric && b != i && leafIdx[b] >= 0 && t.count[i] <= 128 && t.count[b] <= 128) {
                 if (i < b) canonSrc.push_back(b);
                 continue;
             }
@@ -376,11 +378,12 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
             S += t.count[b];
         }
         nearPtr.push_back((int64_t)nearSrc.size());
-        nearKTotal += S * (t.count[i] + (t.count[i] & 1));  // rows padded to even: 16-B aligned columns
+        nearKTotal += S * ((t.count[i] + 3) & ~(int64_t)3);  // rows padded to a multiple of 4: 32-B row quads
         storedNear += S * t.count[i];
         if (S > (int64_t)1 << 30 || partTotal > ((int64_t)1 << 31) - 1)
             throw std::invalid_argument("leaf neighbourhood too large");
         leafInfo.push_back({i, (int)t.begin[i], (int)t.count[i], (int)S});
+        nearMaxLeaf = std::max<int>(nearMaxLeaf, (int)t.count[i]);
         nearSym.push_back({(int)Sdir, (int)partBase});
     }
     nearPartTotal = partTotal;

@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(256) k_cache_m2l(int64_t total, const int* __r
 }
 
 // downPassCache's U/W blocks (bbfmm.h:991-1011): per target leaf, column-major
-// nT x S over the concatenated source points of its U then W members.
+// nT4 x S (nT rounded up to a multiple of 4, zero rows) over the concatenated source points of its U then W members.
 __global__ void __launch_bounds__(256) k_cache_near(int nl, const int* __restrict__ leaves,
                                                     const int64_t* __restrict__ nearPtr,
                                                     const int* __restrict__ nearSrc,
@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(256) k_cache_near(int nl, const int* __restric
     __syncthreads();
     const int S = sOff[ns];
     double* Kl = K + nearKOff[li];
-    const int nTs = nT + (nT & 1);  // rows padded to even (16-B loads in k_near)
+    const int nTs = (nT + 3) & ~3;  // rows padded to a multiple of 4 (32-B row quads in k_near)
     const int64_t total = (int64_t)nTs * S;
     for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
         int sc = (int)(e / nTs), t = (int)(e - (int64_t)sc * nTs);

@@ -47,6 +47,7 @@ constexpr int kUpThreads = 256;
 // apply it to the base inputs on the fly (rhs i = sum_b mix[i][b] base b).
 bool rhs_supported(int k);
 int rhs_padded(int k);  // smallest supported count >= k, or -1
+int rhs_stride(int k);  // row stride (doubles) of the tree-order charge arrays fT / cT
 void launch_prepare(int K, int64_t N, const double* xin, int64_t ldi, int treeIn, const int* perm,
                     const double* sigT, const double* wT, double* fT, double* cT, hipStream_t s);
 size_t up_tier_lds(int maxTask, int K);
@@ -64,10 +65,15 @@ void launch_m2l_gather(int K, int ntgt, const int* tgt, const int* inPtr, const 
 // Output index mode of k_near / k_down_tier / k_corr: operm = perm writes the
 // original-order vector out[perm[k]]; operm = nullptr writes the owned tree-order
 // slice out[k - obase].  ldo = the stride between right-hand sides of out.
-void launch_near(int K, int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
-                 const int64_t* nearKOff, const int2* nearSym, const double* Kop, const double* fT, const double* mix,
-                 const int* operm, int64_t obase, int64_t ldo, int maxS, int flags, double sgn, double scale,
-                 int accum, double* partial, double* out, hipStream_t s);
+// near field with symmetric U storage (K = 1 handles): partial products to `partial`
+void launch_near_sym(int K, int nl, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
+                     const int64_t* nearKOff, const int2* nearSym, const double* Kop, const double* fT,
+                     const double* mix, const int* operm, int64_t obase, int64_t ldo, int maxS, int flags, double sgn,
+                     double scale, int accum, double* partial, double* out, hipStream_t s);
+// near field with directed storage; maxLeaf = the largest target leaf (points)
+void launch_near(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
+                 const int64_t* nearKOff, const double* Kop, const double* fT, const double* mix, const int* operm,
+                 int64_t obase, int64_t ldo, int flags, double scale, int accum, double* out, hipStream_t s);
 void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* desc, const int* grpFix,
                       const int4* dn, const double* local, const Params* P, const int* leafSlot, const int* leafBegin,
                       const int2* leafNear, const double4* leafGeom, const double* pxT, const double* pyT,

@@ -72,3 +72,11 @@ def gather_index(ranges, L):
     """Positions in the flattened (nranks, L) all-gather buffer of tree positions
     0 .. N-1: tree[k] = gathered.reshape(-1)[idx[k]]."""
     return np.concatenate([r * L + np.arange(e - b, dtype=np.int64) for r, (b, e) in enumerate(ranges)])
+
+
+def block_gather_index(ranges, L, nb):
+    """Positions in the flattened (nranks, nb, L) all-gather buffer of the block
+    vector (nb, N) in tree order: y.reshape(-1)[b * N + k] = gathered.reshape(-1)[idx]."""
+    g = gather_index(ranges, L)
+    r, off = g // L, g % L
+    return np.concatenate([r * nb * L + b * L + off for b in range(nb)])

@@ -2,20 +2,26 @@
 """bench.py -- GMRES matvec throughput of the MI355X path at 1M quadrature points.
 
 Workload (BASELINE.json metric "GMRES matvec/s & pair-interactions/s at 1M quad
-points"): the configs[2] geometry (sz=1024, d=1, ns=10, np=4, maxLevel=20,
-N = 1,048,576), main.cpp's coefficient functions, and main.cpp's GMRES matvec
-forwardOperator u - K_0(sigma_s .* u) (main.cpp:125-136): one apply of mode 0 per
-matvec.  A "step" is one matvec; steps are chained (v <- A v) with every vector
-resident in HBM, kept in tree order (a fixed relabelling of the unknowns, so no
-permutation gathers on the data path).  fp64 throughout.
+points"; configs[2] = SURVEY.md §8(d) config 3): the aniso.m / demo.m problem --
+sz=1024, d=1, ns=10, np=4, maxLevel=20, ks=5 Fourier blocks (9 modes), g=0.8,
+N = 1,048,576 points, sigma_s = 20, sigma_a = 0.2 (demo.m:15-16), the Gaussian
+charge in block 0 (demo.m:24-29) -- and its GMRES matvec x - mforward(x)
+(aniso.m:138-157, 155): 45 mode-applies of the reference per matvec, computed as
+ONE batched apply (one up pass over the 5 blocks, every mode's cached operators
+streamed once for all 5 right-hand sides, one down pass).  A "step" is one block
+matvec; steps are chained (v <- A v) with every vector resident in HBM, in tree
+order (a fixed relabelling of the unknowns: no permutation gathers on the data
+path).  fp64 throughout.  --workload mode0 instead times main.cpp's matvec
+u - K_0(sigma_s .* u) (main.cpp:125-136) with main.cpp's coefficients; the block
+run also reports that number as `mode0_matvec_per_s`.
 
-N GPUs (torchrun, one process per GPU, RCCL): the target set is sharded by FMM
+N GPUs (torchrun, one process per GPU, RCCL): the targets are sharded by FMM
 subtree (strong scaling: total work fixed).  Each rank applies its shard; one
-all-gather of tree-ordered slices rebuilds the replicated output vector.
+all-gather of tree-ordered slices rebuilds the replicated block vector.
 
 Also reported on the same JSON line:
-  roofline      HBM roofline of the dominant kernel (k_m2l), timed with HIP events
-                on the apply stream over the timed region;
+  roofline      HBM roofline of the dominant kernel (k_m2l, one launch per mode),
+                timed with HIP events on the apply stream over the timed region;
   cpu_baseline  the CPU oracle (a faithful port of the reference apply) on this
                 host's cores, on a bounded sample of the same geometry family;
   rel_err_vs_cpu  GPU vs CPU oracle on that sample's inputs.
@@ -41,18 +47,31 @@ def main_coeffs(xy):
     return ss, ss + 0.2
 
 
+def demo_coeffs(xy):
+    """demo.m:15-16 through aniso.m:96-100: sigma_s = 20, sigma_t = sigma_s + 0.2"""
+    ss = np.full(xy.shape[0], 20.0)
+    return ss, ss + 0.2
+
+
 def gaussian(xy):
-    """main.cpp:29-32"""
+    """main.cpp:29-32 / demo.m:24"""
     return np.exp(-25 * ((xy[:, 0] - 0.5) ** 2 + (xy[:, 1] - 0.5) ** 2))
 
 
 def ref_pairs(sz, d, ns, s):
-    """Reference pair interactions per apply: 2 P_U + 2 P_M + P_rem + P_R + P_S."""
+    """Reference pair interactions per mode-apply: 2 P_U + 2 P_M + P_rem + P_R + P_S."""
     N = sz * sz * d * d
     p_rem = d ** 4 * (3 * sz - 2) ** 2
     p_r = 16 * d ** 4 * ((3 * sz - 2) ** 2 - sz ** 2)
     p_s = 8 * ns * ns * N
     return 2 * s["near_entries"] + 2 * s["m2l_entries"] + p_rem + p_r + p_s
+
+
+def ref_bytes(sz, d, ns, s):
+    """Reference cached-operator stream per mode-apply: 8 (2P_U + 2P_M + P_R + P_S) + 8 * 6N."""
+    N = sz * sz * d * d
+    p_r = 16 * d ** 4 * ((3 * sz - 2) ** 2 - sz ** 2)
+    return 8 * (2 * s["near_entries"] + 2 * s["m2l_entries"] + p_r + 8 * ns * ns * N) + 8 * 6 * N
 
 
 def pmc_traffic(kernel):
@@ -70,38 +89,70 @@ def pmc_traffic(kernel):
     return int(k["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(args, gpu_check):
+def block_ref(o, U, ss, g):
+    """aniso.m:138-157 x - mforward(x) composed from oracle mode applies (45 in the
+    reference's loop; each distinct (block, mode) product computed once here)."""
+    nb = U.shape[0]
+    out = np.zeros_like(U)
+    memo = {}
+    for i in range(-(nb - 1), 1):
+        for j in range(-(nb - 1), nb):
+            b, m = abs(j), abs(i - j)
+            if (b, m) not in memo:
+                memo[(b, m)] = o.mapping(U[b] * ss, m)
+            out[abs(i)] += (g ** b - g ** nb) / (1 - g ** nb) * memo[(b, m)]
+    return U - out
+
+
+def cpu_baseline(args, coeffs, gpu_check):
     """Oracle (oracle/, a faithful CPU port of the reference apply incl. the per-apply
     tree rebuild) on a bounded sample; returns (baseline dict, rel err vs GPU)."""
     from oracle.oracle_py import Oracle
 
     sz = args.cpu_sz
-    o = Oracle(sz, args.d, 1, 0.8, args.ns, 4, args.max_level)
+    block = args.workload == "block"
+    ks = args.ks if block else 1
+    o = Oracle(sz, args.d, ks, args.g, args.ns, 4, args.max_level)
     xy = o.getNodes()
-    ss, st = main_coeffs(xy)
+    ss, st = coeffs(xy)
     o.setCoeff(ss, st)
+    modes = list(range(2 * ks - 1))
     t0 = time.time()
-    o.cache(0)
+    for m in modes:
+        o.cache(m)
     t_cache = time.time() - t0
-    q = gaussian(xy)
-    u = q * ss
+    rng = np.random.default_rng(0)
+    u = gaussian(xy) * ss
     o.mapping(u, 0)  # warm-up
-    reps, t0 = 0, time.time()
-    while reps < 3 or time.time() - t0 < args.cpu_seconds:
-        ref = o.mapping(u, 0)
+    # per-mode apply time: round-robin over the modes until the budget is spent
+    reps, t_sum, t0 = 0, 0.0, time.time()
+    while reps < max(3, len(modes)) or time.time() - t0 < args.cpu_seconds:
+        m = modes[reps % len(modes)]
+        t1 = time.perf_counter()
+        o.mapping(u, m)
+        t_sum += time.perf_counter() - t1
         reps += 1
-    t_apply = (time.time() - t0) / reps
-    rel = gpu_check(sz, u, ref)
+    t_apply = t_sum / reps
+    per_matvec = ks * (2 * ks - 1) if block else 1  # aniso.m's loop: ks x (2ks-1) mapping calls per mforward
+    if block:
+        U = rng.uniform(-1, 1, (ks, o.N))
+        U[0] += gaussian(xy)
+        ref = block_ref(o, U, ss, args.g)
+        rel = gpu_check(sz, U, ref)
+    else:
+        ref = o.mapping(u, 0)
+        rel = gpu_check(sz, u, ref)
     scale = float(args.sz * args.sz) / float(sz * sz)  # O(N) extrapolation to the workload
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {
-        "value": 1.0 / (t_apply * scale),
+        "value": 1.0 / (per_matvec * t_apply * scale),
         "unit": "matvec/s",
         "cores": cores,
         "kind": "port",
-        "sample": (f"oracle apply (mode 0, tree rebuilt per apply as in the reference) at sz={sz} "
-                   f"(N={sz * sz * args.d ** 2}) of the same d={args.d}, ns={args.ns} geometry, {reps} reps, "
-                   f"{t_apply * 1e3:.1f} ms/apply, extrapolated linearly in N to N={args.sz * args.sz * args.d ** 2}; "
+        "sample": (f"oracle mode-apply (tree rebuilt per apply as in the reference) at sz={sz} "
+                   f"(N={sz * sz * args.d ** 2}) of the same d={args.d}, ns={args.ns} geometry, {reps} applies over "
+                   f"modes {modes[0]}..{modes[-1]}, {t_apply * 1e3:.1f} ms/apply; one matvec = {per_matvec} "
+                   f"mode-applies (the reference's loop), extrapolated linearly in N to N={args.sz * args.sz * args.d ** 2}; "
                    f"cache build {t_cache:.1f} s not timed; OMP threads={cores}"),
     }, rel
 
@@ -111,11 +162,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="block", choices=["block", "mode0"])
     ap.add_argument("--sz", type=int, default=1024)
     ap.add_argument("--d", type=int, default=1)
     ap.add_argument("--ns", type=int, default=10)
+    ap.add_argument("--ks", type=int, default=5)
+    ap.add_argument("--g", type=float, default=0.8)
     ap.add_argument("--max-level", type=int, default=20)
-    ap.add_argument("--cpu-sz", type=int, default=512, help="CPU baseline sample size (sz; N = sz^2 d^2)")
+    ap.add_argument("--cpu-sz", type=int, default=256, help="CPU baseline sample size (sz; N = sz^2 d^2)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline timing budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -142,81 +196,106 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    op = aniso_amd.Aniso(args.sz, args.d, 5, 0.8, args.ns, 4, args.max_level)
+    block = args.workload == "block"
+    ks = args.ks if block else 1
+    nb = ks if block else 1
+    coeffs = demo_coeffs if block else main_coeffs
+    op = aniso_amd.Aniso(args.sz, args.d, ks, args.g, args.ns, 4, args.max_level)
     N = op.N
     xy = op.getNodes()
-    ss, st = main_coeffs(xy)
+    ss, st = coeffs(xy)
     full_stats = op.stats()
     perm = torch.tensor(op.tree_perm(), device="cuda", dtype=torch.int64)
     if world > 1:
         ranges = adist.shard_ranges(op, world)
         op.set_shard(rank, world)
         L = adist.pad_len(ranges)
-        slice_buf = torch.zeros(L, dtype=torch.float64, device="cuda")
-        gathered = torch.zeros(world, L, dtype=torch.float64, device="cuda")
-        gidx = torch.tensor(adist.gather_index(ranges, L), device="cuda")
-        b_own, e_own = ranges[rank]
+        slab = torch.zeros(nb, L, dtype=torch.float64, device="cuda")
+        gathered = torch.zeros(world * nb * L, dtype=torch.float64, device="cuda")
+        gidx = torch.tensor(adist.block_gather_index(ranges, L, nb), device="cuda")
     op.setCoeff(ss, st)
+    modes = list(range(2 * ks - 1))
     t0 = time.time()
-    op.cache(0)
+    for m in modes:
+        op.cache(m)
     torch.cuda.synchronize()
     t_cache = time.time() - t0
     # GMRES vectors live in tree order (a fixed relabelling of the unknowns): the
-    # forward operator then needs no permutation gathers, and the shards' output
-    # slices concatenate to the next iterate
-    v = torch.tensor(gaussian(xy), device="cuda")[perm].contiguous()
+    # operator then needs no permutation gathers, and the shards' output slices
+    # concatenate to the next iterate.  Block 0 holds the Gaussian (demo.m:27-29).
+    v = torch.zeros(nb, N, dtype=torch.float64, device="cuda")
+    v[0] = torch.tensor(gaussian(xy), device="cuda")[perm]
     w = torch.zeros_like(v)
+
+    def local_apply(x, y):
+        if block:
+            op.block_op_dev(2, x, y, tree=True)
+        else:
+            op.forward_tree_dev(x[0], y[0])
 
     def matvec(x, y):
         if world == 1:
-            op.forward_tree_dev(x, y)
+            local_apply(x, y)
             return
-        op.forward_tree_dev(x, slice_buf)  # writes the owned e_own - b_own entries
+        local_apply(x, slab)  # writes the owned entries of every block
         if args.backend == "nccl":
-            dist.all_gather_into_tensor(gathered, slice_buf)
+            dist.all_gather_into_tensor(gathered, slab.view(-1))
         else:  # gloo rehearsal: stage through host memory
-            parts = [torch.zeros(L, dtype=torch.float64) for _ in range(world)]
-            dist.all_gather(parts, slice_buf.cpu())
-            gathered.copy_(torch.stack(parts))
-        torch.index_select(gathered.view(-1), 0, gidx, out=y)
+            parts = [torch.zeros(nb * L, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(parts, slab.view(-1).cpu())
+            gathered.copy_(torch.cat(parts))
+        torch.index_select(gathered, 0, gidx, out=y.view(-1))
 
-    for _ in range(args.warmup):
-        matvec(v, w)
-        v, w = w, v
-    op.set_timing(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        matvec(v, w)
-        v, w = w, v
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    times = op.stage_times()  # per-apply averages over the timed region (HIP events)
-    op.set_timing(False)
-    if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(fn, steps, warmup):
+        nonlocal v, w
+        for _ in range(warmup):
+            fn(v, w)
+            v, w = w, v
+        op.set_timing(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn(v, w)
+            v, w = w, v
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        times = op.stage_times()  # per-apply averages over the timed region (HIP events)
+        op.set_timing(False)
+        if world > 1:
+            t = torch.tensor([el], device="cuda", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, times
+
+    elapsed, times = timed(matvec, args.steps, args.warmup)
     my_stats = op.stats()
     ms = 1e3 * elapsed / args.steps
     value = args.steps / elapsed
-    # dominant kernel: k_m2l (streams the stored merged 16x16 M2L operators once:
-    # 2 KB per stored block, + multipole read and local write per target node, +
-    # one 128-B transposed partial per canonical pair)
-    m2l_bytes = (2048.0 * my_stats["stored_m2l"] + 2.0 * 128.0 * my_stats["m2l_targets"]
-                 + 128.0 * my_stats["m2l_canon"])
-    m2l_ms = times["m2l"]
+    # dominant kernel: k_m2l, one launch per mode per matvec.  Algorithmic bytes per
+    # launch: the stored merged 16x16 M2L operators once (2 KB per stored block),
+    # the multipoles read and locals written per target node (16 x nb doubles
+    # each), one transposed partial (16 x nb doubles) per canonical pair
+    launches = len(modes) if block else 1
+    m2l_bytes = (2048.0 * my_stats["stored_m2l"] + 2.0 * 128.0 * nb * my_stats["m2l_targets"]
+                 + 128.0 * nb * my_stats["m2l_canon"])
+    m2l_ms = times["m2l"] / launches
     achieved = m2l_bytes / (m2l_ms * 1e-3) / 1e9 if m2l_ms > 0 else 0.0
-    traffic, tsrc = pmc_traffic("aniso::k_m2l") if world == 1 and args.sz == 1024 and args.d == 1 else (None, None)
+    pmc_name = f"aniso::k_m2l<{nb}>"
+    traffic, tsrc = pmc_traffic(pmc_name) if world == 1 and args.sz == 1024 and args.d == 1 else (None, None)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": "k_m2l",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": f"k_m2l<{nb}> (per mode)",
                 "kernel_ms": round(m2l_ms, 5), "algorithmic_bytes": int(m2l_bytes), "traffic_source": tsrc}
+    applies = ks * (2 * ks - 1) if block else 1  # the reference's mapping calls per matvec
+    cfg = (f"configs[2] (1M points, d=1, ns=10, np=4, maxLevel=20, g={args.g}): aniso.m GMRES block matvec "
+           f"x - mforward(x), {ks} blocks x {2 * ks - 1} modes = {applies} mode-applies per matvec"
+           if block else "configs[2] geometry, main.cpp GMRES matvec of mode 0")
     line = {
-        "metric": "GMRES matvec/s at 1M quadrature points (main.cpp forwardOperator, mode 0)",
+        "metric": ("GMRES matvec/s at 1M quad points (aniso.m block matvec, g=0.8, 45 mode-applies)" if block
+                   else "GMRES matvec/s at 1M quadrature points (main.cpp forwardOperator, mode 0)"),
         "value": round(value, 3),
         "unit": "matvec/s",
         "n_gpus": world,
@@ -227,39 +306,71 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: main.cpp coefficient functions and Gaussian source on the unit square",
-        "config": {"workload": "configs[2] geometry (1M points, d=1, ns=10, np=4, maxLevel=20), GMRES matvec of mode 0",
-                   "N": N, "sz": args.sz, "d": args.d, "ns": args.ns, "np": 4, "maxLevel": args.max_level,
+        "data": ("synthetic: demo.m coefficients (sigma_s=20, sigma_a=0.2), Gaussian charge in block 0, chained matvecs"
+                 if block else "synthetic: main.cpp coefficient functions and Gaussian source, chained matvecs"),
+        "config": {"workload": cfg, "N": N, "sz": args.sz, "d": args.d, "ns": args.ns, "np": 4, "ks": ks,
+                   "g": args.g, "maxLevel": args.max_level, "rhs_per_apply": nb,
                    "parallelism": f"fmm-subtree-shard x{world}" if world > 1 else "single-gpu"},
-        "pair_interactions_per_s": round(value * ref_pairs(args.sz, args.d, args.ns, full_stats), 1),
+        "mode_applies_per_s": round(value * applies, 1),
+        "pair_interactions_per_s": round(value * applies * ref_pairs(args.sz, args.d, args.ns, full_stats), 1),
+        "ref_equivalent_stream_GBps": round(value * applies * ref_bytes(args.sz, args.d, args.ns, full_stats) / 1e9, 1),
         "stage_ms": {k: round(v_, 5) for k, v_ in times.items()},
         "cache_build_s": round(t_cache, 3),
         "roofline": roofline,
     }
+    if block:
+        # main.cpp's mode-0 matvec on the same operator (secondary number)
+        def mode0(x, y):
+            if world == 1:
+                op.forward_tree_dev(x[0], y[0])
+                return
+            op.forward_tree_dev(x[0], slab[0])
+            if args.backend == "nccl":
+                dist.all_gather_into_tensor(gathered, slab.view(-1))
+            else:
+                parts = [torch.zeros(nb * L, dtype=torch.float64) for _ in range(world)]
+                dist.all_gather(parts, slab.view(-1).cpu())
+                gathered.copy_(torch.cat(parts))
+            torch.index_select(gathered, 0, gidx, out=y.view(-1))
+
+        el0, t0s = timed(mode0, args.steps, 2)
+        line["mode0_matvec_per_s"] = round(args.steps / el0, 3)
+        line["mode0_stage_ms"] = {k: round(v_, 5) for k, v_ in t0s.items()}
     if args.verify:
-        # one matvec of a fixed vector through this (possibly sharded) path vs an
-        # unsharded operator on the same device
-        u = torch.tensor(gaussian(xy), device="cuda")
-        got = torch.zeros_like(u)
-        matvec(u[perm].contiguous(), got)  # tree order in and out
-        ref_op = aniso_amd.Aniso(args.sz, args.d, 5, 0.8, args.ns, 4, args.max_level)
+        # one matvec of a fixed block vector through this (possibly sharded) path vs
+        # an unsharded operator on the same device
+        U = torch.tensor(np.random.default_rng(1).uniform(-1, 1, (nb, N)), device="cuda")
+        got = torch.zeros_like(U)
+        matvec(U[:, perm].contiguous(), got)  # tree order in and out
+        ref_op = aniso_amd.Aniso(args.sz, args.d, ks, args.g, args.ns, 4, args.max_level)
         ref_op.setCoeff(ss, st)
-        ref_op.cache(0)
-        ref = torch.zeros_like(u)
-        ref_op.forward_dev(u, ref)  # original order, unsharded
+        for m in modes:
+            ref_op.cache(m)
+        ref = torch.zeros_like(U)
+        if block:
+            ref_op.block_op_dev(2, U, ref)  # original order, unsharded
+        else:
+            ref_op.forward_dev(U[0], ref[0])
         torch.cuda.synchronize()
-        ref = ref[perm]
+        ref = ref[:, perm]
         line["verify_rel_err_vs_unsharded"] = float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref))
         del ref_op
     if rank == 0 and world == 1 and not args.no_cpu:
         def gpu_check(sz, u, ref):
-            a = aniso_amd.Aniso(sz, args.d, 1, 0.8, args.ns, 4, args.max_level)
-            a.setCoeff(*main_coeffs(a.getNodes()))
-            a.cache(0)
-            got = a.mapping(u, 0)
+            a = aniso_amd.Aniso(sz, args.d, ks, args.g, args.ns, 4, args.max_level)
+            a.setCoeff(*coeffs(a.getNodes()))
+            for m in modes:
+                a.cache(m)
+            if block:
+                Ud = torch.tensor(u, device="cuda")
+                out = torch.zeros_like(Ud)
+                a.block_op_dev(2, Ud, out)
+                got = out.cpu().numpy()
+            else:
+                got = a.mapping(u, 0)
             return float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
 
-        base, rel = cpu_baseline(args, gpu_check)
+        base, rel = cpu_baseline(args, coeffs, gpu_check)
         line["cpu_baseline"] = base
         line["rel_err_vs_cpu"] = rel
         line["speedup_vs_cpu"] = round(value / base["value"], 1)

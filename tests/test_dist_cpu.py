@@ -76,3 +76,16 @@ def test_gloo_sharded_assembly(world):
     for r, err, n in res:
         assert n > 0, err
         assert err == 0.0, (r, err)
+
+
+def test_block_gather_index_assembles_block_slices():
+    from aniso_amd import dist as adist
+
+    ranges = [(0, 5), (5, 7), (7, 13)]
+    L, nb, N = 6, 3, 13
+    full = np.arange(nb * N, dtype=np.float64).reshape(nb, N)
+    gathered = np.zeros((3, nb, L))
+    for r, (b, e) in enumerate(ranges):
+        gathered[r, :, : e - b] = full[:, b:e]
+    idx = adist.block_gather_index(ranges, L, nb)
+    assert np.array_equal(gathered.reshape(-1)[idx].reshape(nb, N), full)

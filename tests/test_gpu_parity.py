@@ -55,6 +55,7 @@ CASES = [
     (8, 2, 1, 8, 0, "main", [0]),            # maxLevel 0: one 256-point leaf, near field only
     (1, 3, 1, 8, 20, "main", [0]),           # single square: the root is the only leaf
     (15, 3, 2, 8, 2, "rough", [0, 1]),       # ~127-point leaves: symmetric and directed U pairs mixed
+    (12, 2, 2, 8, 0, "main", [0, 1]),        # one 576-point leaf, directed near: > 64 row quads per wave
 ]
 
 
@@ -280,7 +281,9 @@ def test_symmetric_storage_matches_directed(sz, d, ks, ml, monkeypatch):
     import aniso_amd
 
     _torch()
+    monkeypatch.setenv("ANISO_NEAR_SYMMETRIC", "1")
     a, o, xy = _pair(sz, d, ks, 8, ml, "rough", seed=3)
+    monkeypatch.delenv("ANISO_NEAR_SYMMETRIC")
     monkeypatch.setenv("ANISO_SYMMETRIC", "0")
     b = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, ml)
     monkeypatch.delenv("ANISO_SYMMETRIC")
@@ -378,12 +381,15 @@ def test_block_operator_matches_oracle(sz, d, ks, coeffs):
         assert _rel(out.cpu().numpy(), ref) <= TOL, (which, _rel(out.cpu().numpy(), ref))
 
 
-@pytest.mark.parametrize("nrhs", [1, 2, 3, 4, 5, 6, 8])
-def test_apply_block_generic_mixes(nrhs):
+@pytest.mark.parametrize("nrhs,near_sym", [(1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (8, 0), (2, 1), (5, 1)])
+def test_apply_block_generic_mixes(nrhs, near_sym, monkeypatch):
     """Arbitrary mixes and mode terms, every right-hand-side count (3, 6 pad to 4, 8),
-    strided input/output rows, with and without sigma_s."""
+    strided input/output rows, with and without sigma_s; directed and symmetric
+    near-field storage."""
     torch = _torch()
+    monkeypatch.setenv("ANISO_NEAR_SYMMETRIC", str(near_sym))
     a, o, xy = _pair(11, 2, 3, 8, 20, "rough", seed=2)
+    assert (a.stats()["near_partial"] > 0) == bool(near_sym)
     ss = rough_coeffs(xy, 2)[0]
     ids = [0, 3, 1]
     for m in ids:
