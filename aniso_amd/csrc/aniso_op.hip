@@ -71,6 +71,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     // ANISO_NEAR_SYMMETRIC=0/1 overrides.
     plan.nearSymmetric = ks == 1;
     if (const char* e = std::getenv("ANISO_NEAR_SYMMETRIC")) plan.nearSymmetric = e[0] == '1';
+    plan.maxCanon = ks == 1 ? kMaxCanon : kMaxCanonBlock;
     plan.build(tree, np, 0, 1);
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
@@ -504,7 +505,8 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         if (mask & kStageFar)
             launch_m2l(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(),
                        dM2LCanonBase.as<int>(), dM2LOutSlot.as<int>(), dM2LSrc.as<int>(), mc.Km2l.as<double>(),
-                       dMult.as<double>(), mix, sgn, acc, dM2LPart.as<double>(), dLocal.as<double>(), s);
+                       dMult.as<double>(), mix, sgn, acc, plan.m2lMaxCanon, dM2LPart.as<double>(),
+                       dLocal.as<double>(), s);
         e = tm ? mark(s) : -1;
         span(2, ep, e);
         ep = e;

@@ -19,6 +19,7 @@
 // M2L partials [slot][16][K]; near partials [column][K]; outputs [K][ldo].
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 #include <string>
@@ -290,8 +291,12 @@ __global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ t
                                              const int* __restrict__ nDir, const int* __restrict__ canonBase,
                                              const int* __restrict__ outSlot, const int* __restrict__ src,
                                              const double* __restrict__ Kop, const double* __restrict__ mult,
-                                             MixK<K> mix, double sgn, int accum, double* __restrict__ partial,
-                                             double* __restrict__ local) {
+                                             MixK<K> mix, double sgn, int accum, int maxCanon,
+                                             double* __restrict__ partial, double* __restrict__ local) {
+    // K >= 4: the transposed products wait in LDS (maxCanon x 16 x K doubles per
+    // wave) instead of registers
+    constexpr bool kLdsY = K >= 4;
+    extern __shared__ double ysh[];
     const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) / kWave));
     const int lane = threadIdx.x & (kWave - 1);
     if (wave >= ntgt) return;
@@ -334,45 +339,75 @@ __global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ t
             for (int i = 0; i < K; ++i) mn[j][i] *= sgn;
         }
         // transposed products stay in registers (lane (s, q) keeps entry s of pair
-        // 4g + q, every right-hand side) and are stored after the stream: on CDNA
-        // vmcnt also counts stores, so stores inside the loop would stall it
-        constexpr int kGroups = (kMaxCanon + 3) / 4;
+        // 4g + q, every right-hand side; K >= 4: in LDS) and are stored after the
+        // stream: on CDNA vmcnt also counts stores, so stores inside the loop would
+        // stall it
+        constexpr int kGroups = kLdsY ? 1 : (kMaxCanon + 3) / 4;
         double y[kGroups][K];
+        double* yl = ysh + (size_t)(threadIdx.x / kWave) * maxCanon * kRank * K;
+        // one group: CG blocks in flight (4; 2 with LDS staging, for registers),
+        // forward + transposed products; lane q keeps (or stages) pair CG g + q
+        constexpr int CG = kLdsY ? 2 : 4;
+        auto group = [&](int g, double (&yg)[K]) {
+            const int j = CG * g;
+            dbl2 kb[CG][2];
+            double xm[CG][K];
 #pragma unroll
-        for (int g = 0; g < kGroups; ++g) {
+            for (int u = 0; u < CG; ++u) load_block(Kop, pd + j + u, lane, j + u < nC, kb[u][0], kb[u][1]);
 #pragma unroll
-            for (int i = 0; i < K; ++i) y[g][i] = 0.0;
-            const int j = 4 * g;
-            if (j < nC) {
-                dbl2 kb[4][2];
-                double xm[4][K];
+            for (int u = 0; u < CG; ++u)
+                m2l_source<K>(mult, __builtin_amdgcn_readlane(cSrc, min(j + u, nC - 1)), s, xm[u]);
+            m2l_forward<K, CG>(kb, xm, c);
 #pragma unroll
-                for (int u = 0; u < 4; ++u) load_block(Kop, pd + j + u, lane, j + u < nC, kb[u][0], kb[u][1]);
+            for (int u = 0; u < CG; ++u)
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    m2l_source<K>(mult, __builtin_amdgcn_readlane(cSrc, min(j + u, nC - 1)), s, xm[u]);
-                m2l_forward<K, 4>(kb, xm, c);
+                for (int i = 0; i < K; ++i) {
+                    const double v = quad_sum(kb[u][0].x * mn[0][i] + kb[u][0].y * mn[1][i] +
+                                              kb[u][1].x * mn[2][i] + kb[u][1].y * mn[3][i]);
+                    if (u == q) yg[i] = v;
+                }
+        };
+        if constexpr (kLdsY) {
+            for (int g = 0; CG * g < nC; ++g) {
+                group(g, y[0]);
+                if (q < CG && CG * g + q < nC)
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
+                    for (int i = 0; i < K; ++i) yl[((size_t)(CG * g + q) * kRank + s) * K + i] = y[0][i];
+            }
+        } else {
 #pragma unroll
-                    for (int i = 0; i < K; ++i) {
-                        const double v = quad_sum(kb[u][0].x * mn[0][i] + kb[u][0].y * mn[1][i] +
-                                                  kb[u][1].x * mn[2][i] + kb[u][1].y * mn[3][i]);
-                        if (u == q) y[g][i] = v;
-                    }
+            for (int g = 0; g < kGroups; ++g) {
+#pragma unroll
+                for (int i = 0; i < K; ++i) y[g][i] = 0.0;
+                if (4 * g < nC) group(g, y[g]);
             }
         }
-        // partial slots: lane (s, q) stores entry s of pair 4g + q (K contiguous
-        // doubles; 16 K contiguous per pair); slot ids shuffled with every lane active
+        if constexpr (kLdsY) {
+            // partial slots: pair p's 16 K doubles are contiguous in LDS and in its
+            // slot; slot ids shuffled with every lane active
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            constexpr int PE = kRank * K;
+            for (int e0 = 0; e0 < nC * PE; e0 += kWave) {
+                const int e = e0 + lane;
+                const int pr = min(e / PE, nC - 1);
+                const int slot = __shfl(cSlot, pr);
+                if (e < nC * PE) partial[(size_t)slot * PE + (e - pr * PE)] = yl[e];
+            }
+        } else {
+            // partial slots: lane (s, q) stores entry s of pair 4g + q (K contiguous
+            // doubles; 16 K contiguous per pair); slot ids shuffled with every lane active
 #pragma unroll
-        for (int g = 0; g < kGroups; ++g) {
-            if (4 * g < nC) {
-                const int jj = 4 * g + q;
-                const int slot = __shfl(cSlot, jj);
-                if (jj < nC) {
-                    double* dst = partial + ((size_t)slot * kRank + s) * K;
+            for (int g = 0; g < kGroups; ++g) {
+                if (4 * g < nC) {
+                    const int jj = 4 * g + q;
+                    const int slot = __shfl(cSlot, jj);
+                    if (jj < nC) {
+                        double* dst = partial + ((size_t)slot * kRank + s) * K;
 #pragma unroll
-                    for (int i = 0; i < K; ++i) dst[i] = y[g][i];
+                        for (int i = 0; i < K; ++i) dst[i] = y[g][i];
+                    }
                 }
             }
         }
@@ -1120,13 +1155,15 @@ void launch_up_tier(int K, int ntask, int taskBase, int maxTask, const int4* des
 
 void launch_m2l(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
                 const int* outSlot, const int* src, const double* Kop, const double* mult, const double* mix,
-                double sgn, int accum, double* partial, double* local, hipStream_t s) {
+                double sgn, int accum, int maxCanon, double* partial, double* local, hipStream_t s) {
     if (ntgt <= 0) return;
+    if (maxCanon > kMaxCanon) throw std::invalid_argument("k_m2l: more canonical pairs per target than staged");
     const unsigned nb = blocks_for((int64_t)ntgt * kWave, 256);
+    const size_t shm = K >= 4 ? (size_t)4 * std::max(maxCanon, 1) * kRank * K * sizeof(double) : 0;
     // blocks in flight per wave: 4 (8 KB) for one or two right-hand sides, 2 above
-    ANISO_DISPATCH_K(K, (k_m2l<KK, (KK <= 2 ? 4 : 2)><<<nb, 256, 0, s>>>(ntgt, tgt, ptr, nDir, canonBase, outSlot, src,
-                                                                          Kop, mult, make_mix<KK>(mix), sgn, accum,
-                                                                          partial, local)));
+    ANISO_DISPATCH_K(K, (k_m2l<KK, (KK <= 2 ? 4 : 2)><<<nb, 256, shm, s>>>(ntgt, tgt, ptr, nDir, canonBase, outSlot,
+                                                                            src, Kop, mult, make_mix<KK>(mix), sgn,
+                                                                            accum, maxCanon, partial, local)));
     HIP_LAUNCH_CHECK();
 }
 

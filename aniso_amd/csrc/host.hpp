@@ -15,7 +15,8 @@ namespace aniso {
 constexpr double kEps = 1e-12;  // bbfmm/utils.h:46
 constexpr int kLeafCode = -2147483647 - 1;  // upCode of a leaf (P2M from its points)
 constexpr int kTaskLevels = 7;  // levels per up/down task record (tasks span <= 4)
-constexpr int kMaxCanon = 32;   // canonical (symmetric) M2L pairs per target: k_m2l's LDS staging
+constexpr int kMaxCanon = 32;       // canonical (symmetric) M2L pairs per target (k_m2l's register staging)
+constexpr int kMaxCanonBlock = 16;  // the same on block handles (ks > 1; LDS staging at K >= 4)
 
 // Geometry::Geometry (Geometry.cpp:10-114) + the singular Duffy rule
 // (KernelFactory.cpp:15-16, 863-986).
@@ -74,6 +75,10 @@ struct Plan {
     // sides; block applies read every block directed)
     bool nearSymmetric = true;
     int nearMaxLeaf = 0;  // largest owned target leaf (points)
+    // input: canonical M2L pairs kept per target (<= kMaxCanon; block handles use
+    // fewer: k_m2l stages their transposed products in LDS)
+    int maxCanon = kMaxCanon;
+    int m2lMaxCanon = 0;  // largest canonical count of a target
     std::vector<int> m2lNDir, m2lCanonBase, m2lInPtr, m2lOutSlot;
     int m2lCanon = 0;
     int64_t storedM2L = 0, storedNear = 0, nearPartTotal = 0;

@@ -214,8 +214,10 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     (void)np;
     if (nranks_ < 1 || rank_ < 0 || rank_ >= nranks_) throw std::invalid_argument("bad shard rank/nranks");
     const bool symNear = nearSymmetric;
+    const int capCanon = maxCanon;
     *this = Plan();
     nearSymmetric = symNear;
+    maxCanon = std::max(0, std::min(kMaxCanon, capCanon));
     rank = rank_;
     nranks = nranks_;
     const int64_t N = t.count[0];
@@ -280,8 +282,8 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     // are numbered receiver-contiguously so k_m2l_gather reads one range per node.
     const char* symEnv = std::getenv("ANISO_SYMMETRIC");
     symmetric = !(symEnv && symEnv[0] == '0');
-    int maxCanon = kMaxCanon;  // ANISO_MAX_CANON: tuning/experiments only (<= kMaxCanon)
-    if (const char* mc = std::getenv("ANISO_MAX_CANON")) maxCanon = std::max(0, std::min(kMaxCanon, std::atoi(mc)));
+    if (const char* mc = std::getenv("ANISO_MAX_CANON"))  // tuning/experiments only (<= kMaxCanon)
+        maxCanon = std::max(0, std::min(kMaxCanon, std::atoi(mc)));
     std::vector<char> m2lActive(t.nn, 0);
     for (int i = 0; i < t.nn; ++i) m2lActive[i] = !t.isEmpty[i] && t.parent[i] != -1 && intersects(i);
     std::vector<std::vector<int>> inCanon(t.nn), inFrom(t.nn);  // per receiver: canonical ids, their senders
@@ -313,6 +315,7 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
             }
         m2lNDir.push_back((int)(m2lSrc.size() - m2lPtr.back()));
         m2lCanonBase.push_back(canon);
+        m2lMaxCanon = std::max<int>(m2lMaxCanon, (int)canonSrc.size());
         for (int b : canonSrc) {
             m2lSrc.push_back(b);
             inCanon[b].push_back(canon++);

@@ -59,7 +59,7 @@ void launch_up_tier(int K, int ntask, int taskBase, int maxTask, const int4* des
 // accum = 0 stores local, 1 adds to it (later modes of a block apply)
 void launch_m2l(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
                 const int* outSlot, const int* src, const double* Kop, const double* mult, const double* mix,
-                double sgn, int accum, double* partial, double* local, hipStream_t s);
+                double sgn, int accum, int maxCanon, double* partial, double* local, hipStream_t s);
 void launch_m2l_gather(int K, int ntgt, const int* tgt, const int* inPtr, const double* partial, double* local,
                        hipStream_t s);
 // Output index mode of k_near / k_down_tier / k_corr: operm = perm writes the
