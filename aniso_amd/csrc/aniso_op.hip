@@ -418,6 +418,35 @@ int Operator::mark(hipStream_t s) {
     return evUsed++;
 }
 
+// Device table of the mode terms of a batched apply (operator pointers, sign and
+// K x K mix per term).  Tables are cached by content: a block operator reuses one
+// table every call, so no upload sits on the apply's path.
+const ModeArgs* Operator::modeTable(int K, int nterm, const int* ids, const double* mixes) {
+    std::vector<ModeArgs> tab(nterm);
+    std::memset(tab.data(), 0, tab.size() * sizeof(ModeArgs));
+    for (int t = 0; t < nterm; ++t) {
+        const ModeCache& mc = modes[ids[t]];
+        ModeArgs& m = tab[t];
+        m.Km2l = mc.Km2l.as<double>();
+        m.Knear = mc.Knear.as<double>();
+        m.C = mc.C.as<double>();
+        m.mu = mc.mu.as<double>();
+        m.sgn = (ids[t] % 2 == 0) ? 1.0 : -1.0;  // K_{B<-A} = (-1)^m K_{A<-B}^T
+        for (int i = 0; i < K; ++i)
+            for (int b = 0; b < K; ++b) m.mix[i][b] = mixes[((size_t)t * K + i) * K + b];
+    }
+    std::string key(reinterpret_cast<const char*>(tab.data()), tab.size() * sizeof(ModeArgs));
+    auto it = modeTabs.find(key);
+    if (it != modeTabs.end()) return it->second.as<ModeArgs>();
+    if (modeTabs.size() >= 64) {  // bound the cache; hipFree waits for work that may still read a table
+        HIP_CHECK(hipDeviceSynchronize());
+        modeTabs.clear();
+    }
+    DevBuf& buf = modeTabs[key];
+    buf.upload(tab.data(), tab.size() * sizeof(ModeArgs));
+    return buf.as<ModeArgs>();
+}
+
 // One batched apply: the up pass over the K base vectors, then per term t (mode
 // ids[t], mix mixes[t]) the near field, the corrections, the M2L stream and its
 // gather, each accumulating; then one down pass.  sigT (sigma_s in tree order, or
@@ -478,45 +507,46 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                        dMult.as<double>(), s);
     int ep = tm ? mark(s) : -1;
     span(1, e0, ep);
-    for (int t = 0; t < nterm; ++t) {
-        const int id = ids[t];
-        const ModeCache& mc = modes[id];
-        const double* mix = mixes + (size_t)t * K * K;
-        const int acc = t > 0 ? 1 : 0;
-        // K_{B<-A} = (-1)^m K_{A<-B}^T for the merged kernel; Id = m
-        const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
-        if (plan.nearPartTotal > 0)  // symmetric U storage: transposed products to partials
+    const ModeArgs* tab = modeTable(K, nterm, ids, mixes);
+    // near field: symmetric U storage (K = 1 handles) one launch per term (its
+    // transposed products go to partials, summed over the terms); directed
+    // storage all terms in one launch
+    if (plan.nearPartTotal > 0) {
+        for (int t = 0; t < nterm; ++t) {
+            const int id = ids[t];
+            // K_{B<-A} = (-1)^m K_{A<-B}^T for the merged kernel; Id = m
+            const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
             launch_near_sym(K, (int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
-                            dNearPts.as<int>(), dNearKOff.as<int64_t>(), dNearSym.as<int2>(), mc.Knear.as<double>(),
-                            dFT.as<double>(), mix, operm, obase, ldo, maxNearS, mask, sgn, scale, acc,
-                            dNearPart.as<double>(), out, s);
-        else
-            launch_near(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
-                        dNearPts.as<int>(), dNearKOff.as<int64_t>(), mc.Knear.as<double>(), dFT.as<double>(), mix, operm,
-                        obase, ldo, mask, scale, acc, out, s);
-        int e = tm ? mark(s) : -1;
-        span(4, ep, e);
-        ep = e;
-        launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
-                    dFT.as<double>(), mix, mc.C.as<double>(), mc.mu.as<double>(), P, mask, scale, treeOut, ldo, out, s);
-        e = tm ? mark(s) : -1;
-        span(6, ep, e);
-        ep = e;
-        if (mask & kStageFar)
-            launch_m2l(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(),
-                       dM2LCanonBase.as<int>(), dM2LOutSlot.as<int>(), dM2LSrc.as<int>(), mc.Km2l.as<double>(),
-                       dMult.as<double>(), mix, sgn, acc, plan.m2lMaxCanon, dM2LPart.as<double>(),
-                       dLocal.as<double>(), s);
-        e = tm ? mark(s) : -1;
-        span(2, ep, e);
-        ep = e;
-        if ((mask & kStageFar) && plan.m2lCanon > 0)
-            launch_m2l_gather(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LInPtr.as<int>(),
-                              dM2LPart.as<double>(), dLocal.as<double>(), s);
-        e = tm ? mark(s) : -1;
-        span(3, ep, e);
-        ep = e;
+                            dNearPts.as<int>(), dNearKOff.as<int64_t>(), dNearSym.as<int2>(),
+                            modes[id].Knear.as<double>(), dFT.as<double>(), mixes + (size_t)t * K * K, operm, obase,
+                            ldo, maxNearS, mask, sgn, scale, t > 0 ? 1 : 0, dNearPart.as<double>(), out, s);
+        }
+    } else {
+        launch_near(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
+                    dNearPts.as<int>(), dNearKOff.as<int64_t>(), tab, nterm, dFT.as<double>(), operm, obase, ldo, mask,
+                    scale, 0, out, s);
     }
+    int e = tm ? mark(s) : -1;
+    span(4, ep, e);
+    ep = e;
+    launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
+                dFT.as<double>(), tab, nterm, P, mask, scale, treeOut, ldo, out, s);
+    e = tm ? mark(s) : -1;
+    span(6, ep, e);
+    ep = e;
+    if (mask & kStageFar)
+        launch_m2l(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(),
+                   dM2LCanonBase.as<int>(), dM2LOutSlot.as<int>(), dM2LSrc.as<int>(), tab, nterm, dMult.as<double>(),
+                   plan.m2lMaxCanon, dM2LPart.as<double>(), dLocal.as<double>(), s);
+    e = tm ? mark(s) : -1;
+    span(2, ep, e);
+    ep = e;
+    if ((mask & kStageFar) && plan.m2lCanon > 0)
+        launch_m2l_gather(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LInPtr.as<int>(), dM2LPart.as<double>(),
+                          dLocal.as<double>(), s);
+    e = tm ? mark(s) : -1;
+    span(3, ep, e);
+    ep = e;
     // down pass (owned part): L2L + L2P + gathered transposed near products, once
     // for the sum over the terms (both are linear in the locals / partials)
     if (mask & (kStageFar | kStageNear))

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "host.hpp"
+#include "kernels.hpp"
 
 namespace aniso {
 
@@ -110,6 +111,8 @@ private:
     void applyBlock(int K, const double* x, int64_t ldx, bool treeIn, const double* sigT, int nterm, const int* ids,
                     const double* mixes, double* out, int64_t ldo, bool treeOut, hipStream_t s, int mask);
     void ensureWork(int K);  // work arrays for K right-hand sides
+    const ModeArgs* modeTable(int K, int nterm, const int* ids, const double* mixes);
+    std::map<std::string, DevBuf> modeTabs;
     int workK = 0;
 
     void ensureDevice();

@@ -66,6 +66,18 @@ __device__ __forceinline__ void mix_apply(const MixK<K>& m, const double* base, 
     }
 }
 
+// The same with a term's mix from the device mode table.
+template <int K>
+__device__ __forceinline__ void mix_apply_t(const ModeArgs& m, const double* base, double* v) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        double a = 0.0;
+#pragma unroll
+        for (int b = 0; b < K; ++b) a += m.mix[i][b] * base[b];
+        v[i] = a;
+    }
+}
+
 // Output slot of tree position k: the original index perm[k] (original-order
 // output) or the owned tree-order slice k - obase (operm == nullptr).
 __device__ __forceinline__ int64_t out_index(const int* __restrict__ operm, int64_t obase, int64_t k) {
@@ -287,11 +299,11 @@ __device__ __forceinline__ void m2l_forward(const dbl2 (&kb)[G][2], const double
 }
 
 template <int K, int PG>
-__global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ tgt, const int64_t* __restrict__ ptr,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K >= 8 ? 1 : 3))) k_m2l(int ntgt, const int* __restrict__ tgt, const int64_t* __restrict__ ptr,
                                              const int* __restrict__ nDir, const int* __restrict__ canonBase,
                                              const int* __restrict__ outSlot, const int* __restrict__ src,
-                                             const double* __restrict__ Kop, const double* __restrict__ mult,
-                                             MixK<K> mix, double sgn, int accum, int maxCanon,
+                                             const ModeArgs* __restrict__ tab, int nterm,
+                                             const double* __restrict__ mult, int maxCanon,
                                              double* __restrict__ partial, double* __restrict__ local) {
     // K >= 4: the transposed products wait in LDS (maxCanon x 16 x K doubles per
     // wave) instead of registers
@@ -303,141 +315,156 @@ __global__ void __launch_bounds__(256) k_m2l(int ntgt, const int* __restrict__ t
     const int n = tgt[wave];
     const int s = lane >> 2, q = lane & 3;  // column s, rows 4q .. 4q+3
     const int64_t p0 = ptr[wave], p1 = ptr[wave + 1], pd = p0 + nDir[wave];
-    const int nC = (int)(p1 - pd);  // canonical pairs, <= kMaxCanon (host plan)
+    const int nC = (int)(p1 - pd);  // canonical pairs, <= maxCanon (host plan)
     const int cSrc = lane < nC ? src[pd + lane] : 0;
     const int cSlot = lane < nC ? outSlot[canonBase[wave] + lane] : 0;
-    double c[4][K];  // forward: rows 4q+j, this lane's column, each right-hand side
+    // transposed products, summed over the terms: registers (lane (s, q) keeps
+    // entry s of pair 4g + q, every right-hand side) or, K >= 4, LDS; stored after
+    // the stream (on CDNA vmcnt also counts stores: stores inside the loop stall it)
+    constexpr int kGroups = kLdsY ? 1 : (kMaxCanon + 3) / 4;
+    double y[kGroups][K];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int g = 0; g < kGroups; ++g)
 #pragma unroll
-        for (int i = 0; i < K; ++i) c[j][i] = 0.0;
-    // ---- directed pairs, PG blocks in flight
-    for (int64_t cb = p0; cb < pd; cb += kWave) {
-        const int cnt = (int)min<int64_t>(kWave, pd - cb);
-        const int mySrc = lane < cnt ? src[cb + lane] : 0;
-        for (int j = 0; j < cnt; j += PG) {
-            dbl2 kb[PG][2];
-            double xm[PG][K];
-#pragma unroll
-            for (int g = 0; g < PG; ++g) load_block(Kop, cb + j + g, lane, j + g < cnt, kb[g][0], kb[g][1]);
-#pragma unroll
-            for (int g = 0; g < PG; ++g)  // a skipped block's source is a valid clamp; its block is zero
-                m2l_source<K>(mult, __builtin_amdgcn_readlane(mySrc, min(j + g, cnt - 1)), s, xm[g]);
-            m2l_forward<K, PG>(kb, xm, c);
-        }
+        for (int i = 0; i < K; ++i) y[g][i] = 0.0;
+    double* yl = ysh + (size_t)(threadIdx.x / kWave) * maxCanon * kRank * K;
+    if constexpr (kLdsY) {
+        for (int e = lane; e < nC * kRank * K; e += kWave) yl[e] = 0.0;
     }
-    // ---- canonical pairs: both products from one read of the block, 4 in flight
-    if (nC > 0) {
-        double mn[4][K];  // the target's mixed multipole, rows 4q+j, times sgn
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            double base[K];
-#pragma unroll
-            for (int b = 0; b < K; ++b) base[b] = mult[((size_t)n * kRank + 4 * q + j) * K + b];
-            mix_apply(mix, base, mn[j]);
-#pragma unroll
-            for (int i = 0; i < K; ++i) mn[j][i] *= sgn;
-        }
-        // transposed products stay in registers (lane (s, q) keeps entry s of pair
-        // 4g + q, every right-hand side; K >= 4: in LDS) and are stored after the
-        // stream: on CDNA vmcnt also counts stores, so stores inside the loop would
-        // stall it
-        constexpr int kGroups = kLdsY ? 1 : (kMaxCanon + 3) / 4;
-        double y[kGroups][K];
-        double* yl = ysh + (size_t)(threadIdx.x / kWave) * maxCanon * kRank * K;
-        // one group: CG blocks in flight (4; 2 with LDS staging, for registers),
-        // forward + transposed products; lane q keeps (or stages) pair CG g + q
-        constexpr int CG = kLdsY ? 2 : 4;
-        auto group = [&](int g, double (&yg)[K]) {
-            const int j = CG * g;
-            dbl2 kb[CG][2];
-            double xm[CG][K];
-#pragma unroll
-            for (int u = 0; u < CG; ++u) load_block(Kop, pd + j + u, lane, j + u < nC, kb[u][0], kb[u][1]);
-#pragma unroll
-            for (int u = 0; u < CG; ++u)
-                m2l_source<K>(mult, __builtin_amdgcn_readlane(cSrc, min(j + u, nC - 1)), s, xm[u]);
-            m2l_forward<K, CG>(kb, xm, c);
-#pragma unroll
-            for (int u = 0; u < CG; ++u)
-#pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    const double v = quad_sum(kb[u][0].x * mn[0][i] + kb[u][0].y * mn[1][i] +
-                                              kb[u][1].x * mn[2][i] + kb[u][1].y * mn[3][i]);
-                    if (u == q) yg[i] = v;
-                }
-        };
-        if constexpr (kLdsY) {
-            for (int g = 0; CG * g < nC; ++g) {
-                group(g, y[0]);
-                if (q < CG && CG * g + q < nC)
-#pragma unroll
-                    for (int i = 0; i < K; ++i) yl[((size_t)(CG * g + q) * kRank + s) * K + i] = y[0][i];
-            }
-        } else {
-#pragma unroll
-            for (int g = 0; g < kGroups; ++g) {
-#pragma unroll
-                for (int i = 0; i < K; ++i) y[g][i] = 0.0;
-                if (4 * g < nC) group(g, y[g]);
-            }
-        }
-        if constexpr (kLdsY) {
-            // partial slots: pair p's 16 K doubles are contiguous in LDS and in its
-            // slot; slot ids shuffled with every lane active
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            constexpr int PE = kRank * K;
-            for (int e0 = 0; e0 < nC * PE; e0 += kWave) {
-                const int e = e0 + lane;
-                const int pr = min(e / PE, nC - 1);
-                const int slot = __shfl(cSlot, pr);
-                if (e < nC * PE) partial[(size_t)slot * PE + (e - pr * PE)] = yl[e];
-            }
-        } else {
-            // partial slots: lane (s, q) stores entry s of pair 4g + q (K contiguous
-            // doubles; 16 K contiguous per pair); slot ids shuffled with every lane active
-#pragma unroll
-            for (int g = 0; g < kGroups; ++g) {
-                if (4 * g < nC) {
-                    const int jj = 4 * g + q;
-                    const int slot = __shfl(cSlot, jj);
-                    if (jj < nC) {
-                        double* dst = partial + ((size_t)slot * kRank + s) * K;
-#pragma unroll
-                        for (int i = 0; i < K; ++i) dst[i] = y[g][i];
-                    }
-                }
-            }
-        }
-    }
-    // ---- sum the forward partials over the 16 columns (lane bits 2..5); then row
-    // t = 4q' + j is entry j of the lanes with q == q' (e.g. lane 4t + (t>>2))
-#pragma unroll
-    for (int off = 4; off < kWave; off <<= 1)
+    // this lane's outputs: row t = s, right-hand sides i = q and q + 4
+    double lo[2] = {0.0, 0.0};
+#pragma unroll 1
+    for (int term = 0; term < nterm; ++term) {
+        const ModeArgs& md = tab[term];
+        const double* __restrict__ Kop = md.Km2l;
+        double c[4][K];  // forward: rows 4q+j, this lane's column, each base vector
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int i = 0; i < K; ++i) c[j][i] += __shfl_xor(c[j][i], off);
-    // The forward sums are over base multipoles: the mode's mix is applied once
-    // per target row here (linear), not per pair.
-    const int t = s;  // this lane writes row t (= its column index), right-hand sides i == q (mod 4)
-    const int jr = t & 3, srcLane = 4 * t + (t >> 2);
-    double v[K];
+            for (int i = 0; i < K; ++i) c[j][i] = 0.0;
+        // ---- directed pairs, PG blocks in flight
+        for (int64_t cb = p0; cb < pd; cb += kWave) {
+            const int cnt = (int)min<int64_t>(kWave, pd - cb);
+            const int mySrc = lane < cnt ? src[cb + lane] : 0;
+            for (int j = 0; j < cnt; j += PG) {
+                dbl2 kb[PG][2];
+                double xm[PG][K];
 #pragma unroll
-    for (int b = 0; b < K; ++b) {
-        const double sel = jr == 0 ? c[0][b] : jr == 1 ? c[1][b] : jr == 2 ? c[2][b] : c[3][b];
-        v[b] = __shfl(sel, srcLane);
+                for (int g = 0; g < PG; ++g) load_block(Kop, cb + j + g, lane, j + g < cnt, kb[g][0], kb[g][1]);
+#pragma unroll
+                for (int g = 0; g < PG; ++g)  // a skipped block's source is a valid clamp; its block is zero
+                    m2l_source<K>(mult, __builtin_amdgcn_readlane(mySrc, min(j + g, cnt - 1)), s, xm[g]);
+                m2l_forward<K, PG>(kb, xm, c);
+            }
+        }
+        // ---- canonical pairs: both products from one read of the block
+        if (nC > 0) {
+            double mn[4][K];  // the target's multipole, mixed, rows 4q+j, times sgn
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                double base[K];
+#pragma unroll
+                for (int b = 0; b < K; ++b) base[b] = mult[((size_t)n * kRank + 4 * q + j) * K + b];
+                mix_apply_t<K>(md, base, mn[j]);
+#pragma unroll
+                for (int i = 0; i < K; ++i) mn[j][i] *= md.sgn;
+            }
+            // one group: CG blocks in flight (4; 2 with LDS staging, for registers),
+            // forward + transposed products; lane q adds pair CG g + q
+            constexpr int CG = kLdsY ? 2 : 4;
+            auto group = [&](int g, double (&yg)[K]) {
+                const int j = CG * g;
+                dbl2 kb[CG][2];
+                double xm[CG][K];
+#pragma unroll
+                for (int u = 0; u < CG; ++u) load_block(Kop, pd + j + u, lane, j + u < nC, kb[u][0], kb[u][1]);
+#pragma unroll
+                for (int u = 0; u < CG; ++u)
+                    m2l_source<K>(mult, __builtin_amdgcn_readlane(cSrc, min(j + u, nC - 1)), s, xm[u]);
+                m2l_forward<K, CG>(kb, xm, c);
+#pragma unroll
+                for (int u = 0; u < CG; ++u)
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        const double v = quad_sum(kb[u][0].x * mn[0][i] + kb[u][0].y * mn[1][i] +
+                                                  kb[u][1].x * mn[2][i] + kb[u][1].y * mn[3][i]);
+                        if (u == q) yg[i] += v;
+                    }
+            };
+            if constexpr (kLdsY) {
+                for (int g = 0; CG * g < nC; ++g) {
+                    double yt[K];
+#pragma unroll
+                    for (int i = 0; i < K; ++i) yt[i] = 0.0;
+                    group(g, yt);
+                    if (q < CG && CG * g + q < nC)
+#pragma unroll
+                        for (int i = 0; i < K; ++i) yl[((size_t)(CG * g + q) * kRank + s) * K + i] += yt[i];
+                }
+            } else {
+#pragma unroll
+                for (int g = 0; g < kGroups; ++g)
+                    if (4 * g < nC) group(g, y[g]);
+            }
+        }
+        // ---- sum the forward partials over the 16 columns (lane bits 2..5); then
+        // row t = 4q' + j is entry j of the lanes with q == q' (e.g. lane 4t + (t>>2));
+        // the sums are over base multipoles: the term's mix is applied here, per row
+#pragma unroll
+        for (int off = 4; off < kWave; off <<= 1)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int i = 0; i < K; ++i) c[j][i] += __shfl_xor(c[j][i], off);
+        const int jr = s & 3, srcLane = 4 * s + (s >> 2);
+        double v[K];
+#pragma unroll
+        for (int b = 0; b < K; ++b) {
+            const double sel = jr == 0 ? c[0][b] : jr == 1 ? c[1][b] : jr == 2 ? c[2][b] : c[3][b];
+            v[b] = __shfl(sel, srcLane);
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            if ((i & 3) != q) continue;
+            double w = 0.0;
+#pragma unroll
+            for (int b = 0; b < K; ++b) w += md.mix[i][b] * v[b];
+            lo[i >> 2] += w;
+        }
     }
-    double* dst = local + ((size_t)n * kRank + t) * K;
+    double* dst = local + ((size_t)n * kRank + s) * K;
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-        if ((i & 3) != q) continue;
-        double w = 0.0;
+    for (int i = 0; i < K; ++i)
+        if ((i & 3) == q) dst[i] = lo[i >> 2];
+    if (nC == 0) return;
+    if constexpr (kLdsY) {
+        // partial slots: pair p's 16 K doubles are contiguous in LDS and in its
+        // slot; slot ids shuffled with every lane active
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        constexpr int PE = kRank * K;
+        for (int e0 = 0; e0 < nC * PE; e0 += kWave) {
+            const int e = e0 + lane;
+            const int pr = min(e / PE, nC - 1);
+            const int slot = __shfl(cSlot, pr);
+            if (e < nC * PE) partial[(size_t)slot * PE + (e - pr * PE)] = yl[e];
+        }
+    } else {
+        // partial slots: lane (s, q) stores entry s of pair 4g + q (K contiguous
+        // doubles; 16 K contiguous per pair); slot ids shuffled with every lane active
 #pragma unroll
-        for (int b = 0; b < K; ++b) w += mix.c[i][b] * v[b];
-        dst[i] = accum ? dst[i] + w : w;
+        for (int g = 0; g < kGroups; ++g) {
+            if (4 * g < nC) {
+                const int jj = 4 * g + q;
+                const int slot = __shfl(cSlot, jj);
+                if (jj < nC) {
+                    double* dstp = partial + ((size_t)slot * kRank + s) * K;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) dstp[i] = y[g][i];
+                }
+            }
+        }
     }
 }
 
@@ -687,19 +714,19 @@ __device__ __forceinline__ void load_charges(const double* __restrict__ p, doubl
 }
 
 // U/W near field, directed storage (every U/W block stored for its target; the
-// layout of block applies): G lanes per target leaf (G = 16 when
-// every leaf has <= 16 points, 4 leaves per wave; else 64).  The block is
-// column-major nT4 x S (rows padded to a multiple of 4); lane (row quad rq, column
-// phase) reads 32 B = rows 4rq..4rq+3 of a column and the column's K base charges
-// straight from fT (L1/L2: the lanes of a column share the line), U columns in
-// flight per lane.  Forward sums per lane over its columns, one reduction over the
-// column phases (DPP row rotations for G = 16), then the mode's mix at the nT
-// outputs.  No LDS, no partials.
+// layout of block handles), all mode terms in one launch: G lanes
+// per target leaf (G = 16 when every leaf has <= 16 points, 4 leaves per wave;
+// else 64).  The block is column-major nT4 x S (rows padded to a multiple of 4);
+// lane (row quad rq, column phase) reads 32 B = rows 4rq..4rq+3 of a column and
+// the column's K base charges straight from fT (L1/L2: the lanes of a column
+// share the line), U columns in flight per lane.  Per term: forward sums per lane
+// over its columns, one reduction over the column phases (DPP row rotations for
+// G = 16), the term's mix at the outputs; out is written once.  No LDS, no partials.
 template <int K, int G, int U>
 __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ leafInfo,
                                               const int64_t* __restrict__ nearPtsPtr, const int* __restrict__ nearPts,
-                                              const int64_t* __restrict__ nearKOff, const double* __restrict__ Kop,
-                                              const double* __restrict__ fT, MixK<K> mix,
+                                              const int64_t* __restrict__ nearKOff, const ModeArgs* __restrict__ tab,
+                                              int nterm, const double* __restrict__ fT,
                                               const int* __restrict__ operm, int64_t obase, int64_t ldo, int flags,
                                               double scale, int accum, double* __restrict__ out) {
     static_assert(G == 16 || G == 64, "leaf group of 16 or 64 lanes");
@@ -727,75 +754,96 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
     for (int rc = 0; rc < nq || rc == 0; rc += G) {  // > 64 row quads: leaves over 256 points
         const int rq = rc + (gl & (lpc - 1));
         const bool rowOk = active && rq < nq;
-        const dbl2* kc = reinterpret_cast<const dbl2*>(Kop + koff) + 2 * rq;
-        double a[4][K];  // rows 4rq+j, base charges
+        // outputs of this lane summed over the terms: G = 16 row 4rq + cph; G = 64
+        // rows 4rq + j on column phase 0
+        constexpr int NR = (G == 16) ? 1 : 4;
+        double o[NR][K];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int r = 0; r < NR; ++r)
 #pragma unroll
-            for (int b = 0; b < K; ++b) a[j][b] = 0.0;
-        if (rowOk) {
-            for (int c0 = cph; c0 < S; c0 += U * cps) {
-                int ix[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int sc = c0 + u * cps;
-                    ix[u] = nearPts[pb + min(sc, S - 1)];
-                }
-                dbl2 kk[U][2];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int sc = c0 + u * cps;
-                    const dbl2* p = kc + (size_t)min(sc, S - 1) * cstr;
-                    const bool ok = sc < S;
-                    kk[u][0] = ok ? __builtin_nontemporal_load(p) : dbl2{0.0, 0.0};
-                    kk[u][1] = ok ? __builtin_nontemporal_load(p + 1) : dbl2{0.0, 0.0};
-                }
-                double f[U][K];
-#pragma unroll
-                for (int u = 0; u < U; ++u) load_charges<K>(fT + (size_t)ix[u] * KS, f[u]);
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-#pragma unroll
-                    for (int b = 0; b < K; ++b) {
-                        a[0][b] += kk[u][0].x * f[u][b];
-                        a[1][b] += kk[u][0].y * f[u][b];
-                        a[2][b] += kk[u][1].x * f[u][b];
-                        a[3][b] += kk[u][1].y * f[u][b];
-                    }
-            }
-        }
-        // sum over the column phases: G = 16 -> lanes 4 and 8 apart in a 16-lane row
-        if constexpr (G == 16) {
+            for (int b = 0; b < K; ++b) o[r][b] = 0.0;
+        for (int term = 0; term < nterm; ++term) {
+            const ModeArgs& md = tab[term];
+            const dbl2* kc = reinterpret_cast<const dbl2*>(md.Knear + koff) + 2 * rq;
+            double a[4][K];  // rows 4rq+j, base charges
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int b = 0; b < K; ++b) {
-                    double v = a[j][b];
-                    v += dpp_f64<0x124>(v);  // row_ror:4
-                    v += dpp_f64<0x128>(v);  // row_ror:8
-                    a[j][b] = v;
+                for (int b = 0; b < K; ++b) a[j][b] = 0.0;
+            if (rowOk) {
+                for (int c0 = cph; c0 < S; c0 += U * cps) {
+                    int ix[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) ix[u] = nearPts[pb + min(c0 + u * cps, S - 1)];
+                    dbl2 kk[U][2];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int sc = c0 + u * cps;
+                        const dbl2* p = kc + (size_t)min(sc, S - 1) * cstr;
+                        const bool ok = sc < S;
+                        kk[u][0] = ok ? __builtin_nontemporal_load(p) : dbl2{0.0, 0.0};
+                        kk[u][1] = ok ? __builtin_nontemporal_load(p + 1) : dbl2{0.0, 0.0};
+                    }
+                    double f[U][K];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) load_charges<K>(fT + (size_t)ix[u] * KS, f[u]);
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+#pragma unroll
+                        for (int b = 0; b < K; ++b) {
+                            a[0][b] += kk[u][0].x * f[u][b];
+                            a[1][b] += kk[u][0].y * f[u][b];
+                            a[2][b] += kk[u][1].x * f[u][b];
+                            a[3][b] += kk[u][1].y * f[u][b];
+                        }
                 }
-        } else {
-            for (int off = lpc; off < kWave; off <<= 1)
+            }
+            // sum over the column phases: G = 16 -> lanes 4 and 8 apart in a 16-lane row
+            if constexpr (G == 16) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
 #pragma unroll
-                    for (int b = 0; b < K; ++b) a[j][b] += __shfl_xor(a[j][b], off);
+                    for (int b = 0; b < K; ++b) {
+                        double v = a[j][b];
+                        v += dpp_f64<0x124>(v);  // row_ror:4
+                        v += dpp_f64<0x128>(v);  // row_ror:8
+                        a[j][b] = v;
+                    }
+                // this lane's row 4rq + cph, mixed
+                double r[K];
+#pragma unroll
+                for (int b = 0; b < K; ++b) r[b] = cph == 0 ? a[0][b] : cph == 1 ? a[1][b] : cph == 2 ? a[2][b] : a[3][b];
+                double v[K];
+                mix_apply_t<K>(md, r, v);
+#pragma unroll
+                for (int i = 0; i < K; ++i) o[0][i] += v[i];
+            } else {
+                for (int off = lpc; off < kWave; off <<= 1)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int b = 0; b < K; ++b) a[j][b] += __shfl_xor(a[j][b], off);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    double v[K];
+                    mix_apply_t<K>(md, a[j], v);
+#pragma unroll
+                    for (int i = 0; i < K; ++i) o[NR == 4 ? j : 0][i] += v[i];
+                }
+            }
         }
-        // column phase p writes rows 4rq + p of its quad (G = 16: 4 phases = 4 rows)
         if (rowOk) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int t = 4 * rq + j;
                 const bool mine = (G == 16) ? (cph == j) : (cph == 0);
                 if (!mine || t >= nT) continue;
-                const int64_t o = out_index(operm, obase, tb + t);
-                double v[K];
-                mix_apply(mix, a[j], v);
+                const int64_t oi = out_index(operm, obase, tb + t);
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
-                    double* dst = out + (size_t)i * ldo + o;
-                    *dst = accum ? *dst + scale * v[i] : scale * v[i];
+                    const double v = scale * o[NR == 4 ? j : 0][i];
+                    double* dst = out + (size_t)i * ldo + oi;
+                    *dst = accum ? *dst + v : v;
                 }
             }
         }
@@ -990,47 +1038,25 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
 template <int D, int K>
 __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* __restrict__ perm,
                                               const int* __restrict__ iperm, const double* __restrict__ cT,
-                                              const double* __restrict__ fT, MixK<K> mix,
-                                              const double* __restrict__ C, const double* __restrict__ mu,
-                                              const Params* __restrict__ P, int flags, double scale, bool treeOut,
-                                              int64_t ldo, double* __restrict__ out) {
+                                              const double* __restrict__ fT, const ModeArgs* __restrict__ tab,
+                                              int nterm, const Params* __restrict__ P, int flags, double scale,
+                                              bool treeOut, int64_t ldo, double* __restrict__ out) {
     constexpr int D2 = D * D;
+    constexpr int KS = kStride<K>;
+    // Legendre coefficients of every base charge kept across the terms when small
+    constexpr bool kKeepCoef = D2 * K <= 48;
     int64_t k = b + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= e) return;
     const int t = perm[k];
     const int sz = P->sz;
     const int sq = t / D2, tq = t - sq * D2;
     const int i = sq / sz, j = sq - i * sz;
-    double acc[K];
-#pragma unroll
-    for (int r = 0; r < K; ++r) acc[r] = 0.0;
-    if (flags & kStageStencil) {
-        double base[K];  // the stencil is linear: weight the base charges, mix once
-#pragma unroll
-        for (int r = 0; r < K; ++r) base[r] = 0.0;
-#pragma unroll
-        for (int dr = -1; dr <= 1; ++dr) {
-            if (i + dr < 0 || i + dr >= sz) continue;
-#pragma unroll
-            for (int dc = -1; dc <= 1; ++dc) {
-                if (j + dc < 0 || j + dc >= sz) continue;
-                const int q9 = (dr + 1) * 3 + (dc + 1);
-                const double* w = C + ((size_t)tq * 9 + q9) * D2;
-                const int* it = iperm + (size_t)(sq + dr * sz + dc) * D2;  // the square's points, tree positions
-#pragma unroll
-                for (int c = 0; c < D2; ++c) {
-                    const double* f = fT + (size_t)it[c] * kStride<K>;
-#pragma unroll
-                    for (int r = 0; r < K; ++r) base[r] += w[c] * f[r];
-                }
-            }
-        }
-        mix_apply(mix, base, acc);
-    }
+    const int* itS = iperm + (size_t)sq * D2;  // the target square's points, tree positions
+    // singular term geometry (independent of the mode): shifted Legendre bases
+    double bx[D][D], by[D][D];
+    double cf[kKeepCoef ? K : 1][kKeepCoef ? D2 : 1];
     if (flags & kStageSing) {
-        const int* it = iperm + (size_t)sq * D2;
         const double X = (0.5 + i) * P->dx, Y = (0.5 + j) * P->dx;
-        double bx[D][D], by[D][D];
 #pragma unroll
         for (int n = 0; n < D; ++n)
 #pragma unroll
@@ -1047,42 +1073,95 @@ __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* _
                 bx[n][a] = sx;
                 by[n][a] = sy;
             }
-        const double* m = mu + (size_t)tq * D * D;
-        double mom[D][D];  // the square's moments, shared by every right-hand side
+        if constexpr (kKeepCoef) {
 #pragma unroll
-        for (int n = 0; n < D; ++n)
+            for (int r = 0; r < K; ++r) {
+                double hw[D2];
 #pragma unroll
-            for (int kk = 0; kk < D; ++kk) {
-                double a2 = 0.0;
+                for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cT[(size_t)itS[c] * KS + r];
 #pragma unroll
-                for (int a = 0; a <= n; ++a)
+                for (int nk = 0; nk < D2; ++nk) {
+                    // Legendre coefficient c_{n,k} = (interpolate * (sqrtW .* h))_{nk} / norm_nk
+                    double c = 0.0;
 #pragma unroll
-                    for (int bb = 0; bb <= kk; ++bb) a2 += bx[n][a] * by[kk][bb] * m[a * D + bb];
-                mom[n][kk] = a2;
+                    for (int q = 0; q < D2; ++q) c += P->interp[nk + q * D2] * hw[q];
+                    cf[r][nk] = c * P->coefScale[nk];
+                }
             }
-        double base[K];  // the term is linear in the charges: per base charge, then mixed
-#pragma unroll 1
-        for (int r = 0; r < K; ++r) {
-            double hw[D2];
+        }
+    }
+    double acc[K];
 #pragma unroll
-            for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cT[(size_t)it[c] * kStride<K> + r];
-            double sg = 0.0;
+    for (int r = 0; r < K; ++r) acc[r] = 0.0;
+    for (int term = 0; term < nterm; ++term) {
+        const ModeArgs& md = tab[term];
+        double base[K];  // stencil + singular of the base charges (linear), mixed once per term
+#pragma unroll
+        for (int r = 0; r < K; ++r) base[r] = 0.0;
+        if (flags & kStageStencil) {
+#pragma unroll
+            for (int dr = -1; dr <= 1; ++dr) {
+                if (i + dr < 0 || i + dr >= sz) continue;
+#pragma unroll
+                for (int dc = -1; dc <= 1; ++dc) {
+                    if (j + dc < 0 || j + dc >= sz) continue;
+                    const int q9 = (dr + 1) * 3 + (dc + 1);
+                    const double* w = md.C + ((size_t)tq * 9 + q9) * D2;
+                    const int* it = iperm + (size_t)(sq + dr * sz + dc) * D2;
+#pragma unroll
+                    for (int c = 0; c < D2; ++c) {
+                        double f[K];
+                        load_charges<K>(fT + (size_t)it[c] * KS, f);
+#pragma unroll
+                        for (int r = 0; r < K; ++r) base[r] += w[c] * f[r];
+                    }
+                }
+            }
+        }
+        if (flags & kStageSing) {
+            const double* m = md.mu + (size_t)tq * D * D;
+            double mom[D2];  // the square's moments under this mode
 #pragma unroll
             for (int n = 0; n < D; ++n)
 #pragma unroll
                 for (int kk = 0; kk < D; ++kk) {
-                    // Legendre coefficient c_{n,k} = (interpolate * (sqrtW .* h))_{nk} / norm_nk
-                    double cf = 0.0;
+                    double a2 = 0.0;
 #pragma unroll
-                    for (int q = 0; q < D2; ++q) cf += P->interp[(n * D + kk) + q * D2] * hw[q];
-                    sg += cf * P->coefScale[n * D + kk] * mom[n][kk];
+                    for (int a = 0; a <= n; ++a)
+#pragma unroll
+                        for (int bb = 0; bb <= kk; ++bb) a2 += bx[n][a] * by[kk][bb] * m[a * D + bb];
+                    mom[n * D + kk] = a2;
                 }
-            base[r] = sg;
-        }
-        double sing[K];
-        mix_apply(mix, base, sing);
+            if constexpr (kKeepCoef) {
 #pragma unroll
-        for (int r = 0; r < K; ++r) acc[r] += sing[r];
+                for (int r = 0; r < K; ++r) {
+                    double sg = 0.0;
+#pragma unroll
+                    for (int nk = 0; nk < D2; ++nk) sg += cf[r][nk] * mom[nk];
+                    base[r] += sg;
+                }
+            } else {
+#pragma unroll 1
+                for (int r = 0; r < K; ++r) {
+                    double hw[D2];
+#pragma unroll
+                    for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cT[(size_t)itS[c] * KS + r];
+                    double sg = 0.0;
+#pragma unroll
+                    for (int nk = 0; nk < D2; ++nk) {
+                        double c = 0.0;
+#pragma unroll
+                        for (int q = 0; q < D2; ++q) c += P->interp[nk + q * D2] * hw[q];
+                        sg += c * P->coefScale[nk] * mom[nk];
+                    }
+                    base[r] += sg;
+                }
+            }
+        }
+        double v[K];
+        mix_apply_t<K>(md, base, v);
+#pragma unroll
+        for (int r = 0; r < K; ++r) acc[r] += v[r];
     }
     const int64_t o = treeOut ? k - b : (int64_t)t;
 #pragma unroll
@@ -1154,16 +1233,16 @@ void launch_up_tier(int K, int ntask, int taskBase, int maxTask, const int4* des
 }
 
 void launch_m2l(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
-                const int* outSlot, const int* src, const double* Kop, const double* mult, const double* mix,
-                double sgn, int accum, int maxCanon, double* partial, double* local, hipStream_t s) {
+                const int* outSlot, const int* src, const ModeArgs* tab, int nterm, const double* mult, int maxCanon,
+                double* partial, double* local, hipStream_t s) {
     if (ntgt <= 0) return;
     if (maxCanon > kMaxCanon) throw std::invalid_argument("k_m2l: more canonical pairs per target than staged");
     const unsigned nb = blocks_for((int64_t)ntgt * kWave, 256);
     const size_t shm = K >= 4 ? (size_t)4 * std::max(maxCanon, 1) * kRank * K * sizeof(double) : 0;
     // blocks in flight per wave: 4 (8 KB) for one or two right-hand sides, 2 above
     ANISO_DISPATCH_K(K, (k_m2l<KK, (KK <= 2 ? 4 : 2)><<<nb, 256, shm, s>>>(ntgt, tgt, ptr, nDir, canonBase, outSlot,
-                                                                            src, Kop, mult, make_mix<KK>(mix), sgn,
-                                                                            accum, maxCanon, partial, local)));
+                                                                            src, tab, nterm, mult, maxCanon, partial,
+                                                                            local)));
     HIP_LAUNCH_CHECK();
 }
 
@@ -1191,17 +1270,17 @@ void launch_near_sym(int K, int nl, const int4* leafInfo, const int64_t* nearPts
 }
 
 void launch_near(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
-                 const int64_t* nearKOff, const double* Kop, const double* fT, const double* mix, const int* operm,
+                 const int64_t* nearKOff, const ModeArgs* tab, int nterm, const double* fT, const int* operm,
                  int64_t obase, int64_t ldo, int flags, double scale, int accum, double* out, hipStream_t s) {
     if (nl <= 0) return;
     if (maxLeaf <= 16) {  // 4 leaves per wave
         ANISO_DISPATCH_K(K, (k_near<KK, 16, 4><<<blocks_for((int64_t)nl * 16, 256), 256, 0, s>>>(
-                                nl, leafInfo, nearPtsPtr, nearPts, nearKOff, Kop, fT, make_mix<KK>(mix), operm, obase,
-                                ldo, flags, scale, accum, out)));
+                                nl, leafInfo, nearPtsPtr, nearPts, nearKOff, tab, nterm, fT, operm, obase, ldo, flags,
+                                scale, accum, out)));
     } else {
         ANISO_DISPATCH_K(K, (k_near<KK, 64, 4><<<blocks_for((int64_t)nl * 64, 256), 256, 0, s>>>(
-                                nl, leafInfo, nearPtsPtr, nearPts, nearKOff, Kop, fT, make_mix<KK>(mix), operm, obase,
-                                ldo, flags, scale, accum, out)));
+                                nl, leafInfo, nearPtsPtr, nearPts, nearKOff, tab, nterm, fT, operm, obase, ldo, flags,
+                                scale, accum, out)));
     }
     HIP_LAUNCH_CHECK();
 }
@@ -1223,24 +1302,24 @@ void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* 
 
 template <int D>
 static void corr_d(int K, unsigned nb, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT,
-                   const double* fT, const double* mix, const double* C, const double* mu, const Params* P, int flags,
-                   double scale, bool treeOut, int64_t ldo, double* out, hipStream_t s) {
-    ANISO_DISPATCH_K(K, (k_corr<D, KK><<<nb, 256, 0, s>>>(b, e, perm, iperm, cT, fT, make_mix<KK>(mix), C, mu, P,
-                                                          flags, scale, treeOut, ldo, out)));
+                   const double* fT, const ModeArgs* tab, int nterm, const Params* P, int flags, double scale,
+                   bool treeOut, int64_t ldo, double* out, hipStream_t s) {
+    ANISO_DISPATCH_K(K, (k_corr<D, KK><<<nb, 256, 0, s>>>(b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale,
+                                                          treeOut, ldo, out)));
 }
 
 void launch_corr(int K, int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT,
-                 const double* fT, const double* mix, const double* C, const double* mu, const Params* P, int flags,
-                 double scale, bool treeOut, int64_t ldo, double* out, hipStream_t s) {
+                 const double* fT, const ModeArgs* tab, int nterm, const Params* P, int flags, double scale,
+                 bool treeOut, int64_t ldo, double* out, hipStream_t s) {
     if (e <= b) return;
     const unsigned nb = blocks_for(e - b, 256);
     switch (d) {
-        case 1: corr_d<1>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
-        case 2: corr_d<2>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
-        case 3: corr_d<3>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
-        case 4: corr_d<4>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
-        case 5: corr_d<5>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
-        case 6: corr_d<6>(K, nb, b, e, perm, iperm, cT, fT, mix, C, mu, P, flags, scale, treeOut, ldo, out, s); break;
+        case 1: corr_d<1>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
+        case 2: corr_d<2>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
+        case 3: corr_d<3>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
+        case 4: corr_d<4>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
+        case 5: corr_d<5>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
+        case 6: corr_d<6>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
         default: throw std::invalid_argument("quadRule out of range");
     }
     HIP_LAUNCH_CHECK();

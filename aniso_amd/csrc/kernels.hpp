@@ -26,6 +26,20 @@ struct Params {
     double legB[kMaxD * kMaxD * kMaxD];     // Taylor-shifted Legendre coefficients
 };
 
+constexpr int kMaxRhs = 8;  // right-hand sides of one batched apply
+
+// One mode term of a batched apply (device-side table, one entry per term): the
+// mode's cached operators and its K x K mix (rhs i = sum_b mix[i][b] base b).
+struct ModeArgs {
+    const double* Km2l;   // stored M2L blocks (column-major 16 x 16)
+    const double* Knear;  // near-field blocks
+    const double* C;      // stencil weights (d2 x 9 x d2)
+    const double* mu;     // singular moments
+    double sgn;           // (-1)^m: K_{B<-A} = sgn K_{A<-B}^T
+    double pad;
+    double mix[kMaxRhs][kMaxRhs];
+};
+
 enum StageMask : int {
     kStageFar = 1,      // M2L + L2L + L2P (both kernels)
     kStageNear = 2,     // U/W near field (both kernels)
@@ -56,10 +70,11 @@ void launch_up_tier(int K, int ntask, int taskBase, int maxTask, const int4* des
                     const int4* code, const double4* geom, const int2* leafRange, const double* pxT, const double* pyT,
                     const double* xin, int64_t ldi, int treeIn, const int* perm, const double* sigT, const double* wT,
                     double* fT, double* cT, const Params* P, double* mult, hipStream_t s);
-// accum = 0 stores local, 1 adds to it (later modes of a block apply)
+// All terms in one launch: local = sum over the terms (stored), transposed
+// canonical products summed over the terms into their partial slots (stored).
 void launch_m2l(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
-                const int* outSlot, const int* src, const double* Kop, const double* mult, const double* mix,
-                double sgn, int accum, int maxCanon, double* partial, double* local, hipStream_t s);
+                const int* outSlot, const int* src, const ModeArgs* tab, int nterm, const double* mult, int maxCanon,
+                double* partial, double* local, hipStream_t s);
 void launch_m2l_gather(int K, int ntgt, const int* tgt, const int* inPtr, const double* partial, double* local,
                        hipStream_t s);
 // Output index mode of k_near / k_down_tier / k_corr: operm = perm writes the
@@ -70,9 +85,10 @@ void launch_near_sym(int K, int nl, const int4* leafInfo, const int64_t* nearPts
                      const int64_t* nearKOff, const int2* nearSym, const double* Kop, const double* fT,
                      const double* mix, const int* operm, int64_t obase, int64_t ldo, int maxS, int flags, double sgn,
                      double scale, int accum, double* partial, double* out, hipStream_t s);
-// near field with directed storage; maxLeaf = the largest target leaf (points)
+// near field with directed storage, all terms in one launch (out stored, or added
+// with accum); maxLeaf = the largest target leaf (points)
 void launch_near(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
-                 const int64_t* nearKOff, const double* Kop, const double* fT, const double* mix, const int* operm,
+                 const int64_t* nearKOff, const ModeArgs* tab, int nterm, const double* fT, const int* operm,
                  int64_t obase, int64_t ldo, int flags, double scale, int accum, double* out, hipStream_t s);
 void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* desc, const int* grpFix,
                       const int4* dn, const double* local, const Params* P, const int* leafSlot, const int* leafBegin,
@@ -80,9 +96,10 @@ void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* 
                       const int* operm, int64_t obase, int64_t ldo, const int* nearOff, int maxNear,
                       const double* nearPart, const int2* chain, int maxChain, int flags, double scale, double* out,
                       hipStream_t s);
+// corrections of all terms in one launch, added to out
 void launch_corr(int K, int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT,
-                 const double* fT, const double* mix, const double* C, const double* mu, const Params* P, int flags,
-                 double scale, bool treeOut, int64_t ldo, double* out, hipStream_t s);
+                 const double* fT, const ModeArgs* tab, int nterm, const Params* P, int flags, double scale,
+                 bool treeOut, int64_t ldo, double* out, hipStream_t s);
 void launch_sub_slice(int64_t n, int nrhs, const double* x, int64_t ldx, const double* a, int64_t lda, double* y,
                       int64_t ldy, hipStream_t s);
 
