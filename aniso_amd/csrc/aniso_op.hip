@@ -73,6 +73,10 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_NEAR_SYMMETRIC")) plan.nearSymmetric = e[0] == '1';
     plan.maxCanon = ks == 1 ? kMaxCanon : kMaxCanonBlock;
     plan.build(tree, np, 0, 1);
+    // block handles apply aniso.m's operator through the mode-shared E caches
+    // (DESIGN.md §3.9); ANISO_HARMONIC=0 keeps the per-mode operator stream
+    useAtt = ks > 1 && !plan.nearSymmetric;
+    if (const char* e = std::getenv("ANISO_HARMONIC")) useAtt = useAtt && e[0] != '0';
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
     modes.resize(kernelSize);
@@ -235,6 +239,15 @@ void Operator::uploadPlan() {
             pairTgt[p] = p < plan.m2lPtr[i] + plan.m2lNDir[i] ? plan.m2lTgt[i] : ~plan.m2lTgt[i];
     up(dM2LPairTgt, pairTgt);
     up(dM2LNDir, plan.m2lNDir);
+    if (useAtt) {
+        up(dAttPtr, plan.attPtr);
+        up(dAttSrc, plan.attSrc);
+        std::vector<int> apt(plan.attSrc.size());
+        for (size_t i = 0; i < plan.m2lTgt.size(); ++i)
+            for (int64_t p = plan.attPtr[i]; p < plan.attPtr[i + 1]; ++p) apt[p] = plan.m2lTgt[i];
+        up(dAttPairTgt, apt);
+        attReady = false;
+    }
     up(dM2LCanonBase, plan.m2lCanonBase);
     up(dM2LInPtr, plan.m2lInPtr);
     up(dM2LOutSlot, plan.m2lOutSlot);
@@ -307,6 +320,7 @@ void Operator::setCoeff(const double* ss, const double* st) {
     for (int64_t k = 0; k < geo.N; ++k) sT[k] = sigma_s[tree.perm[k]];
     up(dSigmaT, sT);
     for (auto& m : modes) m.ready = false;
+    attReady = false;
     coeffSet = true;
 }
 
@@ -330,12 +344,73 @@ void Operator::cache(int id) {
     launch_cache_near((int)plan.leaves.size(), dLeaves.as<int>(), dNearPtr.as<int64_t>(), dNearSrc.as<int>(),
                       dNearKOff.as<int64_t>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dPxT.as<double>(),
                       dPyT.as<double>(), dStCoef.as<double>(), P, id, maxSrc, mc.Knear.as<double>(), own);
+    if (useAtt && !attReady) buildAttCache();
     CorrTables ct;
     ct.build(geo, id);
     up(mc.C, ct.C);
     up(mc.mu, ct.mu);
     HIP_CHECK(hipStreamSynchronize(own));
     mc.ready = true;
+}
+
+// The mode-shared caches: E = e^-tau for every directed M2L pair
+// (column-major 16 x 16) and near block (the directed near layout), and sigma_t at
+// every point (the mode-0 diagonal).  Built once per setCoeff on a block handle.
+void Operator::buildAttCache() {
+    const Params* P = dParams.as<Params>();
+    const int64_t npairs = (int64_t)plan.attSrc.size();
+    dAttM2L.alloc((size_t)npairs * 256 * sizeof(double));
+    dAttNear.alloc((size_t)plan.nearKTotal * sizeof(double));
+    dSigDiag.alloc((size_t)geo.N * sizeof(double));
+    int maxSrc = 1;
+    for (size_t li = 0; li < plan.leaves.size(); ++li)
+        maxSrc = std::max<int>(maxSrc, (int)(plan.nearPtr[li + 1] - plan.nearPtr[li]));
+    launch_cache_att_m2l(npairs, dAttPairTgt.as<int>(), dAttSrc.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
+                         dNrx.as<double>(), dNry.as<double>(), dStCoef.as<double>(), P, dAttM2L.as<double>(), own);
+    launch_cache_near((int)plan.leaves.size(), dLeaves.as<int>(), dNearPtr.as<int64_t>(), dNearSrc.as<int>(),
+                      dNearKOff.as<int64_t>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dPxT.as<double>(),
+                      dPyT.as<double>(), dStCoef.as<double>(), P, kAttMode, maxSrc, dAttNear.as<double>(), own);
+    launch_sigma_diag(geo.N, dPxT.as<double>(), dPyT.as<double>(), dStCoef.as<double>(), P, dSigDiag.as<double>(),
+                      own);
+    HIP_CHECK(hipStreamSynchronize(own));
+    attReady = true;
+}
+
+// Do the terms of a batched apply have aniso.m's harmonic structure (harmonic.hip)?
+// Terms must be modes 0, 1, ..., nterm-1 with mix[m][i][b] = sum over j with |j| = b,
+// |i + j| = m of w_b; w comes from output row 0 (mix[b][0][b] = hw_b).  Rows that are
+// all zero (padded right-hand sides) are masked out.
+bool Operator::harmonicWeights(int K, int nterm, const int* ids, const double* mixes, HarmWeights& hw) const {
+    if (!useAtt || !attReady || plan.nearPartTotal > 0 || K < 2 || K > kMaxRhs || nterm > 2 * K - 1) return false;
+    if (!(K == 2 || K == 4 || K == 5 || K == 8)) return false;
+    for (int t = 0; t < nterm; ++t)
+        if (ids[t] != t) return false;
+    std::memset(&hw, 0, sizeof(hw));
+    auto mx = [&](int m, int i, int b) { return m < nterm ? mixes[((size_t)m * K + i) * K + b] : 0.0; };
+    double mag = 0.0;
+    for (int t = 0; t < nterm * K * K; ++t) mag = std::max(mag, std::fabs(mixes[t]));
+    for (int i = 0; i < K; ++i) {
+        bool any = false;
+        for (int m = 0; m < nterm; ++m)
+            for (int b = 0; b < K; ++b) any = any || mx(m, i, b) != 0.0;
+        hw.om[i] = any ? 1.0 : 0.0;
+    }
+    if (hw.om[0] == 0.0) return false;
+    for (int b = 0; b < K; ++b) hw.hw[b] = mx(b, 0, b);
+    std::vector<double> want((size_t)(2 * K - 1) * K * K, 0.0);
+    for (int i = 0; i < K; ++i)
+        for (int j = -(K - 1); j <= K - 1; ++j) {
+            const int b = std::abs(j), m = std::abs(i + j);
+            want[((size_t)m * K + i) * K + b] += b == 0 ? hw.hw[0] : 0.5 * hw.hw[b];
+        }
+    for (int i = 0; i < K; ++i) {
+        if (hw.om[i] == 0.0) continue;
+        hw.dw[i] = want[((size_t)0 * K + i) * K + i];
+        for (int m = 0; m < 2 * K - 1; ++m)
+            for (int b = 0; b < K; ++b)
+                if (std::fabs(want[((size_t)m * K + i) * K + b] - mx(m, i, b)) > 1e-13 * mag) return false;
+    }
+    return true;
 }
 
 void Operator::mappingHost(const double* charge, int id, double* out) {
@@ -508,6 +583,29 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     int ep = tm ? mark(s) : -1;
     span(1, e0, ep);
     const ModeArgs* tab = modeTable(K, nterm, ids, mixes);
+    HarmWeights hw;
+    if (harmonicWeights(K, nterm, ids, mixes, hw)) {
+        // every mode of aniso.m's block operator from one read of the E caches
+        launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
+                       dNearPts.as<int>(), dNearKOff.as<int64_t>(), dAttNear.as<double>(), dPxT.as<double>(),
+                       dPyT.as<double>(), dSigDiag.as<double>(), hw, dFT.as<double>(), operm, obase, ldo, mask, scale,
+                       out, s);
+        int e = tm ? mark(s) : -1;
+        span(4, ep, e);
+        ep = e;
+        launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
+                    dFT.as<double>(), tab, nterm, P, mask, scale, treeOut, ldo, out, s);
+        e = tm ? mark(s) : -1;
+        span(6, ep, e);
+        ep = e;
+        if (mask & kStageFar)
+            launch_m2l_hm(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dAttPtr.as<int64_t>(), dAttSrc.as<int>(),
+                          dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
+                          dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
+        e = tm ? mark(s) : -1;
+        span(2, ep, e);
+        ep = e;
+    } else {
     // near field: symmetric U storage (K = 1 handles) one launch per term (its
     // transposed products go to partials, summed over the terms); directed
     // storage all terms in one launch
@@ -547,6 +645,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     e = tm ? mark(s) : -1;
     span(3, ep, e);
     ep = e;
+    }  // per-mode operator stream
     // down pass (owned part): L2L + L2P + gathered transposed near products, once
     // for the sum over the terms (both are linear in the locals / partials)
     if (mask & (kStageFar | kStageNear))

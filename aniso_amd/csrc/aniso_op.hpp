@@ -84,6 +84,7 @@ public:
     int gmresHost(const double* q, double* x, int m, int maxit, double tol, double* hist, int maxhist,
                   double* finalResid);
     hipStream_t stream() const { return own; }
+    bool harmonicReady() const { return useAtt && attReady; }
     bool modeCached(int id) const { return id >= 0 && id < kernelSize && modes[id].ready; }
     int kernelSize = 0;
     // stage timing with HIP events recorded in-stream (no host sync per apply);
@@ -112,6 +113,12 @@ private:
                     const double* mixes, double* out, int64_t ldo, bool treeOut, hipStream_t s, int mask);
     void ensureWork(int K);  // work arrays for K right-hand sides
     const ModeArgs* modeTable(int K, int nterm, const int* ids, const double* mixes);
+    // harmonic (mode-shared) block apply, DESIGN.md §3.9: the E caches of every
+    // directed M2L pair and near block, built at the first cache() of a block handle
+    bool harmonicWeights(int K, int nterm, const int* ids, const double* mixes, HarmWeights& hw) const;
+    void buildAttCache();
+    bool useAtt = false, attReady = false;
+    DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttPairTgt;
     std::map<std::string, DevBuf> modeTabs;
     int workK = 0;
 

@@ -45,11 +45,6 @@ extern "C" int aniso_probe_read(unsigned long long* host) {
     } while (0)
 #endif
 
-// Row stride of the tree-order charge arrays fT/cT [N][KS]: K rounded up to even
-// (K > 1) so a row is whole 16-B vectors.
-template <int K>
-constexpr int kStride = (K == 1 || K % 2 == 0) ? K : K + 1;
-
 template <int K>
 struct MixK {
     double c[K][K];  // rhs i = sum_b c[i][b] * base b
@@ -76,12 +71,6 @@ __device__ __forceinline__ void mix_apply_t(const ModeArgs& m, const double* bas
         for (int b = 0; b < K; ++b) a += m.mix[i][b] * base[b];
         v[i] = a;
     }
-}
-
-// Output slot of tree position k: the original index perm[k] (original-order
-// output) or the owned tree-order slice k - obase (operm == nullptr).
-__device__ __forceinline__ int64_t out_index(const int* __restrict__ operm, int64_t obase, int64_t k) {
-    return operm ? (int64_t)operm[k] : k - obase;
 }
 
 // Base charge b of tree position k: x_tree[b][k] (treeIn) or x[b][perm[k]], times
@@ -695,21 +684,6 @@ __global__ void __launch_bounds__(256) k_near_sym(int nl, const int4* __restrict
         double* dst = partial + (size_t)sym.y * K;
         const double* src = fs + (size_t)Sdir * K;
         for (int i = lane; i < nv; i += kWave) dst[i] = accum ? dst[i] + src[i] : src[i];
-    }
-}
-
-// Load the K charges of one tree position (row of fT / cT, stride kStride<K>).
-template <int K>
-__device__ __forceinline__ void load_charges(const double* __restrict__ p, double (&c)[K]) {
-    if constexpr (K == 1) {
-        c[0] = p[0];
-    } else {
-#pragma unroll
-        for (int v = 0; v < kStride<K> / 2; ++v) {
-            const dbl2 x = reinterpret_cast<const dbl2*>(p)[v];
-            c[2 * v] = x.x;
-            if (2 * v + 1 < K) c[2 * v + 1] = x.y;
-        }
     }
 }
 

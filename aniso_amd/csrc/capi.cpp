@@ -337,6 +337,8 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[9] = op.plan.storedM2L;
         s[10] = op.plan.m2lCanon;
         s[11] = op.plan.nearPartTotal;
+        s[12] = op.harmonicReady() ? 1 : 0;
+        s[13] = (int64_t)op.plan.attSrc.size();
     });
 }
 

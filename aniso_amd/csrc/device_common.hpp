@@ -80,7 +80,30 @@ __device__ __forceinline__ void load_block(const double* __restrict__ K, int64_t
     }
 }
 
+// Row stride of the tree-order charge arrays fT/cT [N][KS]: K rounded up to even
+// (K > 1) so a row is whole 16-B vectors.
+template <int K>
+constexpr int kStride = (K == 1 || K % 2 == 0) ? K : K + 1;
 
+// Output slot of tree position k: the original index perm[k] (original-order
+// output) or the owned tree-order slice k - obase (operm == nullptr).
+__device__ __forceinline__ int64_t out_index(const int* __restrict__ operm, int64_t obase, int64_t k) {
+    return operm ? (int64_t)operm[k] : k - obase;
+}
 
+// Load the K charges of one tree position (row of fT / cT, stride kStride<K>).
+template <int K>
+__device__ __forceinline__ void load_charges(const double* __restrict__ p, double (&c)[K]) {
+    if constexpr (K == 1) {
+        c[0] = p[0];
+    } else {
+#pragma unroll
+        for (int v = 0; v < kStride<K> / 2; ++v) {
+            const dbl2 x = reinterpret_cast<const dbl2*>(p)[v];
+            c[2 * v] = x.x;
+            if (2 * v + 1 < K) c[2 * v + 1] = x.y;
+        }
+    }
+}
 
 }  // namespace aniso

@@ -1,0 +1,325 @@
+// harmonic.hip -- the mode-shared ("harmonic") block apply of aniso.m's operator:
+// all 2 nb - 1 Fourier modes of the block matvec from ONE read of a
+// mode-independent cache.
+//
+// Reference behaviour (file:line under lowrank/aniso):
+//   block caller  aniso.m:139-157   out_iid = sum_j chi_|j| K_|iid+j| (sigma_s u_|j|)
+//   kernels       KernelFactory.cpp:240-267   K_m = e^-tau cos(m theta) / r (merged)
+//   M2L / near    bbfmm.h:1051-1065, 1081-1099
+//
+// The identity.  Every mode's merged kernel is K_m(t <- s) = E(t, s) cos(m theta) / r
+// with E = e^-tau(s, t) independent of m.  aniso.m's output block iid sums, over
+// j in [-(nb-1), nb-1], the weight w_|j| times K_|iid+j| applied to block |j|.
+// cos is even, so cos(|iid + j| theta) = cos(iid theta) cos(j theta) -
+// sin(iid theta) sin(j theta), and the sine part cancels between j and -j (its
+// weight and block are even in j).  Hence, per matrix entry,
+//
+//     sum_j w_|j| K_|iid+j|(t,s) x_|j|(s) = (E/r) cos(iid theta) V(t,s),
+//     V(t,s) = sum_b hw_b cos(b theta) x_b(s),   hw_0 = w_0, hw_b = 2 w_b,
+//
+// with cos(b theta) = T_b(c), c = dx / r (Chebyshev recurrence).  The 45
+// mode-applies of one block matvec become one pass over E (8 B per directed
+// entry, shared by all modes) at ~K + 10 FMAs per entry.  At r = 0 (a point's own
+// entry of the near field) only mode 0 has a value, sigma_t (KernelFactory.cpp:260):
+// its term dw_iid sigma_t f_iid (dw_iid = the mode-0 weight of block iid) is added
+// apart.  The host checks that the mixes have this structure (Operator::applyBlock).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+#include "device_common.hpp"
+
+namespace aniso {
+
+// 1/sqrt(x) to full double precision: v_rsq_f64 (about 2^-22 relative) and two
+// Newton steps.  x = 0 gives a non-finite value; callers select it away.
+__device__ __forceinline__ double rsqrt_f64(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    double h = x * y;
+    double e = __builtin_fma(-h, y, 1.0);
+    y = __builtin_fma(0.5 * y, e, y);
+    h = x * y;
+    e = __builtin_fma(-h, y, 1.0);
+    return __builtin_fma(0.5 * y, e, y);
+}
+
+// T_0 .. T_{K-1} at c (cos(b theta) for c = cos theta)
+template <int K>
+__device__ __forceinline__ void cheb_T(double c, double (&T)[K]) {
+    T[0] = 1.0;
+    if constexpr (K > 1) T[1] = c;
+    const double c2 = c + c;
+#pragma unroll
+    for (int i = 2; i < K; ++i) T[i] = __builtin_fma(c2, T[i - 1], -T[i - 2]);
+}
+
+// One entry: E at (dx, dy) from the source, harmonic-weighted source charges xw;
+// o[i] += T_i(c) (E / r) V.  guard0: r = 0 possible (near field), the entry adds 0.
+template <int K, bool guard0>
+__device__ __forceinline__ void hm_entry(double e, double dx, double dy2, const double (&xw)[K], double (&o)[K]) {
+    const double r2 = __builtin_fma(dx, dx, dy2);
+    double ri = rsqrt_f64(r2);
+    if constexpr (guard0) ri = r2 > 0.0 ? ri : 0.0;
+    const double c = dx * ri;
+    double T[K];
+    cheb_T<K>(c, T);
+    double v = xw[0];
+#pragma unroll
+    for (int b = 1; b < K; ++b) v = __builtin_fma(T[b], xw[b], v);
+    const double av = (e * ri) * v;
+#pragma unroll
+    for (int i = 0; i < K; ++i) o[i] = __builtin_fma(T[i], av, o[i]);
+}
+
+// ----------------------------------------------------------------- M2L
+
+// M2L over V then X (bbfmm.h:1051-1065) for every mode of the block matvec: one
+// wave per target node, every directed pair's 2 KB E block read once as 64 lanes
+// x 32 B (column-major: lane (s, q) holds column s, rows 4q..4q+3); the lane's
+// target rows are the Chebyshev points (x_j, y_q) of the target, its column the
+// point s of the source (kernels.hip k_cache_att_m2l); PG blocks in flight.
+// local[n][t][i] = sum over pairs of sum_s (E/r) T_i V (the unscaled locals of all
+// output blocks; L2L / L2P in k_down_tier are mode-independent).
+template <int K, int PG>
+__global__ void __launch_bounds__(256) k_m2l_hm(int ntgt, const int* __restrict__ tgt,
+                                                const int64_t* __restrict__ ptr, const int* __restrict__ src,
+                                                const double* __restrict__ E, const double* __restrict__ ncx,
+                                                const double* __restrict__ ncy, const double* __restrict__ nrx,
+                                                const double* __restrict__ nry, const Params* __restrict__ P,
+                                                HarmWeights hw, const double* __restrict__ mult,
+                                                double* __restrict__ local) {
+    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) / kWave));
+    const int lane = threadIdx.x & (kWave - 1);
+    if (wave >= ntgt) return;
+    const int n = tgt[wave];
+    const int s = lane >> 2, q = lane & 3;
+    double bx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bx[j] = ncx[n] + nrx[n] * P->cheb[j];
+    const double by = ncy[n] + nry[n] * P->cheb[q];
+    const double chx = P->cheb[s & 3], chy = P->cheb[s >> 2];
+    double c[4][K];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < K; ++i) c[j][i] = 0.0;
+    const int64_t p0 = ptr[wave], p1 = ptr[wave + 1];
+    for (int64_t cb = p0; cb < p1; cb += kWave) {
+        const int cnt = (int)min<int64_t>(kWave, p1 - cb);
+        const int mySrc = lane < cnt ? src[cb + lane] : 0;
+        for (int j0 = 0; j0 < cnt; j0 += PG) {
+            dbl2 kb[PG][2];
+            double xm[PG][K];
+            int B[PG];
+#pragma unroll
+            for (int g = 0; g < PG; ++g) load_block(E, cb + j0 + g, lane, j0 + g < cnt, kb[g][0], kb[g][1]);
+#pragma unroll
+            for (int g = 0; g < PG; ++g) {  // a skipped block's source is a valid clamp; its E is zero
+                B[g] = __builtin_amdgcn_readlane(mySrc, min(j0 + g, cnt - 1));
+                const double* m = mult + ((size_t)B[g] * kRank + s) * K;
+#pragma unroll
+                for (int b = 0; b < K; ++b) xm[g][b] = m[b];
+            }
+#pragma unroll
+            for (int g = 0; g < PG; ++g) {
+                const double ax = ncx[B[g]] + nrx[B[g]] * chx;
+                const double dy = (ncy[B[g]] + nry[B[g]] * chy) - by;
+                const double dy2 = dy * dy;
+                double xw[K];
+#pragma unroll
+                for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * xm[g][b];
+                const double e4[4] = {kb[g][0].x, kb[g][0].y, kb[g][1].x, kb[g][1].y};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) hm_entry<K, false>(e4[j], ax - bx[j], dy2, xw, c[j]);
+            }
+        }
+    }
+    // sum over the 16 columns (lane bits 2..5); row t = 4q' + j is entry j of the
+    // lanes with q == q' (lane 4t + (t >> 2) for row t = s)
+#pragma unroll
+    for (int off = 4; off < kWave; off <<= 1)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < K; ++i) c[j][i] += __shfl_xor(c[j][i], off);
+    const int jr = s & 3, srcLane = 4 * s + (s >> 2);
+    double* dst = local + ((size_t)n * kRank + s) * K;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const double sel = jr == 0 ? c[0][i] : jr == 1 ? c[1][i] : jr == 2 ? c[2][i] : c[3][i];
+        const double v = __shfl(sel, srcLane);
+        if ((i & 3) == q) dst[i] = hw.om[i] * v;
+    }
+}
+
+// ----------------------------------------------------------------- near field
+
+// U/W near field (bbfmm.h:1081-1099) for every mode of the block matvec, directed
+// E blocks (column-major nT4 x S per target leaf, rows padded to a multiple of 4,
+// the layout of k_cache_near): G lanes per target leaf (G = 16: leaves <= 16 points,
+// 4 leaves per wave; else 64), lane (row quad rq, column phase) computes rows
+// 4rq..4rq+3 for its columns, U columns in flight; the sources' points and charges
+// are read straight from pxT / pyT / fT (the lanes of a column share the lines).
+// out (stored, not added) = scale * (sum over sources + the mode-0 diagonal).
+template <int K, int G, int U>
+__global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict__ leafInfo,
+                                                 const int64_t* __restrict__ nearPtsPtr,
+                                                 const int* __restrict__ nearPts, const int64_t* __restrict__ nearKOff,
+                                                 const double* __restrict__ E, const double* __restrict__ pxT,
+                                                 const double* __restrict__ pyT, const double* __restrict__ sigDiag,
+                                                 HarmWeights hw, const double* __restrict__ fT,
+                                                 const int* __restrict__ operm, int64_t obase, int64_t ldo,
+                                                 int flags, double scale, double* __restrict__ out) {
+    static_assert(G == 16 || G == 64, "leaf group of 16 or 64 lanes");
+    constexpr int KS = kStride<K>;
+    const int gl = threadIdx.x & (G - 1);
+    const int li = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
+    const bool active = li < nl;
+    int4 info = make_int4(0, 0, 0, 0);
+    int64_t pb = 0, koff = 0;
+    if (active) {
+        info = leafInfo[li];
+        pb = nearPtsPtr[li];
+        koff = nearKOff[li];
+    }
+    const bool nearOn = (flags & kStageNear) != 0;
+    const int nT = info.z, S = nearOn ? info.w : 0;
+    const int64_t tb = info.y;
+    const int nq = (nT + 3) >> 2;  // row quads
+    const int cstr = 2 * nq;       // column stride in 16-B units
+    int lpc = 4;                   // lanes per column (G = 16: leaves <= 16 points, 4 quads)
+    if constexpr (G == 64) {
+        lpc = 1;
+        while (lpc < nq && lpc < kWave) lpc <<= 1;
+    }
+    const int cps = G / lpc, cph = gl / lpc;
+    for (int rc = 0; rc < nq || rc == 0; rc += G) {  // > 64 row quads: leaves over 256 points
+        const int rq = rc + (gl & (lpc - 1));
+        const bool rowOk = active && rq < nq;
+        double tx[4], ty[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = min(4 * rq + j, max(nT - 1, 0));  // padded rows: E is zero there
+            tx[j] = rowOk ? pxT[tb + t] : 0.0;
+            ty[j] = rowOk ? pyT[tb + t] : 0.0;
+        }
+        double a[4][K];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < K; ++i) a[j][i] = 0.0;
+        if (rowOk) {
+            const dbl2* kc = reinterpret_cast<const dbl2*>(E + koff) + 2 * rq;
+            for (int c0 = cph; c0 < S; c0 += U * cps) {
+                int ix[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) ix[u] = nearPts[pb + min(c0 + u * cps, S - 1)];
+                dbl2 kk[U][2];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int sc = c0 + u * cps;
+                    const dbl2* p = kc + (size_t)min(sc, S - 1) * cstr;
+                    const bool ok = sc < S;
+                    kk[u][0] = ok ? __builtin_nontemporal_load(p) : dbl2{0.0, 0.0};
+                    kk[u][1] = ok ? __builtin_nontemporal_load(p + 1) : dbl2{0.0, 0.0};
+                }
+                double f[U][K], sx[U], sy[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    load_charges<K>(fT + (size_t)ix[u] * KS, f[u]);
+                    sx[u] = pxT[ix[u]];
+                    sy[u] = pyT[ix[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    double xw[K];
+#pragma unroll
+                    for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * f[u][b];
+                    const double e4[4] = {kk[u][0].x, kk[u][0].y, kk[u][1].x, kk[u][1].y};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const double dy = sy[u] - ty[j];
+                        hm_entry<K, true>(e4[j], sx[u] - tx[j], dy * dy, xw, a[j]);
+                    }
+                }
+            }
+        }
+        // sum over the column phases
+        if constexpr (G == 16) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    double v = a[j][i];
+                    v += dpp_f64<0x124>(v);  // row_ror:4
+                    v += dpp_f64<0x128>(v);  // row_ror:8
+                    a[j][i] = v;
+                }
+        } else {
+            for (int off = lpc; off < kWave; off <<= 1)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int i = 0; i < K; ++i) a[j][i] += __shfl_xor(a[j][i], off);
+        }
+        if (rowOk) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int t = 4 * rq + j;
+                const bool mine = (G == 16) ? (cph == j) : (cph == 0);
+                if (!mine || t >= nT) continue;
+                const int64_t k = tb + t;
+                double f[K];
+                load_charges<K>(fT + (size_t)k * KS, f);
+                const double sd = nearOn ? sigDiag[k] : 0.0;
+                const int64_t oi = out_index(operm, obase, k);
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+                    out[(size_t)i * ldo + oi] = hw.om[i] * scale * __builtin_fma(hw.dw[i] * sd, f[i], a[j][i]);
+            }
+        }
+        if constexpr (G == 16) break;
+    }
+}
+
+// ----------------------------------------------------------------- launchers
+
+#define ANISO_HM_DISPATCH_K(k, CALL)                                                                    \
+    switch (k) {                                                                                        \
+        case 2: { constexpr int KK = 2; CALL; } break;                                                  \
+        case 4: { constexpr int KK = 4; CALL; } break;                                                  \
+        case 5: { constexpr int KK = 5; CALL; } break;                                                  \
+        case 8: { constexpr int KK = 8; CALL; } break;                                                  \
+        default: throw std::invalid_argument("harmonic apply: unsupported block count " + std::to_string(k)); \
+    }
+
+void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* src, const double* E,
+                   const double* ncx, const double* ncy, const double* nrx, const double* nry, const Params* P,
+                   const HarmWeights& hw, const double* mult, double* local, hipStream_t s) {
+    if (ntgt <= 0) return;
+    const unsigned nb = blocks_for((int64_t)ntgt * kWave, 256);
+    ANISO_HM_DISPATCH_K(K, (k_m2l_hm<KK, 4><<<nb, 256, 0, s>>>(ntgt, tgt, ptr, src, E, ncx, ncy, nrx, nry, P, hw,
+                                                                mult, local)));
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
+                    const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
+                    const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
+                    int64_t ldo, int flags, double scale, double* out, hipStream_t s) {
+    if (nl <= 0) return;
+    if (maxLeaf <= 16) {  // 4 leaves per wave
+        ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, 16, 4><<<blocks_for((int64_t)nl * 16, 256), 256, 0, s>>>(
+                                   nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm,
+                                   obase, ldo, flags, scale, out)));
+    } else {
+        ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, 64, 4><<<blocks_for((int64_t)nl * 64, 256), 256, 0, s>>>(
+                                   nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm,
+                                   obase, ldo, flags, scale, out)));
+    }
+    HIP_LAUNCH_CHECK();
+}
+
+}  // namespace aniso

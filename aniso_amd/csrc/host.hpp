@@ -90,6 +90,10 @@ struct Plan {
     std::vector<int> m2lTgt;                   // active target nodes with M2L work
     std::vector<int64_t> m2lPtr;               // CSR over m2lTgt -> source nodes
     std::vector<int> m2lSrc;
+    // mode-shared (attenuation) plan of block handles: every V then
+    // X source of each m2lTgt, directed (no symmetric reduction)
+    std::vector<int64_t> attPtr;
+    std::vector<int> attSrc;
     // tiered up / down passes: tier k has root level
     // tierRootLevel[k] and bottom level tierBottomLevel[k] (k = 0 is the deepest).
     std::vector<int> tierRootLevel, tierBottomLevel;

@@ -288,6 +288,8 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     for (int i = 0; i < t.nn; ++i) m2lActive[i] = !t.isEmpty[i] && t.parent[i] != -1 && intersects(i);
     std::vector<std::vector<int>> inCanon(t.nn), inFrom(t.nn);  // per receiver: canonical ids, their senders
     m2lPtr.push_back(0);
+    attPtr.assign(1, 0);
+    attSrc.clear();
     int canon = 0;
     std::vector<int> canonSrc;
     for (int i = 0; i < t.nn; ++i) {
@@ -298,6 +300,7 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
             int b = t.vIdx[k];
             if (t.isEmpty[b]) continue;
             ++pairsM2L;
+            attSrc.push_back(b);
             if (symmetric && m2lActive[b]) {
                 if (i < b && (int)canonSrc.size() < maxCanon) {
                     canonSrc.push_back(b);
@@ -311,8 +314,10 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         for (int64_t k = t.xPtr[i]; k < t.xPtr[i + 1]; ++k)
             if (!t.isEmpty[t.xIdx[k]]) {
                 m2lSrc.push_back(t.xIdx[k]);
+                attSrc.push_back(t.xIdx[k]);
                 ++pairsM2L;
             }
+        attPtr.push_back((int64_t)attSrc.size());
         m2lNDir.push_back((int)(m2lSrc.size() - m2lPtr.back()));
         m2lCanonBase.push_back(canon);
         m2lMaxCanon = std::max<int>(m2lMaxCanon, (int)canonSrc.size());

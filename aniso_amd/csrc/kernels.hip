@@ -119,11 +119,14 @@ __device__ double sigma_eval(const Params* __restrict__ P, const double* __restr
     return s;
 }
 
-// imag_m + real_m (makeKernels, KernelFactory.cpp:240-267); a = source, b = target
+// imag_m + real_m (makeKernels, KernelFactory.cpp:240-267); a = source, b = target.
+// m = kAttMode: the mode-independent factor e^-tau alone (0 at r = 0), the entry of
+// the mode-shared cache.
 __device__ double pair_kernel(const Params* __restrict__ P, const double* __restrict__ stcoef, int m, double ax,
                               double ay, double bx, double by) {
     double ddx = ax - bx, ddy = ay - by;
     double dist = sqrt(ddx * ddx + ddy * ddy);
+    if (m == kAttMode) return dist == 0.0 ? 0.0 : exp(-line_integral(P, stcoef, ax, ay, bx, by));
     if (dist == 0.0) return m == 0 ? sigma_eval(P, stcoef, ax, ay) : 0.0;
     double gk = (m == 0) ? 1.0 / dist : cos(m * atan2(ddy, ddx)) / dist;
     double tau = line_integral(P, stcoef, ax, ay, bx, by);
@@ -159,6 +162,37 @@ __global__ void __launch_bounds__(256) k_cache_m2l(int64_t total, const int* __r
     double ax = ncx[sn] + nrx[sn] * P->cheb[s & 3];
     double ay = ncy[sn] + nry[sn] * P->cheb[s >> 2];
     K[e] = pair_kernel(P, stcoef, mode, ax, ay, bx, by);
+}
+
+// Mode-shared M2L cache: E[t][s] = e^-tau(cheb_s(src), cheb_t(tgt))
+// for every directed (target, source) pair, column-major (pair*256 + s*16 + t), the
+// layout k_m2l_hm streams (lane (column s, row quad) reads 32 contiguous bytes).
+__global__ void __launch_bounds__(256) k_cache_att_m2l(int64_t total, const int* __restrict__ pairTgt,
+                                                       const int* __restrict__ src, const double* __restrict__ ncx,
+                                                       const double* __restrict__ ncy, const double* __restrict__ nrx,
+                                                       const double* __restrict__ nry,
+                                                       const double* __restrict__ stcoef,
+                                                       const Params* __restrict__ P, double* __restrict__ E) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    int64_t p = e >> 8;
+    const int s = (int)((e >> 4) & 15), t = (int)(e & 15);
+    const int tn = pairTgt[p], sn = src[p];
+    double bx = ncx[tn] + nrx[tn] * P->cheb[t & 3];
+    double by = ncy[tn] + nry[tn] * P->cheb[t >> 2];
+    double ax = ncx[sn] + nrx[sn] * P->cheb[s & 3];
+    double ay = ncy[sn] + nry[sn] * P->cheb[s >> 2];
+    E[e] = pair_kernel(P, stcoef, kAttMode, ax, ay, bx, by);
+}
+
+// The mode-0 diagonal of the merged kernel, sigma_t at each point (evaluate(a),
+// KernelFactory.cpp:260), tree order: the r = 0 entry the mode-shared near field
+// adds apart from its blocks.
+__global__ void k_sigma_diag(int64_t N, const double* __restrict__ pxT, const double* __restrict__ pyT,
+                             const double* __restrict__ stcoef, const Params* __restrict__ P,
+                             double* __restrict__ out) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < N) out[k] = sigma_eval(P, stcoef, pxT[k], pyT[k]);
 }
 
 // downPassCache's U/W blocks (bbfmm.h:991-1011): per target leaf, column-major
@@ -226,6 +260,22 @@ void launch_cache_m2l(int64_t npairs, const int* pairTgt, const int* src, const 
     if (npairs <= 0) return;
     int64_t total = npairs * 256;
     k_cache_m2l<<<blocks_for(total, 256), 256, 0, s>>>(total, pairTgt, src, ncx, ncy, nrx, nry, stcoef, P, mode, K);
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_cache_att_m2l(int64_t npairs, const int* pairTgt, const int* src, const double* ncx, const double* ncy,
+                          const double* nrx, const double* nry, const double* stcoef, const Params* P, double* E,
+                          hipStream_t s) {
+    if (npairs <= 0) return;
+    int64_t total = npairs * 256;
+    k_cache_att_m2l<<<blocks_for(total, 256), 256, 0, s>>>(total, pairTgt, src, ncx, ncy, nrx, nry, stcoef, P, E);
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_sigma_diag(int64_t N, const double* pxT, const double* pyT, const double* stcoef, const Params* P,
+                       double* out, hipStream_t s) {
+    if (N <= 0) return;
+    k_sigma_diag<<<blocks_for(N, 256), 256, 0, s>>>(N, pxT, pyT, stcoef, P, out);
     HIP_LAUNCH_CHECK();
 }
 

@@ -40,6 +40,16 @@ struct ModeArgs {
     double mix[kMaxRhs][kMaxRhs];
 };
 
+// Harmonic weights of a block apply (harmonic.hip): the mixes of
+// aniso.m's forward / mforward, out_i = sum_j w_|j| K_|i+j| x_|j|, as hw_b = w_0
+// (b = 0) or 2 w_b, dw_i = the mode-0 (diagonal) weight of output i, and om_i = 0
+// for an output the mixes leave empty (a padded right-hand side).
+struct HarmWeights {
+    double hw[kMaxRhs];
+    double dw[kMaxRhs];
+    double om[kMaxRhs];
+};
+
 enum StageMask : int {
     kStageFar = 1,      // M2L + L2L + L2P (both kernels)
     kStageNear = 2,     // U/W near field (both kernels)
@@ -100,6 +110,14 @@ void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* 
 void launch_corr(int K, int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT,
                  const double* fT, const ModeArgs* tab, int nterm, const Params* P, int flags, double scale,
                  bool treeOut, int64_t ldo, double* out, hipStream_t s);
+// harmonic block apply (harmonic.hip): all modes from the mode-shared E caches
+void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* src, const double* E,
+                   const double* ncx, const double* ncy, const double* nrx, const double* nry, const Params* P,
+                   const HarmWeights& hw, const double* mult, double* local, hipStream_t s);
+void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
+                    const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
+                    const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
+                    int64_t ldo, int flags, double scale, double* out, hipStream_t s);
 void launch_sub_slice(int64_t n, int nrhs, const double* x, int64_t ldx, const double* a, int64_t lda, double* y,
                       int64_t ldy, hipStream_t s);
 
@@ -110,6 +128,14 @@ void launch_cache_m2l(int64_t npairs, const int* pairTgt, const int* src, const 
 void launch_cache_near(int nl, const int* leaves, const int64_t* nearPtr, const int* nearSrc, const int64_t* nearKOff,
                        const int64_t* begin, const int64_t* count, const double* pxT, const double* pyT,
                        const double* stcoef, const Params* P, int mode, int maxSrc, double* K, hipStream_t s);
+// mode-shared cache: pair_kernel's mode argument kAttMode gives
+// e^-tau alone (0 at r = 0); launch_cache_near takes it as well
+constexpr int kAttMode = -1;
+void launch_cache_att_m2l(int64_t npairs, const int* pairTgt, const int* src, const double* ncx, const double* ncy,
+                          const double* nrx, const double* nry, const double* stcoef, const Params* P, double* E,
+                          hipStream_t s);
+void launch_sigma_diag(int64_t N, const double* pxT, const double* pyT, const double* stcoef, const Params* P,
+                       double* out, hipStream_t s);
 void launch_permute(int64_t N, const int* perm, const double* orig, double* tree, hipStream_t s);
 
 // host-callable device helpers used by tests through the C ABI

@@ -7,8 +7,9 @@ sz=1024, d=1, ns=10, np=4, maxLevel=20, ks=5 Fourier blocks (9 modes), g=0.8,
 N = 1,048,576 points, sigma_s = 20, sigma_a = 0.2 (demo.m:15-16), the Gaussian
 charge in block 0 (demo.m:24-29) -- and its GMRES matvec x - mforward(x)
 (aniso.m:138-157, 155): 45 mode-applies of the reference per matvec, computed as
-ONE batched apply (one up pass over the 5 blocks, every mode's cached operators
-streamed once for all 5 right-hand sides, one down pass).  A "step" is one block
+ONE harmonic block apply (one up pass over the 5 blocks, one read
+of the mode-shared e^-tau caches for all 9 modes and 5 outputs, the per-mode
+correction stencils, one down pass).  A "step" is one block
 matvec; steps are chained (v <- A v) with every vector resident in HBM, in tree
 order (a fixed relabelling of the unknowns: no permutation gathers on the data
 path).  fp64 throughout.  --workload mode0 instead times main.cpp's matvec
@@ -20,8 +21,9 @@ subtree (strong scaling: total work fixed).  Each rank applies its shard; one
 all-gather of tree-ordered slices rebuilds the replicated block vector.
 
 Also reported on the same JSON line:
-  roofline      HBM roofline of the dominant kernel (k_m2l, one launch per mode),
-                timed with HIP events on the apply stream over the timed region;
+  roofline      HBM roofline of the dominant kernel (the M2L stream, k_m2l_hm, one
+                launch per matvec), timed with HIP events on the apply stream over
+                the timed region;
   cpu_baseline  the CPU oracle (a faithful port of the reference apply) on this
                 host's cores, on a bounded sample of the same geometry family;
   rel_err_vs_cpu  GPU vs CPU oracle on that sample's inputs.
@@ -275,19 +277,27 @@ def main():
     my_stats = op.stats()
     ms = 1e3 * elapsed / args.steps
     value = args.steps / elapsed
-    # dominant kernel: k_m2l, one launch per mode per matvec.  Algorithmic bytes per
-    # launch: the stored merged 16x16 M2L operators once (2 KB per stored block),
-    # the multipoles read and locals written per target node (16 x nb doubles
-    # each), one transposed partial (16 x nb doubles) per canonical pair
-    launches = len(modes) if block else 1
-    m2l_bytes = (2048.0 * my_stats["stored_m2l"] + 2.0 * 128.0 * nb * my_stats["m2l_targets"]
-                 + 128.0 * nb * my_stats["m2l_canon"])
-    m2l_ms = times["m2l"] / launches
+    # dominant kernel: the M2L stream, one launch per matvec.
+    # Harmonic block apply (k_m2l_hm, §3.9): the mode-shared E block of every
+    # directed pair (2 KB) once, plus the multipoles read and the locals written per
+    # target node (16 x nb doubles each).  Per-mode stream (k_m2l): the stored merged
+    # operators of every mode term, the same per-target bytes per term, one
+    # transposed partial (16 x nb doubles) per canonical pair and term.
+    harmonic = block and my_stats["harmonic"] == 1
+    if harmonic:
+        m2l_bytes = 2048.0 * my_stats["att_m2l_blocks"] + 2.0 * 128.0 * nb * my_stats["m2l_targets"]
+        kname, pmc_name = f"k_m2l_hm<{nb}>", f"void aniso::k_m2l_hm<{nb}, 4>"
+    else:
+        terms = len(modes) if block else 1
+        m2l_bytes = terms * (2048.0 * my_stats["stored_m2l"] + 2.0 * 128.0 * nb * my_stats["m2l_targets"]
+                             + 128.0 * nb * my_stats["m2l_canon"])
+        kname = f"k_m2l<{nb}> ({terms} mode terms)"
+        pmc_name = f"void aniso::k_m2l<{nb}, {4 if nb <= 2 else 2}>"
+    m2l_ms = times["m2l"]
     achieved = m2l_bytes / (m2l_ms * 1e-3) / 1e9 if m2l_ms > 0 else 0.0
-    pmc_name = f"aniso::k_m2l<{nb}>"
     traffic, tsrc = pmc_traffic(pmc_name) if world == 1 and args.sz == 1024 and args.d == 1 else (None, None)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": f"k_m2l<{nb}> (per mode)",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
                 "kernel_ms": round(m2l_ms, 5), "algorithmic_bytes": int(m2l_bytes), "traffic_source": tsrc}
     applies = ks * (2 * ks - 1) if block else 1  # the reference's mapping calls per matvec
     cfg = (f"configs[2] (1M points, d=1, ns=10, np=4, maxLevel=20, g={args.g}): aniso.m GMRES block matvec "

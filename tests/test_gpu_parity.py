@@ -486,3 +486,49 @@ def test_block_matvec_at_config3_size_matches_mode_applies():
     torch.cuda.synchronize()
     assert torch.equal(y1, y2)
     assert float(torch.linalg.norm(y1 - ref) / torch.linalg.norm(ref)) <= 1e-13
+
+
+@pytest.mark.parametrize("sz,d,ks,ml,coeffs", [(16, 1, 5, 20, "main"), (13, 2, 3, 20, "rough"), (20, 1, 2, 20, "rough"),
+                                                (11, 3, 4, 20, "rough"), (24, 1, 5, 2, "rough"), (12, 2, 2, 0, "main")])
+def test_harmonic_block_apply_matches_per_mode_stream(sz, d, ks, ml, coeffs, monkeypatch):
+    """The mode-shared (harmonic) block apply (one read of the
+    e^-tau caches for all 2ks-1 modes) against the per-mode operator stream and the
+    oracle, for aniso.m's forward / mforward / GMRES matvec; odd sz (X/W lists),
+    maxLevel-limited 64-point leaves, a single 576-point leaf (G = 64 lanes per leaf),
+    padded block counts (3 -> 4)."""
+    torch = _torch()
+    import aniso_amd
+    from oracle.oracle_py import Oracle
+
+    def make(harmonic):
+        monkeypatch.setenv("ANISO_HARMONIC", "1" if harmonic else "0")
+        a = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, ml)
+        xy = a.getNodes()
+        a.setCoeff(*(main_coeffs(xy) if coeffs == "main" else rough_coeffs(xy, 4)))
+        for m in range(2 * ks - 1):
+            a.cache(m)
+        return a, xy
+
+    h, xy = make(True)
+    p, _ = make(False)
+    assert h.stats()["harmonic"] == 1 and p.stats()["harmonic"] == 0
+    o = Oracle(sz, d, ks, 0.8, 8, 4, ml)
+    ss, st = main_coeffs(xy) if coeffs == "main" else rough_coeffs(xy, 4)
+    o.setCoeff(ss, st)
+    for m in range(2 * ks - 1):
+        o.cache(m)
+    U = np.random.default_rng(ks + sz).uniform(-1, 1, (ks, h.N))
+    U[0] += gaussian_charge(xy)
+    Ud = torch.tensor(U, device="cuda")
+    for which in (0, 1, 2):
+        oh, op_ = torch.zeros_like(Ud), torch.zeros_like(Ud)
+        h.block_op_dev(which, Ud, oh)
+        p.block_op_dev(which, Ud, op_)
+        torch.cuda.synchronize()
+        ref = _block_ref(o, U, h.g, ss, which)
+        assert _rel(oh.cpu().numpy(), op_.cpu().numpy()) <= 1e-13, which
+        assert _rel(oh.cpu().numpy(), ref) <= TOL, (which, _rel(oh.cpu().numpy(), ref))
+    # single-mode applies on a harmonic handle keep the per-mode caches
+    q = gaussian_charge(xy)
+    for m in (0, 2 * ks - 2):
+        assert _rel(h.mapping(q, m), o.mapping(q, m)) <= TOL
