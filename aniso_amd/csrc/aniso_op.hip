@@ -242,10 +242,9 @@ void Operator::uploadPlan() {
     if (useAtt) {
         up(dAttPtr, plan.attPtr);
         up(dAttSrc, plan.attSrc);
-        std::vector<int> apt(plan.attSrc.size());
-        for (size_t i = 0; i < plan.m2lTgt.size(); ++i)
-            for (int64_t p = plan.attPtr[i]; p < plan.attPtr[i + 1]; ++p) apt[p] = plan.m2lTgt[i];
-        up(dAttPairTgt, apt);
+        up(dAttBlk, plan.attBlk);
+        up(dAttOwner, plan.attOwner);
+        up(dAttOther, plan.attOther);
         attReady = false;
     }
     up(dM2LCanonBase, plan.m2lCanonBase);
@@ -349,6 +348,10 @@ void Operator::cache(int id) {
     ct.build(geo, id);
     up(mc.C, ct.C);
     up(mc.mu, ct.mu);
+    mc.hostC = ct.C;
+    mc.hostMu = ct.mu;
+    HIP_CHECK(hipStreamSynchronize(own));  // folded tables may still be read by queued work
+    corrTabs.clear();
     HIP_CHECK(hipStreamSynchronize(own));
     mc.ready = true;
 }
@@ -358,14 +361,14 @@ void Operator::cache(int id) {
 // every point (the mode-0 diagonal).  Built once per setCoeff on a block handle.
 void Operator::buildAttCache() {
     const Params* P = dParams.as<Params>();
-    const int64_t npairs = (int64_t)plan.attSrc.size();
+    const int64_t npairs = (int64_t)plan.attOwner.size();  // stored blocks
     dAttM2L.alloc((size_t)npairs * 256 * sizeof(double));
     dAttNear.alloc((size_t)plan.nearKTotal * sizeof(double));
     dSigDiag.alloc((size_t)geo.N * sizeof(double));
     int maxSrc = 1;
     for (size_t li = 0; li < plan.leaves.size(); ++li)
         maxSrc = std::max<int>(maxSrc, (int)(plan.nearPtr[li + 1] - plan.nearPtr[li]));
-    launch_cache_att_m2l(npairs, dAttPairTgt.as<int>(), dAttSrc.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
+    launch_cache_att_m2l(npairs, dAttOwner.as<int>(), dAttOther.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
                          dNrx.as<double>(), dNry.as<double>(), dStCoef.as<double>(), P, dAttM2L.as<double>(), own);
     launch_cache_near((int)plan.leaves.size(), dLeaves.as<int>(), dNearPtr.as<int64_t>(), dNearSrc.as<int>(),
                       dNearKOff.as<int64_t>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dPxT.as<double>(),
@@ -522,6 +525,42 @@ const ModeArgs* Operator::modeTable(int K, int nterm, const int* ids, const doub
     return buf.as<ModeArgs>();
 }
 
+// The correction tables of a batched apply, folded over its terms on the host:
+// Wc[tq][q9][c][i][b] = sum_t mix_t[i][b] C_t[tq][q9][c] and
+// Wm[tq][i][b][a][bb] = sum_t mix_t[i][b] mu_t[tq][a][bb] (k_corr).  Cached by
+// content, like the mode table.
+const CorrFold& Operator::corrTable(int K, int nterm, const int* ids, const double* mixes) {
+    std::string key(reinterpret_cast<const char*>(&K), sizeof(int));
+    key.append(reinterpret_cast<const char*>(ids), nterm * sizeof(int));
+    key.append(reinterpret_cast<const char*>(mixes), (size_t)nterm * K * K * sizeof(double));
+    auto it = corrTabs.find(key);
+    if (it != corrTabs.end()) return it->second;
+    const int d = geo.d, d2 = geo.d2;
+    std::vector<double> wc((size_t)d2 * 9 * d2 * K * K, 0.0), wm((size_t)d2 * K * K * d2, 0.0);
+    for (int t = 0; t < nterm; ++t) {
+        const ModeCache& mc = modes[ids[t]];
+        for (int i = 0; i < K; ++i)
+            for (int b = 0; b < K; ++b) {
+                const double w = mixes[((size_t)t * K + i) * K + b];
+                if (w == 0.0) continue;
+                for (int tq = 0; tq < d2; ++tq) {
+                    for (int q = 0; q < 9 * d2; ++q)  // (q9, c)
+                        wc[(((size_t)tq * 9 * d2 + q) * K + i) * K + b] += w * mc.hostC[(size_t)tq * 9 * d2 + q];
+                    for (int ab = 0; ab < d * d; ++ab)
+                        wm[(((size_t)tq * K + i) * K + b) * d2 + ab] += w * mc.hostMu[(size_t)tq * d * d + ab];
+                }
+            }
+    }
+    if (corrTabs.size() >= 64) {  // bound the cache; hipFree waits for work that may still read a table
+        HIP_CHECK(hipDeviceSynchronize());
+        corrTabs.clear();
+    }
+    CorrFold& f = corrTabs[key];
+    up(f.Wc, wc);
+    up(f.Wm, wm);
+    return f;
+}
+
 // One batched apply: the up pass over the K base vectors, then per term t (mode
 // ids[t], mix mixes[t]) the near field, the corrections, the M2L stream and its
 // gather, each accumulating; then one down pass.  sigT (sigma_s in tree order, or
@@ -583,6 +622,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     int ep = tm ? mark(s) : -1;
     span(1, e0, ep);
     const ModeArgs* tab = modeTable(K, nterm, ids, mixes);
+    const CorrFold& cf = corrTable(K, nterm, ids, mixes);
     HarmWeights hw;
     if (harmonicWeights(K, nterm, ids, mixes, hw)) {
         // every mode of aniso.m's block operator from one read of the E caches
@@ -594,13 +634,13 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         span(4, ep, e);
         ep = e;
         launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
-                    dFT.as<double>(), tab, nterm, P, mask, scale, treeOut, ldo, out, s);
+                    dFT.as<double>(), cf.Wc.as<double>(), cf.Wm.as<double>(), P, mask, scale, treeOut, ldo, out, s);
         e = tm ? mark(s) : -1;
         span(6, ep, e);
         ep = e;
         if (mask & kStageFar)
             launch_m2l_hm(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dAttPtr.as<int64_t>(), dAttSrc.as<int>(),
-                          dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
+                          dAttBlk.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
                           dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
         e = tm ? mark(s) : -1;
         span(2, ep, e);
@@ -628,7 +668,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     span(4, ep, e);
     ep = e;
     launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
-                dFT.as<double>(), tab, nterm, P, mask, scale, treeOut, ldo, out, s);
+                dFT.as<double>(), cf.Wc.as<double>(), cf.Wm.as<double>(), P, mask, scale, treeOut, ldo, out, s);
     e = tm ? mark(s) : -1;
     span(6, ep, e);
     ep = e;

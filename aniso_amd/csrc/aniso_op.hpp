@@ -34,7 +34,14 @@ struct DevBuf {
 
 struct ModeCache {
     DevBuf Knear, Km2l, C, mu;
+    std::vector<double> hostC, hostMu;  // the correction tables (folded per batched apply)
     bool ready = false;
+};
+
+// Correction tables of one batched apply: every term's stencil / singular table
+// folded with its mix (launch_corr).
+struct CorrFold {
+    DevBuf Wc, Wm;
 };
 
 struct StageTimes {
@@ -118,8 +125,10 @@ private:
     bool harmonicWeights(int K, int nterm, const int* ids, const double* mixes, HarmWeights& hw) const;
     void buildAttCache();
     bool useAtt = false, attReady = false;
-    DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttPairTgt;
+    DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
     std::map<std::string, DevBuf> modeTabs;
+    const CorrFold& corrTable(int K, int nterm, const int* ids, const double* mixes);
+    std::map<std::string, CorrFold> corrTabs;
     int workK = 0;
 
     void ensureDevice();

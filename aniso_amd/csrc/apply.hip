@@ -1005,32 +1005,59 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
 
 // Corrections (nearRemoval + refineAddOnFast + singularAddFast,
 // KernelFactory.cpp:445-478, 662-709, 828-860) as a 3x3-square stencil with
-// per-mode translation-invariant d2 x 9 x d2 weights, plus the singular term
-// from Legendre coefficients of the target's own square (O(d^4) moments).  Every
-// contribution carries the final 1/(2 pi) (AnisoWrapper.cpp:129-130): k_near
-// stores (or adds) its scaled sum, k_corr and k_down_tier add theirs.
+// translation-invariant d2 x 9 x d2 weights, plus the singular term from Legendre
+// coefficients of the target's own square (O(d^4) moments).  Both are linear in
+// the charges and their per-mode tables are small, so every mode term of a batched
+// apply is folded into ONE table on the host with the terms' mixes
+// (Operator::corrTable): Wc[tq][q9][c][i][b] = sum_t mix_t[i][b] C_t[tq][q9][c],
+// Wm[tq][i][b][a][bb] = sum_t mix_t[i][b] mu_t[tq][a][bb].  One pass per point:
+// each neighbour charge is loaded once (d = 1: every weight is wave-uniform).
+// Every contribution carries the final 1/(2 pi) (AnisoWrapper.cpp:129-130): the
+// near field stores its scaled sum, k_corr and k_down_tier add theirs.
 template <int D, int K>
 __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* __restrict__ perm,
                                               const int* __restrict__ iperm, const double* __restrict__ cT,
-                                              const double* __restrict__ fT, const ModeArgs* __restrict__ tab,
-                                              int nterm, const Params* __restrict__ P, int flags, double scale,
-                                              bool treeOut, int64_t ldo, double* __restrict__ out) {
+                                              const double* __restrict__ fT, const double* __restrict__ Wc,
+                                              const double* __restrict__ Wm, const Params* __restrict__ P, int flags,
+                                              double scale, bool treeOut, int64_t ldo, double* __restrict__ out) {
     constexpr int D2 = D * D;
     constexpr int KS = kStride<K>;
-    // Legendre coefficients of every base charge kept across the terms when small
-    constexpr bool kKeepCoef = D2 * K <= 48;
     int64_t k = b + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= e) return;
     const int t = perm[k];
     const int sz = P->sz;
     const int sq = t / D2, tq = t - sq * D2;
     const int i = sq / sz, j = sq - i * sz;
-    const int* itS = iperm + (size_t)sq * D2;  // the target square's points, tree positions
-    // singular term geometry (independent of the mode): shifted Legendre bases
-    double bx[D][D], by[D][D];
-    double cf[kKeepCoef ? K : 1][kKeepCoef ? D2 : 1];
+    double acc[K];
+#pragma unroll
+    for (int r = 0; r < K; ++r) acc[r] = 0.0;
+    if (flags & kStageStencil) {
+#pragma unroll
+        for (int dr = -1; dr <= 1; ++dr) {
+            if (i + dr < 0 || i + dr >= sz) continue;
+#pragma unroll
+            for (int dc = -1; dc <= 1; ++dc) {
+                if (j + dc < 0 || j + dc >= sz) continue;
+                const int q9 = (dr + 1) * 3 + (dc + 1);
+                const int* it = iperm + (size_t)(sq + dr * sz + dc) * D2;
+#pragma unroll
+                for (int c = 0; c < D2; ++c) {
+                    double f[K];
+                    load_charges<K>(fT + (size_t)it[c] * KS, f);
+                    const double* w = Wc + (((size_t)tq * 9 + q9) * D2 + c) * K * K;
+#pragma unroll
+                    for (int r = 0; r < K; ++r)
+#pragma unroll
+                        for (int bb = 0; bb < K; ++bb) acc[r] += w[r * K + bb] * f[bb];
+                }
+            }
+        }
+    }
     if (flags & kStageSing) {
+        // shifted Legendre bases of the square (singularAddFast evaluates the
+        // expansion at global coordinates, quirk 1): P_n(X + h u) = sum_a bx[n][a] u^a
         const double X = (0.5 + i) * P->dx, Y = (0.5 + j) * P->dx;
+        double bx[D][D], by[D][D];
 #pragma unroll
         for (int n = 0; n < D; ++n)
 #pragma unroll
@@ -1047,95 +1074,41 @@ __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* _
                 bx[n][a] = sx;
                 by[n][a] = sy;
             }
-        if constexpr (kKeepCoef) {
-#pragma unroll
-            for (int r = 0; r < K; ++r) {
-                double hw[D2];
-#pragma unroll
-                for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cT[(size_t)itS[c] * KS + r];
-#pragma unroll
-                for (int nk = 0; nk < D2; ++nk) {
-                    // Legendre coefficient c_{n,k} = (interpolate * (sqrtW .* h))_{nk} / norm_nk
-                    double c = 0.0;
-#pragma unroll
-                    for (int q = 0; q < D2; ++q) c += P->interp[nk + q * D2] * hw[q];
-                    cf[r][nk] = c * P->coefScale[nk];
-                }
-            }
-        }
-    }
-    double acc[K];
-#pragma unroll
-    for (int r = 0; r < K; ++r) acc[r] = 0.0;
-    for (int term = 0; term < nterm; ++term) {
-        const ModeArgs& md = tab[term];
-        double base[K];  // stencil + singular of the base charges (linear), mixed once per term
-#pragma unroll
-        for (int r = 0; r < K; ++r) base[r] = 0.0;
-        if (flags & kStageStencil) {
-#pragma unroll
-            for (int dr = -1; dr <= 1; ++dr) {
-                if (i + dr < 0 || i + dr >= sz) continue;
-#pragma unroll
-                for (int dc = -1; dc <= 1; ++dc) {
-                    if (j + dc < 0 || j + dc >= sz) continue;
-                    const int q9 = (dr + 1) * 3 + (dc + 1);
-                    const double* w = md.C + ((size_t)tq * 9 + q9) * D2;
-                    const int* it = iperm + (size_t)(sq + dr * sz + dc) * D2;
-#pragma unroll
-                    for (int c = 0; c < D2; ++c) {
-                        double f[K];
-                        load_charges<K>(fT + (size_t)it[c] * KS, f);
-#pragma unroll
-                        for (int r = 0; r < K; ++r) base[r] += w[c] * f[r];
-                    }
-                }
-            }
-        }
-        if (flags & kStageSing) {
-            const double* m = md.mu + (size_t)tq * D * D;
-            double mom[D2];  // the square's moments under this mode
-#pragma unroll
-            for (int n = 0; n < D; ++n)
-#pragma unroll
-                for (int kk = 0; kk < D; ++kk) {
-                    double a2 = 0.0;
-#pragma unroll
-                    for (int a = 0; a <= n; ++a)
-#pragma unroll
-                        for (int bb = 0; bb <= kk; ++bb) a2 += bx[n][a] * by[kk][bb] * m[a * D + bb];
-                    mom[n * D + kk] = a2;
-                }
-            if constexpr (kKeepCoef) {
-#pragma unroll
-                for (int r = 0; r < K; ++r) {
-                    double sg = 0.0;
-#pragma unroll
-                    for (int nk = 0; nk < D2; ++nk) sg += cf[r][nk] * mom[nk];
-                    base[r] += sg;
-                }
-            } else {
+        const int* itS = iperm + (size_t)sq * D2;  // the target square's points, tree positions
 #pragma unroll 1
-                for (int r = 0; r < K; ++r) {
-                    double hw[D2];
+        for (int r = 0; r < K; ++r) {
+            double hw[D2];
 #pragma unroll
-                    for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cT[(size_t)itS[c] * KS + r];
-                    double sg = 0.0;
+            for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cT[(size_t)itS[c] * KS + r];
+            // Legendre coefficients cf_{n,k} = (interpolate * (sqrtW .* h))_{nk} / norm_nk,
+            // contracted with the bases: pb[a][bb] = sum_{n >= a, k >= bb} cf_nk bx[n][a] by[k][bb]
+            double pb[D][D];
 #pragma unroll
-                    for (int nk = 0; nk < D2; ++nk) {
-                        double c = 0.0;
+            for (int a = 0; a < D; ++a)
 #pragma unroll
-                        for (int q = 0; q < D2; ++q) c += P->interp[nk + q * D2] * hw[q];
-                        sg += c * P->coefScale[nk] * mom[nk];
-                    }
-                    base[r] += sg;
-                }
+                for (int bb = 0; bb < D; ++bb) pb[a][bb] = 0.0;
+#pragma unroll
+            for (int nk = 0; nk < D2; ++nk) {
+                double c = 0.0;
+#pragma unroll
+                for (int q = 0; q < D2; ++q) c += P->interp[nk + q * D2] * hw[q];
+                c *= P->coefScale[nk];
+                const int n = nk / D, kk = nk % D;
+#pragma unroll
+                for (int a = 0; a < D; ++a)
+#pragma unroll
+                    for (int bb = 0; bb < D; ++bb)
+                        if (a <= n && bb <= kk) pb[a][bb] += c * bx[n][a] * by[kk][bb];
+            }
+            const double* wm = Wm + ((size_t)tq * K * K + r) * D2;  // [tq][i][b = r][a][bb], i stride K D2
+#pragma unroll
+            for (int ii = 0; ii < K; ++ii) {
+                double sg = 0.0;
+#pragma unroll
+                for (int ab = 0; ab < D2; ++ab) sg += pb[ab / D][ab % D] * wm[(size_t)ii * K * D2 + ab];
+                acc[ii] += sg;
             }
         }
-        double v[K];
-        mix_apply_t<K>(md, base, v);
-#pragma unroll
-        for (int r = 0; r < K; ++r) acc[r] += v[r];
     }
     const int64_t o = treeOut ? k - b : (int64_t)t;
 #pragma unroll
@@ -1276,24 +1249,24 @@ void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* 
 
 template <int D>
 static void corr_d(int K, unsigned nb, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT,
-                   const double* fT, const ModeArgs* tab, int nterm, const Params* P, int flags, double scale,
+                   const double* fT, const double* Wc, const double* Wm, const Params* P, int flags, double scale,
                    bool treeOut, int64_t ldo, double* out, hipStream_t s) {
-    ANISO_DISPATCH_K(K, (k_corr<D, KK><<<nb, 256, 0, s>>>(b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale,
-                                                          treeOut, ldo, out)));
+    ANISO_DISPATCH_K(K, (k_corr<D, KK><<<nb, 256, 0, s>>>(b, e, perm, iperm, cT, fT, Wc, Wm, P, flags, scale, treeOut,
+                                                          ldo, out)));
 }
 
 void launch_corr(int K, int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT,
-                 const double* fT, const ModeArgs* tab, int nterm, const Params* P, int flags, double scale,
+                 const double* fT, const double* Wc, const double* Wm, const Params* P, int flags, double scale,
                  bool treeOut, int64_t ldo, double* out, hipStream_t s) {
     if (e <= b) return;
     const unsigned nb = blocks_for(e - b, 256);
     switch (d) {
-        case 1: corr_d<1>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
-        case 2: corr_d<2>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
-        case 3: corr_d<3>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
-        case 4: corr_d<4>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
-        case 5: corr_d<5>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
-        case 6: corr_d<6>(K, nb, b, e, perm, iperm, cT, fT, tab, nterm, P, flags, scale, treeOut, ldo, out, s); break;
+        case 1: corr_d<1>(K, nb, b, e, perm, iperm, cT, fT, Wc, Wm, P, flags, scale, treeOut, ldo, out, s); break;
+        case 2: corr_d<2>(K, nb, b, e, perm, iperm, cT, fT, Wc, Wm, P, flags, scale, treeOut, ldo, out, s); break;
+        case 3: corr_d<3>(K, nb, b, e, perm, iperm, cT, fT, Wc, Wm, P, flags, scale, treeOut, ldo, out, s); break;
+        case 4: corr_d<4>(K, nb, b, e, perm, iperm, cT, fT, Wc, Wm, P, flags, scale, treeOut, ldo, out, s); break;
+        case 5: corr_d<5>(K, nb, b, e, perm, iperm, cT, fT, Wc, Wm, P, flags, scale, treeOut, ldo, out, s); break;
+        case 6: corr_d<6>(K, nb, b, e, perm, iperm, cT, fT, Wc, Wm, P, flags, scale, treeOut, ldo, out, s); break;
         default: throw std::invalid_argument("quadRule out of range");
     }
     HIP_LAUNCH_CHECK();

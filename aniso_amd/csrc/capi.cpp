@@ -338,7 +338,7 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[10] = op.plan.m2lCanon;
         s[11] = op.plan.nearPartTotal;
         s[12] = op.harmonicReady() ? 1 : 0;
-        s[13] = (int64_t)op.plan.attSrc.size();
+        s[13] = (int64_t)op.plan.attOwner.size();
     });
 }
 

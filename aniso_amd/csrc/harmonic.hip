@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -82,9 +83,16 @@ __device__ __forceinline__ void hm_entry(double e, double dx, double dy2, const 
 // point s of the source (kernels.hip k_cache_att_m2l); PG blocks in flight.
 // local[n][t][i] = sum over pairs of sum_s (E/r) T_i V (the unscaled locals of all
 // output blocks; L2L / L2P in k_down_tier are mode-independent).
+// Symmetric storage: a V pair whose ends are both targets here has one stored
+// block (its smaller id's orientation); blk >= 0 reads block blk as stored, ~blk
+// reads it transposed (E(t, s) = E_stored(s, t): tau is symmetric), lane (s, q)
+// then loading rows 4q..4q+3 of its column with stride 16 (each of the 4 loads
+// covers four 128-B lines across the wave).  Plain loads: the partner's read of a
+// shared block should find it in the Infinity Cache.
 template <int K, int PG>
 __global__ void __launch_bounds__(256) k_m2l_hm(int ntgt, const int* __restrict__ tgt,
                                                 const int64_t* __restrict__ ptr, const int* __restrict__ src,
+                                                const int* __restrict__ blk,
                                                 const double* __restrict__ E, const double* __restrict__ ncx,
                                                 const double* __restrict__ ncy, const double* __restrict__ nrx,
                                                 const double* __restrict__ nry, const Params* __restrict__ P,
@@ -109,12 +117,20 @@ __global__ void __launch_bounds__(256) k_m2l_hm(int ntgt, const int* __restrict_
     for (int64_t cb = p0; cb < p1; cb += kWave) {
         const int cnt = (int)min<int64_t>(kWave, p1 - cb);
         const int mySrc = lane < cnt ? src[cb + lane] : 0;
+        const int myBlk = lane < cnt ? blk[cb + lane] : 0;
         for (int j0 = 0; j0 < cnt; j0 += PG) {
-            dbl2 kb[PG][2];
+            double e4[PG][4];
             double xm[PG][K];
             int B[PG];
 #pragma unroll
-            for (int g = 0; g < PG; ++g) load_block(E, cb + j0 + g, lane, j0 + g < cnt, kb[g][0], kb[g][1]);
+            for (int g = 0; g < PG; ++g) {
+                const int b = __builtin_amdgcn_readlane(myBlk, min(j0 + g, cnt - 1));
+                const bool tr = b < 0;
+                const double* p = E + (size_t)(tr ? ~b : b) * 256 + (tr ? 64 * q + s : 16 * s + 4 * q);
+                const int st = tr ? 16 : 1;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) e4[g][j] = j0 + g < cnt ? p[j * st] : 0.0;
+            }
 #pragma unroll
             for (int g = 0; g < PG; ++g) {  // a skipped block's source is a valid clamp; its E is zero
                 B[g] = __builtin_amdgcn_readlane(mySrc, min(j0 + g, cnt - 1));
@@ -130,9 +146,8 @@ __global__ void __launch_bounds__(256) k_m2l_hm(int ntgt, const int* __restrict_
                 double xw[K];
 #pragma unroll
                 for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * xm[g][b];
-                const double e4[4] = {kb[g][0].x, kb[g][0].y, kb[g][1].x, kb[g][1].y};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) hm_entry<K, false>(e4[j], ax - bx[j], dy2, xw, c[j]);
+                for (int j = 0; j < 4; ++j) hm_entry<K, false>(e4[g][j], ax - bx[j], dy2, xw, c[j]);
             }
         }
     }
@@ -295,13 +310,25 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
         default: throw std::invalid_argument("harmonic apply: unsupported block count " + std::to_string(k)); \
     }
 
-void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* src, const double* E,
+void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* src, const int* blk, const double* E,
                    const double* ncx, const double* ncy, const double* nrx, const double* nry, const Params* P,
                    const HarmWeights& hw, const double* mult, double* local, hipStream_t s) {
     if (ntgt <= 0) return;
     const unsigned nb = blocks_for((int64_t)ntgt * kWave, 256);
-    ANISO_HM_DISPATCH_K(K, (k_m2l_hm<KK, 4><<<nb, 256, 0, s>>>(ntgt, tgt, ptr, src, E, ncx, ncy, nrx, nry, P, hw,
-                                                                mult, local)));
+    static const int pg = [] {  // blocks in flight per wave (tuning knob, default 2)
+        const char* e = std::getenv("ANISO_HM_PG");
+        return e ? std::atoi(e) : 2;
+    }();
+    if (pg == 4) {
+        ANISO_HM_DISPATCH_K(K, (k_m2l_hm<KK, 4><<<nb, 256, 0, s>>>(ntgt, tgt, ptr, src, blk, E, ncx, ncy, nrx, nry, P, hw,
+                                                                    mult, local)));
+    } else if (pg == 1) {
+        ANISO_HM_DISPATCH_K(K, (k_m2l_hm<KK, 1><<<nb, 256, 0, s>>>(ntgt, tgt, ptr, src, blk, E, ncx, ncy, nrx, nry, P, hw,
+                                                                    mult, local)));
+    } else {
+        ANISO_HM_DISPATCH_K(K, (k_m2l_hm<KK, 2><<<nb, 256, 0, s>>>(ntgt, tgt, ptr, src, blk, E, ncx, ncy, nrx, nry, P, hw,
+                                                                    mult, local)));
+    }
     HIP_LAUNCH_CHECK();
 }
 

@@ -91,9 +91,12 @@ struct Plan {
     std::vector<int64_t> m2lPtr;               // CSR over m2lTgt -> source nodes
     std::vector<int> m2lSrc;
     // mode-shared (attenuation) plan of block handles: every V then
-    // X source of each m2lTgt, directed (no symmetric reduction)
+    // X source of each m2lTgt with the E block it reads: attBlk >= 0 a stored block
+    // read as stored, ~attBlk a stored block read transposed (tau is symmetric: the
+    // V pair's block is stored once, by its smaller id, when both ends are targets
+    // here).  Stored block k: target attOwner[k], source attOther[k].
     std::vector<int64_t> attPtr;
-    std::vector<int> attSrc;
+    std::vector<int> attSrc, attBlk, attOwner, attOther;
     // tiered up / down passes: tier k has root level
     // tierRootLevel[k] and bottom level tierBottomLevel[k] (k = 0 is the deepest).
     std::vector<int> tierRootLevel, tierBottomLevel;

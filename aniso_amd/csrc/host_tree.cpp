@@ -7,6 +7,7 @@
 #include <cmath>
 #include <stdexcept>
 #include <thread>
+#include <unordered_map>
 
 #include "host.hpp"
 
@@ -290,6 +291,16 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     m2lPtr.push_back(0);
     attPtr.assign(1, 0);
     attSrc.clear();
+    attBlk.clear();
+    attOwner.clear();
+    attOther.clear();
+    std::unordered_map<int64_t, int> attStored;  // (owner << 32 | other) -> stored V block
+    auto attDirected = [&](int i, int b) {
+        attSrc.push_back(b);
+        attBlk.push_back((int)attOwner.size());
+        attOwner.push_back(i);
+        attOther.push_back(b);
+    };
     int canon = 0;
     std::vector<int> canonSrc;
     for (int i = 0; i < t.nn; ++i) {
@@ -300,7 +311,18 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
             int b = t.vIdx[k];
             if (t.isEmpty[b]) continue;
             ++pairsM2L;
-            attSrc.push_back(b);
+            if (symmetric && m2lActive[b] && b < i) {
+                auto it = attStored.find(((int64_t)b << 32) | (uint32_t)i);
+                if (it != attStored.end()) {
+                    attSrc.push_back(b);
+                    attBlk.push_back(~it->second);
+                } else {
+                    attDirected(i, b);
+                }
+            } else {
+                if (symmetric && m2lActive[b]) attStored[((int64_t)i << 32) | (uint32_t)b] = (int)attOwner.size();
+                attDirected(i, b);
+            }
             if (symmetric && m2lActive[b]) {
                 if (i < b && (int)canonSrc.size() < maxCanon) {
                     canonSrc.push_back(b);
@@ -314,7 +336,7 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         for (int64_t k = t.xPtr[i]; k < t.xPtr[i + 1]; ++k)
             if (!t.isEmpty[t.xIdx[k]]) {
                 m2lSrc.push_back(t.xIdx[k]);
-                attSrc.push_back(t.xIdx[k]);
+                attDirected(i, t.xIdx[k]);
                 ++pairsM2L;
             }
         attPtr.push_back((int64_t)attSrc.size());

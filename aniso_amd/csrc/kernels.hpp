@@ -106,12 +106,13 @@ void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* 
                       const int* operm, int64_t obase, int64_t ldo, const int* nearOff, int maxNear,
                       const double* nearPart, const int2* chain, int maxChain, int flags, double scale, double* out,
                       hipStream_t s);
-// corrections of all terms in one launch, added to out
+// corrections of all terms in one launch, added to out: Wc / Wm the terms'
+// stencil and singular tables folded with their mixes (Operator::corrTable)
 void launch_corr(int K, int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT,
-                 const double* fT, const ModeArgs* tab, int nterm, const Params* P, int flags, double scale,
+                 const double* fT, const double* Wc, const double* Wm, const Params* P, int flags, double scale,
                  bool treeOut, int64_t ldo, double* out, hipStream_t s);
 // harmonic block apply (harmonic.hip): all modes from the mode-shared E caches
-void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* src, const double* E,
+void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* src, const int* blk, const double* E,
                    const double* ncx, const double* ncy, const double* nrx, const double* nry, const Params* P,
                    const HarmWeights& hw, const double* mult, double* local, hipStream_t s);
 void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,

@@ -532,3 +532,32 @@ def test_harmonic_block_apply_matches_per_mode_stream(sz, d, ks, ml, coeffs, mon
     q = gaussian_charge(xy)
     for m in (0, 2 * ks - 2):
         assert _rel(h.mapping(q, m), o.mapping(q, m)) <= TOL
+
+
+@pytest.mark.parametrize("sz,d,ks", [(16, 1, 5), (11, 3, 2)])
+def test_harmonic_symmetric_blocks_match_directed(sz, d, ks, monkeypatch):
+    """Stored-once V blocks read transposed by the partner (tau symmetric) against
+    every directed block stored (ANISO_SYMMETRIC=0): same matvec to rounding."""
+    torch = _torch()
+    import aniso_amd
+
+    outs = []
+    for sym in ("1", "0"):
+        monkeypatch.setenv("ANISO_SYMMETRIC", sym)
+        a = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, 20)
+        xy = a.getNodes()
+        a.setCoeff(*rough_coeffs(xy, 6))
+        for m in range(2 * ks - 1):
+            a.cache(m)
+        st = a.stats()
+        assert st["harmonic"] == 1
+        if sym == "1":
+            assert st["att_m2l_blocks"] < st["m2l_pairs"]
+        else:
+            assert st["att_m2l_blocks"] == st["m2l_pairs"]
+        U = torch.tensor(np.random.default_rng(1).uniform(-1, 1, (ks, a.N)), device="cuda")
+        out = torch.zeros_like(U)
+        a.block_op_dev(2, U, out)
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy())
+    assert _rel(outs[0], outs[1]) <= 1e-13

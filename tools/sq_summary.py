@@ -6,7 +6,7 @@ from collections import defaultdict
 
 tag = sys.argv[1]
 acc = defaultdict(lambda: defaultdict(list))
-for f in glob.glob(f"gpurun_out/sq_{tag}/p*/**/*counter_collection.csv", recursive=True):
+for f in glob.glob(f"gpurun_out/{tag if tag.startswith('l2_') else 'sq_' + tag}/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
