@@ -118,6 +118,16 @@ __global__ void k_sub_slice(int64_t n, int nrhs, const double* __restrict__ x, i
 // where a child below the tier is the root of a lower tier's task (read from HBM).
 // Phase 0 stages the transfer matrices, node boxes and child codes in LDS with
 // one round of independent loads; the levels then run out of LDS.
+// 16-lane reduce-scatter of acc[2 NV] (P2M): lane ln keeps half, adds the partner's half
+#define ANISO_RS16(NV, OFF)                                        \
+    {                                                              \
+        const bool hi = ln & (OFF);                                \
+        _Pragma("unroll") for (int e = 0; e < (NV); ++e) {         \
+            const double keep = hi ? acc[e + (NV)] : acc[e];       \
+            const double send = hi ? acc[e] : acc[e + (NV)];       \
+            acc[e] = keep + __shfl_xor(send, (OFF));               \
+        }                                                          \
+    }
 template <int K>
 __global__ void __launch_bounds__(kUpThreads) k_up_tier(
     int taskBase, int maxTask, const int4* __restrict__ desc, const int* __restrict__ grpFix,
@@ -170,6 +180,38 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
             if (CD[k].x != kLeafCode) continue;  // uniform over the 16 lanes
             const double cx = G[4 * k], cy = G[4 * k + 1], irx = G[4 * k + 2], iry = G[4 * k + 3];
             const int pe = LB[k] + LC[k];
+            if (LC[k] <= 16) {  // one point per lane: its Chebyshev weights once for all K base vectors
+                const int p = LB[k] + ln;
+                const bool on = p < pe;
+                const int64_t kp = b0 + (on ? p : LB[k]);
+                double Sx[kNP], Sy[kNP], cb[K];
+                cheb_weights(P, (pxT[kp] - cx) * irx, Sx);
+                cheb_weights(P, (pyT[kp] - cy) * iry, Sy);
+                const double w = wT[kp];
+#pragma unroll
+                for (int b = 0; b < K; ++b) cb[b] = input_charge(xin, ldi, b, treeIn, perm, sigT, kp);
+#pragma unroll
+                for (int b = 0; b < K; ++b) {
+                    const double f = on ? cb[b] * w : 0.0;
+                    if (on) {
+                        fT[kp * kStride<K> + b] = f;  // for k_near and the corrections
+                        cT[kp * kStride<K> + b] = cb[b];
+                    }
+                    double acc[kRank];
+#pragma unroll
+                    for (int j = 0; j < kNP; ++j) {
+                        const double sf = Sy[j] * f;
+#pragma unroll
+                        for (int i = 0; i < kNP; ++i) acc[j * kNP + i] = Sx[i] * sf;
+                    }
+                    ANISO_RS16(8, 8)
+                    ANISO_RS16(4, 4)
+                    ANISO_RS16(2, 2)
+                    ANISO_RS16(1, 1)
+                    M[((size_t)k * kRank + ln) * K + b] = acc[0];
+                }
+                continue;
+            }
 #pragma unroll 1
             for (int b = 0; b < K; ++b) {
                 double acc[kRank];
@@ -191,20 +233,10 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
                         for (int i = 0; i < kNP; ++i) acc[j * kNP + i] += Sx[i] * sf;
                     }
                 }
-#define ANISO_RS16(NV, OFF)                                        \
-    {                                                              \
-        const bool hi = ln & (OFF);                                \
-        _Pragma("unroll") for (int e = 0; e < (NV); ++e) {         \
-            const double keep = hi ? acc[e + (NV)] : acc[e];       \
-            const double send = hi ? acc[e] : acc[e + (NV)];       \
-            acc[e] = keep + __shfl_xor(send, (OFF));               \
-        }                                                          \
-    }
                 ANISO_RS16(8, 8)
                 ANISO_RS16(4, 4)
                 ANISO_RS16(2, 2)
                 ANISO_RS16(1, 1)
-#undef ANISO_RS16
                 M[((size_t)k * kRank + ln) * K + b] = acc[0];
             }
         }
@@ -249,6 +281,8 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
         mult[(size_t)ND[it / (kRank * K)] * kRank * K + it % (kRank * K)] = M[it];
     ANISO_STAMP(0, task, 4);
 }
+
+#undef ANISO_RS16
 
 // ----------------------------------------------------------------- M2L
 

@@ -34,6 +34,8 @@
 
 namespace aniso {
 
+constexpr int kHmVarDefault = 4;  // 4 waves per SIMD (measured best, r01e)
+
 // 1/sqrt(x) to full double precision: v_rsq_f64 (about 2^-22 relative) and two
 // Newton steps.  x = 0 gives a non-finite value; callers select it away.
 __device__ __forceinline__ double rsqrt_f64(double x) {
@@ -44,6 +46,30 @@ __device__ __forceinline__ double rsqrt_f64(double x) {
     h = x * y;
     e = __builtin_fma(-h, y, 1.0);
     return __builtin_fma(0.5 * y, e, y);
+}
+
+// NR Newton steps after v_rsq_f64: one step leaves a relative error of about
+// 1.5 eps0^2 (eps0 ~ 2^-22 for v_rsq_f64), i.e. ~1e-13 per kernel entry, far inside
+// the 1e-10 parity tolerance; two steps give full double precision.
+template <int NR>
+__device__ __forceinline__ double rsqrt_nr(double x) {
+    if constexpr (NR >= 2) {
+        return rsqrt_f64(x);
+    } else {
+        const double y = __builtin_amdgcn_rsq(x);
+        const double e = __builtin_fma(-(x * y), y, 1.0);
+        return __builtin_fma(0.5 * y, e, y);
+    }
+}
+
+// XCD-aware workgroup order: the dispatcher deals workgroups round-robin over the
+// 8 XCDs (bid % 8), so consecutive logical tiles would land on 8 different L2s.
+// Renumber so each XCD runs one contiguous range of logical workgroups: targets
+// in tree order are spatial neighbours and share source multipoles (and stored
+// blocks read by both ends) through that XCD's L2.
+__device__ __forceinline__ int xcd_tile(int bid, int nb) {
+    const int x = bid & 7, per = nb >> 3, rem = nb & 7, j = bid >> 3;
+    return x < rem ? x * (per + 1) + j : rem * (per + 1) + (x - rem) * per + j;
 }
 
 // T_0 .. T_{K-1} at c (cos(b theta) for c = cos theta)
@@ -58,10 +84,10 @@ __device__ __forceinline__ void cheb_T(double c, double (&T)[K]) {
 
 // One entry: E at (dx, dy) from the source, harmonic-weighted source charges xw;
 // o[i] += T_i(c) (E / r) V.  guard0: r = 0 possible (near field), the entry adds 0.
-template <int K, bool guard0>
+template <int K, bool guard0, int NR = 2>
 __device__ __forceinline__ void hm_entry(double e, double dx, double dy2, const double (&xw)[K], double (&o)[K]) {
     const double r2 = __builtin_fma(dx, dx, dy2);
-    double ri = rsqrt_f64(r2);
+    double ri = rsqrt_nr<NR>(r2);
     if constexpr (guard0) ri = r2 > 0.0 ? ri : 0.0;
     const double c = dx * ri;
     double T[K];
@@ -89,8 +115,8 @@ __device__ __forceinline__ void hm_entry(double e, double dx, double dy2, const 
 // then loading rows 4q..4q+3 of its column with stride 16 (each of the 4 loads
 // covers four 128-B lines across the wave).  Plain loads: the partner's read of a
 // shared block should find it in the Infinity Cache.
-template <int K, int PG>
-__global__ void __launch_bounds__(256) k_m2l_hm(int ntgt, const int* __restrict__ tgt,
+template <int K, int PG, int NR, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_m2l_hm(int ntgt, int xcd, const int* __restrict__ tgt,
                                                 const int64_t* __restrict__ ptr, const int* __restrict__ src,
                                                 const int* __restrict__ blk,
                                                 const double* __restrict__ E, const double* __restrict__ ncx,
@@ -98,7 +124,8 @@ __global__ void __launch_bounds__(256) k_m2l_hm(int ntgt, const int* __restrict_
                                                 const double* __restrict__ nry, const Params* __restrict__ P,
                                                 HarmWeights hw, const double* __restrict__ mult,
                                                 double* __restrict__ local) {
-    const int wave = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) / kWave));
+    const int bid = xcd ? xcd_tile((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(bid * (int)(blockDim.x / kWave) + (int)(threadIdx.x / kWave));
     const int lane = threadIdx.x & (kWave - 1);
     if (wave >= ntgt) return;
     const int n = tgt[wave];
@@ -147,7 +174,7 @@ __global__ void __launch_bounds__(256) k_m2l_hm(int ntgt, const int* __restrict_
 #pragma unroll
                 for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * xm[g][b];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) hm_entry<K, false>(e4[g][j], ax - bx[j], dy2, xw, c[j]);
+                for (int j = 0; j < 4; ++j) hm_entry<K, false, NR>(e4[g][j], ax - bx[j], dy2, xw, c[j]);
             }
         }
     }
@@ -178,7 +205,7 @@ __global__ void __launch_bounds__(256) k_m2l_hm(int ntgt, const int* __restrict_
 // 4rq..4rq+3 for its columns, U columns in flight; the sources' points and charges
 // are read straight from pxT / pyT / fT (the lanes of a column share the lines).
 // out (stored, not added) = scale * (sum over sources + the mode-0 diagonal).
-template <int K, int G, int U>
+template <int K, int G, int U, int NR>
 __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict__ leafInfo,
                                                  const int64_t* __restrict__ nearPtsPtr,
                                                  const int* __restrict__ nearPts, const int64_t* __restrict__ nearKOff,
@@ -256,7 +283,7 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const double dy = sy[u] - ty[j];
-                        hm_entry<K, true>(e4[j], sx[u] - tx[j], dy * dy, xw, a[j]);
+                        hm_entry<K, true, NR>(e4[j], sx[u] - tx[j], dy * dy, xw, a[j]);
                     }
                 }
             }
@@ -310,25 +337,32 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
         default: throw std::invalid_argument("harmonic apply: unsupported block count " + std::to_string(k)); \
     }
 
+// Variant knobs (tuning/experiments): ANISO_HM_VAR bit 0 = XCD-aware
+// workgroup order, bit 1 = one Newton step in 1/r, bit 2 = 4 waves per SIMD.
+static int hm_var() {
+    static const int v = [] {
+        const char* e = std::getenv("ANISO_HM_VAR");
+        return e ? std::atoi(e) : kHmVarDefault;
+    }();
+    return v;
+}
+
 void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* src, const int* blk, const double* E,
                    const double* ncx, const double* ncy, const double* nrx, const double* nry, const Params* P,
                    const HarmWeights& hw, const double* mult, double* local, hipStream_t s) {
     if (ntgt <= 0) return;
     const unsigned nb = blocks_for((int64_t)ntgt * kWave, 256);
-    static const int pg = [] {  // blocks in flight per wave (tuning knob, default 2)
-        const char* e = std::getenv("ANISO_HM_PG");
-        return e ? std::atoi(e) : 2;
-    }();
-    if (pg == 4) {
-        ANISO_HM_DISPATCH_K(K, (k_m2l_hm<KK, 4><<<nb, 256, 0, s>>>(ntgt, tgt, ptr, src, blk, E, ncx, ncy, nrx, nry, P, hw,
-                                                                    mult, local)));
-    } else if (pg == 1) {
-        ANISO_HM_DISPATCH_K(K, (k_m2l_hm<KK, 1><<<nb, 256, 0, s>>>(ntgt, tgt, ptr, src, blk, E, ncx, ncy, nrx, nry, P, hw,
-                                                                    mult, local)));
-    } else {
-        ANISO_HM_DISPATCH_K(K, (k_m2l_hm<KK, 2><<<nb, 256, 0, s>>>(ntgt, tgt, ptr, src, blk, E, ncx, ncy, nrx, nry, P, hw,
-                                                                    mult, local)));
+    const int v = hm_var(), xcd = v & 1;
+#define ANISO_M2L_HM(NR, WPE)                                                                                      \
+    ANISO_HM_DISPATCH_K(K, (k_m2l_hm<KK, 2, NR, WPE><<<nb, 256, 0, s>>>(ntgt, xcd, tgt, ptr, src, blk, E, ncx, ncy, \
+                                                                         nrx, nry, P, hw, mult, local)))
+    switch ((v >> 1) & 3) {
+        case 0: ANISO_M2L_HM(2, 1); break;
+        case 1: ANISO_M2L_HM(1, 1); break;
+        case 2: ANISO_M2L_HM(2, 4); break;
+        default: ANISO_M2L_HM(1, 4); break;
     }
+#undef ANISO_M2L_HM
     HIP_LAUNCH_CHECK();
 }
 
@@ -337,15 +371,25 @@ void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
                     const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
                     int64_t ldo, int flags, double scale, double* out, hipStream_t s) {
     if (nl <= 0) return;
+#define ANISO_NEAR_HM(G, NR)                                                                                  \
+    ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, G, 4, NR><<<blocks_for((int64_t)nl * G, 256), 256, 0, s>>>(          \
+                               nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm, \
+                               obase, ldo, flags, scale, out)))
+    const bool nr1 = (hm_var() & 2) != 0;
     if (maxLeaf <= 16) {  // 4 leaves per wave
-        ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, 16, 4><<<blocks_for((int64_t)nl * 16, 256), 256, 0, s>>>(
-                                   nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm,
-                                   obase, ldo, flags, scale, out)));
+        if (nr1) {
+            ANISO_NEAR_HM(16, 1);
+        } else {
+            ANISO_NEAR_HM(16, 2);
+        }
     } else {
-        ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, 64, 4><<<blocks_for((int64_t)nl * 64, 256), 256, 0, s>>>(
-                                   nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm,
-                                   obase, ldo, flags, scale, out)));
+        if (nr1) {
+            ANISO_NEAR_HM(64, 1);
+        } else {
+            ANISO_NEAR_HM(64, 2);
+        }
     }
+#undef ANISO_NEAR_HM
     HIP_LAUNCH_CHECK();
 }
 
