@@ -77,6 +77,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     // (DESIGN.md §3.9); ANISO_HARMONIC=0 keeps the per-mode operator stream
     useAtt = ks > 1 && !plan.nearSymmetric;
     if (const char* e = std::getenv("ANISO_HARMONIC")) useAtt = useAtt && e[0] != '0';
+    if (const char* e = std::getenv("ANISO_HM_CLUSTER")) useClusters = e[0] != '0';
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
     modes.resize(kernelSize);
@@ -245,6 +246,13 @@ void Operator::uploadPlan() {
         up(dAttBlk, plan.attBlk);
         up(dAttOwner, plan.attOwner);
         up(dAttOther, plan.attOther);
+        up(dHmClPtr, plan.hmClPtr);
+        up(dHmTgt, plan.hmTgt);
+        up(dHmPtr, plan.hmPtr);
+        up(dHmSrc, plan.hmSrc);
+        up(dHmBlk, plan.hmBlk);
+        up(dHmSlot, plan.hmSlot);
+        up(dHmNDir, plan.hmNDir);
         attReady = false;
     }
     up(dM2LCanonBase, plan.m2lCanonBase);
@@ -638,7 +646,12 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         e = tm ? mark(s) : -1;
         span(6, ep, e);
         ep = e;
-        if (mask & kStageFar)
+        if ((mask & kStageFar) && useClusters)
+            launch_m2l_hc(K, (int)plan.hmClPtr.size() - 1, plan.hmMaxCl, dHmClPtr.as<int>(), dHmTgt.as<int>(),
+                          dHmPtr.as<int64_t>(), dHmNDir.as<int>(), dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(),
+                          dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
+                          dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
+        else if (mask & kStageFar)
             launch_m2l_hm(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dAttPtr.as<int64_t>(), dAttSrc.as<int>(),
                           dAttBlk.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
                           dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);

@@ -92,6 +92,7 @@ public:
                   double* finalResid);
     hipStream_t stream() const { return own; }
     bool harmonicReady() const { return useAtt && attReady; }
+    bool clustersOn() const { return useClusters; }
     bool modeCached(int id) const { return id >= 0 && id < kernelSize && modes[id].ready; }
     int kernelSize = 0;
     // stage timing with HIP events recorded in-stream (no host sync per apply);
@@ -126,6 +127,8 @@ private:
     void buildAttCache();
     bool useAtt = false, attReady = false;
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
+    DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
+    bool useClusters = true;
     std::map<std::string, DevBuf> modeTabs;
     const CorrFold& corrTable(int K, int nterm, const int* ids, const double* mixes);
     std::map<std::string, CorrFold> corrTabs;

@@ -339,6 +339,10 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[11] = op.plan.nearPartTotal;
         s[12] = op.harmonicReady() ? 1 : 0;
         s[13] = (int64_t)op.plan.attOwner.size();
+        const bool cl = op.harmonicReady() && op.clustersOn();
+        s[14] = cl ? (int64_t)op.plan.hmClPtr.size() - 1 : 0;
+        s[15] = cl ? op.plan.hmDual : 0;
+        s[16] = cl ? (int64_t)op.plan.hmSrc.size() : (int64_t)op.plan.attSrc.size();
     });
 }
 

@@ -196,6 +196,182 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     }
 }
 
+
+// One entry applied both ways (a canonical pair inside a cluster, k_m2l_hc): the
+// forward product o as hm_entry, and the partner's product ob[i] += T_i(c) (E/r) V_A,
+// V_A = sum_b T_b(c) xa[b] with xa[b] = (-1)^b hw_b x_A,b(t) (the reversed direction
+// has cos = -c; its (-1)^i is applied when ob is flushed).
+template <int K, int NR>
+__device__ __forceinline__ void hm_entry2(double e, double dx, double dy2, const double (&xw)[K],
+                                          const double* __restrict__ xa, double (&o)[K], double (&ob)[K]) {
+    const double r2 = __builtin_fma(dx, dx, dy2);
+    const double ri = rsqrt_nr<NR>(r2);
+    const double c = dx * ri;
+    double T[K];
+    cheb_T<K>(c, T);
+    double v = xw[0], va = xa[0];
+#pragma unroll
+    for (int b = 1; b < K; ++b) {
+        v = __builtin_fma(T[b], xw[b], v);
+        va = __builtin_fma(T[b], xa[b], va);
+    }
+    const double er = e * ri;
+    const double av = er * v, ava = er * va;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        o[i] = __builtin_fma(T[i], av, o[i]);
+        ob[i] = __builtin_fma(T[i], ava, ob[i]);
+    }
+}
+
+// The harmonic M2L in clusters: one 4-wave workgroup per
+// cluster (the active targets of one level under one ancestor kClusterDepth levels
+// up), the cluster's locals accumulated in LDS.  Each wave takes the cluster's
+// targets round-robin and streams their pair lists as k_m2l_hm does; a pair whose
+// partner is in the cluster (slot >= 0) is read once, by its smaller id, and also
+// yields the partner's product: per lane the 4 rows are summed in registers, the
+// quad's lanes by DPP, and the 16 x K result is added to the partner's LDS locals
+// (ds_add_f64).  The block stream drops by the in-cluster share (0.65 of the V
+// pairs at 64 targets per cluster, tools/vfrac.py); the summation order of the LDS
+// adds is not fixed (results repeat to rounding, not bitwise).
+template <int K, int NR, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64_t* __restrict__ ptr,
+         const int* __restrict__ ndir, const int* __restrict__ src, const int* __restrict__ blk,
+         const int* __restrict__ slot, const double* __restrict__ E, const double* __restrict__ ncx, const double* __restrict__ ncy,
+         const double* __restrict__ nrx, const double* __restrict__ nry, const Params* __restrict__ P,
+         HarmWeights hw, const double* __restrict__ mult, double* __restrict__ local) {
+    constexpr int RK = kRank * K;
+    constexpr int PG = 2;
+    extern __shared__ double sm[];
+    const int c0 = clPtr[blockIdx.x], nt = clPtr[blockIdx.x + 1] - c0;
+    const int nw = (int)(blockDim.x / kWave);
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+    double* acc = sm;                                    // nt x 16 x K: the cluster's locals
+    double* xa = sm + (size_t)nt * RK + (size_t)w * RK;  // this wave's target multipole, (-1)^b hw_b weighted
+    for (int i = threadIdx.x; i < nt * RK; i += blockDim.x) acc[i] = 0.0;
+    __syncthreads();
+    const int lane = threadIdx.x & (kWave - 1);
+    const int s = lane >> 2, q = lane & 3;
+    const double chx = P->cheb[s & 3], chy = P->cheb[s >> 2];
+    for (int ti = w; ti < nt; ti += nw) {
+        const int n = tgt[c0 + ti];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous target's xa reads are done
+        __builtin_amdgcn_wave_barrier();
+        for (int e = lane; e < RK; e += kWave) {
+            const int b = e % K;
+            xa[e] = ((b & 1) ? -hw.hw[b] : hw.hw[b]) * mult[(size_t)n * RK + e];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // xa visible to every lane of the wave
+        __builtin_amdgcn_wave_barrier();
+        double bx[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bx[j] = ncx[n] + nrx[n] * P->cheb[j];
+        const double by = ncy[n] + nry[n] * P->cheb[q];
+        double c[4][K];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < K; ++i) c[j][i] = 0.0;
+        const int64_t p0 = ptr[c0 + ti], pd = p0 + ndir[c0 + ti], p1 = ptr[c0 + ti + 1];
+        // directed entries: PG blocks in flight, forward product only
+        for (int64_t cb = p0; cb < pd; cb += kWave) {
+            const int cnt = (int)min<int64_t>(kWave, pd - cb);
+            const int mySrc = lane < cnt ? src[cb + lane] : 0;
+            const int myBlk = lane < cnt ? blk[cb + lane] : 0;
+            for (int j0 = 0; j0 < cnt; j0 += PG) {
+                double e4[PG][4];
+                double xm[PG][K];
+                int B[PG];
+#pragma unroll
+                for (int g = 0; g < PG; ++g) {
+                    const int b = __builtin_amdgcn_readlane(myBlk, min(j0 + g, cnt - 1));
+                    const bool tr = b < 0;
+                    const double* p = E + (size_t)(tr ? ~b : b) * 256 + (tr ? 64 * q + s : 16 * s + 4 * q);
+                    const int st = tr ? 16 : 1;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) e4[g][j] = j0 + g < cnt ? p[j * st] : 0.0;
+                }
+#pragma unroll
+                for (int g = 0; g < PG; ++g) {  // a skipped block's source is a valid clamp; its E is zero
+                    B[g] = __builtin_amdgcn_readlane(mySrc, min(j0 + g, cnt - 1));
+                    const double* m = mult + ((size_t)B[g] * kRank + s) * K;
+#pragma unroll
+                    for (int b = 0; b < K; ++b) xm[g][b] = m[b];
+                }
+#pragma unroll
+                for (int g = 0; g < PG; ++g) {
+                    const double ax = ncx[B[g]] + nrx[B[g]] * chx;
+                    const double dy = (ncy[B[g]] + nry[B[g]] * chy) - by;
+                    const double dy2 = dy * dy;
+                    double xw[K];
+#pragma unroll
+                    for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * xm[g][b];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) hm_entry<K, false, NR>(e4[g][j], ax - bx[j], dy2, xw, c[j]);
+                }
+            }
+        }
+        // in-cluster canonical entries (stored as read): both products, one block in flight
+        for (int64_t cb = pd; cb < p1; cb += kWave) {
+            const int cnt = (int)min<int64_t>(kWave, p1 - cb);
+            const int mySrc = lane < cnt ? src[cb + lane] : 0;
+            const int myBlk = lane < cnt ? blk[cb + lane] : 0;
+            const int mySlot = lane < cnt ? slot[cb + lane] : 0;
+            for (int jj = 0; jj < cnt; ++jj) {
+                const int b = __builtin_amdgcn_readlane(myBlk, jj);
+                const int B = __builtin_amdgcn_readlane(mySrc, jj);
+                const int sl = __builtin_amdgcn_readlane(mySlot, jj);
+                const dbl2* p = reinterpret_cast<const dbl2*>(E + (size_t)b * 256 + 16 * s + 4 * q);
+                const dbl2 k0 = p[0], k1 = p[1];
+                double xm[K];
+                const double* m = mult + ((size_t)B * kRank + s) * K;
+#pragma unroll
+                for (int bb = 0; bb < K; ++bb) xm[bb] = m[bb];
+                const double ax = ncx[B] + nrx[B] * chx;
+                const double dy = (ncy[B] + nry[B] * chy) - by;
+                const double dy2 = dy * dy;
+                double xw[K], ob[K];
+#pragma unroll
+                for (int bb = 0; bb < K; ++bb) {
+                    xw[bb] = hw.hw[bb] * xm[bb];
+                    ob[bb] = 0.0;
+                }
+                const double e4[4] = {k0.x, k0.y, k1.x, k1.y};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    hm_entry2<K, NR>(e4[j], ax - bx[j], dy2, xw, xa + (4 * q + j) * K, c[j], ob);
+#pragma unroll
+                for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // rows 4q'+j over the quad
+                if (q == 0) {
+                    double* d = acc + ((size_t)sl * kRank + s) * K;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) atomicAdd(d + i, (i & 1) ? -ob[i] : ob[i]);
+                }
+            }
+        }
+#pragma unroll
+        for (int off = 4; off < kWave; off <<= 1)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int i = 0; i < K; ++i) c[j][i] += __shfl_xor(c[j][i], off);
+        const int jr = s & 3, srcLane = 4 * s + (s >> 2);
+        double* d = acc + ((size_t)ti * kRank + s) * K;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const double sel = jr == 0 ? c[0][i] : jr == 1 ? c[1][i] : jr == 2 ? c[2][i] : c[3][i];
+            const double v = __shfl(sel, srcLane);
+            if ((i & 3) == q) atomicAdd(d + i, v);
+        }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < nt * RK; e += blockDim.x) {
+        const int k = e / RK, r = e - k * RK;
+        local[(size_t)tgt[c0 + k] * RK + r] = hw.om[r % K] * acc[e];
+    }
+}
+
 // ----------------------------------------------------------------- near field
 
 // U/W near field (bbfmm.h:1081-1099) for every mode of the block matvec, directed
@@ -363,6 +539,38 @@ void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const in
         default: ANISO_M2L_HM(1, 4); break;
     }
 #undef ANISO_M2L_HM
+    HIP_LAUNCH_CHECK();
+}
+
+
+template <int K, int NR>
+static void run_m2l_hc(int ncl, size_t shm, const int* clPtr, const int* tgt, const int64_t* ptr, const int* ndir,
+                       const int* src, const int* blk, const int* slot, const double* E, const double* ncx,
+                       const double* ncy, const double* nrx, const double* nry, const Params* P, const HarmWeights& hw,
+                       const double* mult, double* local, hipStream_t s) {
+    auto f = k_m2l_hc<K, NR, 3>;
+    if (shm > 65536) {  // clusters of up to 64 targets at K = 8 need ~68 KB of the 160 KB LDS
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(f),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
+    }
+    f<<<ncl, 256, shm, s>>>(clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry, P, hw, mult, local);
+}
+
+void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, const int64_t* ptr, const int* ndir,
+                   const int* src, const int* blk, const int* slot, const double* E, const double* ncx, const double* ncy,
+                   const double* nrx, const double* nry, const Params* P, const HarmWeights& hw, const double* mult,
+                   double* local, hipStream_t s) {
+    if (ncl <= 0) return;
+    const size_t shm = (size_t)(maxCl + 4) * kRank * K * sizeof(double);
+    if (shm > 160 * 1024) throw std::invalid_argument("harmonic M2L cluster exceeds the LDS");
+    if (hm_var() & 2) {
+        ANISO_HM_DISPATCH_K(K, (run_m2l_hc<KK, 1>(ncl, shm, clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry,
+                                                  P, hw, mult, local, s)));
+    } else {
+        ANISO_HM_DISPATCH_K(K, (run_m2l_hc<KK, 2>(ncl, shm, clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry,
+                                                  P, hw, mult, local, s)));
+    }
     HIP_LAUNCH_CHECK();
 }
 

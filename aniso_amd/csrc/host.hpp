@@ -17,6 +17,7 @@ constexpr int kLeafCode = -2147483647 - 1;  // upCode of a leaf (P2M from its po
 constexpr int kTaskLevels = 7;  // levels per up/down task record (tasks span <= 4)
 constexpr int kMaxCanon = 32;       // canonical (symmetric) M2L pairs per target (k_m2l's register staging)
 constexpr int kMaxCanonBlock = 16;  // the same on block handles (ks > 1; LDS staging at K >= 4)
+constexpr int kClusterDepth = 3;   // harmonic M2L clusters: <= 4^3 = 64 targets
 
 // Geometry::Geometry (Geometry.cpp:10-114) + the singular Duffy rule
 // (KernelFactory.cpp:15-16, 863-986).
@@ -97,6 +98,17 @@ struct Plan {
     // here).  Stored block k: target attOwner[k], source attOther[k].
     std::vector<int64_t> attPtr;
     std::vector<int> attSrc, attBlk, attOwner, attOther;
+    // the same work in clusters: cluster c = the active targets of
+    // one level under one ancestor kClusterDepth levels up (<= 4^kClusterDepth
+    // nodes), one workgroup each, locals accumulated in LDS.  A V pair with both
+    // ends in one cluster is applied from ONE read of its stored block by the
+    // smaller id (hmSlot = the partner's slot in the cluster, which also receives the
+    // transposed product); the partner skips it.  Other pairs as attSrc / attBlk.
+    // per target: [hmNDir directed | in-cluster canonical] entries
+    std::vector<int> hmClPtr, hmTgt, hmSrc, hmBlk, hmSlot, hmNDir;
+    std::vector<int64_t> hmPtr;
+    int hmMaxCl = 0;
+    int64_t hmDual = 0;
     // tiered up / down passes: tier k has root level
     // tierRootLevel[k] and bottom level tierBottomLevel[k] (k = 0 is the deepest).
     std::vector<int> tierRootLevel, tierBottomLevel;
@@ -138,6 +150,7 @@ struct Plan {
 
   private:
     void buildUpTasks(const Tree& t);
+    void buildClusters(const Tree& t);
     void buildDownTasks(const Tree& t);
 };
 

@@ -351,6 +351,7 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         m2lPtr.push_back((int64_t)m2lSrc.size());
     }
     m2lCanon = canon;
+    buildClusters(t);
     storedM2L = (int64_t)m2lSrc.size();
     m2lOutSlot.assign(canon, -1);
     m2lInPtr.push_back(0);
@@ -616,6 +617,74 @@ void Plan::buildDownTasks(const Tree& t) {
     }
     dnTierTask.push_back((int)dnTaskPtr.size() - 1);  // one launch
     dnGrp.push_back((int)dnNode.size());
+}
+
+// Cluster plan of the harmonic M2L from the att lists.
+void Plan::buildClusters(const Tree& t) {
+    hmClPtr.assign(1, 0);
+    hmTgt.clear();
+    hmPtr.assign(1, 0);
+    hmSrc.clear();
+    hmBlk.clear();
+    hmSlot.clear();
+    hmMaxCl = 0;
+    hmDual = 0;
+    const int nt = (int)m2lTgt.size();
+    if (nt == 0) return;
+    // cluster key: (level, ancestor kClusterDepth levels up); targets keep id order
+    std::vector<int> widx(t.nn, -1);
+    for (int w = 0; w < nt; ++w) widx[m2lTgt[w]] = w;
+    std::vector<int64_t> key(nt);
+    for (int w = 0; w < nt; ++w) {
+        int a = m2lTgt[w];
+        for (int k = 0; k < kClusterDepth && t.parent[a] != -1; ++k) a = t.parent[a];
+        key[w] = ((int64_t)t.level[m2lTgt[w]] << 32) | (uint32_t)a;
+    }
+    std::vector<int> order(nt);
+    for (int w = 0; w < nt; ++w) order[w] = w;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
+    std::vector<int> clOf(t.nn, -1), slotOf(t.nn, -1);
+    int nc = 0;
+    for (int k = 0; k < nt; ++k) {
+        if (k > 0 && key[order[k]] != key[order[k - 1]]) {
+            hmClPtr.push_back(k);
+            ++nc;
+        }
+        const int n = m2lTgt[order[k]];
+        clOf[n] = nc;
+        slotOf[n] = k - hmClPtr.back();
+        hmTgt.push_back(n);
+    }
+    hmClPtr.push_back(nt);
+    for (size_t c = 0; c + 1 < hmClPtr.size(); ++c) hmMaxCl = std::max(hmMaxCl, hmClPtr[c + 1] - hmClPtr[c]);
+    hmNDir.clear();
+    std::vector<int> dSrc, dBlk, dSlot;
+    for (int k = 0; k < nt; ++k) {
+        const int n = hmTgt[k], w = widx[n];
+        dSrc.clear();
+        dBlk.clear();
+        dSlot.clear();
+        for (int64_t e = attPtr[w]; e < attPtr[w + 1]; ++e) {
+            const int b = attSrc[e];
+            const bool same = clOf[b] >= 0 && clOf[b] == clOf[n] && t.level[b] == t.level[n];
+            if (same && b > n && attBlk[e] >= 0) {  // canonical end: one read, both products
+                dSrc.push_back(b);
+                dBlk.push_back(attBlk[e]);
+                dSlot.push_back(slotOf[b]);
+                continue;
+            }
+            if (same && b < n) continue;  // applied by b's wave (dual)
+            hmSrc.push_back(b);
+            hmBlk.push_back(attBlk[e]);
+            hmSlot.push_back(-1);
+        }
+        hmNDir.push_back((int)(hmSrc.size() - hmPtr.back()));
+        hmSrc.insert(hmSrc.end(), dSrc.begin(), dSrc.end());
+        hmBlk.insert(hmBlk.end(), dBlk.begin(), dBlk.end());
+        hmSlot.insert(hmSlot.end(), dSlot.begin(), dSlot.end());
+        hmDual += (int64_t)dSrc.size();
+        hmPtr.push_back((int64_t)hmSrc.size());
+    }
 }
 
 }  // namespace aniso

@@ -115,6 +115,10 @@ void launch_corr(int K, int d, int64_t b, int64_t e, const int* perm, const int*
 void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* src, const int* blk, const double* E,
                    const double* ncx, const double* ncy, const double* nrx, const double* nry, const Params* P,
                    const HarmWeights& hw, const double* mult, double* local, hipStream_t s);
+void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, const int64_t* ptr, const int* ndir,
+                   const int* src, const int* blk, const int* slot, const double* E, const double* ncx, const double* ncy,
+                   const double* nrx, const double* nry, const Params* P, const HarmWeights& hw, const double* mult,
+                   double* local, hipStream_t s);
 void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
                     const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
                     const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
