@@ -224,6 +224,119 @@ __device__ __forceinline__ void hm_entry2(double e, double dx, double dy2, const
     }
 }
 
+// Software-pipelined streams of k_m2l_hc (PF): the next block's E column, source
+// multipole row and source-node geometry are loaded before the current block's
+// arithmetic, so each wave keeps one block in flight while it computes the other.
+template <int K>
+struct HcBlk {
+    double e[4];
+    double xm[K];
+    double gx, rx, gy, ry;
+};
+
+template <int K>
+__device__ __forceinline__ void hc_load(HcBlk<K>& h, int b, int B, int s, int q, const double* __restrict__ E,
+                                        const double* __restrict__ ncx, const double* __restrict__ ncy,
+                                        const double* __restrict__ nrx, const double* __restrict__ nry,
+                                        const double* __restrict__ mult) {
+    const bool tr = b < 0;
+    const double* p = E + (size_t)(tr ? ~b : b) * 256 + (tr ? 64 * q + s : 16 * s + 4 * q);
+    if (tr) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) h.e[j] = p[16 * j];
+    } else {
+        const dbl2 k0 = reinterpret_cast<const dbl2*>(p)[0], k1 = reinterpret_cast<const dbl2*>(p)[1];
+        h.e[0] = k0.x;
+        h.e[1] = k0.y;
+        h.e[2] = k1.x;
+        h.e[3] = k1.y;
+    }
+    const double* m = mult + ((size_t)B * kRank + s) * K;
+#pragma unroll
+    for (int b2 = 0; b2 < K; ++b2) h.xm[b2] = m[b2];
+    h.gx = ncx[B];
+    h.rx = nrx[B];
+    h.gy = ncy[B];
+    h.ry = nry[B];
+}
+
+template <int K, int NR>
+__device__ __forceinline__ void hc_directed_pf(int64_t p0, int64_t p1, int lane, int s, int q, const int* __restrict__ src,
+                                               const int* __restrict__ blk, const double* __restrict__ E,
+                                               const double* __restrict__ ncx, const double* __restrict__ ncy,
+                                               const double* __restrict__ nrx, const double* __restrict__ nry,
+                                               double chx, double chy, const double (&bx)[4], double by,
+                                               const HarmWeights& hw, const double* __restrict__ mult,
+                                               double (&c)[4][K]) {
+    for (int64_t cb = p0; cb < p1; cb += kWave) {
+        const int cnt = (int)min<int64_t>(kWave, p1 - cb);
+        const int mySrc = lane < cnt ? src[cb + lane] : 0;
+        const int myBlk = lane < cnt ? blk[cb + lane] : 0;
+        HcBlk<K> nx;
+        hc_load<K>(nx, __builtin_amdgcn_readlane(myBlk, 0), __builtin_amdgcn_readlane(mySrc, 0), s, q, E, ncx, ncy, nrx,
+                   nry, mult);
+        for (int jj = 0; jj < cnt; ++jj) {
+            const HcBlk<K> cu = nx;
+            const int jn = min(jj + 1, cnt - 1);  // the last block reloads itself (no branch)
+            hc_load<K>(nx, __builtin_amdgcn_readlane(myBlk, jn), __builtin_amdgcn_readlane(mySrc, jn), s, q, E, ncx, ncy,
+                       nrx, nry, mult);
+            const double ax = cu.gx + cu.rx * chx;
+            const double dy = (cu.gy + cu.ry * chy) - by;
+            const double dy2 = dy * dy;
+            double xw[K];
+#pragma unroll
+            for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * cu.xm[b];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) hm_entry<K, false, NR>(cu.e[j], ax - bx[j], dy2, xw, c[j]);
+        }
+    }
+}
+
+template <int K, int NR>
+__device__ __forceinline__ void hc_dual_pf(int64_t p0, int64_t p1, int lane, int s, int q, const int* __restrict__ src,
+                                           const int* __restrict__ blk, const int* __restrict__ slot,
+                                           const double* __restrict__ E, const double* __restrict__ ncx,
+                                           const double* __restrict__ ncy, const double* __restrict__ nrx,
+                                           const double* __restrict__ nry, double chx, double chy,
+                                           const double (&bx)[4], double by, const HarmWeights& hw,
+                                           const double* __restrict__ mult, const double* xa, double* acc,
+                                           double (&c)[4][K]) {
+    for (int64_t cb = p0; cb < p1; cb += kWave) {
+        const int cnt = (int)min<int64_t>(kWave, p1 - cb);
+        const int mySrc = lane < cnt ? src[cb + lane] : 0;
+        const int myBlk = lane < cnt ? blk[cb + lane] : 0;
+        const int mySlot = lane < cnt ? slot[cb + lane] : 0;
+        HcBlk<K> nx;
+        hc_load<K>(nx, __builtin_amdgcn_readlane(myBlk, 0), __builtin_amdgcn_readlane(mySrc, 0), s, q, E, ncx, ncy, nrx,
+                   nry, mult);
+        for (int jj = 0; jj < cnt; ++jj) {
+            const HcBlk<K> cu = nx;
+            const int sl = __builtin_amdgcn_readlane(mySlot, jj);
+            const int jn = min(jj + 1, cnt - 1);
+            hc_load<K>(nx, __builtin_amdgcn_readlane(myBlk, jn), __builtin_amdgcn_readlane(mySrc, jn), s, q, E, ncx, ncy,
+                       nrx, nry, mult);
+            const double ax = cu.gx + cu.rx * chx;
+            const double dy = (cu.gy + cu.ry * chy) - by;
+            const double dy2 = dy * dy;
+            double xw[K], ob[K];
+#pragma unroll
+            for (int b = 0; b < K; ++b) {
+                xw[b] = hw.hw[b] * cu.xm[b];
+                ob[b] = 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) hm_entry2<K, NR>(cu.e[j], ax - bx[j], dy2, xw, xa + (4 * q + j) * K, c[j], ob);
+#pragma unroll
+            for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // rows 4q'+j over the quad
+            if (q == 0) {
+                double* d = acc + ((size_t)sl * kRank + s) * K;
+#pragma unroll
+                for (int i = 0; i < K; ++i) atomicAdd(d + i, (i & 1) ? -ob[i] : ob[i]);
+            }
+        }
+    }
+}
+
 // The harmonic M2L in clusters: one 4-wave workgroup per
 // cluster (the active targets of one level under one ancestor kClusterDepth levels
 // up), the cluster's locals accumulated in LDS.  Each wave takes the cluster's
@@ -234,8 +347,8 @@ __device__ __forceinline__ void hm_entry2(double e, double dx, double dy2, const
 // (ds_add_f64).  The block stream drops by the in-cluster share (0.65 of the V
 // pairs at 64 targets per cluster, tools/vfrac.py); the summation order of the LDS
 // adds is not fixed (results repeat to rounding, not bitwise).
-template <int K, int NR, int WPE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+template <int K, int NR, int WPE, int NT, bool PF>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64_t* __restrict__ ptr,
          const int* __restrict__ ndir, const int* __restrict__ src, const int* __restrict__ blk,
          const int* __restrict__ slot, const double* __restrict__ E, const double* __restrict__ ncx, const double* __restrict__ ncy,
@@ -274,79 +387,85 @@ k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64
 #pragma unroll
             for (int i = 0; i < K; ++i) c[j][i] = 0.0;
         const int64_t p0 = ptr[c0 + ti], pd = p0 + ndir[c0 + ti], p1 = ptr[c0 + ti + 1];
-        // directed entries: PG blocks in flight, forward product only
-        for (int64_t cb = p0; cb < pd; cb += kWave) {
-            const int cnt = (int)min<int64_t>(kWave, pd - cb);
-            const int mySrc = lane < cnt ? src[cb + lane] : 0;
-            const int myBlk = lane < cnt ? blk[cb + lane] : 0;
-            for (int j0 = 0; j0 < cnt; j0 += PG) {
-                double e4[PG][4];
-                double xm[PG][K];
-                int B[PG];
-#pragma unroll
-                for (int g = 0; g < PG; ++g) {
-                    const int b = __builtin_amdgcn_readlane(myBlk, min(j0 + g, cnt - 1));
-                    const bool tr = b < 0;
-                    const double* p = E + (size_t)(tr ? ~b : b) * 256 + (tr ? 64 * q + s : 16 * s + 4 * q);
-                    const int st = tr ? 16 : 1;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) e4[g][j] = j0 + g < cnt ? p[j * st] : 0.0;
-                }
-#pragma unroll
-                for (int g = 0; g < PG; ++g) {  // a skipped block's source is a valid clamp; its E is zero
-                    B[g] = __builtin_amdgcn_readlane(mySrc, min(j0 + g, cnt - 1));
-                    const double* m = mult + ((size_t)B[g] * kRank + s) * K;
-#pragma unroll
-                    for (int b = 0; b < K; ++b) xm[g][b] = m[b];
-                }
-#pragma unroll
-                for (int g = 0; g < PG; ++g) {
-                    const double ax = ncx[B[g]] + nrx[B[g]] * chx;
-                    const double dy = (ncy[B[g]] + nry[B[g]] * chy) - by;
-                    const double dy2 = dy * dy;
-                    double xw[K];
-#pragma unroll
-                    for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * xm[g][b];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) hm_entry<K, false, NR>(e4[g][j], ax - bx[j], dy2, xw, c[j]);
+        if constexpr (PF) {
+            hc_directed_pf<K, NR>(p0, pd, lane, s, q, src, blk, E, ncx, ncy, nrx, nry, chx, chy, bx, by, hw, mult, c);
+            hc_dual_pf<K, NR>(pd, p1, lane, s, q, src, blk, slot, E, ncx, ncy, nrx, nry, chx, chy, bx, by, hw, mult, xa,
+                              acc, c);
+        } else {
+            // directed entries: PG blocks in flight, forward product only
+            for (int64_t cb = p0; cb < pd; cb += kWave) {
+                const int cnt = (int)min<int64_t>(kWave, pd - cb);
+                const int mySrc = lane < cnt ? src[cb + lane] : 0;
+                const int myBlk = lane < cnt ? blk[cb + lane] : 0;
+                for (int j0 = 0; j0 < cnt; j0 += PG) {
+                    double e4[PG][4];
+                    double xm[PG][K];
+                    int B[PG];
+    #pragma unroll
+                    for (int g = 0; g < PG; ++g) {
+                        const int b = __builtin_amdgcn_readlane(myBlk, min(j0 + g, cnt - 1));
+                        const bool tr = b < 0;
+                        const double* p = E + (size_t)(tr ? ~b : b) * 256 + (tr ? 64 * q + s : 16 * s + 4 * q);
+                        const int st = tr ? 16 : 1;
+    #pragma unroll
+                        for (int j = 0; j < 4; ++j) e4[g][j] = j0 + g < cnt ? p[j * st] : 0.0;
+                    }
+    #pragma unroll
+                    for (int g = 0; g < PG; ++g) {  // a skipped block's source is a valid clamp; its E is zero
+                        B[g] = __builtin_amdgcn_readlane(mySrc, min(j0 + g, cnt - 1));
+                        const double* m = mult + ((size_t)B[g] * kRank + s) * K;
+    #pragma unroll
+                        for (int b = 0; b < K; ++b) xm[g][b] = m[b];
+                    }
+    #pragma unroll
+                    for (int g = 0; g < PG; ++g) {
+                        const double ax = ncx[B[g]] + nrx[B[g]] * chx;
+                        const double dy = (ncy[B[g]] + nry[B[g]] * chy) - by;
+                        const double dy2 = dy * dy;
+                        double xw[K];
+    #pragma unroll
+                        for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * xm[g][b];
+    #pragma unroll
+                        for (int j = 0; j < 4; ++j) hm_entry<K, false, NR>(e4[g][j], ax - bx[j], dy2, xw, c[j]);
+                    }
                 }
             }
-        }
-        // in-cluster canonical entries (stored as read): both products, one block in flight
-        for (int64_t cb = pd; cb < p1; cb += kWave) {
-            const int cnt = (int)min<int64_t>(kWave, p1 - cb);
-            const int mySrc = lane < cnt ? src[cb + lane] : 0;
-            const int myBlk = lane < cnt ? blk[cb + lane] : 0;
-            const int mySlot = lane < cnt ? slot[cb + lane] : 0;
-            for (int jj = 0; jj < cnt; ++jj) {
-                const int b = __builtin_amdgcn_readlane(myBlk, jj);
-                const int B = __builtin_amdgcn_readlane(mySrc, jj);
-                const int sl = __builtin_amdgcn_readlane(mySlot, jj);
-                const dbl2* p = reinterpret_cast<const dbl2*>(E + (size_t)b * 256 + 16 * s + 4 * q);
-                const dbl2 k0 = p[0], k1 = p[1];
-                double xm[K];
-                const double* m = mult + ((size_t)B * kRank + s) * K;
-#pragma unroll
-                for (int bb = 0; bb < K; ++bb) xm[bb] = m[bb];
-                const double ax = ncx[B] + nrx[B] * chx;
-                const double dy = (ncy[B] + nry[B] * chy) - by;
-                const double dy2 = dy * dy;
-                double xw[K], ob[K];
-#pragma unroll
-                for (int bb = 0; bb < K; ++bb) {
-                    xw[bb] = hw.hw[bb] * xm[bb];
-                    ob[bb] = 0.0;
-                }
-                const double e4[4] = {k0.x, k0.y, k1.x, k1.y};
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    hm_entry2<K, NR>(e4[j], ax - bx[j], dy2, xw, xa + (4 * q + j) * K, c[j], ob);
-#pragma unroll
-                for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // rows 4q'+j over the quad
-                if (q == 0) {
-                    double* d = acc + ((size_t)sl * kRank + s) * K;
-#pragma unroll
-                    for (int i = 0; i < K; ++i) atomicAdd(d + i, (i & 1) ? -ob[i] : ob[i]);
+            // in-cluster canonical entries (stored as read): both products, one block in flight
+            for (int64_t cb = pd; cb < p1; cb += kWave) {
+                const int cnt = (int)min<int64_t>(kWave, p1 - cb);
+                const int mySrc = lane < cnt ? src[cb + lane] : 0;
+                const int myBlk = lane < cnt ? blk[cb + lane] : 0;
+                const int mySlot = lane < cnt ? slot[cb + lane] : 0;
+                for (int jj = 0; jj < cnt; ++jj) {
+                    const int b = __builtin_amdgcn_readlane(myBlk, jj);
+                    const int B = __builtin_amdgcn_readlane(mySrc, jj);
+                    const int sl = __builtin_amdgcn_readlane(mySlot, jj);
+                    const dbl2* p = reinterpret_cast<const dbl2*>(E + (size_t)b * 256 + 16 * s + 4 * q);
+                    const dbl2 k0 = p[0], k1 = p[1];
+                    double xm[K];
+                    const double* m = mult + ((size_t)B * kRank + s) * K;
+    #pragma unroll
+                    for (int bb = 0; bb < K; ++bb) xm[bb] = m[bb];
+                    const double ax = ncx[B] + nrx[B] * chx;
+                    const double dy = (ncy[B] + nry[B] * chy) - by;
+                    const double dy2 = dy * dy;
+                    double xw[K], ob[K];
+    #pragma unroll
+                    for (int bb = 0; bb < K; ++bb) {
+                        xw[bb] = hw.hw[bb] * xm[bb];
+                        ob[bb] = 0.0;
+                    }
+                    const double e4[4] = {k0.x, k0.y, k1.x, k1.y};
+    #pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        hm_entry2<K, NR>(e4[j], ax - bx[j], dy2, xw, xa + (4 * q + j) * K, c[j], ob);
+    #pragma unroll
+                    for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // rows 4q'+j over the quad
+                    if (q == 0) {
+                        double* d = acc + ((size_t)sl * kRank + s) * K;
+    #pragma unroll
+                        for (int i = 0; i < K; ++i) atomicAdd(d + i, (i & 1) ? -ob[i] : ob[i]);
+                    }
                 }
             }
         }
@@ -543,18 +662,18 @@ void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const in
 }
 
 
-template <int K, int NR>
+template <int K, int NR, int NT, bool PF, int WPE>
 static void run_m2l_hc(int ncl, size_t shm, const int* clPtr, const int* tgt, const int64_t* ptr, const int* ndir,
                        const int* src, const int* blk, const int* slot, const double* E, const double* ncx,
                        const double* ncy, const double* nrx, const double* nry, const Params* P, const HarmWeights& hw,
                        const double* mult, double* local, hipStream_t s) {
-    auto f = k_m2l_hc<K, NR, 3>;
+    auto f = k_m2l_hc<K, NR, WPE, NT, PF>;  // WPE 3: no spills without PF (~166 VGPRs)
     if (shm > 65536) {  // clusters of up to 64 targets at K = 8 need ~68 KB of the 160 KB LDS
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(f),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
         if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
     }
-    f<<<ncl, 256, shm, s>>>(clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry, P, hw, mult, local);
+    f<<<ncl, NT, shm, s>>>(clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry, P, hw, mult, local);
 }
 
 void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, const int64_t* ptr, const int* ndir,
@@ -562,15 +681,24 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, 
                    const double* nrx, const double* nry, const Params* P, const HarmWeights& hw, const double* mult,
                    double* local, hipStream_t s) {
     if (ncl <= 0) return;
-    const size_t shm = (size_t)(maxCl + 4) * kRank * K * sizeof(double);
+    constexpr int NT = 256;  // 4 waves per cluster (512 / 768 measured slower, r01f)
+    const size_t shm = (size_t)(maxCl + NT / kWave) * kRank * K * sizeof(double);
     if (shm > 160 * 1024) throw std::invalid_argument("harmonic M2L cluster exceeds the LDS");
-    if (hm_var() & 2) {
-        ANISO_HM_DISPATCH_K(K, (run_m2l_hc<KK, 1>(ncl, shm, clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry,
-                                                  P, hw, mult, local, s)));
+    // ANISO_HM_VAR bit 3: software-pipelined block streams (PF); bit 4: 2 waves per
+    // SIMD instead of 3; bit 5: two Newton steps (default one: ~1e-13 per entry)
+    const int v = hm_var();
+#define ANISO_HC(NR, PF, WPE)                                                                                      \
+    ANISO_HM_DISPATCH_K(K, (run_m2l_hc<KK, NR, NT, PF, WPE>(ncl, shm, clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, \
+                                                             ncy, nrx, nry, P, hw, mult, local, s)))
+    const bool pf = (v >> 3) & 1, w2 = (v >> 4) & 1, nr2 = (v >> 5) & 1;
+    if (nr2) {
+        ANISO_HC(2, false, 3);
+    } else if (pf) {
+        if (w2) { ANISO_HC(1, true, 2); } else { ANISO_HC(1, true, 3); }
     } else {
-        ANISO_HM_DISPATCH_K(K, (run_m2l_hc<KK, 2>(ncl, shm, clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry,
-                                                  P, hw, mult, local, s)));
+        if (w2) { ANISO_HC(1, false, 2); } else { ANISO_HC(1, false, 3); }
     }
+#undef ANISO_HC
     HIP_LAUNCH_CHECK();
 }
 

@@ -634,10 +634,13 @@ void Plan::buildClusters(const Tree& t) {
     // cluster key: (level, ancestor kClusterDepth levels up); targets keep id order
     std::vector<int> widx(t.nn, -1);
     for (int w = 0; w < nt; ++w) widx[m2lTgt[w]] = w;
+    int depth = kClusterDepth;
+    if (const char* e = std::getenv("ANISO_HM_CLDEPTH"))  // tuning/experiments only (1..kClusterDepth)
+        depth = std::max(1, std::min(kClusterDepth, std::atoi(e)));
     std::vector<int64_t> key(nt);
     for (int w = 0; w < nt; ++w) {
         int a = m2lTgt[w];
-        for (int k = 0; k < kClusterDepth && t.parent[a] != -1; ++k) a = t.parent[a];
+        for (int k = 0; k < depth && t.parent[a] != -1; ++k) a = t.parent[a];
         key[w] = ((int64_t)t.level[m2lTgt[w]] << 32) | (uint32_t)a;
     }
     std::vector<int> order(nt);

@@ -40,6 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
+FP64_VALU_PEAK_TF = 78.6  # MI355X fp64 vector (spec): half the 157.3 TF fp32 vector rate of the chip table
 
 
 def main_coeffs(xy):
@@ -85,7 +86,8 @@ def pmc_traffic(kernel):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
     if not files:
         return None, None
-    k = json.load(open(files[-1]))["kernels"].get(kernel)
+    ks = json.load(open(files[-1]))["kernels"]
+    k = ks.get(kernel) or next((v for n, v in ks.items() if n.startswith(kernel)), None)
     if not k:
         return None, None
     return int(k["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
@@ -283,10 +285,16 @@ def main():
     # target node (16 x nb doubles each).  Per-mode stream (k_m2l): the stored merged
     # operators of every mode term, the same per-target bytes per term, one
     # transposed partial (16 x nb doubles) per canonical pair and term.
+    # Clustered (k_m2l_hc, §3.10): an in-cluster pair's stored block is read once for
+    # both ends; a pair crossing clusters is still read by each end (block_reads).
+    # The algorithmic bytes count every stored block once.
     harmonic = block and my_stats["harmonic"] == 1
-    if harmonic:
+    if harmonic and my_stats["hm_clusters"] > 0:
         m2l_bytes = 2048.0 * my_stats["att_m2l_blocks"] + 2.0 * 128.0 * nb * my_stats["m2l_targets"]
-        kname, pmc_name = f"k_m2l_hm<{nb}>", f"void aniso::k_m2l_hm<{nb}, 4>"
+        kname, pmc_name = f"k_m2l_hc<{nb}>", f"void aniso::k_m2l_hc<{nb},"
+    elif harmonic:
+        m2l_bytes = 2048.0 * my_stats["att_m2l_blocks"] + 2.0 * 128.0 * nb * my_stats["m2l_targets"]
+        kname, pmc_name = f"k_m2l_hm<{nb}>", f"void aniso::k_m2l_hm<{nb},"
     else:
         terms = len(modes) if block else 1
         m2l_bytes = terms * (2048.0 * my_stats["stored_m2l"] + 2.0 * 128.0 * nb * my_stats["m2l_targets"]
@@ -299,6 +307,16 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
                 "kernel_ms": round(m2l_ms, 5), "algorithmic_bytes": int(m2l_bytes), "traffic_source": tsrc}
+    if harmonic:
+        # the harmonic M2L is fp64-VALU work per matrix entry: r^2,
+        # 1/r, c = dx/r, T_2..T_{K-1}, V = sum_b T_b xw_b, (E/r) V, K output FMAs =
+        # 6K flops per directed entry (FMA = 2), 256 entries per directed pair
+        flops = 6.0 * nb * 256.0 * my_stats["m2l_pairs"]
+        tf = flops / (m2l_ms * 1e-3) / 1e12 if m2l_ms > 0 else 0.0
+        roofline["e_block_reads"] = my_stats["hm_block_reads"] if my_stats["hm_clusters"] > 0 else my_stats["m2l_pairs"]
+        roofline["compute"] = {"bound": "fp64_valu", "achieved": round(tf, 2), "peak": FP64_VALU_PEAK_TF,
+                               "unit": "TFLOP/s", "frac": round(tf / FP64_VALU_PEAK_TF, 4),
+                               "algorithmic_flops": int(flops)}
     applies = ks * (2 * ks - 1) if block else 1  # the reference's mapping calls per matvec
     cfg = (f"configs[2] (1M points, d=1, ns=10, np=4, maxLevel=20, g={args.g}): aniso.m GMRES block matvec "
            f"x - mforward(x), {ks} blocks x {2 * ks - 1} modes = {applies} mode-applies per matvec"

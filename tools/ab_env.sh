@@ -3,6 +3,6 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for cfg in "$@"; do
-  env $cfg timeout -k 10 200 python bench.py --no-cpu --steps 10 > "gpurun_out/ab_$cfg.log" 2>&1 || exit $?
-  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['stage_ms'])" "gpurun_out/ab_$cfg.log" "$cfg"
+  env $cfg timeout -k 10 200 python bench.py --no-cpu --steps 10 > "gpurun_out/ab_${cfg// /_}.log" 2>&1 || exit $?
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['stage_ms'])" "gpurun_out/ab_${cfg// /_}.log" "$cfg"
 done
