@@ -78,6 +78,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     useAtt = ks > 1 && !plan.nearSymmetric;
     if (const char* e = std::getenv("ANISO_HARMONIC")) useAtt = useAtt && e[0] != '0';
     if (const char* e = std::getenv("ANISO_HM_CLUSTER")) useClusters = e[0] != '0';
+    if (const char* e = std::getenv("ANISO_OVERLAP")) overlap = std::atoi(e);
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
     modes.resize(kernelSize);
@@ -87,6 +88,9 @@ Operator::~Operator() {
     if (device >= 0) {
         (void)hipSetDevice(device);
         for (auto& e : evPool) (void)hipEventDestroy(e);
+        if (evFork) (void)hipEventDestroy(evFork);
+        if (evJoin) (void)hipEventDestroy(evJoin);
+        if (side) (void)hipStreamDestroy(side);
         if (own) (void)hipStreamDestroy(own);
     }
 }
@@ -115,6 +119,14 @@ void Operator::ensureDevice() {
     }
     HIP_CHECK(hipGetDevice(&device));
     HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
+    {
+        int lo = 0, hi = 0;  // ANISO_SIDE_PRIO=1: the side stream at the highest priority
+        HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        const char* e = std::getenv("ANISO_SIDE_PRIO");
+        HIP_CHECK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, e && e[0] == '1' ? hi : lo));
+    }
+    HIP_CHECK(hipEventCreateWithFlags(&evFork, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
     // tree-order coordinates
     std::vector<double> pxT(geo.N), pyT(geo.N);
     for (int64_t k = 0; k < geo.N; ++k) {
@@ -633,31 +645,53 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     const CorrFold& cf = corrTable(K, nterm, ids, mixes);
     HarmWeights hw;
     if (harmonicWeights(K, nterm, ids, mixes, hw)) {
-        // every mode of aniso.m's block operator from one read of the E caches
-        launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
-                       dNearPts.as<int>(), dNearKOff.as<int64_t>(), dAttNear.as<double>(), dPxT.as<double>(),
-                       dPyT.as<double>(), dSigDiag.as<double>(), hw, dFT.as<double>(), operm, obase, ldo, mask, scale,
-                       out, s);
-        int e = tm ? mark(s) : -1;
-        span(4, ep, e);
-        ep = e;
-        launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
-                    dFT.as<double>(), cf.Wc.as<double>(), cf.Wm.as<double>(), P, mask, scale, treeOut, ldo, out, s);
-        e = tm ? mark(s) : -1;
-        span(6, ep, e);
-        ep = e;
-        if ((mask & kStageFar) && useClusters)
-            launch_m2l_hc(K, (int)plan.hmClPtr.size() - 1, plan.hmMaxCl, dHmClPtr.as<int>(), dHmTgt.as<int>(),
-                          dHmPtr.as<int64_t>(), dHmNDir.as<int>(), dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(),
-                          dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
-                          dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
-        else if (mask & kStageFar)
-            launch_m2l_hm(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dAttPtr.as<int64_t>(), dAttSrc.as<int>(),
-                          dAttBlk.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
-                          dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
-        e = tm ? mark(s) : -1;
-        span(2, ep, e);
-        ep = e;
+        // every mode of aniso.m's block operator from one read of the E caches.
+        // Near field + corrections (they write `out`) on the side stream beside the
+        // M2L (it writes the locals); the down pass adds into `out` after the join.
+        // overlap 1: near enqueued first; 2: the M2L first.
+        const hipStream_t sn = overlap ? side : s;
+        int e = -1;
+        auto nearStage = [&] {
+            int en = tm ? (overlap ? mark(sn) : ep) : -1;
+            launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
+                           dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(), dNearKOff.as<int64_t>(),
+                           dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dSigDiag.as<double>(), hw,
+                           dFT.as<double>(), operm, obase, ldo, mask, scale, out, sn);
+            int e1 = tm ? mark(sn) : -1;
+            span(4, en, e1);
+            launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
+                        dFT.as<double>(), cf.Wc.as<double>(), cf.Wm.as<double>(), P, mask, scale, treeOut, ldo, out,
+                        sn);
+            int e2 = tm ? mark(sn) : -1;
+            span(6, e1, e2);
+            if (!overlap) ep = e2;
+            if (overlap) HIP_CHECK(hipEventRecord(evJoin, side));
+        };
+        auto farStage = [&] {
+            if ((mask & kStageFar) && useClusters)
+                launch_m2l_hc(K, (int)plan.hmClPtr.size() - 1, plan.hmMaxCl, dHmClPtr.as<int>(), dHmTgt.as<int>(),
+                              dHmPtr.as<int64_t>(), dHmNDir.as<int>(), dHmSrc.as<int>(), dHmBlk.as<int>(),
+                              dHmSlot.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(),
+                              dNrx.as<double>(), dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
+            else if (mask & kStageFar)
+                launch_m2l_hm(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dAttPtr.as<int64_t>(), dAttSrc.as<int>(),
+                              dAttBlk.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(),
+                              dNrx.as<double>(), dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
+            e = tm ? mark(s) : -1;
+            span(2, ep, e);
+            ep = e;
+        };
+        if (overlap) HIP_CHECK(hipEventRecord(evFork, s));
+        if (overlap == 2) {
+            farStage();
+            HIP_CHECK(hipStreamWaitEvent(side, evFork, 0));
+            nearStage();
+        } else {
+            if (overlap) HIP_CHECK(hipStreamWaitEvent(side, evFork, 0));
+            nearStage();
+            farStage();
+        }
+        if (overlap) HIP_CHECK(hipStreamWaitEvent(s, evJoin, 0));
     } else {
     // near field: symmetric U storage (K = 1 handles) one launch per term (its
     // transposed products go to partials, summed over the terms); directed

@@ -138,6 +138,11 @@ private:
     void uploadPlan();
     int device = -1;
     hipStream_t own = nullptr;
+    // side stream of the harmonic block apply: near field + corrections run beside
+    // the M2L (both HBM-bound, neither saturates alone)
+    hipStream_t side = nullptr;
+    hipEvent_t evFork = nullptr, evJoin = nullptr;
+    int overlap = 1;
     // stage timing: events recorded in-stream, (stage, start, end) spans per apply
     std::vector<hipEvent_t> evPool;
     int evUsed = 0;
