@@ -79,6 +79,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_HARMONIC")) useAtt = useAtt && e[0] != '0';
     if (const char* e = std::getenv("ANISO_HM_CLUSTER")) useClusters = e[0] != '0';
     if (const char* e = std::getenv("ANISO_OVERLAP")) overlap = std::atoi(e);
+    if (const char* e = std::getenv("ANISO_NEAR_CLUSTER")) useNearClusters = e[0] != '0';
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
     modes.resize(kernelSize);
@@ -265,6 +266,11 @@ void Operator::uploadPlan() {
         up(dHmBlk, plan.hmBlk);
         up(dHmSlot, plan.hmSlot);
         up(dHmNDir, plan.hmNDir);
+        up(dNcPtr, plan.ncPtr);
+        up(dNcLeaf, plan.ncLeaf);
+        up(dNcSlot, plan.ncSlot);
+        up(dNcSegPtr, plan.ncSegPtr);
+        up(dNcSeg, to_int4(plan.ncSeg));
         attReady = false;
     }
     up(dM2LCanonBase, plan.m2lCanonBase);
@@ -633,18 +639,25 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     if (plan.upTierTask.size() < 2)  // a lone leaf: no up pass
         launch_prepare(K, geo.N, x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(),
                        dCT.as<double>(), s);
-    for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k)
+    HarmWeights hw;
+    const bool harmonic = harmonicWeights(K, nterm, ids, mixes, hw);
+    // the harmonic block apply forks its near field off as soon as the charges are
+    // complete: after the last up tier with a P2M leaf (the tiers above only M2M)
+    const bool fork = harmonic && overlap;
+    if (fork && plan.upTierTask.size() < 2) HIP_CHECK(hipEventRecord(evFork, s));
+    for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k) {
         launch_up_tier(K, plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask,
                        dUpDesc.as<int4>(), dUpGrpFix.as<int>(), dUpNode.as<int>(), dUpCode.as<int4>(),
                        dUpGeom.as<double4>(), dUpLeaf.as<int2>(), dPxT.as<double>(), dPyT.as<double>(), x, ldx,
                        treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(), dCT.as<double>(), P,
                        dMult.as<double>(), s);
+        if (fork && (int)k == plan.upLastLeafTier) HIP_CHECK(hipEventRecord(evFork, s));
+    }
     int ep = tm ? mark(s) : -1;
     span(1, e0, ep);
     const ModeArgs* tab = modeTable(K, nterm, ids, mixes);
     const CorrFold& cf = corrTable(K, nterm, ids, mixes);
-    HarmWeights hw;
-    if (harmonicWeights(K, nterm, ids, mixes, hw)) {
+    if (harmonic) {
         // every mode of aniso.m's block operator from one read of the E caches.
         // Near field + corrections (they write `out`) on the side stream beside the
         // M2L (it writes the locals); the down pass adds into `out` after the join.
@@ -653,10 +666,16 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         int e = -1;
         auto nearStage = [&] {
             int en = tm ? (overlap ? mark(sn) : ep) : -1;
-            launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
-                           dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(), dNearKOff.as<int64_t>(),
-                           dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dSigDiag.as<double>(), hw,
-                           dFT.as<double>(), operm, obase, ldo, mask, scale, out, sn);
+            if (nearClustersOn(K) && (mask & kStageNear))
+                launch_near_hc(K, (int)plan.ncPtr.size() - 1, dNcPtr.as<int>(), dNcLeaf.as<int>(), dNcSlot.as<int>(),
+                               plan.ncMaxPts, dNcSegPtr.as<int64_t>(), dNcSeg.as<int4>(), dLeafInfo.as<int4>(),
+                               dNearKOff.as<int64_t>(), dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(),
+                               dSigDiag.as<double>(), hw, dFT.as<double>(), operm, obase, ldo, scale, out, sn);
+            else
+                launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
+                               dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(), dNearKOff.as<int64_t>(),
+                               dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dSigDiag.as<double>(), hw,
+                               dFT.as<double>(), operm, obase, ldo, mask, scale, out, sn);
             int e1 = tm ? mark(sn) : -1;
             span(4, en, e1);
             launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
@@ -681,7 +700,6 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             span(2, ep, e);
             ep = e;
         };
-        if (overlap) HIP_CHECK(hipEventRecord(evFork, s));
         if (overlap == 2) {
             farStage();
             HIP_CHECK(hipStreamWaitEvent(side, evFork, 0));

@@ -93,6 +93,10 @@ public:
     hipStream_t stream() const { return own; }
     bool harmonicReady() const { return useAtt && attReady; }
     bool clustersOn() const { return useClusters; }
+    // near clusters: the plan has them (leaves <= 16 points, 64 KB LDS) and they are on
+    bool nearClustersOn(int K = 5) const {
+        return useNearClusters && plan.ncPtr.size() > 1 && ((size_t)plan.ncMaxPts + 256) * K * 8 <= 64 * 1024;
+    }
     bool modeCached(int id) const { return id >= 0 && id < kernelSize && modes[id].ready; }
     int kernelSize = 0;
     // stage timing with HIP events recorded in-stream (no host sync per apply);
@@ -129,6 +133,8 @@ private:
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
     bool useClusters = true;
+    DevBuf dNcPtr, dNcLeaf, dNcSlot, dNcSegPtr, dNcSeg;  // near cluster plan
+    bool useNearClusters = false;  // measured slower than the per-leaf kernel
     std::map<std::string, DevBuf> modeTabs;
     const CorrFold& corrTable(int K, int nterm, const int* ids, const double* mixes);
     std::map<std::string, CorrFold> corrTabs;

@@ -343,6 +343,9 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[14] = cl ? (int64_t)op.plan.hmClPtr.size() - 1 : 0;
         s[15] = cl ? op.plan.hmDual : 0;
         s[16] = cl ? (int64_t)op.plan.hmSrc.size() : (int64_t)op.plan.attSrc.size();
+        const bool nc = op.harmonicReady() && op.nearClustersOn();
+        s[17] = nc ? (int64_t)op.plan.ncPtr.size() - 1 : 0;
+        s[18] = nc ? op.plan.ncDual : 0;
     });
 }
 

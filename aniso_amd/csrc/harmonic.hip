@@ -201,11 +201,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 // forward product o as hm_entry, and the partner's product ob[i] += T_i(c) (E/r) V_A,
 // V_A = sum_b T_b(c) xa[b] with xa[b] = (-1)^b hw_b x_A,b(t) (the reversed direction
 // has cos = -c; its (-1)^i is applied when ob is flushed).
-template <int K, int NR>
+template <int K, int NR, bool guard0 = false>
 __device__ __forceinline__ void hm_entry2(double e, double dx, double dy2, const double (&xw)[K],
                                           const double* __restrict__ xa, double (&o)[K], double (&ob)[K]) {
     const double r2 = __builtin_fma(dx, dx, dy2);
-    const double ri = rsqrt_nr<NR>(r2);
+    double ri = rsqrt_nr<NR>(r2);
+    if constexpr (guard0) ri = r2 > 0.0 ? ri : 0.0;
     const double c = dx * ri;
     double T[K];
     cheb_T<K>(c, T);
@@ -621,6 +622,152 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
     }
 }
 
+
+// The harmonic near field in clusters: one 256-thread workgroup
+// per cluster of leaves (<= 16 points each; same level, one ancestor
+// kClusterDepth levels up), 16 lanes per target leaf as in k_near_hm (row quad rq
+// = lane & 3, column phase lane >> 2), the cluster's sums in LDS.  A U pair of two
+// cluster leaves is applied by the smaller id from one read of its sub-block: the
+// forward product, and per column (source point) the partner's product
+// T_i(c)(E/r) sum_b T_b(c) (-1)^b hw_b f_A,b(t) summed over the target rows (in
+// lane, then over the quad by DPP) and added to the partner's LDS sum with
+// (-1)^i (the reversed direction has cos = -c).  After the barrier every point's
+// output is stored: scale * om_i * (sum + dw_i sigma_t f_i).
+template <int K, int NR, int U>
+__global__ void __launch_bounds__(256) k_near_hc(const int* __restrict__ clPtr, const int* __restrict__ clLeaf,
+                                                 const int* __restrict__ clSlot, int maxPts,
+                                                 const int64_t* __restrict__ segPtr, const int4* __restrict__ seg,
+                                                 const int4* __restrict__ leafInfo,
+                                                 const int64_t* __restrict__ nearKOff, const double* __restrict__ E,
+                                                 const double* __restrict__ pxT, const double* __restrict__ pyT,
+                                                 const double* __restrict__ sigDiag, HarmWeights hw,
+                                                 const double* __restrict__ fT, const int* __restrict__ operm,
+                                                 int64_t obase, int64_t ldo, double scale, double* __restrict__ out) {
+    constexpr int KS = kStride<K>;
+    extern __shared__ double sm[];
+    const int c0 = clPtr[blockIdx.x], nlc = clPtr[blockIdx.x + 1] - c0;
+    const int npts = clSlot[c0 + nlc - 1] + leafInfo[clLeaf[c0 + nlc - 1]].z;
+    double* acc = sm;  // npts x K
+    const int grp = threadIdx.x >> 4, gl = threadIdx.x & 15;
+    double* xa = sm + (size_t)maxPts * K + (size_t)grp * 16 * K;  // the group's target charges, (-1)^b hw_b
+    for (int i = threadIdx.x; i < npts * K; i += blockDim.x) acc[i] = 0.0;
+    __syncthreads();
+    const int rq = gl & 3, cph = gl >> 2;
+    for (int lk = grp; lk < nlc; lk += 16) {
+        const int li = clLeaf[c0 + lk];
+        const int4 info = leafInfo[li];
+        const int nT = info.z, nq = (nT + 3) >> 2, cstr = 2 * nq;
+        const int64_t tb = info.y;
+        const bool rowOk = rq < nq;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous leaf's xa reads are done
+        __builtin_amdgcn_wave_barrier();
+        for (int e = gl; e < 16 * K; e += 16) {
+            const int t = e / K, b = e - t * K;
+            xa[e] = t < nT ? ((b & 1) ? -hw.hw[b] : hw.hw[b]) * fT[(size_t)(tb + t) * KS + b] : 0.0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        double tx[4], ty[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = min(4 * rq + j, nT - 1);  // padded rows: E is zero there
+            tx[j] = rowOk ? pxT[tb + t] : 0.0;
+            ty[j] = rowOk ? pyT[tb + t] : 0.0;
+        }
+        double a[4][K];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < K; ++i) a[j][i] = 0.0;
+        const dbl2* kc = reinterpret_cast<const dbl2*>(E + nearKOff[li]) + 2 * (rowOk ? rq : 0);
+        for (int64_t sg = segPtr[li]; sg < segPtr[li + 1]; ++sg) {
+            const int4 d = seg[sg];  // first source point, points, first column, partner slot
+            for (int cb = 0; cb < d.y; cb += 4 * U) {  // group-uniform trip count: whole quads stay active
+                dbl2 kk[U][2];
+                double f[U][K], sx[U], sy[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {  // U columns in flight per lane
+                    const int sc = cb + cph + 4 * u;
+                    const bool ok = rowOk && sc < d.y;
+                    const int scc = min(sc, d.y - 1);
+                    const dbl2* p = kc + (size_t)(d.z + scc) * cstr;
+                    kk[u][0] = ok ? __builtin_nontemporal_load(p) : dbl2{0.0, 0.0};
+                    kk[u][1] = ok ? __builtin_nontemporal_load(p + 1) : dbl2{0.0, 0.0};
+                    const int64_t ks = (int64_t)d.x + scc;
+                    load_charges<K>(fT + (size_t)ks * KS, f[u]);
+                    sx[u] = pxT[ks];
+                    sy[u] = pyT[ks];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int sc = cb + cph + 4 * u;
+                    double xw[K];
+#pragma unroll
+                    for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * f[u][b];
+                    const double e4[4] = {kk[u][0].x, kk[u][0].y, kk[u][1].x, kk[u][1].y};
+                    if (d.w < 0) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const double dy = sy[u] - ty[j];
+                            hm_entry<K, true, NR>(e4[j], sx[u] - tx[j], dy * dy, xw, a[j]);
+                        }
+                    } else {
+                        double ob[K];
+#pragma unroll
+                        for (int i = 0; i < K; ++i) ob[i] = 0.0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const double dy = sy[u] - ty[j];
+                            hm_entry2<K, NR, true>(e4[j], sx[u] - tx[j], dy * dy, xw, xa + (4 * rq + j) * K, a[j], ob);
+                        }
+#pragma unroll
+                        for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // the 4 row quads of column sc
+                        if (rq == 0 && sc < d.y) {
+                            double* dst = acc + (size_t)(d.w + sc) * K;
+#pragma unroll
+                            for (int i = 0; i < K; ++i) atomicAdd(dst + i, (i & 1) ? -ob[i] : ob[i]);
+                        }
+                    }
+                }
+            }
+        }
+        // sum over the column phases (the group is one DPP row of 16 lanes)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                double v = a[j][i];
+                v += dpp_f64<0x124>(v);  // row_ror:4
+                v += dpp_f64<0x128>(v);  // row_ror:8
+                a[j][i] = v;
+            }
+        const int slot = clSlot[c0 + lk];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = 4 * rq + j;
+            if (cph != j || !rowOk || t >= nT) continue;
+            double* dst = acc + (size_t)(slot + t) * K;
+#pragma unroll
+            for (int i = 0; i < K; ++i) atomicAdd(dst + i, a[j][i]);
+        }
+    }
+    __syncthreads();
+    for (int lk = grp; lk < nlc; lk += 16) {
+        const int li = clLeaf[c0 + lk];
+        const int4 info = leafInfo[li];
+        if (gl >= info.z) continue;
+        const int64_t k = (int64_t)info.y + gl;
+        const double* sum = acc + (size_t)(clSlot[c0 + lk] + gl) * K;
+        double f[K];
+        load_charges<K>(fT + (size_t)k * KS, f);
+        const double sd = sigDiag[k];
+        const int64_t oi = out_index(operm, obase, k);
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            out[(size_t)i * ldo + oi] = hw.om[i] * scale * __builtin_fma(hw.dw[i] * sd, f[i], sum[i]);
+    }
+}
+
 // ----------------------------------------------------------------- launchers
 
 #define ANISO_HM_DISPATCH_K(k, CALL)                                                                    \
@@ -726,6 +873,35 @@ void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
         }
     }
 #undef ANISO_NEAR_HM
+    HIP_LAUNCH_CHECK();
+}
+
+
+void launch_near_hc(int K, int ncl, const int* clPtr, const int* clLeaf, const int* clSlot, int maxPts,
+                    const int64_t* segPtr, const int4* seg, const int4* leafInfo, const int64_t* nearKOff,
+                    const double* E, const double* pxT, const double* pyT, const double* sigDiag,
+                    const HarmWeights& hw, const double* fT, const int* operm, int64_t obase, int64_t ldo,
+                    double scale, double* out, hipStream_t s) {
+    if (ncl <= 0) return;
+    const size_t shm = ((size_t)maxPts + 16 * 16) * K * sizeof(double);
+    if (shm > 64 * 1024) throw std::invalid_argument("harmonic near cluster exceeds 64 KB of LDS");
+    static const int u = [] {  // ANISO_NEAR_U: source columns in flight per lane (1, 2, 4)
+        const char* e = std::getenv("ANISO_NEAR_U");
+        const int v = e ? std::atoi(e) : 4;
+        return v == 1 || v == 2 ? v : 4;
+    }();
+#define ANISO_NHC(UU)                                                                                              \
+    ANISO_HM_DISPATCH_K(K, (k_near_hc<KK, 2, UU><<<ncl, 256, shm, s>>>(clPtr, clLeaf, clSlot, maxPts, segPtr, seg,  \
+                                                                       leafInfo, nearKOff, E, pxT, pyT, sigDiag, hw, \
+                                                                       fT, operm, obase, ldo, scale, out)))
+    if (u == 1) {
+        ANISO_NHC(1);
+    } else if (u == 2) {
+        ANISO_NHC(2);
+    } else {
+        ANISO_NHC(4);
+    }
+#undef ANISO_NHC
     HIP_LAUNCH_CHECK();
 }
 

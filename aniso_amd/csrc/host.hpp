@@ -109,6 +109,18 @@ struct Plan {
     std::vector<int64_t> hmPtr;
     int hmMaxCl = 0;
     int64_t hmDual = 0;
+    // near field in clusters, block handles with leaves <= 16
+    // points: cluster c = leaves ncLeaf[ncPtr[c] .. ncPtr[c+1]) (same level, one
+    // ancestor kClusterDepth levels up), their points at LDS offsets ncSlot.  Per
+    // leaf li the source segments ncSeg[ncSegPtr[li] ..): {first source point (tree
+    // position), points, first column of li's E block, LDS point offset of the
+    // source leaf when li applies the pair both ways (-1: forward only)}; the
+    // partner of a two-way pair has no segment for it.
+    std::vector<int> ncPtr, ncLeaf, ncSlot;
+    std::vector<int64_t> ncSegPtr;
+    std::vector<std::array<int, 4>> ncSeg;
+    int ncMaxPts = 0;
+    int64_t ncDual = 0;
     // tiered up / down passes: tier k has root level
     // tierRootLevel[k] and bottom level tierBottomLevel[k] (k = 0 is the deepest).
     std::vector<int> tierRootLevel, tierBottomLevel;
@@ -118,6 +130,7 @@ struct Plan {
     std::vector<int> upTierTask, upTaskPtr, upGrpPtr, upGrp, upNode;
     std::vector<std::array<int, 4>> upCode;
     int upMaxTask = 1;
+    int upLastLeafTier = 0;  // last up tier with a P2M leaf: fT / cT are complete after it
     // the same, as records the kernel loads in one round: per task (first node,
     // nodes, first point, levels) + kTaskLevels+1 level starts; per node the box
     // (cx, cy, 1/rx, 1/ry) and the point range relative to the task's first point
@@ -151,6 +164,7 @@ struct Plan {
   private:
     void buildUpTasks(const Tree& t);
     void buildClusters(const Tree& t);
+    void buildNearClusters(const Tree& t);
     void buildDownTasks(const Tree& t);
 };
 

@@ -268,9 +268,11 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         if (D >= 1) {
             tierRootLevel.push_back(std::max(1, D - 3));
             tierBottomLevel.push_back(D);
+            int span = 4;  // levels per upper tier; ANISO_TOP_SPAN (1..4): tuning/experiments only
+            if (const char* e = std::getenv("ANISO_TOP_SPAN")) span = std::max(1, std::min(4, std::atoi(e)));
             while (tierRootLevel.back() > 1) {
                 tierBottomLevel.push_back(tierRootLevel.back() - 1);
-                tierRootLevel.push_back(std::max(1, tierRootLevel.back() - 4));
+                tierRootLevel.push_back(std::max(1, tierRootLevel.back() - span));
             }
         }
     }
@@ -432,6 +434,7 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         }
         nearPtsPtr.push_back((int64_t)nearPts.size());
     }
+    buildNearClusters(t);
     buildDownTasks(t);
 }
 
@@ -513,6 +516,11 @@ void Plan::buildUpTasks(const Tree& t) {
         }
         upTierTask.push_back((int)upTaskPtr.size() - 1);
     }
+    upLastLeafTier = 0;
+    for (size_t k = 0; k + 1 < upTierTask.size(); ++k)
+        for (int task = upTierTask[k]; task < upTierTask[k + 1]; ++task)
+            for (int i = upTaskPtr[task]; i < upTaskPtr[task + 1]; ++i)
+                if (upCode[i][0] == kLeafCode) upLastLeafTier = (int)k;
     upGrp.push_back((int)upNode.size());  // sentinel: group g spans [upGrp[g], upGrp[g+1])
 }
 
@@ -687,6 +695,76 @@ void Plan::buildClusters(const Tree& t) {
         hmSlot.insert(hmSlot.end(), dSlot.begin(), dSlot.end());
         hmDual += (int64_t)dSrc.size();
         hmPtr.push_back((int64_t)hmSrc.size());
+    }
+}
+
+// Cluster plan of the harmonic near field from the directed near
+// lists (block handles only: nearSymmetric off, every leaf <= 16 points).
+void Plan::buildNearClusters(const Tree& t) {
+    ncPtr.assign(1, 0);
+    ncLeaf.clear();
+    ncSlot.clear();
+    ncSegPtr.assign(1, 0);
+    ncSeg.clear();
+    ncMaxPts = 0;
+    ncDual = 0;
+    const int nl = (int)leaves.size();
+    if (nl == 0 || nearSymmetric || nearMaxLeaf > 16) return;
+    int depth = kClusterDepth;
+    if (const char* e = std::getenv("ANISO_NEAR_CLDEPTH"))  // tuning/experiments only (1..kClusterDepth)
+        depth = std::max(1, std::min(kClusterDepth, std::atoi(e)));
+    std::vector<int64_t> key(nl);
+    for (int li = 0; li < nl; ++li) {
+        int a = leaves[li];
+        for (int k = 0; k < depth && t.parent[a] != -1; ++k) a = t.parent[a];
+        key[li] = ((int64_t)t.level[leaves[li]] << 32) | (uint32_t)a;
+    }
+    std::vector<int> order(nl);
+    for (int li = 0; li < nl; ++li) order[li] = li;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
+    std::vector<int> clOf(t.nn, -1), slotOf(t.nn, -1);
+    int nc = 0, pts = 0;
+    for (int k = 0; k < nl; ++k) {
+        if (k > 0 && key[order[k]] != key[order[k - 1]]) {
+            ncPtr.push_back(k);
+            ncMaxPts = std::max(ncMaxPts, pts);
+            ++nc;
+            pts = 0;
+        }
+        const int n = leaves[order[k]];
+        clOf[n] = nc;
+        slotOf[n] = pts;
+        ncLeaf.push_back(order[k]);
+        ncSlot.push_back(pts);
+        pts += (int)t.count[n];
+    }
+    ncPtr.push_back(nl);
+    ncMaxPts = std::max(ncMaxPts, pts);
+    for (int li = 0; li < nl; ++li) {
+        const int a = leaves[li];
+        int col = 0;
+        for (int64_t j = nearPtr[li]; j < nearPtr[li + 1]; ++j) {
+            const int b = nearSrc[j];
+            const int cnt = (int)t.count[b];
+            // U members (j before the W part) that are leaves of a's cluster: the
+            // pair is applied both ways by the smaller node id.  The U relation is
+            // symmetric between leaves, so b's list holds a as well.
+            bool isU = false;
+            for (int64_t k = t.uPtr[a]; k < t.uPtr[a + 1]; ++k)
+                if (t.uIdx[k] == b) {
+                    isU = true;
+                    break;
+                }
+            const bool same = isU && b != a && clOf[b] >= 0 && clOf[b] == clOf[a];
+            if (same && b < a) {  // applied by b
+                col += cnt;
+                continue;
+            }
+            ncSeg.push_back({(int)t.begin[b], cnt, col, same ? slotOf[b] : -1});
+            if (same) ++ncDual;
+            col += cnt;
+        }
+        ncSegPtr.push_back((int64_t)ncSeg.size());
     }
 }
 

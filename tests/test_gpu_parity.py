@@ -594,3 +594,34 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatc
     assert st[0]["harmonic"] == 1 and st[0]["hm_clusters"] > 0 and st[1]["hm_clusters"] == 0
     assert st[0]["hm_dual_pairs"] > 0 and st[0]["hm_block_reads"] < st[1]["hm_block_reads"]
     assert _rel(outs[0], outs[1]) <= 1e-13
+
+
+@pytest.mark.parametrize("sz,d,ks,ml", [(32, 1, 5, 20), (19, 2, 3, 20), (64, 1, 2, 20), (40, 1, 5, 3), (27, 3, 4, 20)])
+def test_harmonic_near_clusters_match_per_leaf_groups(sz, d, ks, ml, monkeypatch):
+    """The clustered harmonic near field (a U pair of two cluster
+    leaves applied both ways from one read of its sub-block, sums in LDS) against the
+    per-leaf kernel (ANISO_NEAR_CLUSTER=0); odd sz, d = 2 and 3, and a maxLevel-limited
+    tree whose leaves exceed 16 points (clusters off, per-leaf kernel)."""
+    torch = _torch()
+    import aniso_amd
+
+    outs, st = [], []
+    for cl in ("1", "0"):
+        monkeypatch.setenv("ANISO_NEAR_CLUSTER", cl)
+        a = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, ml)
+        xy = a.getNodes()
+        a.setCoeff(*rough_coeffs(xy, 3))
+        for m in range(2 * ks - 1):
+            a.cache(m)
+        st.append(a.stats())
+        U = torch.tensor(np.random.default_rng(7).uniform(-1, 1, (ks, a.N)), device="cuda")
+        out = torch.zeros_like(U)
+        a.block_op_dev(2, U, out)
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy())
+    assert st[0]["harmonic"] == 1 and st[1]["near_clusters"] == 0
+    if st[0]["max_leaf"] <= 16:
+        assert st[0]["near_clusters"] > 0 and st[0]["near_dual_pairs"] > 0
+    else:
+        assert st[0]["near_clusters"] == 0
+    assert _rel(outs[0], outs[1]) <= 1e-13
