@@ -30,7 +30,7 @@
 namespace aniso {
 
 #ifdef ANISO_PROBE  // development build only (make probe): phase stamps of task 0..kProbeWG-1
-constexpr int kProbeWG = 2048;
+constexpr int kProbeWG = 8192;
 __device__ unsigned long long g_probe[2][kProbeWG][8];
 #define ANISO_STAMP(Q, W, I)                                                       \
     do {                                                                            \

@@ -266,9 +266,11 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         tierRootLevel.clear();
         tierBottomLevel.clear();
         if (D >= 1) {
-            tierRootLevel.push_back(std::max(1, D - 3));
+            int bspan = 3;  // levels of the bottom tier (3: 4x the tasks at 1/4 the LDS; down 0.124 -> 0.090 ms, r01g); ANISO_BOTTOM_SPAN (1..4): experiments
+            if (const char* e = std::getenv("ANISO_BOTTOM_SPAN")) bspan = std::max(1, std::min(4, std::atoi(e)));
+            tierRootLevel.push_back(std::max(1, D - (bspan - 1)));
             tierBottomLevel.push_back(D);
-            int span = 4;  // levels per upper tier; ANISO_TOP_SPAN (1..4): tuning/experiments only
+            int span = 2;  // levels per upper tier; ANISO_TOP_SPAN (1..4): experiments
             if (const char* e = std::getenv("ANISO_TOP_SPAN")) span = std::max(1, std::min(4, std::atoi(e)));
             while (tierRootLevel.back() > 1) {
                 tierBottomLevel.push_back(tierRootLevel.back() - 1);
