@@ -625,3 +625,45 @@ def test_harmonic_near_clusters_match_per_leaf_groups(sz, d, ks, ml, monkeypatch
     else:
         assert st[0]["near_clusters"] == 0
     assert _rel(outs[0], outs[1]) <= 1e-13
+
+
+def test_block_matvec_eight_shards_at_config3_size():
+    """The driver's 8-GPU bench path at full size, on one GPU: BASELINE's 1M-point
+    block matvec (config 3) sharded by FMM subtree over 8 ranks (each rank: its own
+    handle, tree-order input, owned slice out, assembled through the bench's
+    all-gather index) equals the unsharded matvec."""
+    torch = _torch()
+    import aniso_amd
+    from aniso_amd import dist as adist
+
+    sz, d, ks, g = 1024, 1, 5, 0.8
+    full = aniso_amd.Aniso(sz, d, ks, g, 10, 4, 20)
+    xy = full.getNodes()
+    coef = rough_coeffs(xy, 9)
+    full.setCoeff(*coef)
+    for m in range(2 * ks - 1):
+        full.cache(m)
+    perm = torch.tensor(full.tree_perm(), device="cuda", dtype=torch.int64)
+    U = torch.tensor(np.random.default_rng(11).uniform(-1, 1, (ks, full.N)), device="cuda")[:, perm].contiguous()
+    ref = torch.zeros_like(U)
+    full.block_op_dev(2, U, ref, tree=True)
+    torch.cuda.synchronize()
+    world = 8
+    ranges = adist.shard_ranges(full, world)
+    del full
+    L = adist.pad_len(ranges)
+    gathered = torch.zeros(world, ks, L, dtype=torch.float64, device="cuda")
+    for r in range(world):
+        sh = aniso_amd.Aniso(sz, d, ks, g, 10, 4, 20)
+        sh.set_shard(r, world)
+        sh.setCoeff(*coef)
+        for m in range(2 * ks - 1):
+            sh.cache(m)
+        b, e = sh.shard()
+        assert (b, e) == ranges[r]
+        sh.block_op_dev(2, U, gathered[r], tree=True)
+        torch.cuda.synchronize()
+        del sh
+    gidx = torch.tensor(adist.block_gather_index(ranges, L, ks), device="cuda")
+    got = torch.index_select(gathered.view(-1), 0, gidx).view(ks, -1)
+    assert float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref)) <= 1e-13
