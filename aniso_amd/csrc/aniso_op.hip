@@ -79,6 +79,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_HARMONIC")) useAtt = useAtt && e[0] != '0';
     if (const char* e = std::getenv("ANISO_HM_CLUSTER")) useClusters = e[0] != '0';
     if (const char* e = std::getenv("ANISO_OVERLAP")) overlap = std::atoi(e);
+    if (const char* e = std::getenv("ANISO_EARLY_M2L")) earlyM2L = e[0] != '0';
     if (const char* e = std::getenv("ANISO_NEAR_CLUSTER")) useNearClusters = e[0] != '0';
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
@@ -92,6 +93,9 @@ Operator::~Operator() {
         if (evFork) (void)hipEventDestroy(evFork);
         if (evJoin) (void)hipEventDestroy(evJoin);
         if (side) (void)hipStreamDestroy(side);
+        if (evTier0) (void)hipEventDestroy(evTier0);
+        if (evJoin2) (void)hipEventDestroy(evJoin2);
+        if (side2) (void)hipStreamDestroy(side2);
         if (own) (void)hipStreamDestroy(own);
     }
 }
@@ -127,6 +131,9 @@ void Operator::ensureDevice() {
         HIP_CHECK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, e && e[0] == '1' ? hi : lo));
     }
     HIP_CHECK(hipEventCreateWithFlags(&evFork, hipEventDisableTiming));
+    HIP_CHECK(hipStreamCreateWithFlags(&side2, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&evTier0, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&evJoin2, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
     // tree-order coordinates
     std::vector<double> pxT(geo.N), pyT(geo.N);
@@ -644,6 +651,9 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     // the harmonic block apply forks its near field off as soon as the charges are
     // complete: after the last up tier with a P2M leaf (the tiers above only M2M)
     const bool fork = harmonic && overlap;
+    // and, when the clustered M2L has "early" clusters, starts
+    // them on a second side stream right after up tier 0
+    const bool split = fork && useClusters && earlyM2L && (mask & kStageFar) && plan.hmEarly > 0;
     if (fork && plan.upTierTask.size() < 2) HIP_CHECK(hipEventRecord(evFork, s));
     for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k) {
         launch_up_tier(K, plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask,
@@ -652,6 +662,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                        treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(), dCT.as<double>(), P,
                        dMult.as<double>(), s);
         if (fork && (int)k == plan.upLastLeafTier) HIP_CHECK(hipEventRecord(evFork, s));
+        if (split && k == 0) HIP_CHECK(hipEventRecord(evTier0, s));
     }
     int ep = tm ? mark(s) : -1;
     span(1, e0, ep);
@@ -686,12 +697,31 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             if (!overlap) ep = e2;
             if (overlap) HIP_CHECK(hipEventRecord(evJoin, side));
         };
+        auto m2lClusters = [&](int c0, int c1, hipStream_t st) {
+            launch_m2l_hc(K, c1 - c0, plan.hmMaxCl, dHmClPtr.as<int>() + c0, dHmTgt.as<int>(), dHmPtr.as<int64_t>(),
+                          dHmNDir.as<int>(), dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(),
+                          dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
+                          dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), st);
+        };
+        const int ncl = (int)plan.hmClPtr.size() - 1;
+        int eEarly = -1;
+        if (split) {  // early clusters beside the upper up tiers and the near field
+            HIP_CHECK(hipStreamWaitEvent(side2, evTier0, 0));
+            eEarly = tm ? mark(side2) : -1;
+            m2lClusters(0, plan.hmEarly, side2);
+            HIP_CHECK(hipEventRecord(evJoin2, side2));
+        }
         auto farStage = [&] {
+            if (split) {
+                m2lClusters(plan.hmEarly, ncl, s);
+                HIP_CHECK(hipStreamWaitEvent(s, evJoin2, 0));
+                e = tm ? mark(s) : -1;
+                span(2, eEarly, e);  // both launches
+                ep = e;
+                return;
+            }
             if ((mask & kStageFar) && useClusters)
-                launch_m2l_hc(K, (int)plan.hmClPtr.size() - 1, plan.hmMaxCl, dHmClPtr.as<int>(), dHmTgt.as<int>(),
-                              dHmPtr.as<int64_t>(), dHmNDir.as<int>(), dHmSrc.as<int>(), dHmBlk.as<int>(),
-                              dHmSlot.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(),
-                              dNrx.as<double>(), dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
+                m2lClusters(0, ncl, s);
             else if (mask & kStageFar)
                 launch_m2l_hm(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dAttPtr.as<int64_t>(), dAttSrc.as<int>(),
                               dAttBlk.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(),

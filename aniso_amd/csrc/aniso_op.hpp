@@ -148,6 +148,10 @@ private:
     // the M2L (both HBM-bound, neither saturates alone)
     hipStream_t side = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr;
+    // second side stream: the early M2L clusters after up tier 0
+    hipStream_t side2 = nullptr;
+    hipEvent_t evTier0 = nullptr, evJoin2 = nullptr;
+    bool earlyM2L = false;  // measured slower (611 vs 620 block matvec/s): ANISO_EARLY_M2L=1
     int overlap = 1;
     // stage timing: events recorded in-stream, (stage, start, end) spans per apply
     std::vector<hipEvent_t> evPool;

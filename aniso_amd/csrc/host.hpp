@@ -108,6 +108,7 @@ struct Plan {
     std::vector<int> hmClPtr, hmTgt, hmSrc, hmBlk, hmSlot, hmNDir;
     std::vector<int64_t> hmPtr;
     int hmMaxCl = 0;
+    int hmEarly = 0;  // clusters [0, hmEarly) need only up tier 0's multipoles (§3.13)
     int64_t hmDual = 0;
     // near field in clusters, block handles with leaves <= 16
     // points: cluster c = leaves ncLeaf[ncPtr[c] .. ncPtr[c+1]) (same level, one

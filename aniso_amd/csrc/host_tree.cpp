@@ -653,6 +653,22 @@ void Plan::buildClusters(const Tree& t) {
         for (int k = 0; k < depth && t.parent[a] != -1; ++k) a = t.parent[a];
         key[w] = ((int64_t)t.level[m2lTgt[w]] << 32) | (uint32_t)a;
     }
+    // "early" clusters first: every target and every source at or
+    // below the bottom up tier's root level, so their multipoles are final after
+    // up tier 0 and the cluster can run while the upper tiers climb
+    const int root0 = tierRootLevel.empty() ? (1 << 30) : tierRootLevel[0];
+    std::unordered_map<int64_t, bool> clusterEarly;
+    for (int w = 0; w < nt; ++w) {
+        bool early = t.level[m2lTgt[w]] >= root0;
+        for (int64_t e = attPtr[w]; e < attPtr[w + 1] && early; ++e) early = t.level[attSrc[e]] >= root0;
+        auto it = clusterEarly.find(key[w]);
+        if (it == clusterEarly.end())
+            clusterEarly[key[w]] = early;
+        else
+            it->second = it->second && early;
+    }
+    for (int w = 0; w < nt; ++w)
+        if (!clusterEarly[key[w]]) key[w] |= (int64_t)1 << 62;
     std::vector<int> order(nt);
     for (int w = 0; w < nt; ++w) order[w] = w;
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
@@ -669,7 +685,11 @@ void Plan::buildClusters(const Tree& t) {
         hmTgt.push_back(n);
     }
     hmClPtr.push_back(nt);
-    for (size_t c = 0; c + 1 < hmClPtr.size(); ++c) hmMaxCl = std::max(hmMaxCl, hmClPtr[c + 1] - hmClPtr[c]);
+    hmEarly = 0;
+    for (size_t c = 0; c + 1 < hmClPtr.size(); ++c) {
+        hmMaxCl = std::max(hmMaxCl, hmClPtr[c + 1] - hmClPtr[c]);
+        if (!(key[order[hmClPtr[c]]] >> 62)) hmEarly = (int)c + 1;
+    }
     hmNDir.clear();
     std::vector<int> dSrc, dBlk, dSlot;
     for (int k = 0; k < nt; ++k) {
