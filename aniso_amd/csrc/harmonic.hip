@@ -828,8 +828,10 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, 
                    const double* nrx, const double* nry, const Params* P, const HarmWeights& hw, const double* mult,
                    double* local, hipStream_t s) {
     if (ncl <= 0) return;
-    constexpr int NT = 256;  // 4 waves per cluster (512 / 768 measured slower, r01f)
-    const size_t shm = (size_t)(maxCl + NT / kWave) * kRank * K * sizeof(double);
+    // 4 waves per cluster of <= 64 targets (512 / 768 measured slower, r01f); 8 for
+    // larger clusters (ANISO_HM_CL128)
+    const int nt = maxCl > 64 ? 512 : 256;
+    const size_t shm = (size_t)(maxCl + nt / kWave) * kRank * K * sizeof(double);
     if (shm > 160 * 1024) throw std::invalid_argument("harmonic M2L cluster exceeds the LDS");
     // ANISO_HM_VAR bit 3: software-pipelined block streams (PF); bit 4: 2 waves per
     // SIMD instead of 3; bit 5: two Newton steps (default one: ~1e-13 per entry)
@@ -838,12 +840,18 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, 
     ANISO_HM_DISPATCH_K(K, (run_m2l_hc<KK, NR, NT, PF, WPE>(ncl, shm, clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, \
                                                              ncy, nrx, nry, P, hw, mult, local, s)))
     const bool pf = (v >> 3) & 1, w2 = (v >> 4) & 1, nr2 = (v >> 5) & 1;
-    if (nr2) {
-        ANISO_HC(2, false, 3);
-    } else if (pf) {
-        if (w2) { ANISO_HC(1, true, 2); } else { ANISO_HC(1, true, 3); }
+    if (nt == 512) {
+        constexpr int NT = 512;
+        ANISO_HC(1, false, 2);
     } else {
-        if (w2) { ANISO_HC(1, false, 2); } else { ANISO_HC(1, false, 3); }
+        constexpr int NT = 256;
+        if (nr2) {
+            ANISO_HC(2, false, 3);
+        } else if (pf) {
+            if (w2) { ANISO_HC(1, true, 2); } else { ANISO_HC(1, true, 3); }
+        } else {
+            if (w2) { ANISO_HC(1, false, 2); } else { ANISO_HC(1, false, 3); }
+        }
     }
 #undef ANISO_HC
     HIP_LAUNCH_CHECK();

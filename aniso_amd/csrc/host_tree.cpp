@@ -647,11 +647,22 @@ void Plan::buildClusters(const Tree& t) {
     int depth = kClusterDepth;
     if (const char* e = std::getenv("ANISO_HM_CLDEPTH"))  // tuning/experiments only (1..kClusterDepth)
         depth = std::max(1, std::min(kClusterDepth, std::atoi(e)));
+    // ANISO_HM_CL128=1 (experiment): half of the 256 targets under one ancestor 4
+    // levels up (the depth-3 subtrees of child quadrants {0,1} or {2,3}): 128 targets
+    const char* c128 = std::getenv("ANISO_HM_CL128");
+    const bool half = c128 && c128[0] == '1';
     std::vector<int64_t> key(nt);
     for (int w = 0; w < nt; ++w) {
         int a = m2lTgt[w];
         for (int k = 0; k < depth && t.parent[a] != -1; ++k) a = t.parent[a];
-        key[w] = ((int64_t)t.level[m2lTgt[w]] << 32) | (uint32_t)a;
+        int64_t h = 0;
+        if (half && t.parent[a] != -1) {
+            const int p = t.parent[a];
+            for (int q = 0; q < 4; ++q)
+                if (t.child[p][q] == a) h = q >> 1;
+            a = p;
+        }
+        key[w] = ((int64_t)t.level[m2lTgt[w]] << 36) | (h << 32) | (uint32_t)a;
     }
     // "early" clusters first: every target and every source at or
     // below the bottom up tier's root level, so their multipoles are final after
