@@ -80,6 +80,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_HM_CLUSTER")) useClusters = e[0] != '0';
     if (const char* e = std::getenv("ANISO_OVERLAP")) overlap = std::atoi(e);
     if (const char* e = std::getenv("ANISO_EARLY_M2L")) earlyM2L = e[0] != '0';
+    if (const char* e = std::getenv("ANISO_FUSE_SUB")) fuseSub = e[0] != '0';
     if (const char* e = std::getenv("ANISO_NEAR_CLUSTER")) useNearClusters = e[0] != '0';
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
@@ -788,7 +789,8 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                          dDnGrpFix.as<int>(), dDnNode.as<int4>(), dLocal.as<double>(), P, dDnLeafSlot.as<int>(),
                          dDnLeafPts.as<int>(), dDnLeafNear.as<int2>(), dDnLeafGeom.as<double4>(), dPxT.as<double>(),
                          dPyT.as<double>(), operm, obase, ldo, dDnNearOff.as<int>(), plan.dnMaxNear,
-                         dNearPart.as<double>(), dDnChain.as<int2>(), plan.dnMaxChain, mask, scale, out, s);
+                         dNearPart.as<double>(), dDnChain.as<int2>(), plan.dnMaxChain, mask, scale, out, subX, subLd,
+                         s);
     if (tm) {
         const int e = mark(s);
         span(5, ep, e);
@@ -829,9 +831,23 @@ void Operator::blockOpDev(int which, const double* x, int64_t ldx, double* out, 
     // x - mforward(x) on the owned targets (aniso.m:155)
     const int64_t nOut = treeIo ? plan.ownEnd - plan.ownBegin : geo.N;
     if (!treeIo && plan.nranks != 1) throw std::logic_error("block matvec in original order on a sharded handle: use tree order");
+    const double* xo = x + (treeIo ? plan.ownBegin : 0);  // x at the output positions
+    if (fuseSub && rhs_supported(nb) && !plan.dnDesc.empty()) {
+        // the down pass, last writer of every owned point, stores x - (near + corr + far)
+        subX = xo;
+        subLd = ldx;
+        try {
+            applyBlockDev(nb, x, ldx, treeIo, true, nm, ids.data(), mix.data(), out, ldo, treeIo, s);
+        } catch (...) {
+            subX = nullptr;
+            throw;
+        }
+        subX = nullptr;
+        return;
+    }
     dBlk.alloc((size_t)nb * nOut * sizeof(double));
     applyBlockDev(nb, x, ldx, treeIo, true, nm, ids.data(), mix.data(), dBlk.as<double>(), nOut, treeIo, s);
-    launch_sub_slice(nOut, nb, x + (treeIo ? plan.ownBegin : 0), ldx, dBlk.as<double>(), nOut, out, ldo, s);
+    launch_sub_slice(nOut, nb, xo, ldx, dBlk.as<double>(), nOut, out, ldo, s);
 }
 
 void Operator::setTiming(bool on) {

@@ -151,7 +151,11 @@ private:
     // second side stream: the early M2L clusters after up tier 0
     hipStream_t side2 = nullptr;
     hipEvent_t evTier0 = nullptr, evJoin2 = nullptr;
-    bool earlyM2L = false;  // measured slower (611 vs 620 block matvec/s): ANISO_EARLY_M2L=1
+    bool earlyM2L = false;
+    // x - mforward(x) fused into the down pass (blockOpDev sets subX for one apply)
+    bool fuseSub = true;
+    const double* subX = nullptr;
+    int64_t subLd = 0;  // measured slower (611 vs 620 block matvec/s): ANISO_EARLY_M2L=1
     int overlap = 1;
     // stage timing: events recorded in-stream, (stage, start, end) spans per apply
     std::vector<hipEvent_t> evPool;

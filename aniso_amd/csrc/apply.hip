@@ -878,7 +878,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     const double4* __restrict__ leafGeom, const double* __restrict__ pxT, const double* __restrict__ pyT,
     const int* __restrict__ operm, int64_t obase, int64_t ldo, const int* __restrict__ nearOff, int maxNear,
     const double* __restrict__ nearPart, const int2* __restrict__ chain, int maxChain, int flags, double scale,
-    double* __restrict__ out) {
+    double* __restrict__ out, const double* __restrict__ xsub, int64_t ldx) {
     constexpr int RK = kRank * K;
     extern __shared__ double sm[];
     int4* DN = reinterpret_cast<int4*>(sm);                // maxTask node records
@@ -1029,8 +1029,14 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             for (int i = 0; i < K; ++i) v[i] += l2p[i];
         }
         const int64_t o = out_index(operm, obase, kpos);
+        if (xsub) {  // aniso.m's x - mforward(x) fused into the last writer (aniso.m:155)
 #pragma unroll
-        for (int i = 0; i < K; ++i) out[(size_t)i * ldo + o] += scale * v[i];
+            for (int i = 0; i < K; ++i)
+                out[(size_t)i * ldo + o] = xsub[(size_t)i * ldx + o] - (out[(size_t)i * ldo + o] + scale * v[i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i) out[(size_t)i * ldo + o] += scale * v[i];
+        }
     }
     ANISO_STAMP(1, task, 4);
 }
@@ -1271,13 +1277,13 @@ void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* 
                       const int2* leafNear, const double4* leafGeom, const double* pxT, const double* pyT,
                       const int* operm, int64_t obase, int64_t ldo, const int* nearOff, int maxNear,
                       const double* nearPart, const int2* chain, int maxChain, int flags, double scale, double* out,
-                      hipStream_t s) {
+                      const double* xsub, int64_t ldx, hipStream_t s) {
     if (ntask <= 0) return;
     const size_t shm = down_tier_lds(maxTask, maxLeaves, maxNear, maxChain, K);
     ANISO_DISPATCH_K(K, (k_down_tier<KK><<<ntask, kTierThreads, shm, s>>>(
                             maxTask, maxLeaves, desc, grpFix, dn, local, P, leafSlot, leafBegin, leafNear, leafGeom,
                             pxT, pyT, operm, obase, ldo, nearOff, maxNear, nearPart, chain, maxChain, flags, scale,
-                            out)));
+                            out, xsub, ldx)));
     HIP_LAUNCH_CHECK();
 }
 

@@ -105,6 +105,7 @@ void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* 
                       const int2* leafNear, const double4* leafGeom, const double* pxT, const double* pyT,
                       const int* operm, int64_t obase, int64_t ldo, const int* nearOff, int maxNear,
                       const double* nearPart, const int2* chain, int maxChain, int flags, double scale, double* out,
+                      const double* xsub, int64_t ldx,
                       hipStream_t s);
 // corrections of all terms in one launch, added to out: Wc / Wm the terms'
 // stencil and singular tables folded with their mixes (Operator::corrTable)
