@@ -243,36 +243,34 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
     }
     __syncthreads();
     ANISO_STAMP(0, task, 2);
+    // M2M (bbfmm.h:855-859), one item per (node, row r, child q): 4x the items of a
+    // per-(node, row) loop, so a level's child reads (LDS, or HBM for the roots of
+    // the tier below) are all in flight at once; the 4 child partials of a row are
+    // adjacent lanes, summed by a DPP quad reduction in a fixed order.
     for (int g = 0; g < ngrp; ++g) {
         const int s0 = gs[g], s1 = gs[g + 1];
-        for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
-            const int k = s0 + (it >> 4), r = it & (kRank - 1);
+        for (int it = threadIdx.x; it < (s1 - s0) * kRank * 4; it += blockDim.x) {
+            const int k = s0 + (it >> 6), r = (it >> 2) & (kRank - 1), q = it & 3;
             const int4 c = CD[k];
-            if (c.x == kLeafCode) continue;  // P2M above
+            const int cq = q == 0 ? c.x : q == 1 ? c.y : q == 2 ? c.z : c.w;
             double acc[K];
 #pragma unroll
             for (int b = 0; b < K; ++b) acc[b] = 0.0;
-            const int cs[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (cs[q] == -1) continue;
+            if (c.x != kLeafCode && cq != -1) {
                 const double* R = Rl + q * kRank * kRank + r;  // transposed: R[rr * 16 + r]
-                if (cs[q] >= 0) {  // child in this task (LDS)
-                    const double* cm = M + (size_t)cs[q] * kRank * K;
+                const double* cm = cq >= 0 ? M + (size_t)cq * kRank * K             // child in this task (LDS)
+                                           : mult + (size_t)(-cq - 2) * kRank * K;  // root of the tier below
 #pragma unroll
-                    for (int rr = 0; rr < kRank; ++rr)
+                for (int rr = 0; rr < kRank; ++rr)
 #pragma unroll
-                        for (int b = 0; b < K; ++b) acc[b] += R[rr * kRank] * cm[rr * K + b];
-                } else {  // root of the tier below (HBM)
-                    const double* cm = mult + (size_t)(-cs[q] - 2) * kRank * K;
-#pragma unroll
-                    for (int rr = 0; rr < kRank; ++rr)
-#pragma unroll
-                        for (int b = 0; b < K; ++b) acc[b] += R[rr * kRank] * cm[rr * K + b];
-                }
+                    for (int b = 0; b < K; ++b) acc[b] += R[rr * kRank] * cm[rr * K + b];
             }
 #pragma unroll
-            for (int b = 0; b < K; ++b) M[((size_t)k * kRank + r) * K + b] = acc[b];
+            for (int b = 0; b < K; ++b) acc[b] = quad_sum(acc[b]);
+            if (q == 0 && c.x != kLeafCode) {  // leaves: P2M above
+#pragma unroll
+                for (int b = 0; b < K; ++b) M[((size_t)k * kRank + r) * K + b] = acc[b];
+            }
         }
         __syncthreads();
     }
