@@ -501,7 +501,7 @@ k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64
 // 4rq..4rq+3 for its columns, U columns in flight; the sources' points and charges
 // are read straight from pxT / pyT / fT (the lanes of a column share the lines).
 // out (stored, not added) = scale * (sum over sources + the mode-0 diagonal).
-template <int K, int G, int U, int NR>
+template <int K, int G, int U, int NR, bool XCD = false>
 __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict__ leafInfo,
                                                  const int64_t* __restrict__ nearPtsPtr,
                                                  const int* __restrict__ nearPts, const int64_t* __restrict__ nearKOff,
@@ -513,7 +513,8 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
     static_assert(G == 16 || G == 64, "leaf group of 16 or 64 lanes");
     constexpr int KS = kStride<K>;
     const int gl = threadIdx.x & (G - 1);
-    const int li = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
+    const int bid = XCD ? xcd_tile((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;  // XCD: contiguous leaves per L2
+    const int li = (int)(((int64_t)bid * blockDim.x + threadIdx.x) / G);
     const bool active = li < nl;
     int4 info = make_int4(0, 0, 0, 0);
     int64_t pb = 0, koff = 0;
@@ -866,8 +867,23 @@ void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
     ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, G, 4, NR><<<blocks_for((int64_t)nl * G, 256), 256, 0, s>>>(          \
                                nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm, \
                                obase, ldo, flags, scale, out)))
+#define ANISO_NEAR_HMV(UU, XX)                                                                                  \
+    ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, 16, UU, 2, XX><<<blocks_for((int64_t)nl * 16, 256), 256, 0, s>>>(       \
+                               nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm, \
+                               obase, ldo, flags, scale, out)))
     const bool nr1 = (hm_var() & 2) != 0;
-    if (maxLeaf <= 16) {  // 4 leaves per wave
+    static const int nv = [] {  // ANISO_NEAR_VAR (experiments): 1 U = 2, 2 U = 8, 3 XCD order, 4 U = 8 + XCD order
+        const char* e = std::getenv("ANISO_NEAR_VAR");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (maxLeaf <= 16 && !nr1 && nv > 0) {
+        switch (nv) {
+            case 1: ANISO_NEAR_HMV(2, false); break;
+            case 2: ANISO_NEAR_HMV(8, false); break;
+            case 3: ANISO_NEAR_HMV(4, true); break;
+            default: ANISO_NEAR_HMV(8, true); break;
+        }
+    } else if (maxLeaf <= 16) {  // 4 leaves per wave
         if (nr1) {
             ANISO_NEAR_HM(16, 1);
         } else {
@@ -880,6 +896,7 @@ void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
             ANISO_NEAR_HM(64, 2);
         }
     }
+#undef ANISO_NEAR_HMV
 #undef ANISO_NEAR_HM
     HIP_LAUNCH_CHECK();
 }
