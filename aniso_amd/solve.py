@@ -1,0 +1,177 @@
+"""Multi-right-hand-side, mixed-precision GMRES over the device block apply
+(the a15 caller, main.cpp:121-141 / gmres.cpp:53-169,
+for k right-hand sides at once).
+
+    A(u) = u - K_0(sigma_s .* u)     (main.cpp:125-136 forwardOperator, mode 0)
+
+* The operator runs in fp64 on the MI355X: `Aniso.apply_block_dev` applies K_0 to
+  up to 8 right-hand sides per launch sequence from one read of the cached
+  operators; 16 right-hand sides are two batches.
+* Inner solver: restarted GMRES(m) with the Krylov basis stored in fp32 (modified
+  Gram-Schmidt; dot products accumulated in fp64), Givens rotations per right-hand
+  side on the host, to a loose relative tolerance.
+* Outer loop: iterative refinement in fp64, r = b - A x, x += inner(r), until
+  ||r|| / ||b|| <= tol for every right-hand side.
+
+This is host orchestration over torch tensors (device memory and BLAS-1 plumbing);
+the operator it calls is the HIP path.  The fp32 *caches* of config 5 are not built:
+the operator stays fp64.
+"""
+import numpy as np
+
+MAX_BATCH = 8
+
+
+class MT19937_64:
+    """std::mt19937_64 (the survey's config-5 centre generator)."""
+
+    def __init__(self, seed):
+        self.mt = [0] * 312
+        self.mt[0] = seed & 0xFFFFFFFFFFFFFFFF
+        for i in range(1, 312):
+            p = self.mt[i - 1]
+            self.mt[i] = (6364136223846793005 * (p ^ (p >> 62)) + i) & 0xFFFFFFFFFFFFFFFF
+        self.i = 312
+
+    def _twist(self):
+        mt = self.mt
+        for i in range(312):
+            x = (mt[i] & 0xFFFFFFFF80000000) | (mt[(i + 1) % 312] & 0x7FFFFFFF)
+            xa = x >> 1
+            if x & 1:
+                xa ^= 0xB5026F5AA96619E9
+            mt[i] = mt[(i + 156) % 312] ^ xa
+        self.i = 0
+
+    def __call__(self):
+        if self.i >= 312:
+            self._twist()
+        y = self.mt[self.i]
+        self.i += 1
+        y ^= (y >> 29) & 0x5555555555555555
+        y ^= (y << 17) & 0x71D67FFFEDA60000
+        y ^= (y << 37) & 0xFFF7EEE000000000
+        y ^= y >> 43
+        return y & 0xFFFFFFFFFFFFFFFF
+
+    def uniform(self, a, b):
+        """std::uniform_real_distribution<double>(a, b) as libstdc++ draws it from a
+        64-bit engine: one draw, generate_canonical = double(g()) / 2^64."""
+        r = float(self()) / 18446744073709551616.0
+        if r >= 1.0:
+            r = np.nextafter(1.0, 0.0)
+        return a + (b - a) * r
+
+
+def config5_charges(xy, k, width=25.0):
+    """q_k = exp(-width |x - c_k|^2), c_k uniform in [0.2, 0.8]^2 from mt19937_64(seed=k)."""
+    g = MT19937_64(k)
+    cx = g.uniform(0.2, 0.8)
+    cy = g.uniform(0.2, 0.8)
+    return np.exp(-width * ((xy[:, 0] - cx) ** 2 + (xy[:, 1] - cy) ** 2))
+
+
+def forward_block(op, X, Y):
+    """Y = X - K_0(sigma_s .* X) for the rows of X (fp64 device tensors), <= 8 per apply."""
+    for b0 in range(0, X.shape[0], MAX_BATCH):
+        xs, ys = X[b0:b0 + MAX_BATCH], Y[b0:b0 + MAX_BATCH]
+        k = xs.shape[0]
+        op.apply_block_dev(xs, [0], np.eye(k)[None], ys, use_sigma=True)
+        ys.neg_().add_(xs)
+
+
+def rhs_block(op, Q):
+    """rhs_k = K_0 q_k (main.cpp:121-124: the right-hand side is the mapping of q)."""
+    import torch
+
+    R = torch.empty_like(Q)
+    for b0 in range(0, Q.shape[0], MAX_BATCH):
+        qs = Q[b0:b0 + MAX_BATCH]
+        op.apply_block_dev(qs, [0], np.eye(qs.shape[0])[None], R[b0:b0 + MAX_BATCH], use_sigma=False)
+    return R
+
+
+def _inner_gmres(op, R, m, tol, max_cycles):
+    """Approximately solve A D = R (rows independent) with an fp32 Krylov basis."""
+    import torch
+
+    k, n = R.shape
+    D = torch.zeros_like(R)
+    r0 = torch.linalg.norm(R, dim=1).cpu().numpy()
+    W = torch.empty_like(R)
+    its = 0
+    for _ in range(max_cycles):
+        Rc = R.clone()
+        if its:
+            forward_block(op, D, W)
+            Rc -= W
+        beta = torch.linalg.norm(Rc, dim=1).cpu().numpy()
+        done = beta <= tol * r0
+        if done.all():
+            break
+        V = torch.zeros(m + 1, k, n, dtype=torch.float32, device=R.device)
+        V[0] = (Rc / torch.tensor(np.where(beta > 0, beta, 1.0), device=R.device)[:, None]).float()
+        H = np.zeros((k, m + 1, m))
+        cs, sn = np.zeros((k, m)), np.zeros((k, m))
+        g = np.zeros((k, m + 1))
+        g[:, 0] = beta
+        j_used = 0
+        for j in range(m):
+            forward_block(op, V[j].double(), W)
+            w = W
+            for i in range(j + 1):  # modified Gram-Schmidt, fp64 accumulation of fp32 vectors
+                h = (V[i].double() * w).sum(1)
+                w = w - h[:, None] * V[i].double()
+                H[:, i, j] = h.cpu().numpy()
+            hn = torch.linalg.norm(w, dim=1)
+            H[:, j + 1, j] = hn.cpu().numpy()
+            V[j + 1] = (w / torch.where(hn > 0, hn, torch.ones_like(hn))[:, None]).float()
+            for r in range(k):  # Givens (gmres.cpp:120-150) per right-hand side
+                for i in range(j):
+                    t = cs[r, i] * H[r, i, j] + sn[r, i] * H[r, i + 1, j]
+                    H[r, i + 1, j] = -sn[r, i] * H[r, i, j] + cs[r, i] * H[r, i + 1, j]
+                    H[r, i, j] = t
+                a, b = H[r, j, j], H[r, j + 1, j]
+                den = np.hypot(a, b)
+                cs[r, j], sn[r, j] = (1.0, 0.0) if den == 0 else (a / den, b / den)
+                H[r, j, j] = cs[r, j] * a + sn[r, j] * b
+                H[r, j + 1, j] = 0.0
+                g[r, j + 1] = -sn[r, j] * g[r, j]
+                g[r, j] = cs[r, j] * g[r, j]
+            its += 1
+            j_used = j + 1
+            if (np.abs(g[:, j + 1]) <= tol * r0).all():
+                break
+        Y = np.zeros((k, j_used))
+        for r in range(k):
+            if done[r]:
+                continue
+            Hr = np.triu(H[r, :j_used, :j_used])
+            try:
+                Y[r] = np.linalg.solve(Hr, g[r, :j_used])
+            except np.linalg.LinAlgError:  # breakdown: least squares on the rotated system
+                Y[r] = np.linalg.lstsq(Hr, g[r, :j_used], rcond=None)[0]
+        Yt = torch.tensor(Y, device=R.device)
+        D += torch.einsum("kj,jkn->kn", Yt, V[:j_used].double())
+    return D, its
+
+
+def gmres_mixed(op, B, tol=1e-12, m=40, inner_tol=1e-6, max_outer=30, max_cycles=20):
+    """Solve A X = B (rows) to ||B - A X|| / ||B|| <= tol per row.  Returns
+    (X, outer iterations, inner iterations, final relative residuals)."""
+    import torch
+
+    X = torch.zeros_like(B)
+    W = torch.empty_like(B)
+    bn = torch.linalg.norm(B, dim=1)
+    inner = 0
+    for outer in range(max_outer + 1):
+        forward_block(op, X, W)
+        R = B - W
+        rel = (torch.linalg.norm(R, dim=1) / bn).cpu().numpy()
+        if (rel <= tol).all() or outer == max_outer:
+            return X, outer, inner, rel
+        D, its = _inner_gmres(op, R, m, inner_tol, max_cycles)
+        inner += its
+        X += D
+    return X, max_outer, inner, rel

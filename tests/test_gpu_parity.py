@@ -667,3 +667,31 @@ def test_block_matvec_eight_shards_at_config3_size():
     gidx = torch.tensor(adist.block_gather_index(ranges, L, ks), device="cuda")
     got = torch.index_select(gathered.view(-1), 0, gidx).view(ks, -1)
     assert float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref)) <= 1e-13
+
+
+@pytest.mark.parametrize("sz", [256, 1024])
+def test_config5_mixed_precision_16_rhs_matches_fp64_gmres(sz):
+    """the config-3 geometry (sz = 1024 is the full 1M
+    points), mode 0, 16 right-hand sides q_k (Gaussian bumps centred by
+    mt19937_64(seed = k)), solved with an fp32 Krylov basis and fp64 refinement over
+    the batched device apply (8 right-hand sides per apply); each solution matches the
+    fp64 single-RHS device GMRES (main.cpp:121-141) to 1e-10."""
+    torch = _torch()
+    import aniso_amd
+    from aniso_amd.solve import config5_charges, gmres_mixed, rhs_block
+
+    a = aniso_amd.Aniso(sz, 1, 1, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    a.setCoeff(*main_coeffs(xy))
+    a.cache(0)
+    k = 16
+    Q = np.stack([config5_charges(xy, s) for s in range(k)])
+    B = rhs_block(a, torch.tensor(Q, device="cuda"))
+    X, outer, inner, rel = gmres_mixed(a, B, tol=1e-12, m=40, inner_tol=1e-6)
+    torch.cuda.synchronize()
+    assert (rel <= 1e-12).all() and outer >= 2
+    Xh = X.cpu().numpy()
+    for s in (0, 7, 15):  # fp64 reference solves (the C ABI's device GMRES)
+        its, x, hist, fr = a.gmres(Q[s], m=80, maxit=400, tol=1e-12)
+        assert its > 0
+        assert _rel(Xh[s], x) <= 1e-10, (s, _rel(Xh[s], x))
