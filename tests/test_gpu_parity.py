@@ -695,3 +695,62 @@ def test_config5_mixed_precision_16_rhs_matches_fp64_gmres(sz):
         its, x, hist, fr = a.gmres(Q[s], m=80, maxit=400, tol=1e-12)
         assert its > 0
         assert _rel(Xh[s], x) <= 1e-10, (s, _rel(Xh[s], x))
+
+
+def test_config2_full_size_matches_oracle():
+    """BASELINE configs[1] at its full size (sz = 120, d = 3,
+    ns = 8, maxLevel = 5, N = 129,600, ~127-point leaves): the device apply against the
+    oracle for a random and a Gaussian charge (the oracle's cache takes ~20 s here)."""
+    a, o, xy = _pair(120, 3, 1, 8, 5, "main")
+    a.cache(0)
+    o.cache(0)
+    rng = np.random.default_rng(120)
+    for q in (rng.uniform(-1, 1, a.N), gaussian_charge(xy)):
+        assert _rel(a.mapping(q, 0), o.mapping(q, 0)) <= TOL
+
+
+def test_config4_four_million_points_properties_and_shard():
+    """BASELINE configs[3]'s geometry at full size (sz = 2048,
+    d = 1, ns = 10, N = 4,194,304, mode 0): linearity, bitwise determinism and
+    positivity of the device apply, and one rank of its 8-way subtree sharding
+    reproducing the owned slice of the unsharded tree-order forward operator."""
+    torch = _torch()
+    import aniso_amd
+
+    sz = 2048
+    a = aniso_amd.Aniso(sz, 1, 1, 0.8, 10, 4, 20)
+    assert a.N == 4 * 1024 * 1024
+    xy = a.getNodes()
+    coef = main_coeffs(xy)
+    a.setCoeff(*coef)
+    a.cache(0)
+    rng = np.random.default_rng(4)
+    q1 = torch.tensor(rng.uniform(-1, 1, a.N), device="cuda")
+    q2 = torch.tensor(gaussian_charge(xy), device="cuda")
+    o1, o2, o3, o4 = (torch.zeros_like(q1) for _ in range(4))
+    a.mapping_dev(q1, 0, o1)
+    a.mapping_dev(q2, 0, o2)
+    a.mapping_dev(2.5 * q1 - 0.75 * q2, 0, o3)
+    a.mapping_dev(q1, 0, o4)
+    torch.cuda.synchronize()
+    lin = 2.5 * o1 - 0.75 * o2
+    assert float(torch.linalg.norm(o3 - lin) / torch.linalg.norm(lin)) <= 1e-13
+    assert torch.equal(o1, o4)
+    assert float(o2.min()) > 0
+    perm = torch.tensor(a.tree_perm(), device="cuda", dtype=torch.int64)
+    xt = q1[perm].contiguous()
+    full = torch.zeros_like(xt)
+    a.forward_tree_dev(xt, full)
+    torch.cuda.synchronize()
+    del a
+    r, world = 5, 8
+    sh = aniso_amd.Aniso(sz, 1, 1, 0.8, 10, 4, 20)
+    sh.set_shard(r, world)
+    sh.setCoeff(*coef)
+    sh.cache(0)
+    b, e = sh.shard()
+    part = torch.zeros(e - b, dtype=torch.float64, device="cuda")
+    sh.forward_tree_dev(xt, part)
+    torch.cuda.synchronize()
+    ref = full[b:e]
+    assert float(torch.linalg.norm(part - ref) / torch.linalg.norm(ref)) <= 1e-14
