@@ -125,7 +125,7 @@ __global__ void k_sub_slice(int64_t n, int nrhs, const double* __restrict__ x, i
         _Pragma("unroll") for (int e = 0; e < (NV); ++e) {         \
             const double keep = hi ? acc[e + (NV)] : acc[e];       \
             const double send = hi ? acc[e] : acc[e + (NV)];       \
-            acc[e] = keep + __shfl_xor(send, (OFF));               \
+            acc[e] = keep + xor16_f64<(OFF)>(send, r4);            \
         }                                                          \
     }
 template <int K>
@@ -176,6 +176,7 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
     // apply's input (the reference's charge .* weights, AnisoWrapper.cpp:105-110).
     {
         const int gi = threadIdx.x >> 4, ln = threadIdx.x & 15, ngr = blockDim.x >> 4;
+        const bool r4 = xor16_r4((int)threadIdx.x);  // DPP rotate for the xor-4 step
         for (int k = gi; k < nt; k += ngr) {
             if (CD[k].x != kLeafCode) continue;  // uniform over the 16 lanes
             const double cx = G[4 * k], cy = G[4 * k + 1], irx = G[4 * k + 2], iry = G[4 * k + 3];

@@ -60,6 +60,31 @@ __device__ __forceinline__ double dpp_f64(double v) {
     const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
+// v of lane (lane ^ OFF) within a 16-lane DPP row, OFF in {1, 2, 4, 8}, on the VALU
+// (no LDS permute): quad_perm for 1 and 2, row_ror:8 for 8; for 4 it is row_ror:4
+// on half of the lanes and row_ror:12 on the other half -- r4 (from
+// xor16_r4(lane)) says which, measured from the hardware's own lane ids, so the
+// rotate direction is not assumed.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ bool xor16_r4(int lane) {
+    const int ln = lane & 15;
+    return dpp_i32<0x124>(ln) == (ln ^ 4);
+}
+template <int OFF>
+__device__ __forceinline__ double xor16_f64(double v, bool r4) {
+    if constexpr (OFF == 1) return dpp_f64<0xB1>(v);
+    else if constexpr (OFF == 2) return dpp_f64<0x4E>(v);
+    else if constexpr (OFF == 8) return dpp_f64<0x128>(v);
+    else {
+        static_assert(OFF == 4, "xor16_f64: OFF in {1, 2, 4, 8}");
+        const double a = dpp_f64<0x124>(v), b = dpp_f64<0x12C>(v);
+        return r4 ? a : b;
+    }
+}
+
 __device__ __forceinline__ double quad_sum(double v) {
     v += dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
     v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
