@@ -85,6 +85,26 @@ __device__ __forceinline__ double xor16_f64(double v, bool r4) {
     }
 }
 
+// v(lane) + v(lane ^ 16) and v(lane) + v(lane ^ 32) through gfx950's
+// v_permlane16/32_swap (row exchange on the VALU; the sum of both swap outputs is
+// the pair sum whichever row each output holds).
+__device__ __forceinline__ double xsum16_f64(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    const double a = __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]);
+    const double c = __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
+    return a + c;
+}
+__device__ __forceinline__ double xsum32_f64(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    const double a = __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]);
+    const double c = __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
+    return a + c;
+}
+
 __device__ __forceinline__ double quad_sum(double v) {
     v += dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
     v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]

@@ -470,12 +470,19 @@ k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64
                 }
             }
         }
-#pragma unroll
-        for (int off = 4; off < kWave; off <<= 1)
+        {  // sum over the 16 columns (lane bits 2..5) on the VALU: DPP in-row, permlane swaps across rows
+            const bool r4 = xor16_r4(lane);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int i = 0; i < K; ++i) c[j][i] += __shfl_xor(c[j][i], off);
+                for (int i = 0; i < K; ++i) {
+                    double v = c[j][i];
+                    v += xor16_f64<4>(v, r4);
+                    v += xor16_f64<8>(v, r4);
+                    v = xsum16_f64(v);
+                    c[j][i] = xsum32_f64(v);
+                }
+        }
         const int jr = s & 3, srcLane = 4 * s + (s >> 2);
         double* d = acc + ((size_t)ti * kRank + s) * K;
 #pragma unroll

@@ -1,5 +1,6 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -x -v -m gpu -k "config4_four" --timeout 300 --timeout-method thread --durations=3 > gpurun_out/c4_tests.log 2>&1 || { tail -60 gpurun_out/c4_tests.log; exit 1; }
-grep -E "passed|failed|s call" gpurun_out/c4_tests.log | tail -4
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu -k "harmonic or block or config3 or eight" --timeout 300 --timeout-method thread > gpurun_out/cl_tests.log 2>&1 || { tail -60 gpurun_out/cl_tests.log; exit 1; }
+tail -1 gpurun_out/cl_tests.log
+bash tools/ab_env.sh "ANISO_OVERLAP=1" "ANISO_OVERLAP=0" "ANISO_OVERLAP=1" "ANISO_OVERLAP=0"
