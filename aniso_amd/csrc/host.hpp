@@ -18,6 +18,7 @@ constexpr int kTaskLevels = 7;  // levels per up/down task record (tasks span <=
 constexpr int kMaxCanon = 32;       // canonical (symmetric) M2L pairs per target (k_m2l's register staging)
 constexpr int kMaxCanonBlock = 16;  // the same on block handles (ks > 1; LDS staging at K >= 4)
 constexpr int kClusterDepth = 3;   // harmonic M2L clusters: <= 4^3 = 64 targets
+constexpr int kMinClusters = 512;  // ... but no fewer workgroups than this (shards of N-GPU runs)
 
 // Geometry::Geometry (Geometry.cpp:10-114) + the singular Duffy rule
 // (KernelFactory.cpp:15-16, 863-986).
@@ -108,7 +109,8 @@ struct Plan {
     std::vector<int> hmClPtr, hmTgt, hmSrc, hmBlk, hmSlot, hmNDir;
     std::vector<int64_t> hmPtr;
     int hmMaxCl = 0;
-    int hmEarly = 0;  // clusters [0, hmEarly) need only up tier 0's multipoles (§3.13)
+    int hmEarly = 0;
+    int hmDepth = 0;  // cluster depth chosen (ancestor levels up)  // clusters [0, hmEarly) need only up tier 0's multipoles (§3.13)
     int64_t hmDual = 0;
     // near field in clusters, block handles with leaves <= 16
     // points: cluster c = leaves ncLeaf[ncPtr[c] .. ncPtr[c+1]) (same level, one

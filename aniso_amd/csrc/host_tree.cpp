@@ -644,9 +644,24 @@ void Plan::buildClusters(const Tree& t) {
     // cluster key: (level, ancestor kClusterDepth levels up); targets keep id order
     std::vector<int> widx(t.nn, -1);
     for (int w = 0; w < nt; ++w) widx[m2lTgt[w]] = w;
+    // cluster depth: the deepest (largest clusters, most in-cluster pairs) that still
+    // gives >= kMinClusters workgroups, so a shard of an N-GPU run keeps the chip
+    // busy (1M points, 8 ranks: depth 3 = 174 clusters, M2L 0.31 ms; depth 2 = 685,
+    // 0.17 ms; one rank: depth 3 = 1,367 clusters is best; tools/shard_time.py)
+    auto clusterCount = [&](int dp) {
+        std::unordered_map<int64_t, char> seen;
+        for (int w = 0; w < nt; ++w) {
+            int a = m2lTgt[w];
+            for (int k = 0; k < dp && t.parent[a] != -1; ++k) a = t.parent[a];
+            seen[((int64_t)t.level[m2lTgt[w]] << 32) | (uint32_t)a] = 1;
+        }
+        return (int)seen.size();
+    };
     int depth = kClusterDepth;
+    while (depth > 1 && clusterCount(depth) < kMinClusters) --depth;
     if (const char* e = std::getenv("ANISO_HM_CLDEPTH"))  // tuning/experiments only (1..kClusterDepth)
         depth = std::max(1, std::min(kClusterDepth, std::atoi(e)));
+    hmDepth = depth;
     // ANISO_HM_CL128=1 (experiment): half of the 256 targets under one ancestor 4
     // levels up (the depth-3 subtrees of child quadrants {0,1} or {2,3}): 128 targets
     const char* c128 = std::getenv("ANISO_HM_CL128");

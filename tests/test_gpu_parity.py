@@ -577,6 +577,9 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatc
     import aniso_amd
 
     monkeypatch.setenv("ANISO_SYMMETRIC", sym)
+    # 64-target clusters even at these sizes (the default depth keeps >= 512
+    # clusters, which small trees only reach with 4-target clusters: no in-cluster pairs)
+    monkeypatch.setenv("ANISO_HM_CLDEPTH", "3")
     outs, st = [], []
     for cl in ("1", "0"):
         monkeypatch.setenv("ANISO_HM_CLUSTER", cl)
