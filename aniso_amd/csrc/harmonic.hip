@@ -354,11 +354,14 @@ k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64
          const int* __restrict__ ndir, const int* __restrict__ src, const int* __restrict__ blk,
          const int* __restrict__ slot, const double* __restrict__ E, const double* __restrict__ ncx, const double* __restrict__ ncy,
          const double* __restrict__ nrx, const double* __restrict__ nry, const Params* __restrict__ P,
-         HarmWeights hw, const double* __restrict__ mult, double* __restrict__ local) {
+         HarmWeights hw, const double* __restrict__ mult, double* __restrict__ local, int xcdOrder) {
     constexpr int RK = kRank * K;
     constexpr int PG = 2;
     extern __shared__ double sm[];
-    const int c0 = clPtr[blockIdx.x], nt = clPtr[blockIdx.x + 1] - c0;
+    // XCD (ANISO_HM_VAR bit 6): each XCD takes a contiguous range of clusters, so
+    // spatial neighbours share source multipoles and cross-cluster blocks in one L2
+    const int cid = xcdOrder ? xcd_tile((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int c0 = clPtr[cid], nt = clPtr[cid + 1] - c0;
     const int nw = (int)(blockDim.x / kWave);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
     double* acc = sm;                                    // nt x 16 x K: the cluster's locals
@@ -828,7 +831,8 @@ static void run_m2l_hc(int ncl, size_t shm, const int* clPtr, const int* tgt, co
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
         if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
     }
-    f<<<ncl, NT, shm, s>>>(clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry, P, hw, mult, local);
+    f<<<ncl, NT, shm, s>>>(clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry, P, hw, mult, local,
+                           (hm_var() >> 6) & 1);
 }
 
 void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, const int64_t* ptr, const int* ndir,
