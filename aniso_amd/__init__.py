@@ -74,6 +74,9 @@ def lib():
             "aniso_apply_block_dev": [P, I, P, I64, I, I, ip, dp, P, I64, I, P],
             "aniso_block_op_dev": [P, I, P, I64, P, I64, I, P],
             "aniso_block_mixes": [I, D, I, dp],
+            "aniso_block_op": [P, I, dp, dp],
+            "aniso_apply_block": [P, dp, dp, D, dp],
+            "aniso_shard_cuts": [P, I, lp],
             "aniso_last_error": [ctypes.c_char_p, ctypes.c_size_t],
         }
         for name, args in sig.items():
@@ -110,6 +113,27 @@ def _f64(a, n, name):
     if a.size != n:
         raise AnisoError(1, f"{name} has {a.size} entries, expected N = {n}")
     return a
+
+
+def _dev_vec(t, n, name):
+    """A contiguous float64 CUDA tensor of exactly n entries (else AnisoError)."""
+    import torch
+
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()
+            and t.numel() == n):
+        raise AnisoError(1, f"{name} must be a contiguous float64 CUDA tensor of {n} entries")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _dev_rows(t, rows, cols, name):
+    """A float64 CUDA tensor of `rows` rows of at least `cols` entries (unit column
+    stride, row stride >= cols): the kernels touch the first cols of every row."""
+    import torch
+
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64 and t.dim() == 2
+            and t.stride(1) == 1 and t.shape[0] == rows and t.shape[1] >= cols and (rows == 1 or t.stride(0) >= cols)):
+        raise AnisoError(1, f"{name} must be a ({rows}, >= {cols}) float64 CUDA tensor with unit column stride")
+    return ctypes.c_void_p(t.data_ptr())
 
 
 class Aniso:
@@ -181,9 +205,8 @@ class Aniso:
         """charge/out: contiguous float64 torch tensors of N entries on the GPU."""
         import torch
 
-        for t, nm in ((charge, "charge"), (out, "out")):
-            if not (t.is_cuda and t.dtype == torch.float64 and t.is_contiguous() and t.numel() == self.N):
-                raise AnisoError(1, f"{nm} must be a contiguous float64 CUDA tensor of {self.N} entries")
+        _dev_vec(charge, self.N, "charge")
+        _dev_vec(out, self.N, "out")
         s = torch.cuda.current_stream().cuda_stream if stream is None else stream
         if mask == STAGE_ALL:
             _check(lib().aniso_mapping_dev(self.address, ctypes.c_void_p(charge.data_ptr()), int(id_),
@@ -197,27 +220,27 @@ class Aniso:
         """main.cpp forwardOperator on device tensors: out = u - K_0(sigma_s .* u)."""
         import torch
 
+        pu, po = _dev_vec(u, self.N, "u"), _dev_vec(out, self.N, "out")
         s = torch.cuda.current_stream().cuda_stream if stream is None else stream
-        _check(lib().aniso_forward_dev(self.address, ctypes.c_void_p(u.data_ptr()), ctypes.c_void_p(out.data_ptr()),
-                                       ctypes.c_void_p(s)))
+        _check(lib().aniso_forward_dev(self.address, pu, po, ctypes.c_void_p(s)))
         return out
 
     def mapping_tree_dev(self, q_tree, id_, out_slice, stream=None):
         """mapping on a tree-order device vector (all N) into the owned tree-order slice."""
         import torch
 
+        pq, po = _dev_vec(q_tree, self.N, "q_tree"), _dev_vec(out_slice, self.n_owned(), "out_slice")
         s = torch.cuda.current_stream().cuda_stream if stream is None else stream
-        _check(lib().aniso_mapping_tree_dev(self.address, ctypes.c_void_p(q_tree.data_ptr()), int(id_),
-                                            ctypes.c_void_p(out_slice.data_ptr()), ctypes.c_void_p(s)))
+        _check(lib().aniso_mapping_tree_dev(self.address, pq, int(id_), po, ctypes.c_void_p(s)))
         return out_slice
 
     def forward_tree_dev(self, x_tree, y_slice, stream=None):
         """forwardOperator in tree order: y_slice = (x - K_0(sigma_s .* x))[own slice], x tree-ordered."""
         import torch
 
+        px, py = _dev_vec(x_tree, self.N, "x_tree"), _dev_vec(y_slice, self.n_owned(), "y_slice")
         s = torch.cuda.current_stream().cuda_stream if stream is None else stream
-        _check(lib().aniso_forward_tree_dev(self.address, ctypes.c_void_p(x_tree.data_ptr()),
-                                            ctypes.c_void_p(y_slice.data_ptr()), ctypes.c_void_p(s)))
+        _check(lib().aniso_forward_tree_dev(self.address, px, py, ctypes.c_void_p(s)))
         return y_slice
 
     # ---- the block operator of aniso.m (aniso.m:121-157)
@@ -233,11 +256,8 @@ class Aniso:
         ids = np.ascontiguousarray(np.asarray(ids, dtype=np.int32).reshape(-1))
         nrhs = x.shape[0]
         mixes = np.ascontiguousarray(np.asarray(mixes, dtype=np.float64).reshape(len(ids), nrhs, nrhs))
-        for t, nm in ((x, "x"), (out, "out")):
-            if not (t.is_cuda and t.dtype == torch.float64 and t.dim() == 2 and t.stride(1) == 1):
-                raise AnisoError(1, f"{nm} must be a 2-D float64 CUDA tensor with unit column stride")
-        if x.shape[1] != self.N or out.shape[0] != nrhs:
-            raise AnisoError(1, f"x must be (nrhs, {self.N}) and out (nrhs, n_out)")
+        _dev_rows(x, nrhs, self.N, "x")
+        _dev_rows(out, nrhs, self.n_owned() if tree else self.N, "out")
         s = torch.cuda.current_stream().cuda_stream if stream is None else stream
         _check(lib().aniso_apply_block_dev(self.address, int(nrhs), ctypes.c_void_p(x.data_ptr()), int(x.stride(0)),
                                            int(bool(use_sigma)), len(ids),
@@ -252,16 +272,29 @@ class Aniso:
         x: (ks, N) device tensor (block b = u(b*n+1:(b+1)*n)); out: (ks, n_out)."""
         import torch
 
-        for t, nm in ((x, "x"), (out, "out")):
-            if not (t.is_cuda and t.dtype == torch.float64 and t.dim() == 2 and t.stride(1) == 1):
-                raise AnisoError(1, f"{nm} must be a 2-D float64 CUDA tensor with unit column stride")
-        if x.shape[0] != self.ks or x.shape[1] != self.N or out.shape[0] != self.ks:
-            raise AnisoError(1, f"x must be ({self.ks}, {self.N}) and out ({self.ks}, n_out)")
+        _dev_rows(x, self.ks, self.N, "x")
+        _dev_rows(out, self.ks, self.n_owned() if tree else self.N, "out")
         s = torch.cuda.current_stream().cuda_stream if stream is None else stream
         _check(lib().aniso_block_op_dev(self.address, int(which), ctypes.c_void_p(x.data_ptr()), int(x.stride(0)),
                                         ctypes.c_void_p(out.data_ptr()), int(out.stride(0)), int(bool(tree)),
                                         ctypes.c_void_p(s)))
         return out
+
+    def block_op(self, which, u):
+        """aniso.m forward (0) / mforward (1) / x - mforward(x) (2) on host arrays:
+        u is (ks, N) or the stacked ks*N column of aniso.m; returns (ks, N)."""
+        u = _f64(u, self.ks * self.N, "u")
+        out = np.zeros(self.ks * self.N)
+        _check(lib().aniso_block_op(self.address, int(which), _dp(u), _dp(out)))
+        return out.reshape(self.ks, self.N)
+
+    def apply_block(self, u, sigma_s, g):
+        """A(u) = u - mforward(u) with explicit sigma_s and g."""
+        u = _f64(u, self.ks * self.N, "u")
+        s = _f64(sigma_s, self.N, "sigma_s")
+        out = np.zeros(self.ks * self.N)
+        _check(lib().aniso_apply_block(self.address, _dp(u), _dp(s), float(g), _dp(out)))
+        return out.reshape(self.ks, self.N)
 
     def gmres(self, q, m=80, maxit=400, tol=1e-12, x0=None):
         """main.cpp:121-141 on the device: returns (iters, x, residual history, final residual)."""
@@ -282,6 +315,16 @@ class Aniso:
         b, e = ctypes.c_int64(), ctypes.c_int64()
         _check(lib().aniso_get_shard(self.address, ctypes.byref(b), ctypes.byref(e)))
         return b.value, e.value
+
+    def n_owned(self):
+        b, e = self.shard()
+        return e - b
+
+    def shard_cuts(self, nranks):
+        """Every rank's [cuts[r], cuts[r+1]) for nranks ranks (host only, no state change)."""
+        c = np.zeros(int(nranks) + 1, dtype=np.int64)
+        _check(lib().aniso_shard_cuts(self.address, int(nranks), c.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        return c
 
     def tree_perm(self):
         p = np.zeros(self.N, dtype=np.int32)

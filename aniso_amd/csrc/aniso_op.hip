@@ -79,9 +79,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_HARMONIC")) useAtt = useAtt && e[0] != '0';
     if (const char* e = std::getenv("ANISO_HM_CLUSTER")) useClusters = e[0] != '0';
     if (const char* e = std::getenv("ANISO_OVERLAP")) overlap = std::atoi(e);
-    if (const char* e = std::getenv("ANISO_EARLY_M2L")) earlyM2L = e[0] != '0';
     if (const char* e = std::getenv("ANISO_FUSE_SUB")) fuseSub = e[0] != '0';
-    if (const char* e = std::getenv("ANISO_NEAR_CLUSTER")) useNearClusters = e[0] != '0';
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
     modes.resize(kernelSize);
@@ -89,15 +87,15 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
 
 Operator::~Operator() {
     if (device >= 0) {
+        int prev = -1;  // restore the caller's device (the destructor runs from Python __del__)
+        (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
         for (auto& e : evPool) (void)hipEventDestroy(e);
         if (evFork) (void)hipEventDestroy(evFork);
         if (evJoin) (void)hipEventDestroy(evJoin);
         if (side) (void)hipStreamDestroy(side);
-        if (evTier0) (void)hipEventDestroy(evTier0);
-        if (evJoin2) (void)hipEventDestroy(evJoin2);
-        if (side2) (void)hipStreamDestroy(side2);
         if (own) (void)hipStreamDestroy(own);
+        if (prev >= 0) (void)hipSetDevice(prev);
     }
 }
 
@@ -125,16 +123,9 @@ void Operator::ensureDevice() {
     }
     HIP_CHECK(hipGetDevice(&device));
     HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
-    {
-        int lo = 0, hi = 0;  // ANISO_SIDE_PRIO=1: the side stream at the highest priority
-        HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        const char* e = std::getenv("ANISO_SIDE_PRIO");
-        HIP_CHECK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, e && e[0] == '1' ? hi : lo));
-    }
+    // side stream at normal priority (a high-priority one measured slower, r01f)
+    HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&evFork, hipEventDisableTiming));
-    HIP_CHECK(hipStreamCreateWithFlags(&side2, hipStreamNonBlocking));
-    HIP_CHECK(hipEventCreateWithFlags(&evTier0, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&evJoin2, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
     // tree-order coordinates
     std::vector<double> pxT(geo.N), pyT(geo.N);
@@ -274,11 +265,6 @@ void Operator::uploadPlan() {
         up(dHmBlk, plan.hmBlk);
         up(dHmSlot, plan.hmSlot);
         up(dHmNDir, plan.hmNDir);
-        up(dNcPtr, plan.ncPtr);
-        up(dNcLeaf, plan.ncLeaf);
-        up(dNcSlot, plan.ncSlot);
-        up(dNcSegPtr, plan.ncSegPtr);
-        up(dNcSeg, to_int4(plan.ncSeg));
         attReady = false;
     }
     up(dM2LCanonBase, plan.m2lCanonBase);
@@ -611,6 +597,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     }
     ensureDevice();
     const int64_t nOut = treeOut ? plan.ownEnd - plan.ownBegin : geo.N;
+    if (ldx < geo.N || ldo < nOut) throw std::invalid_argument("block apply: leading dimension too small");
     if (!rhs_supported(K)) {  // pad with zero right-hand sides to the next compiled count
         const int Kp = rhs_padded(K);
         dPadIn.alloc((size_t)Kp * geo.N * sizeof(double));
@@ -628,7 +615,6 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                                    K, hipMemcpyDeviceToDevice, s));
         return;
     }
-    if (K > 1 && (ldx < geo.N || ldo < nOut)) throw std::invalid_argument("block apply: leading dimension too small");
     ensureWork(K);
     if (up_tier_lds(plan.upMaxTask, K) > 160 * 1024 ||
         down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, plan.dnMaxNear, plan.dnMaxChain, K) > 160 * 1024)
@@ -652,9 +638,6 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     // the harmonic block apply forks its near field off as soon as the charges are
     // complete: after the last up tier with a P2M leaf (the tiers above only M2M)
     const bool fork = harmonic && overlap;
-    // and, when the clustered M2L has "early" clusters, starts
-    // them on a second side stream right after up tier 0
-    const bool split = fork && useClusters && earlyM2L && (mask & kStageFar) && plan.hmEarly > 0;
     if (fork && plan.upTierTask.size() < 2) HIP_CHECK(hipEventRecord(evFork, s));
     for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k) {
         launch_up_tier(K, plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask,
@@ -663,7 +646,6 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                        treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(), dCT.as<double>(), P,
                        dMult.as<double>(), s);
         if (fork && (int)k == plan.upLastLeafTier) HIP_CHECK(hipEventRecord(evFork, s));
-        if (split && k == 0) HIP_CHECK(hipEventRecord(evTier0, s));
     }
     int ep = tm ? mark(s) : -1;
     span(1, e0, ep);
@@ -678,13 +660,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         int e = -1;
         auto nearStage = [&] {
             int en = tm ? (overlap ? mark(sn) : ep) : -1;
-            if (nearClustersOn(K) && (mask & kStageNear))
-                launch_near_hc(K, (int)plan.ncPtr.size() - 1, dNcPtr.as<int>(), dNcLeaf.as<int>(), dNcSlot.as<int>(),
-                               plan.ncMaxPts, dNcSegPtr.as<int64_t>(), dNcSeg.as<int4>(), dLeafInfo.as<int4>(),
-                               dNearKOff.as<int64_t>(), dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(),
-                               dSigDiag.as<double>(), hw, dFT.as<double>(), operm, obase, ldo, scale, out, sn);
-            else
-                launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
+            launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
                                dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(), dNearKOff.as<int64_t>(),
                                dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dSigDiag.as<double>(), hw,
                                dFT.as<double>(), operm, obase, ldo, mask, scale, out, sn);
@@ -698,31 +674,13 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             if (!overlap) ep = e2;
             if (overlap) HIP_CHECK(hipEventRecord(evJoin, side));
         };
-        auto m2lClusters = [&](int c0, int c1, hipStream_t st) {
-            launch_m2l_hc(K, c1 - c0, plan.hmMaxCl, dHmClPtr.as<int>() + c0, dHmTgt.as<int>(), dHmPtr.as<int64_t>(),
-                          dHmNDir.as<int>(), dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(),
-                          dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
-                          dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), st);
-        };
         const int ncl = (int)plan.hmClPtr.size() - 1;
-        int eEarly = -1;
-        if (split) {  // early clusters beside the upper up tiers and the near field
-            HIP_CHECK(hipStreamWaitEvent(side2, evTier0, 0));
-            eEarly = tm ? mark(side2) : -1;
-            m2lClusters(0, plan.hmEarly, side2);
-            HIP_CHECK(hipEventRecord(evJoin2, side2));
-        }
         auto farStage = [&] {
-            if (split) {
-                m2lClusters(plan.hmEarly, ncl, s);
-                HIP_CHECK(hipStreamWaitEvent(s, evJoin2, 0));
-                e = tm ? mark(s) : -1;
-                span(2, eEarly, e);  // both launches
-                ep = e;
-                return;
-            }
             if ((mask & kStageFar) && useClusters)
-                m2lClusters(0, ncl, s);
+                launch_m2l_hc(K, ncl, plan.hmMaxCl, dHmClPtr.as<int>(), dHmTgt.as<int>(), dHmPtr.as<int64_t>(),
+                              dHmNDir.as<int>(), dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(),
+                              dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
+                              dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
             else if (mask & kStageFar)
                 launch_m2l_hm(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dAttPtr.as<int64_t>(), dAttSrc.as<int>(),
                               dAttBlk.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(),
@@ -818,14 +776,18 @@ std::vector<double> Operator::blockMixes(int nb, double g, bool chi) {
 }
 
 void Operator::blockOpDev(int which, const double* x, int64_t ldx, double* out, int64_t ldo, bool treeIo,
-                          hipStream_t s) {
+                          hipStream_t s, double gval, const double* sigT) {
     if (which < 0 || which > 2) throw std::invalid_argument("block operator: which must be 0, 1 or 2");
+    if (!coeffSet) throw std::runtime_error("block operator before setCoeff");
+    ensureDevice();
     const int nb = ks, nm = 2 * ks - 1;
-    const auto mix = blockMixes(nb, g, which != 0);
+    const auto mix = blockMixes(nb, std::isnan(gval) ? g : gval, which != 0);
+    const double* sig = sigT ? sigT : dSigmaT.as<double>();
     std::vector<int> ids(nm);
     for (int m = 0; m < nm; ++m) ids[m] = m;
     if (which < 2) {
-        applyBlockDev(nb, x, ldx, treeIo, which != 0, nm, ids.data(), mix.data(), out, ldo, treeIo, s);
+        applyBlock(nb, x, ldx, treeIo, which != 0 ? sig : nullptr, nm, ids.data(), mix.data(), out, ldo, treeIo, s,
+                   kStageAll);
         return;
     }
     // x - mforward(x) on the owned targets (aniso.m:155)
@@ -837,7 +799,7 @@ void Operator::blockOpDev(int which, const double* x, int64_t ldx, double* out, 
         subX = xo;
         subLd = ldx;
         try {
-            applyBlockDev(nb, x, ldx, treeIo, true, nm, ids.data(), mix.data(), out, ldo, treeIo, s);
+            applyBlock(nb, x, ldx, treeIo, sig, nm, ids.data(), mix.data(), out, ldo, treeIo, s, kStageAll);
         } catch (...) {
             subX = nullptr;
             throw;
@@ -846,8 +808,30 @@ void Operator::blockOpDev(int which, const double* x, int64_t ldx, double* out, 
         return;
     }
     dBlk.alloc((size_t)nb * nOut * sizeof(double));
-    applyBlockDev(nb, x, ldx, treeIo, true, nm, ids.data(), mix.data(), dBlk.as<double>(), nOut, treeIo, s);
+    applyBlock(nb, x, ldx, treeIo, sig, nm, ids.data(), mix.data(), dBlk.as<double>(), nOut, treeIo, s, kStageAll);
     launch_sub_slice(nOut, nb, xo, ldx, dBlk.as<double>(), nOut, out, ldo, s);
+}
+
+void Operator::blockOpHost(int which, const double* u, const double* sigmaS, double gval, double* out) {
+    if (plan.nranks != 1) throw std::logic_error("host block operator on a sharded handle");
+    if (!coeffSet) throw std::runtime_error("block operator before setCoeff");
+    ensureDevice();
+    const int64_t N = geo.N;
+    const size_t bytes = (size_t)ks * N * sizeof(double);
+    dHostIn.alloc(bytes);
+    dHostOut.alloc(bytes);
+    HIP_CHECK(hipMemcpyAsync(dHostIn.p, u, bytes, hipMemcpyHostToDevice, own));
+    const double* sigT = nullptr;
+    if (sigmaS) {
+        std::vector<double> sT(N);
+        for (int64_t k = 0; k < N; ++k) sT[k] = sigmaS[tree.perm[k]];
+        HIP_CHECK(hipStreamSynchronize(own));  // a previous call may still read dSigAlt
+        dSigAlt.upload(sT.data(), N * sizeof(double));
+        sigT = dSigAlt.as<double>();
+    }
+    blockOpDev(which, dHostIn.as<double>(), N, dHostOut.as<double>(), N, false, own, gval, sigT);
+    HIP_CHECK(hipMemcpyAsync(out, dHostOut.p, bytes, hipMemcpyDeviceToHost, own));
+    HIP_CHECK(hipStreamSynchronize(own));
 }
 
 void Operator::setTiming(bool on) {

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <cmath>
 #include <map>
 #include <memory>
 #include <string>
@@ -76,7 +77,14 @@ public:
     // aniso.m on nb = ks blocks of n = N points: which = 0 forward (the right-hand
     // side, aniso.m:121-136), 1 mforward (aniso.m:138-157), 2 x - mforward(x) (the
     // GMRES matvec, aniso.m:155); tree = tree-order input and owned-slice output.
-    void blockOpDev(int which, const double* x, int64_t ldx, double* out, int64_t ldo, bool tree, hipStream_t s);
+    // gval / sigT (tree-order sigma_s on the device) override the handle's g and
+    // sigma_s when given (NaN / nullptr: the handle's).
+    void blockOpDev(int which, const double* x, int64_t ldx, double* out, int64_t ldo, bool tree, hipStream_t s,
+                    double gval = NAN, const double* sigT = nullptr);
+    // host-pointer block operator (aniso.m:121-157): u and out hold nb = ks blocks of
+    // N points each (block b at b * N, original order); sigmaS (N, or nullptr: the
+    // handle's sigma_s) and gval (NaN: the handle's g) as aniso.m's mforward reads them
+    void blockOpHost(int which, const double* u, const double* sigmaS, double gval, double* out);
     // the (2 nb - 1) mode mixes of forward (chi = false) or mforward (chi = true)
     static std::vector<double> blockMixes(int nb, double g, bool chi);
 
@@ -93,10 +101,6 @@ public:
     hipStream_t stream() const { return own; }
     bool harmonicReady() const { return useAtt && attReady; }
     bool clustersOn() const { return useClusters; }
-    // near clusters: the plan has them (leaves <= 16 points, 64 KB LDS) and they are on
-    bool nearClustersOn(int K = 5) const {
-        return useNearClusters && plan.ncPtr.size() > 1 && ((size_t)plan.ncMaxPts + 256) * K * 8 <= 64 * 1024;
-    }
     bool modeCached(int id) const { return id >= 0 && id < kernelSize && modes[id].ready; }
     int kernelSize = 0;
     // stage timing with HIP events recorded in-stream (no host sync per apply);
@@ -133,14 +137,15 @@ private:
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
     bool useClusters = true;
-    DevBuf dNcPtr, dNcLeaf, dNcSlot, dNcSegPtr, dNcSeg;  // near cluster plan
-    bool useNearClusters = false;  // measured slower than the per-leaf kernel
     std::map<std::string, DevBuf> modeTabs;
     const CorrFold& corrTable(int K, int nterm, const int* ids, const double* mixes);
     std::map<std::string, CorrFold> corrTabs;
     int workK = 0;
 
     void ensureDevice();
+  public:
+    int deviceId() const { return device; }
+  private:
     void uploadPlan();
     int device = -1;
     hipStream_t own = nullptr;
@@ -148,14 +153,10 @@ private:
     // the M2L (both HBM-bound, neither saturates alone)
     hipStream_t side = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr;
-    // second side stream: the early M2L clusters after up tier 0
-    hipStream_t side2 = nullptr;
-    hipEvent_t evTier0 = nullptr, evJoin2 = nullptr;
-    bool earlyM2L = false;
     // x - mforward(x) fused into the down pass (blockOpDev sets subX for one apply)
     bool fuseSub = true;
     const double* subX = nullptr;
-    int64_t subLd = 0;  // measured slower (611 vs 620 block matvec/s): ANISO_EARLY_M2L=1
+    int64_t subLd = 0;
     int overlap = 1;
     // stage timing: events recorded in-stream, (stage, start, end) spans per apply
     std::vector<hipEvent_t> evPool;
@@ -179,6 +180,7 @@ private:
     DevBuf dCharge, dOut, dFT, dCT, dMult, dLocal, dSigmaS, dTmp, dTmp2;
     DevBuf dWT, dSigmaT, dIperm, dTmpS;  // tree-order path
     DevBuf dPadIn, dPadOut, dBlk;       // block operator: padded right-hand sides, x - mforward(x)
+    DevBuf dHostIn, dHostOut, dSigAlt;  // host-pointer block operator: staging, sigma_s override
     std::vector<ModeCache> modes;
 };
 

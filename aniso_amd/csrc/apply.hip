@@ -29,21 +29,6 @@
 
 namespace aniso {
 
-#ifdef ANISO_PROBE  // development build only (make probe): phase stamps of task 0..kProbeWG-1
-constexpr int kProbeWG = 8192;
-__device__ unsigned long long g_probe[2][kProbeWG][8];
-#define ANISO_STAMP(Q, W, I)                                                       \
-    do {                                                                            \
-        if (threadIdx.x == 0 && (W) < kProbeWG) g_probe[Q][W][I] = wall_clock64(); \
-    } while (0)
-extern "C" int aniso_probe_read(unsigned long long* host) {
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_probe), sizeof(g_probe));
-}
-#else
-#define ANISO_STAMP(Q, W, I) \
-    do {                     \
-    } while (0)
-#endif
 
 template <int K>
 struct MixK {
@@ -145,7 +130,6 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
     int* LC = LB + maxTask;
     int* ND = LC + maxTask;
     const int task = taskBase + blockIdx.x;
-    ANISO_STAMP(0, task, 0);
     const int4 d = desc[task];  // first node, nodes, first point, levels
     const int n0 = d.x, nt = d.y, ngrp = d.w;
     const int64_t b0 = d.z;
@@ -169,7 +153,6 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
         ND[k] = node[n0 + k];
     }
     __syncthreads();
-    ANISO_STAMP(0, task, 1);
     // P2M of the task's leaves (bbfmm.h:737-748): 16 lanes per leaf, one point per
     // lane per pass (its 16 products in registers), then a 16-lane reduce-scatter
     // leaves lane l with entry l.  The weighted charges are formed here from the
@@ -243,7 +226,6 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
         }
     }
     __syncthreads();
-    ANISO_STAMP(0, task, 2);
     // M2M (bbfmm.h:855-859), one item per (node, row r, child q): 4x the items of a
     // per-(node, row) loop, so a level's child reads (LDS, or HBM for the roots of
     // the tier below) are all in flight at once; the 4 child partials of a row are
@@ -275,10 +257,8 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
         }
         __syncthreads();
     }
-    ANISO_STAMP(0, task, 3);
     for (int it = threadIdx.x; it < nt * kRank * K; it += blockDim.x)
         mult[(size_t)ND[it / (kRank * K)] * kRank * K + it % (kRank * K)] = M[it];
-    ANISO_STAMP(0, task, 4);
 }
 
 #undef ANISO_RS16
@@ -892,7 +872,6 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     int* NC = NB + maxLeaves;                              // maxLeaves: their count
     int* NO = NC + maxLeaves;                              // maxNear: partial offsets addressed to this task
     const int task = blockIdx.x;
-    ANISO_STAMP(1, task, 0);
     // task record: (first node, nodes, first leaf entry, leaves), (owned points begin,
     // end, first chain entry, chain length), (first near offset, count, levels, 0)
     const int4 d0 = desc[3 * task], d1 = desc[3 * task + 1], d2 = desc[3 * task + 2];
@@ -926,7 +905,6 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     if (threadIdx.x == 0) LB[nl] = pr.y;
     for (int j = threadIdx.x; j < d2.y; j += blockDim.x) NO[j] = nearOff[d2.x + j];
     __syncthreads();
-    ANISO_STAMP(1, task, 1);
     // ---- phase 1: the root's parent total by the L2L chain from level 1
     // (bbfmm.h:1070-1071 along the ancestors), then the task's levels
     if (far) {
@@ -961,7 +939,6 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             }
         }
         __syncthreads();
-        ANISO_STAMP(1, task, 2);
         for (int g = 0; g < ngrp; ++g) {
             const int s0 = gs[g], s1 = gs[g + 1];
             for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
@@ -985,7 +962,6 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             __syncthreads();
         }
     }
-    ANISO_STAMP(1, task, 3);
     // ---- phase 2: owned points: L2P + near gather
     for (int g = threadIdx.x; g < npts; g += blockDim.x) {
         const int kpos = pr.x + g;
@@ -1037,7 +1013,6 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             for (int i = 0; i < K; ++i) out[(size_t)i * ldo + o] += scale * v[i];
         }
     }
-    ANISO_STAMP(1, task, 4);
 }
 
 // ----------------------------------------------------------------- corrections

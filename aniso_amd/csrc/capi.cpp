@@ -1,6 +1,7 @@
 // capi.cpp -- extern "C" boundary over aniso::Operator.  No exception crosses
 // the ABI: every failure becomes a status code + thread-local message.
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <new>
 #include <stdexcept>
@@ -48,18 +49,29 @@ int guarded(F&& f) {
     }
 }
 
+// Every call that may touch the device runs on the handle's device and leaves the
+// caller's current device as it found it (a process driving several GPUs).
+struct DeviceRestore {
+    int prev = -1;
+    explicit DeviceRestore(aniso_handle h) {
+        if (h && h->magic == 0xA2150A2150ULL && h->op.deviceId() >= 0) (void)hipGetDevice(&prev);
+    }
+    ~DeviceRestore() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 aniso::Operator& get(aniso_handle h) {
     if (!h || h->magic != 0xA2150A2150ULL) throw std::invalid_argument("invalid aniso handle");
     return h->op;
 }
 
 #define CHECK_HANDLE(h)                              \
-    do {                                             \
-        if (!h || h->magic != 0xA2150A2150ULL) {     \
-            g_err = "invalid aniso handle";          \
-            return ANISO_ERR_HANDLE;                 \
-        }                                            \
-    } while (0)
+    if (!h || h->magic != 0xA2150A2150ULL) {         \
+        g_err = "invalid aniso handle";              \
+        return ANISO_ERR_HANDLE;                     \
+    }                                                \
+    DeviceRestore restore_device__(h)
 
 #define CHECK_PTR(p)                                                         \
     do {                                                                     \
@@ -217,6 +229,26 @@ int aniso_block_op_dev(aniso_handle h, int which, const double* x, int64_t ldx, 
     });
 }
 
+int aniso_block_op(aniso_handle h, int which, const double* u, double* out) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(u);
+        CHECK_PTR(out);
+        get(h).blockOpHost(which, u, nullptr, NAN, out);
+    });
+}
+
+int aniso_apply_block(aniso_handle h, const double* u, const double* sigma_s, double g, double* out) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(u);
+        CHECK_PTR(sigma_s);
+        CHECK_PTR(out);
+        if (!(g >= 0.0 && g < 1.0)) throw std::invalid_argument("g must be in [0, 1)");
+        get(h).blockOpHost(2, u, sigma_s, g, out);
+    });
+}
+
 int aniso_block_mixes(int nb, double g, int chi, double* mixes) {
     return guarded([&] {
         CHECK_PTR(mixes);
@@ -239,6 +271,15 @@ int aniso_gmres(aniso_handle h, const double* q, double* x, int m, int maxit, do
 int aniso_set_shard(aniso_handle h, int rank, int nranks) {
     CHECK_HANDLE(h);
     return guarded([&] { get(h).setShard(rank, nranks); });
+}
+
+int aniso_shard_cuts(aniso_handle h, int nranks, int64_t* cuts) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(cuts);
+        const auto c = aniso::shard_cuts(get(h).tree, nranks);
+        std::copy(c.begin(), c.end(), cuts);
+    });
 }
 
 int aniso_get_shard(aniso_handle h, int64_t* b, int64_t* e) {
@@ -343,9 +384,8 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[14] = cl ? (int64_t)op.plan.hmClPtr.size() - 1 : 0;
         s[15] = cl ? op.plan.hmDual : 0;
         s[16] = cl ? (int64_t)op.plan.hmSrc.size() : (int64_t)op.plan.attSrc.size();
-        const bool nc = op.harmonicReady() && op.nearClustersOn();
-        s[17] = nc ? (int64_t)op.plan.ncPtr.size() - 1 : 0;
-        s[18] = nc ? op.plan.ncDual : 0;
+        s[17] = 0;  // reserved (near-field clusters, removed in round 2)
+        s[18] = 0;
     });
 }
 

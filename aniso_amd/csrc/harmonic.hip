@@ -34,8 +34,6 @@
 
 namespace aniso {
 
-constexpr int kHmVarDefault = 4;  // 4 waves per SIMD (measured best, r01e)
-
 // 1/sqrt(x) to full double precision: v_rsq_f64 (about 2^-22 relative) and two
 // Newton steps.  x = 0 gives a non-finite value; callers select it away.
 __device__ __forceinline__ double rsqrt_f64(double x) {
@@ -225,119 +223,6 @@ __device__ __forceinline__ void hm_entry2(double e, double dx, double dy2, const
     }
 }
 
-// Software-pipelined streams of k_m2l_hc (PF): the next block's E column, source
-// multipole row and source-node geometry are loaded before the current block's
-// arithmetic, so each wave keeps one block in flight while it computes the other.
-template <int K>
-struct HcBlk {
-    double e[4];
-    double xm[K];
-    double gx, rx, gy, ry;
-};
-
-template <int K>
-__device__ __forceinline__ void hc_load(HcBlk<K>& h, int b, int B, int s, int q, const double* __restrict__ E,
-                                        const double* __restrict__ ncx, const double* __restrict__ ncy,
-                                        const double* __restrict__ nrx, const double* __restrict__ nry,
-                                        const double* __restrict__ mult) {
-    const bool tr = b < 0;
-    const double* p = E + (size_t)(tr ? ~b : b) * 256 + (tr ? 64 * q + s : 16 * s + 4 * q);
-    if (tr) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) h.e[j] = p[16 * j];
-    } else {
-        const dbl2 k0 = reinterpret_cast<const dbl2*>(p)[0], k1 = reinterpret_cast<const dbl2*>(p)[1];
-        h.e[0] = k0.x;
-        h.e[1] = k0.y;
-        h.e[2] = k1.x;
-        h.e[3] = k1.y;
-    }
-    const double* m = mult + ((size_t)B * kRank + s) * K;
-#pragma unroll
-    for (int b2 = 0; b2 < K; ++b2) h.xm[b2] = m[b2];
-    h.gx = ncx[B];
-    h.rx = nrx[B];
-    h.gy = ncy[B];
-    h.ry = nry[B];
-}
-
-template <int K, int NR>
-__device__ __forceinline__ void hc_directed_pf(int64_t p0, int64_t p1, int lane, int s, int q, const int* __restrict__ src,
-                                               const int* __restrict__ blk, const double* __restrict__ E,
-                                               const double* __restrict__ ncx, const double* __restrict__ ncy,
-                                               const double* __restrict__ nrx, const double* __restrict__ nry,
-                                               double chx, double chy, const double (&bx)[4], double by,
-                                               const HarmWeights& hw, const double* __restrict__ mult,
-                                               double (&c)[4][K]) {
-    for (int64_t cb = p0; cb < p1; cb += kWave) {
-        const int cnt = (int)min<int64_t>(kWave, p1 - cb);
-        const int mySrc = lane < cnt ? src[cb + lane] : 0;
-        const int myBlk = lane < cnt ? blk[cb + lane] : 0;
-        HcBlk<K> nx;
-        hc_load<K>(nx, __builtin_amdgcn_readlane(myBlk, 0), __builtin_amdgcn_readlane(mySrc, 0), s, q, E, ncx, ncy, nrx,
-                   nry, mult);
-        for (int jj = 0; jj < cnt; ++jj) {
-            const HcBlk<K> cu = nx;
-            const int jn = min(jj + 1, cnt - 1);  // the last block reloads itself (no branch)
-            hc_load<K>(nx, __builtin_amdgcn_readlane(myBlk, jn), __builtin_amdgcn_readlane(mySrc, jn), s, q, E, ncx, ncy,
-                       nrx, nry, mult);
-            const double ax = cu.gx + cu.rx * chx;
-            const double dy = (cu.gy + cu.ry * chy) - by;
-            const double dy2 = dy * dy;
-            double xw[K];
-#pragma unroll
-            for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * cu.xm[b];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) hm_entry<K, false, NR>(cu.e[j], ax - bx[j], dy2, xw, c[j]);
-        }
-    }
-}
-
-template <int K, int NR>
-__device__ __forceinline__ void hc_dual_pf(int64_t p0, int64_t p1, int lane, int s, int q, const int* __restrict__ src,
-                                           const int* __restrict__ blk, const int* __restrict__ slot,
-                                           const double* __restrict__ E, const double* __restrict__ ncx,
-                                           const double* __restrict__ ncy, const double* __restrict__ nrx,
-                                           const double* __restrict__ nry, double chx, double chy,
-                                           const double (&bx)[4], double by, const HarmWeights& hw,
-                                           const double* __restrict__ mult, const double* xa, double* acc,
-                                           double (&c)[4][K]) {
-    for (int64_t cb = p0; cb < p1; cb += kWave) {
-        const int cnt = (int)min<int64_t>(kWave, p1 - cb);
-        const int mySrc = lane < cnt ? src[cb + lane] : 0;
-        const int myBlk = lane < cnt ? blk[cb + lane] : 0;
-        const int mySlot = lane < cnt ? slot[cb + lane] : 0;
-        HcBlk<K> nx;
-        hc_load<K>(nx, __builtin_amdgcn_readlane(myBlk, 0), __builtin_amdgcn_readlane(mySrc, 0), s, q, E, ncx, ncy, nrx,
-                   nry, mult);
-        for (int jj = 0; jj < cnt; ++jj) {
-            const HcBlk<K> cu = nx;
-            const int sl = __builtin_amdgcn_readlane(mySlot, jj);
-            const int jn = min(jj + 1, cnt - 1);
-            hc_load<K>(nx, __builtin_amdgcn_readlane(myBlk, jn), __builtin_amdgcn_readlane(mySrc, jn), s, q, E, ncx, ncy,
-                       nrx, nry, mult);
-            const double ax = cu.gx + cu.rx * chx;
-            const double dy = (cu.gy + cu.ry * chy) - by;
-            const double dy2 = dy * dy;
-            double xw[K], ob[K];
-#pragma unroll
-            for (int b = 0; b < K; ++b) {
-                xw[b] = hw.hw[b] * cu.xm[b];
-                ob[b] = 0.0;
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) hm_entry2<K, NR>(cu.e[j], ax - bx[j], dy2, xw, xa + (4 * q + j) * K, c[j], ob);
-#pragma unroll
-            for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // rows 4q'+j over the quad
-            if (q == 0) {
-                double* d = acc + ((size_t)sl * kRank + s) * K;
-#pragma unroll
-                for (int i = 0; i < K; ++i) atomicAdd(d + i, (i & 1) ? -ob[i] : ob[i]);
-            }
-        }
-    }
-}
-
 // The harmonic M2L in clusters: one 4-wave workgroup per
 // cluster (the active targets of one level under one ancestor kClusterDepth levels
 // up), the cluster's locals accumulated in LDS.  Each wave takes the cluster's
@@ -348,19 +233,17 @@ __device__ __forceinline__ void hc_dual_pf(int64_t p0, int64_t p1, int lane, int
 // (ds_add_f64).  The block stream drops by the in-cluster share (0.65 of the V
 // pairs at 64 targets per cluster, tools/vfrac.py); the summation order of the LDS
 // adds is not fixed (results repeat to rounding, not bitwise).
-template <int K, int NR, int WPE, int NT, bool PF>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE)))
+template <int K, int NR, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64_t* __restrict__ ptr,
          const int* __restrict__ ndir, const int* __restrict__ src, const int* __restrict__ blk,
          const int* __restrict__ slot, const double* __restrict__ E, const double* __restrict__ ncx, const double* __restrict__ ncy,
          const double* __restrict__ nrx, const double* __restrict__ nry, const Params* __restrict__ P,
-         HarmWeights hw, const double* __restrict__ mult, double* __restrict__ local, int xcdOrder) {
+         HarmWeights hw, const double* __restrict__ mult, double* __restrict__ local) {
     constexpr int RK = kRank * K;
     constexpr int PG = 2;
     extern __shared__ double sm[];
-    // XCD (ANISO_HM_VAR bit 6): each XCD takes a contiguous range of clusters, so
-    // spatial neighbours share source multipoles and cross-cluster blocks in one L2
-    const int cid = xcdOrder ? xcd_tile((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+    const int cid = (int)blockIdx.x;
     const int c0 = clPtr[cid], nt = clPtr[cid + 1] - c0;
     const int nw = (int)(blockDim.x / kWave);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
@@ -391,11 +274,6 @@ k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64
 #pragma unroll
             for (int i = 0; i < K; ++i) c[j][i] = 0.0;
         const int64_t p0 = ptr[c0 + ti], pd = p0 + ndir[c0 + ti], p1 = ptr[c0 + ti + 1];
-        if constexpr (PF) {
-            hc_directed_pf<K, NR>(p0, pd, lane, s, q, src, blk, E, ncx, ncy, nrx, nry, chx, chy, bx, by, hw, mult, c);
-            hc_dual_pf<K, NR>(pd, p1, lane, s, q, src, blk, slot, E, ncx, ncy, nrx, nry, chx, chy, bx, by, hw, mult, xa,
-                              acc, c);
-        } else {
             // directed entries: PG blocks in flight, forward product only
             for (int64_t cb = p0; cb < pd; cb += kWave) {
                 const int cnt = (int)min<int64_t>(kWave, pd - cb);
@@ -472,7 +350,6 @@ k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64
                     }
                 }
             }
-        }
         {  // sum over the 16 columns (lane bits 2..5) on the VALU: DPP in-row, permlane swaps across rows
             const bool r4 = xor16_r4(lane);
 #pragma unroll
@@ -634,151 +511,6 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
 }
 
 
-// The harmonic near field in clusters: one 256-thread workgroup
-// per cluster of leaves (<= 16 points each; same level, one ancestor
-// kClusterDepth levels up), 16 lanes per target leaf as in k_near_hm (row quad rq
-// = lane & 3, column phase lane >> 2), the cluster's sums in LDS.  A U pair of two
-// cluster leaves is applied by the smaller id from one read of its sub-block: the
-// forward product, and per column (source point) the partner's product
-// T_i(c)(E/r) sum_b T_b(c) (-1)^b hw_b f_A,b(t) summed over the target rows (in
-// lane, then over the quad by DPP) and added to the partner's LDS sum with
-// (-1)^i (the reversed direction has cos = -c).  After the barrier every point's
-// output is stored: scale * om_i * (sum + dw_i sigma_t f_i).
-template <int K, int NR, int U>
-__global__ void __launch_bounds__(256) k_near_hc(const int* __restrict__ clPtr, const int* __restrict__ clLeaf,
-                                                 const int* __restrict__ clSlot, int maxPts,
-                                                 const int64_t* __restrict__ segPtr, const int4* __restrict__ seg,
-                                                 const int4* __restrict__ leafInfo,
-                                                 const int64_t* __restrict__ nearKOff, const double* __restrict__ E,
-                                                 const double* __restrict__ pxT, const double* __restrict__ pyT,
-                                                 const double* __restrict__ sigDiag, HarmWeights hw,
-                                                 const double* __restrict__ fT, const int* __restrict__ operm,
-                                                 int64_t obase, int64_t ldo, double scale, double* __restrict__ out) {
-    constexpr int KS = kStride<K>;
-    extern __shared__ double sm[];
-    const int c0 = clPtr[blockIdx.x], nlc = clPtr[blockIdx.x + 1] - c0;
-    const int npts = clSlot[c0 + nlc - 1] + leafInfo[clLeaf[c0 + nlc - 1]].z;
-    double* acc = sm;  // npts x K
-    const int grp = threadIdx.x >> 4, gl = threadIdx.x & 15;
-    double* xa = sm + (size_t)maxPts * K + (size_t)grp * 16 * K;  // the group's target charges, (-1)^b hw_b
-    for (int i = threadIdx.x; i < npts * K; i += blockDim.x) acc[i] = 0.0;
-    __syncthreads();
-    const int rq = gl & 3, cph = gl >> 2;
-    for (int lk = grp; lk < nlc; lk += 16) {
-        const int li = clLeaf[c0 + lk];
-        const int4 info = leafInfo[li];
-        const int nT = info.z, nq = (nT + 3) >> 2, cstr = 2 * nq;
-        const int64_t tb = info.y;
-        const bool rowOk = rq < nq;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous leaf's xa reads are done
-        __builtin_amdgcn_wave_barrier();
-        for (int e = gl; e < 16 * K; e += 16) {
-            const int t = e / K, b = e - t * K;
-            xa[e] = t < nT ? ((b & 1) ? -hw.hw[b] : hw.hw[b]) * fT[(size_t)(tb + t) * KS + b] : 0.0;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        double tx[4], ty[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int t = min(4 * rq + j, nT - 1);  // padded rows: E is zero there
-            tx[j] = rowOk ? pxT[tb + t] : 0.0;
-            ty[j] = rowOk ? pyT[tb + t] : 0.0;
-        }
-        double a[4][K];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int i = 0; i < K; ++i) a[j][i] = 0.0;
-        const dbl2* kc = reinterpret_cast<const dbl2*>(E + nearKOff[li]) + 2 * (rowOk ? rq : 0);
-        for (int64_t sg = segPtr[li]; sg < segPtr[li + 1]; ++sg) {
-            const int4 d = seg[sg];  // first source point, points, first column, partner slot
-            for (int cb = 0; cb < d.y; cb += 4 * U) {  // group-uniform trip count: whole quads stay active
-                dbl2 kk[U][2];
-                double f[U][K], sx[U], sy[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {  // U columns in flight per lane
-                    const int sc = cb + cph + 4 * u;
-                    const bool ok = rowOk && sc < d.y;
-                    const int scc = min(sc, d.y - 1);
-                    const dbl2* p = kc + (size_t)(d.z + scc) * cstr;
-                    kk[u][0] = ok ? __builtin_nontemporal_load(p) : dbl2{0.0, 0.0};
-                    kk[u][1] = ok ? __builtin_nontemporal_load(p + 1) : dbl2{0.0, 0.0};
-                    const int64_t ks = (int64_t)d.x + scc;
-                    load_charges<K>(fT + (size_t)ks * KS, f[u]);
-                    sx[u] = pxT[ks];
-                    sy[u] = pyT[ks];
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int sc = cb + cph + 4 * u;
-                    double xw[K];
-#pragma unroll
-                    for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * f[u][b];
-                    const double e4[4] = {kk[u][0].x, kk[u][0].y, kk[u][1].x, kk[u][1].y};
-                    if (d.w < 0) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const double dy = sy[u] - ty[j];
-                            hm_entry<K, true, NR>(e4[j], sx[u] - tx[j], dy * dy, xw, a[j]);
-                        }
-                    } else {
-                        double ob[K];
-#pragma unroll
-                        for (int i = 0; i < K; ++i) ob[i] = 0.0;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const double dy = sy[u] - ty[j];
-                            hm_entry2<K, NR, true>(e4[j], sx[u] - tx[j], dy * dy, xw, xa + (4 * rq + j) * K, a[j], ob);
-                        }
-#pragma unroll
-                        for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // the 4 row quads of column sc
-                        if (rq == 0 && sc < d.y) {
-                            double* dst = acc + (size_t)(d.w + sc) * K;
-#pragma unroll
-                            for (int i = 0; i < K; ++i) atomicAdd(dst + i, (i & 1) ? -ob[i] : ob[i]);
-                        }
-                    }
-                }
-            }
-        }
-        // sum over the column phases (the group is one DPP row of 16 lanes)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int i = 0; i < K; ++i) {
-                double v = a[j][i];
-                v += dpp_f64<0x124>(v);  // row_ror:4
-                v += dpp_f64<0x128>(v);  // row_ror:8
-                a[j][i] = v;
-            }
-        const int slot = clSlot[c0 + lk];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int t = 4 * rq + j;
-            if (cph != j || !rowOk || t >= nT) continue;
-            double* dst = acc + (size_t)(slot + t) * K;
-#pragma unroll
-            for (int i = 0; i < K; ++i) atomicAdd(dst + i, a[j][i]);
-        }
-    }
-    __syncthreads();
-    for (int lk = grp; lk < nlc; lk += 16) {
-        const int li = clLeaf[c0 + lk];
-        const int4 info = leafInfo[li];
-        if (gl >= info.z) continue;
-        const int64_t k = (int64_t)info.y + gl;
-        const double* sum = acc + (size_t)(clSlot[c0 + lk] + gl) * K;
-        double f[K];
-        load_charges<K>(fT + (size_t)k * KS, f);
-        const double sd = sigDiag[k];
-        const int64_t oi = out_index(operm, obase, k);
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-            out[(size_t)i * ldo + oi] = hw.om[i] * scale * __builtin_fma(hw.dw[i] * sd, f[i], sum[i]);
-    }
-}
-
 // ----------------------------------------------------------------- launchers
 
 #define ANISO_HM_DISPATCH_K(k, CALL)                                                                    \
@@ -790,154 +522,60 @@ __global__ void __launch_bounds__(256) k_near_hc(const int* __restrict__ clPtr, 
         default: throw std::invalid_argument("harmonic apply: unsupported block count " + std::to_string(k)); \
     }
 
-// Variant knobs (tuning/experiments): ANISO_HM_VAR bit 0 = XCD-aware
-// workgroup order, bit 1 = one Newton step in 1/r, bit 2 = 4 waves per SIMD.
-static int hm_var() {
-    static const int v = [] {
-        const char* e = std::getenv("ANISO_HM_VAR");
-        return e ? std::atoi(e) : kHmVarDefault;
-    }();
-    return v;
-}
-
+// per-target M2L (ANISO_HM_CLUSTER=0): two Newton steps in 1/r (full fp64), 4 waves
+// per SIMD (measured best, r01e)
 void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* src, const int* blk, const double* E,
                    const double* ncx, const double* ncy, const double* nrx, const double* nry, const Params* P,
                    const HarmWeights& hw, const double* mult, double* local, hipStream_t s) {
     if (ntgt <= 0) return;
     const unsigned nb = blocks_for((int64_t)ntgt * kWave, 256);
-    const int v = hm_var(), xcd = v & 1;
-#define ANISO_M2L_HM(NR, WPE)                                                                                      \
-    ANISO_HM_DISPATCH_K(K, (k_m2l_hm<KK, 2, NR, WPE><<<nb, 256, 0, s>>>(ntgt, xcd, tgt, ptr, src, blk, E, ncx, ncy, \
-                                                                         nrx, nry, P, hw, mult, local)))
-    switch ((v >> 1) & 3) {
-        case 0: ANISO_M2L_HM(2, 1); break;
-        case 1: ANISO_M2L_HM(1, 1); break;
-        case 2: ANISO_M2L_HM(2, 4); break;
-        default: ANISO_M2L_HM(1, 4); break;
-    }
-#undef ANISO_M2L_HM
+    ANISO_HM_DISPATCH_K(K, (k_m2l_hm<KK, 2, 2, 4><<<nb, 256, 0, s>>>(ntgt, 0, tgt, ptr, src, blk, E, ncx, ncy, nrx, nry,
+                                                                      P, hw, mult, local)));
     HIP_LAUNCH_CHECK();
 }
 
-
-template <int K, int NR, int NT, bool PF, int WPE>
-static void run_m2l_hc(int ncl, size_t shm, const int* clPtr, const int* tgt, const int64_t* ptr, const int* ndir,
-                       const int* src, const int* blk, const int* slot, const double* E, const double* ncx,
-                       const double* ncy, const double* nrx, const double* nry, const Params* P, const HarmWeights& hw,
-                       const double* mult, double* local, hipStream_t s) {
-    auto f = k_m2l_hc<K, NR, WPE, NT, PF>;  // WPE 3: no spills without PF (~166 VGPRs)
-    if (shm > 65536) {  // clusters of up to 64 targets at K = 8 need ~68 KB of the 160 KB LDS
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(f),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-        if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
-    }
-    f<<<ncl, NT, shm, s>>>(clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry, P, hw, mult, local,
-                           (hm_var() >> 6) & 1);
-}
-
+// clustered M2L (the default): 4 waves per cluster of <= 64 targets (512 / 768
+// threads, 2 waves per SIMD, 128-target clusters, a software-pipelined stream and an
+// XCD-contiguous cluster order all measured equal or slower, r01e-r01j), 3 waves per
+// SIMD; 1/r = v_rsq_f64 + ONE Newton step (~1e-13 relative per entry, 4 % faster
+// than two; the reduced-precision choice is tested at 1M points)
 void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, const int64_t* ptr, const int* ndir,
                    const int* src, const int* blk, const int* slot, const double* E, const double* ncx, const double* ncy,
                    const double* nrx, const double* nry, const Params* P, const HarmWeights& hw, const double* mult,
                    double* local, hipStream_t s) {
     if (ncl <= 0) return;
-    // 4 waves per cluster of <= 64 targets (512 / 768 measured slower, r01f); 8 for
-    // larger clusters (ANISO_HM_CL128)
-    const int nt = maxCl > 64 ? 512 : 256;
-    const size_t shm = (size_t)(maxCl + nt / kWave) * kRank * K * sizeof(double);
-    if (shm > 160 * 1024) throw std::invalid_argument("harmonic M2L cluster exceeds the LDS");
-    // ANISO_HM_VAR bit 3: software-pipelined block streams (PF); bit 4: 2 waves per
-    // SIMD instead of 3; bit 5: two Newton steps (default one: ~1e-13 per entry)
-    const int v = hm_var();
-#define ANISO_HC(NR, PF, WPE)                                                                                      \
-    ANISO_HM_DISPATCH_K(K, (run_m2l_hc<KK, NR, NT, PF, WPE>(ncl, shm, clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, \
-                                                             ncy, nrx, nry, P, hw, mult, local, s)))
-    const bool pf = (v >> 3) & 1, w2 = (v >> 4) & 1, nr2 = (v >> 5) & 1;
-    if (nt == 512) {
-        constexpr int NT = 512;
-        ANISO_HC(1, false, 2);
-    } else {
-        constexpr int NT = 256;
-        if (nr2) {
-            ANISO_HC(2, false, 3);
-        } else if (pf) {
-            if (w2) { ANISO_HC(1, true, 2); } else { ANISO_HC(1, true, 3); }
-        } else {
-            if (w2) { ANISO_HC(1, false, 2); } else { ANISO_HC(1, false, 3); }
+    if (maxCl > 64) throw std::invalid_argument("harmonic M2L cluster larger than 64 targets");
+    const size_t shm = (size_t)(maxCl + 256 / kWave) * kRank * K * sizeof(double);
+    ANISO_HM_DISPATCH_K(K, ({
+        auto f = k_m2l_hc<KK, 1, 3>;
+        if (shm > 65536) {  // clusters of up to 64 targets at K = 8 need ~68 KB of the 160 KB LDS
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(f),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+            if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
         }
-    }
-#undef ANISO_HC
+        f<<<ncl, 256, shm, s>>>(clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry, P, hw, mult, local);
+    }));
     HIP_LAUNCH_CHECK();
 }
 
+// near field: 16 lanes per leaf for leaves <= 16 points (4 leaves per wave), a wave
+// per leaf otherwise; 4 source columns in flight per lane (2 and 8, XCD-contiguous
+// leaves and leaf clusters measured slower, r01h); 1/r to full fp64 (two Newton steps)
 void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
                     const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
                     const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
                     int64_t ldo, int flags, double scale, double* out, hipStream_t s) {
     if (nl <= 0) return;
-#define ANISO_NEAR_HM(G, NR)                                                                                  \
-    ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, G, 4, NR><<<blocks_for((int64_t)nl * G, 256), 256, 0, s>>>(          \
+#define ANISO_NEAR_HM(G)                                                                                      \
+    ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, G, 4, 2><<<blocks_for((int64_t)nl * G, 256), 256, 0, s>>>(           \
                                nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm, \
                                obase, ldo, flags, scale, out)))
-#define ANISO_NEAR_HMV(UU, XX)                                                                                  \
-    ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, 16, UU, 2, XX><<<blocks_for((int64_t)nl * 16, 256), 256, 0, s>>>(       \
-                               nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm, \
-                               obase, ldo, flags, scale, out)))
-    const bool nr1 = (hm_var() & 2) != 0;
-    static const int nv = [] {  // ANISO_NEAR_VAR (experiments): 1 U = 2, 2 U = 8, 3 XCD order, 4 U = 8 + XCD order
-        const char* e = std::getenv("ANISO_NEAR_VAR");
-        return e ? std::atoi(e) : 0;
-    }();
-    if (maxLeaf <= 16 && !nr1 && nv > 0) {
-        switch (nv) {
-            case 1: ANISO_NEAR_HMV(2, false); break;
-            case 2: ANISO_NEAR_HMV(8, false); break;
-            case 3: ANISO_NEAR_HMV(4, true); break;
-            default: ANISO_NEAR_HMV(8, true); break;
-        }
-    } else if (maxLeaf <= 16) {  // 4 leaves per wave
-        if (nr1) {
-            ANISO_NEAR_HM(16, 1);
-        } else {
-            ANISO_NEAR_HM(16, 2);
-        }
+    if (maxLeaf <= 16) {
+        ANISO_NEAR_HM(16);
     } else {
-        if (nr1) {
-            ANISO_NEAR_HM(64, 1);
-        } else {
-            ANISO_NEAR_HM(64, 2);
-        }
+        ANISO_NEAR_HM(64);
     }
-#undef ANISO_NEAR_HMV
 #undef ANISO_NEAR_HM
-    HIP_LAUNCH_CHECK();
-}
-
-
-void launch_near_hc(int K, int ncl, const int* clPtr, const int* clLeaf, const int* clSlot, int maxPts,
-                    const int64_t* segPtr, const int4* seg, const int4* leafInfo, const int64_t* nearKOff,
-                    const double* E, const double* pxT, const double* pyT, const double* sigDiag,
-                    const HarmWeights& hw, const double* fT, const int* operm, int64_t obase, int64_t ldo,
-                    double scale, double* out, hipStream_t s) {
-    if (ncl <= 0) return;
-    const size_t shm = ((size_t)maxPts + 16 * 16) * K * sizeof(double);
-    if (shm > 64 * 1024) throw std::invalid_argument("harmonic near cluster exceeds 64 KB of LDS");
-    static const int u = [] {  // ANISO_NEAR_U: source columns in flight per lane (1, 2, 4)
-        const char* e = std::getenv("ANISO_NEAR_U");
-        const int v = e ? std::atoi(e) : 4;
-        return v == 1 || v == 2 ? v : 4;
-    }();
-#define ANISO_NHC(UU)                                                                                              \
-    ANISO_HM_DISPATCH_K(K, (k_near_hc<KK, 2, UU><<<ncl, 256, shm, s>>>(clPtr, clLeaf, clSlot, maxPts, segPtr, seg,  \
-                                                                       leafInfo, nearKOff, E, pxT, pyT, sigDiag, hw, \
-                                                                       fT, operm, obase, ldo, scale, out)))
-    if (u == 1) {
-        ANISO_NHC(1);
-    } else if (u == 2) {
-        ANISO_NHC(2);
-    } else {
-        ANISO_NHC(4);
-    }
-#undef ANISO_NHC
     HIP_LAUNCH_CHECK();
 }
 

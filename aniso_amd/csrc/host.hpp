@@ -109,21 +109,8 @@ struct Plan {
     std::vector<int> hmClPtr, hmTgt, hmSrc, hmBlk, hmSlot, hmNDir;
     std::vector<int64_t> hmPtr;
     int hmMaxCl = 0;
-    int hmEarly = 0;
-    int hmDepth = 0;  // cluster depth chosen (ancestor levels up)  // clusters [0, hmEarly) need only up tier 0's multipoles (§3.13)
+    int hmDepth = 0;  // cluster depth chosen (ancestor levels up)
     int64_t hmDual = 0;
-    // near field in clusters, block handles with leaves <= 16
-    // points: cluster c = leaves ncLeaf[ncPtr[c] .. ncPtr[c+1]) (same level, one
-    // ancestor kClusterDepth levels up), their points at LDS offsets ncSlot.  Per
-    // leaf li the source segments ncSeg[ncSegPtr[li] ..): {first source point (tree
-    // position), points, first column of li's E block, LDS point offset of the
-    // source leaf when li applies the pair both ways (-1: forward only)}; the
-    // partner of a two-way pair has no segment for it.
-    std::vector<int> ncPtr, ncLeaf, ncSlot;
-    std::vector<int64_t> ncSegPtr;
-    std::vector<std::array<int, 4>> ncSeg;
-    int ncMaxPts = 0;
-    int64_t ncDual = 0;
     // tiered up / down passes: tier k has root level
     // tierRootLevel[k] and bottom level tierBottomLevel[k] (k = 0 is the deepest).
     std::vector<int> tierRootLevel, tierBottomLevel;
@@ -167,9 +154,10 @@ struct Plan {
   private:
     void buildUpTasks(const Tree& t);
     void buildClusters(const Tree& t);
-    void buildNearClusters(const Tree& t);
     void buildDownTasks(const Tree& t);
 };
+
+std::vector<int64_t> shard_cuts(const Tree& t, int nranks);
 
 // Small per-mode tables for the correction stencil (nearRemoval + refineAddOn,
 // KernelFactory.cpp:445-478, 662-709) and the singular add-on moments

@@ -211,6 +211,41 @@ void Tree::build(const double* x, const double* y, int64_t n, int rank, int maxL
     }
 }
 
+// Shard boundaries (tree positions, nranks + 1 entries): the first level with at
+// least 16 x nranks nodes (plus the leaves above it) is the frontier; its nodes,
+// in tree order, are cut into nranks contiguous runs balanced by point count, so a
+// boundary never splits a frontier node (nor, therefore, a leaf).  Depends only on
+// the tree: every rank computes every rank's range.
+std::vector<int64_t> shard_cuts(const Tree& t, int nranks) {
+    if (nranks < 1) throw std::invalid_argument("nranks must be >= 1");
+    const int64_t N = t.nn ? t.count[0] : 0;
+    std::vector<int64_t> cuts(nranks + 1, N);
+    cuts[0] = 0;
+    if (nranks == 1) return cuts;
+    int Lc = 0;
+    std::vector<int> frontier;
+    for (;;) {
+        frontier.clear();
+        for (int i = 0; i < t.nn; ++i)
+            if (t.level[i] == Lc || (t.level[i] < Lc && t.isLeaf[i])) frontier.push_back(i);
+        if ((int)frontier.size() >= 16 * nranks || Lc >= t.maxLevel) break;
+        ++Lc;
+    }
+    std::sort(frontier.begin(), frontier.end(), [&](int a, int b) {
+        return t.begin[a] != t.begin[b] ? t.begin[a] < t.begin[b] : t.count[a] < t.count[b];
+    });
+    int r = 1;
+    for (int f : frontier) {
+        while (r < nranks && t.begin[f] + t.count[f] / 2 >= (N * r) / nranks) {
+            cuts[r] = t.begin[f];
+            ++r;
+        }
+    }
+    for (; r < nranks; ++r) cuts[r] = N;
+    for (int k = 1; k <= nranks; ++k) cuts[k] = std::max(cuts[k], cuts[k - 1]);
+    return cuts;
+}
+
 void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     (void)np;
     if (nranks_ < 1 || rank_ < 0 || rank_ >= nranks_) throw std::invalid_argument("bad shard rank/nranks");
@@ -223,37 +258,9 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     nranks = nranks_;
     const int64_t N = t.count[0];
     // ---- ownership: contiguous runs of a subtree frontier (DFS order == tree order)
-    if (nranks == 1) {
-        ownBegin = 0;
-        ownEnd = N;
-    } else {
-        int Lc = 0;
-        std::vector<int> frontier;
-        for (;;) {
-            frontier.clear();
-            for (int i = 0; i < t.nn; ++i)
-                if (t.level[i] == Lc || (t.level[i] < Lc && t.isLeaf[i])) frontier.push_back(i);
-            if ((int)frontier.size() >= 16 * nranks || Lc >= t.maxLevel) break;
-            ++Lc;
-        }
-        std::sort(frontier.begin(), frontier.end(), [&](int a, int b) {
-            return t.begin[a] != t.begin[b] ? t.begin[a] < t.begin[b] : t.count[a] < t.count[b];
-        });
-        // balance by point count; boundaries fall on frontier-node starts
-        std::vector<int64_t> cuts(nranks + 1, N);
-        cuts[0] = 0;
-        int r = 1;
-        for (int f : frontier) {
-            while (r < nranks && t.begin[f] + t.count[f] / 2 >= (N * r) / nranks) {
-                cuts[r] = t.begin[f];
-                ++r;
-            }
-        }
-        for (; r < nranks; ++r) cuts[r] = N;
-        for (int k = 1; k <= nranks; ++k) cuts[k] = std::max(cuts[k], cuts[k - 1]);
-        ownBegin = cuts[rank];
-        ownEnd = cuts[rank + 1];
-    }
+    const std::vector<int64_t> cuts = shard_cuts(t, nranks);
+    ownBegin = cuts[rank];
+    ownEnd = cuts[rank + 1];
     auto intersects = [&](int n) { return t.begin[n] < ownEnd && t.begin[n] + t.count[n] > ownBegin; };
     // ---- tiers for the up / down passes (bbfmm.h:825-861 upPass, 1066-1106
     // downPass): subtrees of at most 4 levels (the top one up to 5), each one
@@ -266,12 +273,10 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         tierRootLevel.clear();
         tierBottomLevel.clear();
         if (D >= 1) {
-            int bspan = 3;  // levels of the bottom tier (3: 4x the tasks at 1/4 the LDS; down 0.124 -> 0.090 ms, r01g); ANISO_BOTTOM_SPAN (1..4): experiments
-            if (const char* e = std::getenv("ANISO_BOTTOM_SPAN")) bspan = std::max(1, std::min(4, std::atoi(e)));
+            const int bspan = 3;  // levels of the bottom tier (3: 4x the tasks at 1/4 the LDS; down 0.124 -> 0.090 ms, r01g)
             tierRootLevel.push_back(std::max(1, D - (bspan - 1)));
             tierBottomLevel.push_back(D);
-            int span = 2;  // levels per upper tier; ANISO_TOP_SPAN (1..4): experiments
-            if (const char* e = std::getenv("ANISO_TOP_SPAN")) span = std::max(1, std::min(4, std::atoi(e)));
+            const int span = 2;  // levels per upper tier (1, 3 and 4 measured equal or slower, r01g)
             while (tierRootLevel.back() > 1) {
                 tierBottomLevel.push_back(tierRootLevel.back() - 1);
                 tierRootLevel.push_back(std::max(1, tierRootLevel.back() - span));
@@ -287,8 +292,6 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     // are numbered receiver-contiguously so k_m2l_gather reads one range per node.
     const char* symEnv = std::getenv("ANISO_SYMMETRIC");
     symmetric = !(symEnv && symEnv[0] == '0');
-    if (const char* mc = std::getenv("ANISO_MAX_CANON"))  // tuning/experiments only (<= kMaxCanon)
-        maxCanon = std::max(0, std::min(kMaxCanon, std::atoi(mc)));
     std::vector<char> m2lActive(t.nn, 0);
     for (int i = 0; i < t.nn; ++i) m2lActive[i] = !t.isEmpty[i] && t.parent[i] != -1 && intersects(i);
     std::vector<std::vector<int>> inCanon(t.nn), inFrom(t.nn);  // per receiver: canonical ids, their senders
@@ -436,7 +439,6 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
         }
         nearPtsPtr.push_back((int64_t)nearPts.size());
     }
-    buildNearClusters(t);
     buildDownTasks(t);
 }
 
@@ -662,39 +664,12 @@ void Plan::buildClusters(const Tree& t) {
     if (const char* e = std::getenv("ANISO_HM_CLDEPTH"))  // tuning/experiments only (1..kClusterDepth)
         depth = std::max(1, std::min(kClusterDepth, std::atoi(e)));
     hmDepth = depth;
-    // ANISO_HM_CL128=1 (experiment): half of the 256 targets under one ancestor 4
-    // levels up (the depth-3 subtrees of child quadrants {0,1} or {2,3}): 128 targets
-    const char* c128 = std::getenv("ANISO_HM_CL128");
-    const bool half = c128 && c128[0] == '1';
     std::vector<int64_t> key(nt);
     for (int w = 0; w < nt; ++w) {
         int a = m2lTgt[w];
         for (int k = 0; k < depth && t.parent[a] != -1; ++k) a = t.parent[a];
-        int64_t h = 0;
-        if (half && t.parent[a] != -1) {
-            const int p = t.parent[a];
-            for (int q = 0; q < 4; ++q)
-                if (t.child[p][q] == a) h = q >> 1;
-            a = p;
-        }
-        key[w] = ((int64_t)t.level[m2lTgt[w]] << 36) | (h << 32) | (uint32_t)a;
+        key[w] = ((int64_t)t.level[m2lTgt[w]] << 32) | (uint32_t)a;
     }
-    // "early" clusters first: every target and every source at or
-    // below the bottom up tier's root level, so their multipoles are final after
-    // up tier 0 and the cluster can run while the upper tiers climb
-    const int root0 = tierRootLevel.empty() ? (1 << 30) : tierRootLevel[0];
-    std::unordered_map<int64_t, bool> clusterEarly;
-    for (int w = 0; w < nt; ++w) {
-        bool early = t.level[m2lTgt[w]] >= root0;
-        for (int64_t e = attPtr[w]; e < attPtr[w + 1] && early; ++e) early = t.level[attSrc[e]] >= root0;
-        auto it = clusterEarly.find(key[w]);
-        if (it == clusterEarly.end())
-            clusterEarly[key[w]] = early;
-        else
-            it->second = it->second && early;
-    }
-    for (int w = 0; w < nt; ++w)
-        if (!clusterEarly[key[w]]) key[w] |= (int64_t)1 << 62;
     std::vector<int> order(nt);
     for (int w = 0; w < nt; ++w) order[w] = w;
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
@@ -711,11 +686,7 @@ void Plan::buildClusters(const Tree& t) {
         hmTgt.push_back(n);
     }
     hmClPtr.push_back(nt);
-    hmEarly = 0;
-    for (size_t c = 0; c + 1 < hmClPtr.size(); ++c) {
-        hmMaxCl = std::max(hmMaxCl, hmClPtr[c + 1] - hmClPtr[c]);
-        if (!(key[order[hmClPtr[c]]] >> 62)) hmEarly = (int)c + 1;
-    }
+    for (size_t c = 0; c + 1 < hmClPtr.size(); ++c) hmMaxCl = std::max(hmMaxCl, hmClPtr[c + 1] - hmClPtr[c]);
     hmNDir.clear();
     std::vector<int> dSrc, dBlk, dSlot;
     for (int k = 0; k < nt; ++k) {
@@ -743,76 +714,6 @@ void Plan::buildClusters(const Tree& t) {
         hmSlot.insert(hmSlot.end(), dSlot.begin(), dSlot.end());
         hmDual += (int64_t)dSrc.size();
         hmPtr.push_back((int64_t)hmSrc.size());
-    }
-}
-
-// Cluster plan of the harmonic near field from the directed near
-// lists (block handles only: nearSymmetric off, every leaf <= 16 points).
-void Plan::buildNearClusters(const Tree& t) {
-    ncPtr.assign(1, 0);
-    ncLeaf.clear();
-    ncSlot.clear();
-    ncSegPtr.assign(1, 0);
-    ncSeg.clear();
-    ncMaxPts = 0;
-    ncDual = 0;
-    const int nl = (int)leaves.size();
-    if (nl == 0 || nearSymmetric || nearMaxLeaf > 16) return;
-    int depth = kClusterDepth;
-    if (const char* e = std::getenv("ANISO_NEAR_CLDEPTH"))  // tuning/experiments only (1..kClusterDepth)
-        depth = std::max(1, std::min(kClusterDepth, std::atoi(e)));
-    std::vector<int64_t> key(nl);
-    for (int li = 0; li < nl; ++li) {
-        int a = leaves[li];
-        for (int k = 0; k < depth && t.parent[a] != -1; ++k) a = t.parent[a];
-        key[li] = ((int64_t)t.level[leaves[li]] << 32) | (uint32_t)a;
-    }
-    std::vector<int> order(nl);
-    for (int li = 0; li < nl; ++li) order[li] = li;
-    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
-    std::vector<int> clOf(t.nn, -1), slotOf(t.nn, -1);
-    int nc = 0, pts = 0;
-    for (int k = 0; k < nl; ++k) {
-        if (k > 0 && key[order[k]] != key[order[k - 1]]) {
-            ncPtr.push_back(k);
-            ncMaxPts = std::max(ncMaxPts, pts);
-            ++nc;
-            pts = 0;
-        }
-        const int n = leaves[order[k]];
-        clOf[n] = nc;
-        slotOf[n] = pts;
-        ncLeaf.push_back(order[k]);
-        ncSlot.push_back(pts);
-        pts += (int)t.count[n];
-    }
-    ncPtr.push_back(nl);
-    ncMaxPts = std::max(ncMaxPts, pts);
-    for (int li = 0; li < nl; ++li) {
-        const int a = leaves[li];
-        int col = 0;
-        for (int64_t j = nearPtr[li]; j < nearPtr[li + 1]; ++j) {
-            const int b = nearSrc[j];
-            const int cnt = (int)t.count[b];
-            // U members (j before the W part) that are leaves of a's cluster: the
-            // pair is applied both ways by the smaller node id.  The U relation is
-            // symmetric between leaves, so b's list holds a as well.
-            bool isU = false;
-            for (int64_t k = t.uPtr[a]; k < t.uPtr[a + 1]; ++k)
-                if (t.uIdx[k] == b) {
-                    isU = true;
-                    break;
-                }
-            const bool same = isU && b != a && clOf[b] >= 0 && clOf[b] == clOf[a];
-            if (same && b < a) {  // applied by b
-                col += cnt;
-                continue;
-            }
-            ncSeg.push_back({(int)t.begin[b], cnt, col, same ? slotOf[b] : -1});
-            if (same) ++ncDual;
-            col += cnt;
-        }
-        ncSegPtr.push_back((int64_t)ncSeg.size());
     }
 }
 

@@ -120,11 +120,6 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, 
                    const int* src, const int* blk, const int* slot, const double* E, const double* ncx, const double* ncy,
                    const double* nrx, const double* nry, const Params* P, const HarmWeights& hw, const double* mult,
                    double* local, hipStream_t s);
-void launch_near_hc(int K, int ncl, const int* clPtr, const int* clLeaf, const int* clSlot, int maxPts,
-                    const int64_t* segPtr, const int4* seg, const int4* leafInfo, const int64_t* nearKOff,
-                    const double* E, const double* pxT, const double* pyT, const double* sigDiag,
-                    const HarmWeights& hw, const double* fT, const int* operm, int64_t obase, int64_t ldo,
-                    double scale, double* out, hipStream_t s);
 void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
                     const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
                     const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,

@@ -21,14 +21,10 @@ def _is_torch(x):
 
 
 def shard_ranges(op, nranks):
-    """[(begin, end)] tree-order ranges of every shard, computed host-side."""
-    from . import Aniso  # noqa: F401
-
-    ranges = []
-    for r in range(nranks):
-        op.set_shard(r, nranks)
-        ranges.append(op.shard())
-    return ranges
+    """[(begin, end)] tree-order ranges of every shard, computed host-side without
+    changing the handle's shard or caches (aniso_shard_cuts)."""
+    c = op.shard_cuts(nranks)
+    return [(int(c[r]), int(c[r + 1])) for r in range(nranks)]
 
 
 def pad_len(ranges):

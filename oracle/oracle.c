@@ -1004,6 +1004,18 @@ static void sing_cache(oracle_t *o, int mode) {
         }
 }
 
+/* release mode id's caches (the reference keeps every mode cached; the bench's
+ * full-size CPU leg caches one mode at a time to bound host memory) */
+void oracle_uncache(oracle_t *o, int id) {
+    if (id < 0 || id >= o->kernelSize) return;
+    fmm_free(&o->imag[id]);
+    fmm_free(&o->real[id]);
+    free(o->nearI[id]);
+    free(o->singI[id]);
+    o->nearI[id] = NULL;
+    o->singI[id] = NULL;
+}
+
 /* cache(Id): runKernelsCache, runKernelsCacheSing, refineAddOnCache, singularAddCache
  * (AnisoWrapper.cpp:72-90, KernelFactory.cpp:279-334) */
 void oracle_cache(oracle_t *o, int id) {

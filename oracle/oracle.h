@@ -36,6 +36,8 @@ void oracle_get_weights(oracle_t *o, double *w);
 void oracle_set_coeff(oracle_t *o, const double *sigma_s, const double *sigma_t);
 /* cache(Id) (AnisoWrapper.cpp:72-90) */
 void oracle_cache(oracle_t *o, int id);
+/* free mode id's caches (not in the reference: bounds the full-size CPU leg's memory) */
+void oracle_uncache(oracle_t *o, int id);
 /* mapping(charge, Id) (AnisoWrapper.cpp:92-136); out: N doubles */
 void oracle_mapping(oracle_t *o, const double *charge, int id, double *out);
 /* Same apply, split by stage; stages is 6*N:

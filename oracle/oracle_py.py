@@ -29,6 +29,7 @@ def lib():
             "oracle_get_weights": (None, [P, dp]),
             "oracle_set_coeff": (None, [P, dp, dp]),
             "oracle_cache": (None, [P, I]),
+            "oracle_uncache": (None, [P, I]),
             "oracle_mapping": (None, [P, dp, I, dp]),
             "oracle_mapping_stages": (None, [P, dp, I, dp]),
             "oracle_set_faithful_rebuild": (None, [P, I]),
@@ -94,6 +95,9 @@ class Oracle:
 
     def cache(self, mode):
         lib().oracle_cache(self.h, int(mode))
+
+    def uncache(self, mode):
+        lib().oracle_uncache(self.h, int(mode))
 
     def mapping(self, charge, mode):
         c = np.ascontiguousarray(charge, dtype=np.float64)

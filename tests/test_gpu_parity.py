@@ -379,6 +379,18 @@ def test_block_operator_matches_oracle(sz, d, ks, coeffs):
         torch.cuda.synchronize()
         ref = _block_ref(o, U, a.g, ss, which)
         assert _rel(out.cpu().numpy(), ref) <= TOL, (which, _rel(out.cpu().numpy(), ref))
+        # the host-pointer boundary (aniso_block_op; the MEX shim's forward /
+        # mforward / blockMatvec ops): stacked aniso.m column in, same result
+        host = a.block_op(which, U.reshape(-1))
+        assert _rel(host, ref) <= TOL, (which, _rel(host, ref))
+    # SURVEY.md §8b aniso_apply_block(h, u, sigma_s, g, out): explicit sigma_s and g,
+    # both different from the handle's (the caches depend on sigma_t only)
+    ss2 = ss * 0.5 + 0.25
+    ref = _block_ref(o, U, 0.6, ss2, 2)
+    host = a.apply_block(U, ss2, 0.6)
+    assert _rel(host, ref) <= TOL, _rel(host, ref)
+    # ... and the handle's own sigma_s / g again afterwards (no state leaks)
+    assert _rel(a.block_op(2, U), _block_ref(o, U, a.g, ss, 2)) <= TOL
 
 
 @pytest.mark.parametrize("nrhs,near_sym", [(1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (8, 0), (2, 1), (5, 1)])
@@ -599,35 +611,32 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatc
     assert _rel(outs[0], outs[1]) <= 1e-13
 
 
-@pytest.mark.parametrize("sz,d,ks,ml", [(32, 1, 5, 20), (19, 2, 3, 20), (64, 1, 2, 20), (40, 1, 5, 3), (27, 3, 4, 20)])
-def test_harmonic_near_clusters_match_per_leaf_groups(sz, d, ks, ml, monkeypatch):
-    """The clustered harmonic near field (a U pair of two cluster
-    leaves applied both ways from one read of its sub-block, sums in LDS) against the
-    per-leaf kernel (ANISO_NEAR_CLUSTER=0); odd sz, d = 2 and 3, and a maxLevel-limited
-    tree whose leaves exceed 16 points (clusters off, per-leaf kernel)."""
+@pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0"])
+def test_block_matvec_knobs_agree(knob, monkeypatch):
+    """Every remaining environment knob of the block apply:
+    the serial near/M2L order, the separate x - mforward(x) subtraction and the
+    per-mode operator stream give the default's block matvec to rounding."""
     torch = _torch()
     import aniso_amd
 
-    outs, st = [], []
-    for cl in ("1", "0"):
-        monkeypatch.setenv("ANISO_NEAR_CLUSTER", cl)
-        a = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, ml)
+    sz, ks = 32, 5
+    outs = []
+    for env in (None, knob):
+        if env:
+            k, v = env.split("=")
+            monkeypatch.setenv(k, v)
+        a = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
         xy = a.getNodes()
-        a.setCoeff(*rough_coeffs(xy, 3))
+        a.setCoeff(*rough_coeffs(xy, 4))
         for m in range(2 * ks - 1):
             a.cache(m)
-        st.append(a.stats())
-        U = torch.tensor(np.random.default_rng(7).uniform(-1, 1, (ks, a.N)), device="cuda")
+        U = torch.tensor(np.random.default_rng(11).uniform(-1, 1, (ks, a.N)), device="cuda")
         out = torch.zeros_like(U)
         a.block_op_dev(2, U, out)
         torch.cuda.synchronize()
         outs.append(out.cpu().numpy())
-    assert st[0]["harmonic"] == 1 and st[1]["near_clusters"] == 0
-    if st[0]["max_leaf"] <= 16:
-        assert st[0]["near_clusters"] > 0 and st[0]["near_dual_pairs"] > 0
-    else:
-        assert st[0]["near_clusters"] == 0
-    assert _rel(outs[0], outs[1]) <= 1e-13
+        a.close()
+    assert _rel(outs[0], outs[1]) <= 1e-12
 
 
 def test_block_matvec_eight_shards_at_config3_size():
