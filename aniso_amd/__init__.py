@@ -115,13 +115,14 @@ def _f64(a, n, name):
     return a
 
 
-def _dev_vec(t, n, name):
-    """A contiguous float64 CUDA tensor of exactly n entries (else AnisoError)."""
+def _dev_vec(t, n, name, at_least=False):
+    """A contiguous float64 CUDA tensor of n entries (at least n for an output slice
+    the kernels fill from the front; else AnisoError)."""
     import torch
 
     if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()
-            and t.numel() == n):
-        raise AnisoError(1, f"{name} must be a contiguous float64 CUDA tensor of {n} entries")
+            and (t.numel() >= n if at_least else t.numel() == n)):
+        raise AnisoError(1, f"{name} must be a contiguous float64 CUDA tensor of {'>= ' if at_least else ''}{n} entries")
     return ctypes.c_void_p(t.data_ptr())
 
 
@@ -229,7 +230,7 @@ class Aniso:
         """mapping on a tree-order device vector (all N) into the owned tree-order slice."""
         import torch
 
-        pq, po = _dev_vec(q_tree, self.N, "q_tree"), _dev_vec(out_slice, self.n_owned(), "out_slice")
+        pq, po = _dev_vec(q_tree, self.N, "q_tree"), _dev_vec(out_slice, self.n_owned(), "out_slice", True)
         s = torch.cuda.current_stream().cuda_stream if stream is None else stream
         _check(lib().aniso_mapping_tree_dev(self.address, pq, int(id_), po, ctypes.c_void_p(s)))
         return out_slice
@@ -238,7 +239,7 @@ class Aniso:
         """forwardOperator in tree order: y_slice = (x - K_0(sigma_s .* x))[own slice], x tree-ordered."""
         import torch
 
-        px, py = _dev_vec(x_tree, self.N, "x_tree"), _dev_vec(y_slice, self.n_owned(), "y_slice")
+        px, py = _dev_vec(x_tree, self.N, "x_tree"), _dev_vec(y_slice, self.n_owned(), "y_slice", True)
         s = torch.cuda.current_stream().cuda_stream if stream is None else stream
         _check(lib().aniso_forward_tree_dev(self.address, px, py, ctypes.c_void_p(s)))
         return y_slice
