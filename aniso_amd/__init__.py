@@ -77,6 +77,13 @@ def lib():
             "aniso_block_op": [P, I, dp, dp],
             "aniso_apply_block": [P, dp, dp, D, dp],
             "aniso_shard_cuts": [P, I, lp],
+            "aniso_shard_exchange": [P, I, lp],
+            "aniso_shard_halo": [P, lp],
+            "aniso_shard_roots": [P, ip, ip, ip],
+            "aniso_forward_tree_begin_dev": [P, P, P, P, P],
+            "aniso_forward_tree_end_dev": [P, P, P, P, P],
+            "aniso_block_op_begin_dev": [P, I, P, I64, P, I64, P, P],
+            "aniso_block_op_end_dev": [P, I, P, I64, P, I64, P, P],
             "aniso_last_error": [ctypes.c_char_p, ctypes.c_size_t],
         }
         for name, args in sig.items():
@@ -281,6 +288,60 @@ class Aniso:
                                         ctypes.c_void_p(s)))
         return out
 
+    # ---- sharded applies in two phases around the caller's root all-gather
+    # (aniso_shard_exchange)
+    def _roots_buf(self, t, n, name):
+        if n == 0:
+            return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() else None
+        return _dev_vec(t, n, name, True)
+
+    def block_op_begin_dev(self, which, x, out, roots_send, stream=None):
+        """Phase 1 of the sharded x - mforward(x) etc.: x (ks, N) tree order, valid at
+        the own range and the halo; out (ks, >= n_owned); roots_send >= C x R doubles."""
+        import torch
+
+        ex = self.shard_exchange(self.ks)
+        _dev_rows(x, self.ks, self.N, "x")
+        _dev_rows(out, self.ks, self.n_owned(), "out")
+        rs = self._roots_buf(roots_send, ex["root_chunk"] * ex["root_record"], "roots_send")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_block_op_begin_dev(self.address, int(which), ctypes.c_void_p(x.data_ptr()),
+                                              int(x.stride(0)), ctypes.c_void_p(out.data_ptr()), int(out.stride(0)),
+                                              rs, ctypes.c_void_p(s)))
+
+    def block_op_end_dev(self, which, x, out, roots_recv, nranks, stream=None):
+        """Phase 2: roots_recv = the all-gather of every rank's roots_send (nranks x C x R)."""
+        import torch
+
+        ex = self.shard_exchange(self.ks)
+        _dev_rows(x, self.ks, self.N, "x")
+        _dev_rows(out, self.ks, self.n_owned(), "out")
+        rr = self._roots_buf(roots_recv, nranks * ex["root_chunk"] * ex["root_record"], "roots_recv")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_block_op_end_dev(self.address, int(which), ctypes.c_void_p(x.data_ptr()), int(x.stride(0)),
+                                            ctypes.c_void_p(out.data_ptr()), int(out.stride(0)), rr,
+                                            ctypes.c_void_p(s)))
+        return out
+
+    def forward_tree_begin_dev(self, x_tree, y_slice, roots_send, stream=None):
+        import torch
+
+        ex = self.shard_exchange(1)
+        px, py = _dev_vec(x_tree, self.N, "x_tree"), _dev_vec(y_slice, self.n_owned(), "y_slice", True)
+        rs = self._roots_buf(roots_send, ex["root_chunk"] * ex["root_record"], "roots_send")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_forward_tree_begin_dev(self.address, px, py, rs, ctypes.c_void_p(s)))
+
+    def forward_tree_end_dev(self, x_tree, y_slice, roots_recv, nranks, stream=None):
+        import torch
+
+        ex = self.shard_exchange(1)
+        px, py = _dev_vec(x_tree, self.N, "x_tree"), _dev_vec(y_slice, self.n_owned(), "y_slice", True)
+        rr = self._roots_buf(roots_recv, nranks * ex["root_chunk"] * ex["root_record"], "roots_recv")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_forward_tree_end_dev(self.address, px, py, rr, ctypes.c_void_p(s)))
+        return y_slice
+
     def block_op(self, which, u):
         """aniso.m forward (0) / mforward (1) / x - mforward(x) (2) on host arrays:
         u is (ks, N) or the stacked ks*N column of aniso.m; returns (ks, N)."""
@@ -327,6 +388,32 @@ class Aniso:
         _check(lib().aniso_shard_cuts(self.address, int(nranks), c.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
         return c
 
+    def shard_exchange(self, nrhs=1):
+        """The exchange plan of this handle's shard (aniso_shard_exchange), host only."""
+        info = np.zeros(9, dtype=np.int64)
+        _check(lib().aniso_shard_exchange(self.address, int(nrhs), info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        keys = ["root_chunk", "root_record", "halo_ranges", "halo_points", "t0_level", "t0_run", "roots_sent",
+                "t0_tasks", "nranks"]
+        return dict(zip(keys, (int(v) for v in info)))
+
+    def shard_halo(self):
+        """(n, 2) array of [b, e) tree-position ranges outside the own range the input must hold."""
+        n = self.shard_exchange()["halo_ranges"]
+        r = np.zeros(2 * n + 1, dtype=np.int64)
+        _check(lib().aniso_shard_halo(self.address, r.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        return r[: 2 * n].reshape(n, 2)
+
+    def shard_roots(self):
+        """(roots sent by this rank, all-gather slot -> node (-1 padding), roots of the tier-0 tasks run here)."""
+        ex = self.shard_exchange()
+        send = np.zeros(ex["roots_sent"] + 1, dtype=np.int32)
+        recv = np.zeros(ex["nranks"] * ex["root_chunk"] + 1, dtype=np.int32)
+        t0 = np.zeros(ex["t0_run"] + 1, dtype=np.int32)
+        ip = ctypes.POINTER(ctypes.c_int)
+        _check(lib().aniso_shard_roots(self.address, send.ctypes.data_as(ip), recv.ctypes.data_as(ip),
+                                       t0.ctypes.data_as(ip)))
+        return send[:-1], recv[:-1], t0[:-1]
+
     def tree_perm(self):
         p = np.zeros(self.N, dtype=np.int32)
         _check(lib().aniso_tree_perm(self.address, p.ctypes.data_as(ctypes.POINTER(ctypes.c_int))))
@@ -367,7 +454,7 @@ class Aniso:
     def stage_times(self):
         t = (ctypes.c_float * 8)()
         _check(lib().aniso_stage_times(self.address, t))
-        return dict(zip(["prep", "up", "m2l", "gather", "near", "down", "corr", "total"], list(t)))
+        return dict(zip(["exchange", "up", "m2l", "gather", "near", "down", "corr", "total"], list(t)))
 
     def line_integrals(self, seg):
         seg = np.ascontiguousarray(np.asarray(seg, dtype=np.float64).reshape(-1, 4))

@@ -73,6 +73,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_NEAR_SYMMETRIC")) plan.nearSymmetric = e[0] == '1';
     plan.maxCanon = ks == 1 ? kMaxCanon : kMaxCanonBlock;
     plan.build(tree, np, 0, 1);
+    plan.buildExchange(tree, geo.sz, geo.d2);
     // block handles apply aniso.m's operator through the mode-shared E caches
     // (DESIGN.md §3.9); ANISO_HARMONIC=0 keeps the per-mode operator stream
     useAtt = ks > 1 && !plan.nearSymmetric;
@@ -108,6 +109,8 @@ void Operator::getNodes(double* xy) const {
 
 void Operator::setShard(int rank, int nranks) {
     plan.build(tree, np, rank, nranks);
+    plan.buildExchange(tree, geo.sz, geo.d2);
+    pend = Pending();
     for (auto& m : modes) {
         m.Knear.alloc(0);
         m.Km2l.alloc(0);
@@ -286,6 +289,10 @@ void Operator::uploadPlan() {
     up(dLeafInfo, to_int4(plan.leafInfo));
     up(dNearPtsPtr, plan.nearPtsPtr);
     up(dNearPts, plan.nearPts);
+    up(dXT0Tasks, plan.xT0Tasks);
+    up(dXRootRecv, plan.xRootRecv);
+    up(dXRootSlot, plan.xRootSlot);
+    up(dXSendSlot, plan.xSendSlot);
     up(dUpTaskPtr, plan.upTaskPtr);
     up(dUpGrpPtr, plan.upGrpPtr);
     up(dUpGrp, plan.upGrp);
@@ -486,7 +493,18 @@ void Operator::mappingTreeDev(const double* qTree, int id, double* outSlice, hip
 // main.cpp forwardOperator (main.cpp:125-136) in tree order: y = x - K_0(sigma_s x)
 // on the owned slice, x tree-ordered (all N).
 void Operator::forwardTreeDev(const double* xTree, double* ySlice, hipStream_t s) {
-    apply(xTree, true, dSigmaT.as<double>(), 0, dTmpS.as<double>(), true, s, kStageAll);
+    forwardTreePhase(0, xTree, ySlice, nullptr, nullptr, s);
+}
+
+void Operator::forwardTreePhase(int phase, const double* xTree, double* ySlice, double* rootsSend,
+                                const double* rootsRecv, hipStream_t s) {
+    if (!modeCached(0)) throw std::runtime_error("forward operator before cache(0)");
+    ensureDevice();
+    const double one = 1.0;
+    const int id = 0;
+    applyBlock(1, xTree, geo.N, true, dSigmaT.as<double>(), 1, &id, &one, dTmpS.as<double>(), geo.N, true, s,
+               kStageAll, phase, rootsSend, rootsRecv);
+    if (phase == 1) return;
     const int64_t n = plan.ownEnd - plan.ownBegin;
     launch_sub_slice(n, 1, xTree + plan.ownBegin, n, dTmpS.as<double>(), n, ySlice, n, s);
 }
@@ -585,9 +603,16 @@ const CorrFold& Operator::corrTable(int K, int nterm, const int* ids, const doub
 // ids[t], mix mixes[t]) the near field, the corrections, the M2L stream and its
 // gather, each accumulating; then one down pass.  sigT (sigma_s in tree order, or
 // nullptr) multiplies the inputs at their tree positions.
+//
+// phase 1 / 2 split a sharded apply around the caller's all-gather of the tier-0
+// root multipoles: phase 1 runs this rank's tier-0 up tasks only
+// (plan.xT0Tasks), packs its roots into rootsSend and starts the near field and
+// corrections (they need only the weighted charges of the rank's own and halo
+// points); phase 2 scatters rootsRecv, runs the upper tiers (every rank), the M2L
+// and the down pass.
 void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, const double* sigT, int nterm,
                           const int* ids, const double* mixes, double* out, int64_t ldo, bool treeOut, hipStream_t s,
-                          int mask) {
+                          int mask, int phase, double* rootsSend, const double* rootsRecv) {
     if (K < 1 || K > 8) throw std::invalid_argument("block apply supports 1..8 right-hand sides, got " + std::to_string(K));
     if (nterm < 1) throw std::invalid_argument("block apply needs at least one mode term");
     for (int t = 0; t < nterm; ++t) {
@@ -595,6 +620,11 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         if (!modes[ids[t]].ready)
             throw std::runtime_error("mapping on kernel id " + std::to_string(ids[t]) + " before cache(" + std::to_string(ids[t]) + ")");
     }
+    if (phase != 0 && !treeIn) throw std::invalid_argument("a sharded (two-phase) apply takes tree-order input");
+    if (phase == 1 && plan.xRootChunk > 0 && !rootsSend) throw std::invalid_argument("sharded apply: null roots_send");
+    if (phase == 2 && plan.xRootChunk > 0 && !rootsRecv) throw std::invalid_argument("sharded apply: null roots_recv");
+    if (phase == 2 && !(pend.active && pend.K == rootRhs(K)))
+        throw std::logic_error("sharded apply: end without a matching begin");
     ensureDevice();
     const int64_t nOut = treeOut ? plan.ownEnd - plan.ownBegin : geo.N;
     if (ldx < geo.N || ldo < nOut) throw std::invalid_argument("block apply: leading dimension too small");
@@ -602,17 +632,20 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         const int Kp = rhs_padded(K);
         dPadIn.alloc((size_t)Kp * geo.N * sizeof(double));
         dPadOut.alloc((size_t)Kp * geo.N * sizeof(double));
-        HIP_CHECK(hipMemsetAsync(dPadIn.p, 0, dPadIn.bytes, s));
-        HIP_CHECK(hipMemcpy2DAsync(dPadIn.p, geo.N * sizeof(double), x, ldx * sizeof(double), geo.N * sizeof(double), K,
-                                   hipMemcpyDeviceToDevice, s));
+        if (phase != 2) {  // phase 2 reads what phase 1 staged
+            HIP_CHECK(hipMemsetAsync(dPadIn.p, 0, dPadIn.bytes, s));
+            HIP_CHECK(hipMemcpy2DAsync(dPadIn.p, geo.N * sizeof(double), x, ldx * sizeof(double),
+                                       geo.N * sizeof(double), K, hipMemcpyDeviceToDevice, s));
+        }
         std::vector<double> mp((size_t)nterm * Kp * Kp, 0.0);
         for (int t = 0; t < nterm; ++t)
             for (int i = 0; i < K; ++i)
                 for (int b = 0; b < K; ++b) mp[((size_t)t * Kp + i) * Kp + b] = mixes[((size_t)t * K + i) * K + b];
         applyBlock(Kp, dPadIn.as<double>(), geo.N, treeIn, sigT, nterm, ids, mp.data(), dPadOut.as<double>(), geo.N,
-                   treeOut, s, mask);
-        HIP_CHECK(hipMemcpy2DAsync(out, ldo * sizeof(double), dPadOut.p, geo.N * sizeof(double), nOut * sizeof(double),
-                                   K, hipMemcpyDeviceToDevice, s));
+                   treeOut, s, mask, phase, rootsSend, rootsRecv);
+        if (phase != 1)
+            HIP_CHECK(hipMemcpy2DAsync(out, ldo * sizeof(double), dPadOut.p, geo.N * sizeof(double),
+                                       nOut * sizeof(double), K, hipMemcpyDeviceToDevice, s));
         return;
     }
     ensureWork(K);
@@ -624,122 +657,148 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     auto span = [&](int stage, int a, int b) {
         if (tm) spans.push_back({stage, a, b});
     };
-    const int e0 = tm ? mark(s) : -1;
     const int* operm = treeOut ? nullptr : dPerm.as<int>();
     const int64_t obase = treeOut ? plan.ownBegin : 0;
     const double scale = M_1_PI / 2.0;  // AnisoWrapper.cpp:129-130
-    // up pass (global, every rank): tiers bottom-up; its P2M also forms the weighted
-    // charges fT (tree order) the near field and the corrections read
-    if (plan.upTierTask.size() < 2)  // a lone leaf: no up pass
-        launch_prepare(K, geo.N, x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(),
-                       dCT.as<double>(), s);
     HarmWeights hw;
     const bool harmonic = harmonicWeights(K, nterm, ids, mixes, hw);
-    // the harmonic block apply forks its near field off as soon as the charges are
-    // complete: after the last up tier with a P2M leaf (the tiers above only M2M)
+    // the harmonic block apply runs its near field + corrections (they write `out`)
+    // on a side stream beside the M2L (it writes the locals), forked as soon as the
+    // weighted charges are complete: after the last up tier with a P2M leaf
     const bool fork = harmonic && overlap;
-    if (fork && plan.upTierTask.size() < 2) HIP_CHECK(hipEventRecord(evFork, s));
-    for (size_t k = 0; k + 1 < plan.upTierTask.size(); ++k) {
-        launch_up_tier(K, plan.upTierTask[k + 1] - plan.upTierTask[k], plan.upTierTask[k], plan.upMaxTask,
-                       dUpDesc.as<int4>(), dUpGrpFix.as<int>(), dUpNode.as<int>(), dUpCode.as<int4>(),
-                       dUpGeom.as<double4>(), dUpLeaf.as<int2>(), dPxT.as<double>(), dPyT.as<double>(), x, ldx,
-                       treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(), dFT.as<double>(), dCT.as<double>(), P,
-                       dMult.as<double>(), s);
-        if (fork && (int)k == plan.upLastLeafTier) HIP_CHECK(hipEventRecord(evFork, s));
+    const hipStream_t sn = fork ? side : s;
+    const ModeArgs* tab = modeTable(K, nterm, ids, mixes);
+    const CorrFold& cf = corrTable(K, nterm, ids, mixes);
+    const int ntier = (int)plan.upTierTask.size() - 1;  // 0: a lone leaf
+    // the near field forks after the whole up pass on one GPU: forked after the
+    // bottom tier it starved the latency-bound upper tiers the M2L waits on (up pass
+    // 0.25 -> 0.14 ms, 644 -> 660 block matvec/s); a sharded apply starts it in
+    // phase 1, beside the root exchange (8 shards: 0.317 vs 0.327 ms per rank)
+    const int forkTier = phase == 0 ? std::max(ntier - 1, 0) : plan.upLastLeafTier;
+    // one up tier; a sharded apply's bottom tier runs this rank's tasks only (list)
+    // and stores its tier-0 roots into send, its next tier reads the gathered ones
+    auto upTier = [&](int k, const int* list, int ntask, const double* recv, double* send) {
+        launch_up_tier(K, ntask, plan.upTierTask[k], list, plan.upMaxTask, dUpDesc.as<int4>(), dUpGrpFix.as<int>(),
+                       dUpNode.as<int>(), dUpCode.as<int4>(), dUpGeom.as<double4>(), dUpLeaf.as<int2>(),
+                       dPxT.as<double>(), dPyT.as<double>(), x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT,
+                       dWT.as<double>(), dFT.as<double>(), dCT.as<double>(), P, dMult.as<double>(),
+                       recv ? dXRootSlot.as<int>() : nullptr, recv, send ? dXSendSlot.as<int>() : nullptr, send, s);
+        if (fork && k == forkTier) HIP_CHECK(hipEventRecord(evFork, s));
+    };
+    auto tierTasks = [&](int k) { return plan.upTierTask[k + 1] - plan.upTierTask[k]; };
+    // near field + corrections (they need only fT / cT)
+    auto nearStage = [&] {
+        if (fork) HIP_CHECK(hipStreamWaitEvent(side, evFork, 0));
+        const int en = tm ? mark(sn) : -1;
+        if (harmonic) {
+            launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
+                           dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(), dNearKOff.as<int64_t>(),
+                           dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dSigDiag.as<double>(), hw,
+                           dFT.as<double>(), operm, obase, ldo, mask, scale, out, sn);
+        } else if (plan.nearPartTotal > 0) {
+            // symmetric U storage (K = 1 handles): one launch per term; the transposed
+            // products go to partials summed over the terms
+            for (int t = 0; t < nterm; ++t) {
+                const int id = ids[t];
+                // K_{B<-A} = (-1)^m K_{A<-B}^T for the merged kernel; Id = m
+                const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
+                launch_near_sym(K, (int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
+                                dNearPts.as<int>(), dNearKOff.as<int64_t>(), dNearSym.as<int2>(),
+                                modes[id].Knear.as<double>(), dFT.as<double>(), mixes + (size_t)t * K * K, operm,
+                                obase, ldo, maxNearS, mask, sgn, scale, t > 0 ? 1 : 0, dNearPart.as<double>(), out, s);
+            }
+        } else {  // directed storage: all terms in one launch
+            launch_near(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
+                        dNearPts.as<int>(), dNearKOff.as<int64_t>(), tab, nterm, dFT.as<double>(), operm, obase, ldo,
+                        mask, scale, 0, out, s);
+        }
+        const int e1 = tm ? mark(sn) : -1;
+        span(4, en, e1);
+        launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
+                    dFT.as<double>(), cf.Wc.as<double>(), cf.Wm.as<double>(), P, mask, scale, treeOut, ldo, out, sn);
+        const int e2 = tm ? mark(sn) : -1;
+        span(6, e1, e2);
+        if (fork) HIP_CHECK(hipEventRecord(evJoin, side));
+    };
+    const bool clustered = harmonic && useClusters;
+    const int ncl = (int)plan.hmClPtr.size() - 1;
+    auto m2lClusters = [&](int c0, int c1, hipStream_t st) {
+        launch_m2l_hc(K, c1 - c0, plan.hmMaxCl, dHmClPtr.as<int>() + c0, dHmTgt.as<int>(), dHmPtr.as<int64_t>(),
+                      dHmNDir.as<int>(), dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(), dAttM2L.as<double>(),
+                      dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), P, hw,
+                      dMult.as<double>(), dLocal.as<double>(), st);
+    };
+    int e0 = -1;
+    bool nearDone = false;
+    if (phase != 2) {
+        // up pass: tiers bottom-up; its P2M also forms the weighted charges fT (tree
+        // order) the near field and the corrections read
+        e0 = tm ? mark(s) : -1;
+        if (ntier < 1) {  // a lone leaf: no up pass
+            launch_prepare(K, geo.N, x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(),
+                           dFT.as<double>(), dCT.as<double>(), s);
+            if (fork) HIP_CHECK(hipEventRecord(evFork, s));
+        }
+        if (phase == 1 && ntier >= 1)
+            upTier(0, dXT0Tasks.as<int>(), (int)plan.xT0Tasks.size(), nullptr, rootsSend);
+        for (int k = 0; k < ntier && phase == 0; ++k) upTier(k, nullptr, tierTasks(k), nullptr, nullptr);
+        if (phase == 1) {
+            const int ep = tm ? mark(s) : -1;
+            span(1, e0, ep);
+            if (ntier < 1 || forkTier == 0) {
+                nearStage();
+                nearDone = true;
+            }
+            pend.active = true;
+            pend.nearDone = nearDone;
+            pend.K = K;
+            pend.e0 = e0;
+            pend.ePack = ep;
+            return;
+        }
+    } else {
+        e0 = pend.e0;
+        nearDone = pend.nearDone;
+        pend.active = false;
+        const int ex = tm ? mark(s) : -1;
+        span(0, pend.ePack, ex);  // the caller's root exchange
+        if (ntier >= 2) {  // the first upper tier reads the gathered roots (and stores them for the M2L)
+            upTier(1, nullptr, tierTasks(1), rootsRecv, nullptr);
+            for (int k = 2; k < ntier; ++k) upTier(k, nullptr, tierTasks(k), nullptr, nullptr);
+        } else {
+            launch_roots_unpack(K, (int)plan.xRootRecv.size(), dXRootRecv.as<int>(), rootsRecv, dMult.as<double>(),
+                                s);
+        }
+        e0 = ex;  // the up span of phase 2: upper tiers
     }
     int ep = tm ? mark(s) : -1;
     span(1, e0, ep);
-    const ModeArgs* tab = modeTable(K, nterm, ids, mixes);
-    const CorrFold& cf = corrTable(K, nterm, ids, mixes);
-    if (harmonic) {
-        // every mode of aniso.m's block operator from one read of the E caches.
-        // Near field + corrections (they write `out`) on the side stream beside the
-        // M2L (it writes the locals); the down pass adds into `out` after the join.
-        // overlap 1: near enqueued first; 2: the M2L first.
-        const hipStream_t sn = overlap ? side : s;
-        int e = -1;
-        auto nearStage = [&] {
-            int en = tm ? (overlap ? mark(sn) : ep) : -1;
-            launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
-                               dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(), dNearKOff.as<int64_t>(),
-                               dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dSigDiag.as<double>(), hw,
-                               dFT.as<double>(), operm, obase, ldo, mask, scale, out, sn);
-            int e1 = tm ? mark(sn) : -1;
-            span(4, en, e1);
-            launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
-                        dFT.as<double>(), cf.Wc.as<double>(), cf.Wm.as<double>(), P, mask, scale, treeOut, ldo, out,
-                        sn);
-            int e2 = tm ? mark(sn) : -1;
-            span(6, e1, e2);
-            if (!overlap) ep = e2;
-            if (overlap) HIP_CHECK(hipEventRecord(evJoin, side));
-        };
-        const int ncl = (int)plan.hmClPtr.size() - 1;
-        auto farStage = [&] {
-            if ((mask & kStageFar) && useClusters)
-                launch_m2l_hc(K, ncl, plan.hmMaxCl, dHmClPtr.as<int>(), dHmTgt.as<int>(), dHmPtr.as<int64_t>(),
-                              dHmNDir.as<int>(), dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(),
-                              dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
-                              dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
-            else if (mask & kStageFar)
-                launch_m2l_hm(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dAttPtr.as<int64_t>(), dAttSrc.as<int>(),
-                              dAttBlk.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(),
-                              dNrx.as<double>(), dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
-            e = tm ? mark(s) : -1;
-            span(2, ep, e);
-            ep = e;
-        };
-        if (overlap == 2) {
-            farStage();
-            HIP_CHECK(hipStreamWaitEvent(side, evFork, 0));
-            nearStage();
+    if (phase == 2) e0 = pend.e0;
+    if (!nearDone) nearStage();
+    if (mask & kStageFar) {
+        if (clustered) {
+            m2lClusters(0, ncl, s);
+        } else if (harmonic) {
+            launch_m2l_hm(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dAttPtr.as<int64_t>(), dAttSrc.as<int>(),
+                          dAttBlk.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(),
+                          dNrx.as<double>(), dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(), s);
         } else {
-            if (overlap) HIP_CHECK(hipStreamWaitEvent(side, evFork, 0));
-            nearStage();
-            farStage();
+            launch_m2l(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(),
+                       dM2LCanonBase.as<int>(), dM2LOutSlot.as<int>(), dM2LSrc.as<int>(), tab, nterm,
+                       dMult.as<double>(), plan.m2lMaxCanon, dM2LPart.as<double>(), dLocal.as<double>(), s);
         }
-        if (overlap) HIP_CHECK(hipStreamWaitEvent(s, evJoin, 0));
-    } else {
-    // near field: symmetric U storage (K = 1 handles) one launch per term (its
-    // transposed products go to partials, summed over the terms); directed
-    // storage all terms in one launch
-    if (plan.nearPartTotal > 0) {
-        for (int t = 0; t < nterm; ++t) {
-            const int id = ids[t];
-            // K_{B<-A} = (-1)^m K_{A<-B}^T for the merged kernel; Id = m
-            const double sgn = (id % 2 == 0) ? 1.0 : -1.0;
-            launch_near_sym(K, (int)plan.leaves.size(), dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
-                            dNearPts.as<int>(), dNearKOff.as<int64_t>(), dNearSym.as<int2>(),
-                            modes[id].Knear.as<double>(), dFT.as<double>(), mixes + (size_t)t * K * K, operm, obase,
-                            ldo, maxNearS, mask, sgn, scale, t > 0 ? 1 : 0, dNearPart.as<double>(), out, s);
-        }
-    } else {
-        launch_near(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
-                    dNearPts.as<int>(), dNearKOff.as<int64_t>(), tab, nterm, dFT.as<double>(), operm, obase, ldo, mask,
-                    scale, 0, out, s);
     }
     int e = tm ? mark(s) : -1;
-    span(4, ep, e);
-    ep = e;
-    launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
-                dFT.as<double>(), cf.Wc.as<double>(), cf.Wm.as<double>(), P, mask, scale, treeOut, ldo, out, s);
-    e = tm ? mark(s) : -1;
-    span(6, ep, e);
-    ep = e;
-    if (mask & kStageFar)
-        launch_m2l(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LPtr.as<int64_t>(), dM2LNDir.as<int>(),
-                   dM2LCanonBase.as<int>(), dM2LOutSlot.as<int>(), dM2LSrc.as<int>(), tab, nterm, dMult.as<double>(),
-                   plan.m2lMaxCanon, dM2LPart.as<double>(), dLocal.as<double>(), s);
-    e = tm ? mark(s) : -1;
     span(2, ep, e);
     ep = e;
-    if ((mask & kStageFar) && plan.m2lCanon > 0)
+    if (!harmonic && (mask & kStageFar) && plan.m2lCanon > 0) {
         launch_m2l_gather(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dM2LInPtr.as<int>(), dM2LPart.as<double>(),
                           dLocal.as<double>(), s);
-    e = tm ? mark(s) : -1;
-    span(3, ep, e);
-    ep = e;
-    }  // per-mode operator stream
+        e = tm ? mark(s) : -1;
+        span(3, ep, e);
+        ep = e;
+    }
+    if (fork) HIP_CHECK(hipStreamWaitEvent(s, evJoin, 0));
     // down pass (owned part): L2L + L2P + gathered transposed near products, once
     // for the sum over the terms (both are linear in the locals / partials)
     if (mask & (kStageFar | kStageNear))
@@ -750,12 +809,14 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                          dNearPart.as<double>(), dDnChain.as<int2>(), plan.dnMaxChain, mask, scale, out, subX, subLd,
                          s);
     if (tm) {
-        const int e = mark(s);
-        span(5, ep, e);
-        span(7, e0, e);
+        const int e2 = mark(s);
+        span(5, ep, e2);
+        span(7, e0, e2);
         ++applies;
     }
 }
+
+int Operator::rootRhs(int nrhs) { return rhs_supported(nrhs) ? nrhs : rhs_padded(nrhs); }
 
 // aniso.m forward / mforward mixes (aniso.m:121-157).  Output block iid takes,
 // for every j in [-(nb-1), nb-1], mode m = |iid + j| of input block |j| with
@@ -776,7 +837,8 @@ std::vector<double> Operator::blockMixes(int nb, double g, bool chi) {
 }
 
 void Operator::blockOpDev(int which, const double* x, int64_t ldx, double* out, int64_t ldo, bool treeIo,
-                          hipStream_t s, double gval, const double* sigT) {
+                          hipStream_t s, double gval, const double* sigT, int phase, double* rootsSend,
+                          const double* rootsRecv) {
     if (which < 0 || which > 2) throw std::invalid_argument("block operator: which must be 0, 1 or 2");
     if (!coeffSet) throw std::runtime_error("block operator before setCoeff");
     ensureDevice();
@@ -787,7 +849,7 @@ void Operator::blockOpDev(int which, const double* x, int64_t ldx, double* out, 
     for (int m = 0; m < nm; ++m) ids[m] = m;
     if (which < 2) {
         applyBlock(nb, x, ldx, treeIo, which != 0 ? sig : nullptr, nm, ids.data(), mix.data(), out, ldo, treeIo, s,
-                   kStageAll);
+                   kStageAll, phase, rootsSend, rootsRecv);
         return;
     }
     // x - mforward(x) on the owned targets (aniso.m:155)
@@ -799,7 +861,8 @@ void Operator::blockOpDev(int which, const double* x, int64_t ldx, double* out, 
         subX = xo;
         subLd = ldx;
         try {
-            applyBlock(nb, x, ldx, treeIo, sig, nm, ids.data(), mix.data(), out, ldo, treeIo, s, kStageAll);
+            applyBlock(nb, x, ldx, treeIo, sig, nm, ids.data(), mix.data(), out, ldo, treeIo, s, kStageAll, phase,
+                       rootsSend, rootsRecv);
         } catch (...) {
             subX = nullptr;
             throw;
@@ -807,9 +870,10 @@ void Operator::blockOpDev(int which, const double* x, int64_t ldx, double* out, 
         subX = nullptr;
         return;
     }
-    dBlk.alloc((size_t)nb * nOut * sizeof(double));
-    applyBlock(nb, x, ldx, treeIo, sig, nm, ids.data(), mix.data(), dBlk.as<double>(), nOut, treeIo, s, kStageAll);
-    launch_sub_slice(nOut, nb, xo, ldx, dBlk.as<double>(), nOut, out, ldo, s);
+    if (phase != 2) dBlk.alloc((size_t)nb * nOut * sizeof(double));
+    applyBlock(nb, x, ldx, treeIo, sig, nm, ids.data(), mix.data(), dBlk.as<double>(), nOut, treeIo, s, kStageAll,
+               phase, rootsSend, rootsRecv);
+    if (phase != 1) launch_sub_slice(nOut, nb, xo, ldx, dBlk.as<double>(), nOut, out, ldo, s);
 }
 
 void Operator::blockOpHost(int which, const double* u, const double* sigmaS, double gval, double* out) {
@@ -854,7 +918,7 @@ StageTimes Operator::stageTimes() {
         acc[sp.stage] += t;
     }
     for (double& a : acc) a /= applies;
-    r.prep = (float)acc[0];
+    r.exch = (float)acc[0];
     r.up = (float)acc[1];
     r.m2l = (float)acc[2];
     r.gather = (float)acc[3];

@@ -46,7 +46,7 @@ struct CorrFold {
 };
 
 struct StageTimes {
-    float prep = 0, up = 0, m2l = 0, gather = 0, near = 0, down = 0, corr = 0, total = 0;
+    float exch = 0, up = 0, m2l = 0, gather = 0, near = 0, down = 0, corr = 0, total = 0;
 };
 
 class Operator {
@@ -64,6 +64,16 @@ public:
     void mappingDev(const double* charge, int id, double* out, hipStream_t s, int stageMask = 0x3f);
     void mappingTreeDev(const double* qTree, int id, double* outSlice, hipStream_t s);
     void forwardTreeDev(const double* xTree, double* ySlice, hipStream_t s);
+    // sharded applies in two phases around the caller's all-gather of the tier-0
+    // root multipoles: begin runs this rank's tier-0 up tasks (input
+    // valid at the own range and plan.xHalo only), packs its roots into rootsSend
+    // (plan.xRootChunk x 16 x K doubles, K = rootRhs(nrhs)) and starts the near
+    // field (it writes the output); end scatters the gathered roots (nranks
+    // chunks), runs the upper tiers, the M2L and the down pass.  The same x and out
+    // in both calls, tree order.
+    void forwardTreePhase(int phase, const double* xTree, double* ySlice, double* rootsSend, const double* rootsRecv,
+                          hipStream_t s);
+    static int rootRhs(int nrhs);  // right-hand sides per root record of an nrhs apply (padded count)
 
     // --- block operator (aniso.m:121-157)
     // out[i] = sum_t sum_b mixes[t][i][b] K_{ids[t]}(sig .* x[b]) for i, b < nrhs <= 8:
@@ -80,7 +90,8 @@ public:
     // gval / sigT (tree-order sigma_s on the device) override the handle's g and
     // sigma_s when given (NaN / nullptr: the handle's).
     void blockOpDev(int which, const double* x, int64_t ldx, double* out, int64_t ldo, bool tree, hipStream_t s,
-                    double gval = NAN, const double* sigT = nullptr);
+                    double gval = NAN, const double* sigT = nullptr, int phase = 0, double* rootsSend = nullptr,
+                    const double* rootsRecv = nullptr);
     // host-pointer block operator (aniso.m:121-157): u and out hold nb = ks blocks of
     // N points each (block b at b * N, original order); sigmaS (N, or nullptr: the
     // handle's sigma_s) and gval (NaN: the handle's g) as aniso.m's mforward reads them
@@ -125,8 +136,15 @@ public:
 private:
     void apply(const double* charge, bool treeIn, const double* sigT, int id, double* out, bool treeOut, hipStream_t s,
                int mask);
+    // phase 0: the whole apply (input valid everywhere, every up task); 1 / 2: the
+    // two halves of a sharded apply (forwardTreeBegin / End)
     void applyBlock(int K, const double* x, int64_t ldx, bool treeIn, const double* sigT, int nterm, const int* ids,
-                    const double* mixes, double* out, int64_t ldo, bool treeOut, hipStream_t s, int mask);
+                    const double* mixes, double* out, int64_t ldo, bool treeOut, hipStream_t s, int mask,
+                    int phase = 0, double* rootsSend = nullptr, const double* rootsRecv = nullptr);
+    struct Pending {  // state between the two phases of a sharded apply
+        bool active = false, nearDone = false;
+        int K = 0, e0 = -1, ePack = -1;
+    } pend;
     void ensureWork(int K);  // work arrays for K right-hand sides
     const ModeArgs* modeTable(int K, int nterm, const int* ids, const double* mixes);
     // harmonic (mode-shared) block apply, DESIGN.md §3.9: the E caches of every
@@ -174,6 +192,7 @@ private:
     DevBuf dUpTaskPtr, dUpGrpPtr, dUpGrp, dUpNode, dUpCode, dUpDesc, dUpGrpFix, dUpGeom, dUpLeaf;                       // up-pass tiers
     DevBuf dDnTaskPtr, dDnGrpPtr, dDnGrp, dDnNode, dDnLeafPtr, dDnLeafSlot, dDnLeafIdx, dDnLeafPts, dDnPtsRange, dDnDesc, dDnGrpFix, dDnLeafGeom;  // down
     DevBuf dLeafInfo, dNearPtsPtr, dNearPts;
+    DevBuf dXT0Tasks, dXRootRecv, dXRootSlot, dXSendSlot;  // sharded up pass (plan.buildExchange)
     DevBuf dM2LNDir, dM2LCanonBase, dM2LInPtr, dM2LOutSlot, dM2LPart;  // symmetric M2L
     DevBuf dNearSym, dNearPart, dDnLeafNear, dDnNearPtr, dDnNearOff, dDnChainPtr, dDnChain;              // symmetric near field
     DevBuf dParams, dStCoef;

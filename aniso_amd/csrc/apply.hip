@@ -113,15 +113,18 @@ __global__ void k_sub_slice(int64_t n, int nrhs, const double* __restrict__ x, i
             acc[e] = keep + xor16_f64<(OFF)>(send, r4);            \
         }                                                          \
     }
+// One up task (workgroup-wide).  rootSlot / recv (sharded applies, may be null):
+// a child that is a tier-0 root with rootSlot >= 0 is read from the all-gathered
+// records recv[rootSlot] (and copied to mult for the M2L) instead of mult.
 template <int K>
-__global__ void __launch_bounds__(kUpThreads) k_up_tier(
-    int taskBase, int maxTask, const int4* __restrict__ desc, const int* __restrict__ grpFix,
+__device__ __forceinline__ void up_task(
+    int task, int maxTask, const int4* __restrict__ desc, const int* __restrict__ grpFix,
     const int* __restrict__ node, const int4* __restrict__ code, const double4* __restrict__ geom,
     const int2* __restrict__ leafRange, const double* __restrict__ pxT, const double* __restrict__ pyT,
     const double* __restrict__ xin, int64_t ldi, int treeIn, const int* __restrict__ perm,
     const double* __restrict__ sigT, const double* __restrict__ wT, double* __restrict__ fT, double* __restrict__ cT,
-    const Params* __restrict__ P, double* __restrict__ mult) {
-    extern __shared__ double sm[];
+    const Params* __restrict__ P, double* __restrict__ mult, const int* __restrict__ rootSlot,
+    const double* __restrict__ recv, const int* __restrict__ sendSlot, double* __restrict__ send, double* sm) {
     int4* CD = reinterpret_cast<int4*>(sm);                // maxTask child codes
     double* Rl = reinterpret_cast<double*>(CD + maxTask);  // 4 x 256 transfer matrices (transposed)
     double* M = Rl + 4 * kRank * kRank;                    // maxTask x 16 x K multipoles
@@ -129,7 +132,6 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
     int* LB = reinterpret_cast<int*>(G + (size_t)maxTask * 4);  // maxTask: leaf point offset, count, node
     int* LC = LB + maxTask;
     int* ND = LC + maxTask;
-    const int task = taskBase + blockIdx.x;
     const int4 d = desc[task];  // first node, nodes, first point, levels
     const int n0 = d.x, nt = d.y, ngrp = d.w;
     const int64_t b0 = d.z;
@@ -153,6 +155,16 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
         ND[k] = node[n0 + k];
     }
     __syncthreads();
+    if (recv) {  // the gathered tier-0 roots under this task: stored for the M2L (all lanes, coalesced)
+        for (int it = threadIdx.x; it < nt * 4 * kRank * K; it += blockDim.x) {
+            const int k = it / (4 * kRank * K), q = (it / (kRank * K)) & 3, e = it % (kRank * K);
+            const int4 c = CD[k];
+            const int cq = q == 0 ? c.x : q == 1 ? c.y : q == 2 ? c.z : c.w;
+            if (c.x == kLeafCode || cq >= -1) continue;
+            const int rs = rootSlot[-cq - 2];
+            if (rs >= 0) mult[(size_t)(-cq - 2) * kRank * K + e] = recv[(size_t)rs * kRank * K + e];
+        }
+    }
     // P2M of the task's leaves (bbfmm.h:737-748): 16 lanes per leaf, one point per
     // lane per pass (its 16 products in registers), then a 16-lane reduce-scatter
     // leaves lane l with entry l.  The weighted charges are formed here from the
@@ -241,8 +253,11 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
             for (int b = 0; b < K; ++b) acc[b] = 0.0;
             if (c.x != kLeafCode && cq != -1) {
                 const double* R = Rl + q * kRank * kRank + r;  // transposed: R[rr * 16 + r]
-                const double* cm = cq >= 0 ? M + (size_t)cq * kRank * K             // child in this task (LDS)
-                                           : mult + (size_t)(-cq - 2) * kRank * K;  // root of the tier below
+                const double* cm = M + (size_t)(cq >= 0 ? cq : 0) * kRank * K;  // child in this task (LDS)
+                if (cq < 0) {  // root of the tier below: HBM (or the gathered records)
+                    const int rs = recv ? rootSlot[-cq - 2] : -1;
+                    cm = rs >= 0 ? recv + (size_t)rs * kRank * K : mult + (size_t)(-cq - 2) * kRank * K;
+                }
 #pragma unroll
                 for (int rr = 0; rr < kRank; ++rr)
 #pragma unroll
@@ -259,6 +274,27 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
     }
     for (int it = threadIdx.x; it < nt * kRank * K; it += blockDim.x)
         mult[(size_t)ND[it / (kRank * K)] * kRank * K + it % (kRank * K)] = M[it];
+    if (send) {  // sharded bottom tier: the task root's record into this rank's all-gather buffer
+        const int ss = sendSlot[ND[nt - 1]];  // the root is the task's last node (deepest level first)
+        if (ss >= 0)
+            for (int e = threadIdx.x; e < kRank * K; e += blockDim.x)
+                send[(size_t)ss * kRank * K + e] = M[(size_t)(nt - 1) * kRank * K + e];
+    }
+}
+
+template <int K>
+__global__ void __launch_bounds__(kUpThreads) k_up_tier(
+    int taskBase, const int* __restrict__ taskList, int maxTask, const int4* __restrict__ desc, const int* __restrict__ grpFix,
+    const int* __restrict__ node, const int4* __restrict__ code, const double4* __restrict__ geom,
+    const int2* __restrict__ leafRange, const double* __restrict__ pxT, const double* __restrict__ pyT,
+    const double* __restrict__ xin, int64_t ldi, int treeIn, const int* __restrict__ perm,
+    const double* __restrict__ sigT, const double* __restrict__ wT, double* __restrict__ fT, double* __restrict__ cT,
+    const Params* __restrict__ P, double* __restrict__ mult, const int* __restrict__ rootSlot,
+    const double* __restrict__ recv, const int* __restrict__ sendSlot, double* __restrict__ send) {
+    extern __shared__ double sm[];
+    const int task = taskList ? taskList[blockIdx.x] : taskBase + (int)blockIdx.x;
+    up_task<K>(task, maxTask, desc, grpFix, node, code, geom, leafRange, pxT, pyT, xin, ldi, treeIn, perm, sigT, wT,
+               fT, cT, P, mult, rootSlot, recv, sendSlot, send, sm);
 }
 
 #undef ANISO_RS16
@@ -1181,15 +1217,35 @@ size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain, int 
            (size_t)(4 * maxLeaves + 4 + maxNear) * sizeof(int) + (size_t)maxTask * sizeof(int4);
 }
 
-void launch_up_tier(int K, int ntask, int taskBase, int maxTask, const int4* desc, const int* grpFix, const int* node,
-                    const int4* code, const double4* geom, const int2* leafRange, const double* pxT, const double* pyT,
-                    const double* xin, int64_t ldi, int treeIn, const int* perm, const double* sigT, const double* wT,
-                    double* fT, double* cT, const Params* P, double* mult, hipStream_t s) {
+void launch_up_tier(int K, int ntask, int taskBase, const int* taskList, int maxTask, const int4* desc,
+                    const int* grpFix, const int* node, const int4* code, const double4* geom, const int2* leafRange,
+                    const double* pxT, const double* pyT, const double* xin, int64_t ldi, int treeIn, const int* perm,
+                    const double* sigT, const double* wT, double* fT, double* cT, const Params* P, double* mult,
+                    const int* rootSlot, const double* recv, const int* sendSlot, double* send, hipStream_t s) {
     if (ntask <= 0) return;
     const size_t shm = up_tier_lds(maxTask, K);
-    ANISO_DISPATCH_K(K, (k_up_tier<KK><<<ntask, kUpThreads, shm, s>>>(taskBase, maxTask, desc, grpFix, node, code, geom,
-                                                                      leafRange, pxT, pyT, xin, ldi, treeIn, perm, sigT,
-                                                                      wT, fT, cT, P, mult)));
+    ANISO_DISPATCH_K(K, (k_up_tier<KK><<<ntask, kUpThreads, shm, s>>>(taskBase, taskList, maxTask, desc, grpFix, node,
+                                                                      code, geom, leafRange, pxT, pyT, xin, ldi, treeIn,
+                                                                      perm, sigT, wT, fT, cT, P, mult, rootSlot, recv,
+                                                                      sendSlot, send)));
+    HIP_LAUNCH_CHECK();
+}
+
+// Tier-0 root records of a sharded apply without upper tiers: one thread per
+// double, records of 16 K contiguous doubles ([node][16][K] multipole layout).
+__global__ void k_roots_unpack(int64_t total, int rec, const int* __restrict__ nodes, const double* __restrict__ recv,
+                               double* __restrict__ mult) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int64_t j = i / rec, e = i - j * rec;
+    const int n = nodes[j];
+    if (n >= 0) mult[(int64_t)n * rec + e] = recv[i];
+}
+
+void launch_roots_unpack(int K, int nslots, const int* nodes, const double* recv, double* mult, hipStream_t s) {
+    const int64_t total = (int64_t)nslots * kRank * K;
+    if (total <= 0) return;
+    k_roots_unpack<<<blocks_for(total, 256), 256, 0, s>>>(total, kRank * K, nodes, recv, mult);
     HIP_LAUNCH_CHECK();
 }
 

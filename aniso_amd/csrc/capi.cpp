@@ -206,6 +206,26 @@ int aniso_forward_tree_dev(aniso_handle h, const double* x_tree, double* y_slice
     });
 }
 
+int aniso_forward_tree_begin_dev(aniso_handle h, const double* x_tree, double* y_slice, double* roots_send,
+                                 void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(x_tree);
+        CHECK_PTR(y_slice);
+        get(h).forwardTreePhase(1, x_tree, y_slice, roots_send, nullptr, (hipStream_t)stream);
+    });
+}
+
+int aniso_forward_tree_end_dev(aniso_handle h, const double* x_tree, double* y_slice, const double* roots_recv,
+                               void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(x_tree);
+        CHECK_PTR(y_slice);
+        get(h).forwardTreePhase(2, x_tree, y_slice, nullptr, roots_recv, (hipStream_t)stream);
+    });
+}
+
 int aniso_apply_block_dev(aniso_handle h, int nrhs, const double* x, int64_t ldx, int use_sigma, int nterm,
                           const int* ids, const double* mixes, double* out, int64_t ldo, int tree, void* stream) {
     CHECK_HANDLE(h);
@@ -226,6 +246,26 @@ int aniso_block_op_dev(aniso_handle h, int which, const double* x, int64_t ldx, 
         CHECK_PTR(x);
         CHECK_PTR(out);
         get(h).blockOpDev(which, x, ldx, out, ldo, tree != 0, (hipStream_t)stream);
+    });
+}
+
+int aniso_block_op_begin_dev(aniso_handle h, int which, const double* x, int64_t ldx, double* out, int64_t ldo,
+                             double* roots_send, void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(x);
+        CHECK_PTR(out);
+        get(h).blockOpDev(which, x, ldx, out, ldo, true, (hipStream_t)stream, NAN, nullptr, 1, roots_send, nullptr);
+    });
+}
+
+int aniso_block_op_end_dev(aniso_handle h, int which, const double* x, int64_t ldx, double* out, int64_t ldo,
+                           const double* roots_recv, void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(x);
+        CHECK_PTR(out);
+        get(h).blockOpDev(which, x, ldx, out, ldo, true, (hipStream_t)stream, NAN, nullptr, 2, nullptr, roots_recv);
     });
 }
 
@@ -279,6 +319,44 @@ int aniso_shard_cuts(aniso_handle h, int nranks, int64_t* cuts) {
         CHECK_PTR(cuts);
         const auto c = aniso::shard_cuts(get(h).tree, nranks);
         std::copy(c.begin(), c.end(), cuts);
+    });
+}
+
+int aniso_shard_exchange(aniso_handle h, int nrhs, int64_t* info) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(info);
+        if (nrhs < 1 || nrhs > 8) throw std::invalid_argument("nrhs must be in 1..8");
+        const auto& p = get(h).plan;
+        info[0] = p.xRootChunk;
+        info[1] = (int64_t)aniso::kRank * aniso::Operator::rootRhs(nrhs);
+        info[2] = (int64_t)p.xHalo.size() / 2;
+        info[3] = p.xHaloPoints;
+        info[4] = p.tierRootLevel.empty() ? -1 : p.tierRootLevel[0];
+        info[5] = (int64_t)p.xT0Tasks.size();
+        info[6] = (int64_t)p.xRootSend.size();
+        info[7] = p.upTierTask.size() >= 2 ? p.upTierTask[1] - p.upTierTask[0] : 0;
+        info[8] = p.nranks;
+    });
+}
+
+int aniso_shard_halo(aniso_handle h, int64_t* ranges) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(ranges);
+        const auto& p = get(h).plan;
+        std::copy(p.xHalo.begin(), p.xHalo.end(), ranges);
+    });
+}
+
+int aniso_shard_roots(aniso_handle h, int* send_nodes, int* recv_nodes, int* t0_roots) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        const auto& p = get(h).plan;
+        if (send_nodes) std::copy(p.xRootSend.begin(), p.xRootSend.end(), send_nodes);
+        if (recv_nodes) std::copy(p.xRootRecv.begin(), p.xRootRecv.end(), recv_nodes);
+        if (t0_roots)
+            for (int k : p.xT0Tasks) *t0_roots++ = p.upTaskRoot[k];
     });
 }
 
@@ -399,7 +477,7 @@ int aniso_stage_times(aniso_handle h, float* t) {
     return guarded([&] {
         CHECK_PTR(t);
         auto s = get(h).stageTimes();
-        t[0] = s.prep; t[1] = s.up; t[2] = s.m2l; t[3] = s.gather; t[4] = s.near; t[5] = s.down; t[6] = s.corr;
+        t[0] = s.exch; t[1] = s.up; t[2] = s.m2l; t[3] = s.gather; t[4] = s.near; t[5] = s.down; t[6] = s.corr;
         t[7] = s.total;
     });
 }

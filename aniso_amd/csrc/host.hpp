@@ -148,8 +148,24 @@ struct Plan {
     std::vector<std::array<double, 4>> dnLeafGeom;
     int dnMaxTask = 1, dnMaxLeaves = 1;
     int64_t pairsNear = 0, pairsM2L = 0;       // kernel entries per apply
+    // sharded up pass: the rank runs only the tier-0 up tasks it
+    // needs -- those holding its own points or anything its M2L, near field or
+    // correction stencil reads below the tier-0 root level -- and exchanges the
+    // tier-0 root multipoles with every rank (one all-gather; the tiers above run
+    // on every rank).  Its input must be valid at its own range and at xHalo.
+    std::vector<int> upTaskRoot;      // per up task: its root node
+    std::vector<int> xT0Tasks;        // tier-0 tasks run by this rank (ascending)
+    std::vector<int> xRootSend;       // tier-0 roots this rank contributes (tree order)
+    std::vector<int> xRootRecv;       // nranks x xRootChunk all-gather slots -> node (-1: padding)
+    std::vector<int> xRootSlot;       // per node: its all-gather slot (-1: not a tier-0 root)
+    std::vector<int> xSendSlot;       // per node: its slot in this rank's send buffer (-1: not sent here)
+    int xRootChunk = 0;               // roots per rank in the all-gather (the largest contribution)
+    std::vector<int64_t> xHalo;       // [b, e) pairs of tree positions needed outside [ownBegin, ownEnd)
+    int64_t xHaloPoints = 0;
 
     void build(const Tree& t, int np, int rank, int nranks);
+    // the exchange plan above; sz / d2: the square grid of the correction stencil
+    void buildExchange(const Tree& t, int sz, int d2);
 
   private:
     void buildUpTasks(const Tree& t);

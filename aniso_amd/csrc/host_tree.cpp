@@ -256,7 +256,6 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     maxCanon = std::max(0, std::min(kMaxCanon, capCanon));
     rank = rank_;
     nranks = nranks_;
-    const int64_t N = t.count[0];
     // ---- ownership: contiguous runs of a subtree frontier (DFS order == tree order)
     const std::vector<int64_t> cuts = shard_cuts(t, nranks);
     ownBegin = cuts[rank];
@@ -466,6 +465,7 @@ void Plan::buildUpTasks(const Tree& t) {
     std::vector<int> slotOf(t.nn, -1);
     auto keep = [&](int n) { return !t.isEmpty[n]; };
     upTierTask.assign(1, 0);
+    upTaskRoot.clear();
     upTaskPtr.assign(1, 0);
     upGrpPtr.assign(1, 0);
     upGrp.clear();
@@ -516,6 +516,7 @@ void Plan::buildUpTasks(const Tree& t) {
             }
             upGrpPtr.push_back((int)upGrp.size());
             upTaskPtr.push_back((int)upNode.size());
+            upTaskRoot.push_back(r);
             upMaxTask = std::max(upMaxTask, (int)upNode.size() - base);
         }
         upTierTask.push_back((int)upTaskPtr.size() - 1);
@@ -715,6 +716,115 @@ void Plan::buildClusters(const Tree& t) {
         hmDual += (int64_t)dSrc.size();
         hmPtr.push_back((int64_t)hmSrc.size());
     }
+}
+
+// Exchange plan of the sharded up pass (the reference
+// runs upPass over the whole tree, bbfmm.h:825-861, and M2L reads src.nodeCharge
+// of any V/X member, bbfmm.h:1051-1065).  What this rank reads below the tier-0
+// root level L0 -- multipoles of its M2L sources there, the weighted charges of its
+// near-field sources, of its correction stencil's 3x3 squares and of its own
+// points -- lives in a few tier-0 subtrees around its range; it runs those tasks.
+// Everything at or above L0 comes from the tier-0 roots, which each rank receives
+// from their owners (the rank holding the root's first point).
+void Plan::buildExchange(const Tree& t, int sz, int d2) {
+    const int64_t N = t.count[0];
+    xT0Tasks.clear();
+    xRootSend.clear();
+    xRootRecv.clear();
+    xRootSlot.clear();
+    xSendSlot.clear();
+    xRootChunk = 0;
+    xHalo.clear();
+    xHaloPoints = 0;
+    std::vector<char> need(N, 0);  // tree positions this rank's kernels read
+    for (int64_t k = ownBegin; k < ownEnd; ++k) need[k] = 1;
+    for (int p : nearPts) need[p] = 1;
+    if (sz > 0 && d2 > 0) {  // k_corr: the 3x3 squares around each own target (incl. its own square)
+        std::vector<int> iperm(N);
+        for (int64_t k = 0; k < N; ++k) iperm[t.perm[k]] = (int)k;
+        for (int64_t k = ownBegin; k < ownEnd; ++k) {
+            const int sq = t.perm[k] / d2, i = sq / sz, j = sq % sz;
+            for (int dr = -1; dr <= 1; ++dr)
+                for (int dc = -1; dc <= 1; ++dc) {
+                    if (i + dr < 0 || i + dr >= sz || j + dc < 0 || j + dc >= sz) continue;
+                    const int64_t q = (int64_t)(sq + dr * sz + dc) * d2;
+                    for (int c = 0; c < d2; ++c) need[iperm[q + c]] = 1;
+                }
+        }
+    }
+    const bool tiers = upTierTask.size() >= 2;
+    if (!tiers) {  // a lone leaf: no up tasks, every point is read by the one apply
+        if (ownBegin > 0) xHalo.insert(xHalo.end(), {0, ownBegin});
+        if (ownEnd < N) xHalo.insert(xHalo.end(), {ownEnd, N});
+        xHaloPoints = N - (ownEnd - ownBegin);
+        return;
+    }
+    const int L0 = tierRootLevel[0];
+    const int t0 = upTierTask[0], t1 = upTierTask[1];
+    std::vector<int> taskOf(t.nn, -1);  // tier-0 root -> task
+    for (int k = t0; k < t1; ++k) taskOf[upTaskRoot[k]] = k;
+    std::vector<char> runs(t1 - t0, 0);
+    auto markNode = [&](int n) {  // a multipole below L0: the tier-0 task that computes it
+        if (t.level[n] <= L0) return;
+        while (t.level[n] > L0) n = t.parent[n];
+        if (taskOf[n] >= 0) runs[taskOf[n] - t0] = 1;
+    };
+    for (int n : m2lTgt) {
+        for (int64_t k = t.vPtr[n]; k < t.vPtr[n + 1]; ++k)
+            if (!t.isEmpty[t.vIdx[k]]) markNode(t.vIdx[k]);
+        for (int64_t k = t.xPtr[n]; k < t.xPtr[n + 1]; ++k)
+            if (!t.isEmpty[t.xIdx[k]]) markNode(t.xIdx[k]);
+    }
+    std::vector<char> valid(N, 0);  // input positions the rank's up tasks read
+    std::vector<char> covered(N, 0);
+    for (int k = t0; k < t1; ++k) {
+        const int r = upTaskRoot[k];
+        const int64_t b = t.begin[r], e = b + t.count[r];
+        for (int64_t p = b; p < e; ++p) {
+            covered[p] = 1;
+            if (need[p]) runs[k - t0] = 1;
+        }
+        if (runs[k - t0]) {
+            xT0Tasks.push_back(k);
+            for (int64_t p = b; p < e; ++p) valid[p] = 1;
+        }
+    }
+    for (int64_t p = 0; p < N; ++p)  // leaves above L0 (P2M in the tiers every rank runs)
+        if (!covered[p]) valid[p] = 1;
+    for (int64_t p = 0; p < N; ++p)
+        if (need[p] && !valid[p]) throw std::logic_error("exchange plan: a read position outside the rank's up tasks");
+    for (int64_t p = 0; p < N;) {
+        if (!valid[p] || (p >= ownBegin && p < ownEnd)) {
+            ++p;
+            continue;
+        }
+        int64_t e = p;
+        while (e < N && valid[e] && !(e >= ownBegin && e < ownEnd)) ++e;
+        xHalo.push_back(p);
+        xHalo.push_back(e);
+        xHaloPoints += e - p;
+        p = e;
+    }
+    // the all-gather of the tier-0 roots: slot layout of every rank's contribution
+    const std::vector<int64_t> cuts = shard_cuts(t, nranks);
+    std::vector<std::vector<int>> owned(nranks);
+    for (int k = t0; k < t1; ++k) {
+        const int r = upTaskRoot[k];
+        const int o = (int)(std::upper_bound(cuts.begin() + 1, cuts.end() - 1, t.begin[r]) - (cuts.begin() + 1));
+        owned[o].push_back(r);
+    }
+    for (auto& v : owned) xRootChunk = std::max<int>(xRootChunk, (int)v.size());
+    xRootRecv.assign((size_t)nranks * xRootChunk, -1);
+    for (int q = 0; q < nranks; ++q)
+        std::copy(owned[q].begin(), owned[q].end(), xRootRecv.begin() + (size_t)q * xRootChunk);
+    xRootSend = owned[rank];
+    xRootSlot.assign(t.nn, -1);
+    for (size_t k = 0; k < xRootRecv.size(); ++k)
+        if (xRootRecv[k] >= 0) xRootSlot[xRootRecv[k]] = (int)k;
+    xSendSlot.assign(t.nn, -1);
+    for (size_t j = 0; j < xRootSend.size(); ++j) xSendSlot[xRootSend[j]] = (int)j;
+    for (int r : xRootSend)
+        if (!runs[taskOf[r] - t0]) throw std::logic_error("exchange plan: a sent root's task does not run here");
 }
 
 }  // namespace aniso

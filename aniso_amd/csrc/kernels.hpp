@@ -76,10 +76,19 @@ void launch_prepare(int K, int64_t N, const double* xin, int64_t ldi, int treeIn
                     const double* sigT, const double* wT, double* fT, double* cT, hipStream_t s);
 size_t up_tier_lds(int maxTask, int K);
 size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain, int K);
-void launch_up_tier(int K, int ntask, int taskBase, int maxTask, const int4* desc, const int* grpFix, const int* node,
-                    const int4* code, const double4* geom, const int2* leafRange, const double* pxT, const double* pyT,
-                    const double* xin, int64_t ldi, int treeIn, const int* perm, const double* sigT, const double* wT,
-                    double* fT, double* cT, const Params* P, double* mult, hipStream_t s);
+// taskList (nullptr: tasks taskBase .. taskBase + ntask - 1): the tasks to run.
+// Sharded applies (all may be null): rootSlot / recv -- children that
+// are tier-0 roots with a slot are read from the all-gathered records recv (and
+// stored to mult for the M2L); sendSlot / send -- a task root with a send slot also
+// stores its record into this rank's all-gather buffer.
+void launch_up_tier(int K, int ntask, int taskBase, const int* taskList, int maxTask, const int4* desc,
+                    const int* grpFix, const int* node, const int4* code, const double4* geom, const int2* leafRange,
+                    const double* pxT, const double* pyT, const double* xin, int64_t ldi, int treeIn, const int* perm,
+                    const double* sigT, const double* wT, double* fT, double* cT, const Params* P, double* mult,
+                    const int* rootSlot, const double* recv, const int* sendSlot, double* send, hipStream_t s);
+// the tier-0 root records of a sharded apply without upper tiers, scattered back
+// from the all-gather (mult[nodes[j]] = recv[j] where nodes[j] >= 0)
+void launch_roots_unpack(int K, int nslots, const int* nodes, const double* recv, double* mult, hipStream_t s);
 // All terms in one launch: local = sum over the terms (stored), transposed
 // canonical products summed over the terms into their partial slots (stored).
 void launch_m2l(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,

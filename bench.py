@@ -17,8 +17,10 @@ u - K_0(sigma_s .* u) (main.cpp:125-136) with main.cpp's coefficients; the block
 run also reports that number as `mode0_matvec_per_s`.
 
 N GPUs (torchrun, one process per GPU, RCCL): the targets are sharded by FMM
-subtree (strong scaling: total work fixed).  Each rank applies its shard; one
-all-gather of tree-ordered slices rebuilds the replicated block vector.
+subtree (strong scaling: total work fixed).  Each rank runs the up pass over its
+own and halo subtrees, exchanges the tier-0 root multipoles with one all-gather
+mid-apply, computes its targets into its slice of the next iterate, and one halo
+all-to-all refreshes the points its neighbours read (aniso_amd/dist.py).
 
 Also reported on the same JSON line:
   roofline      HBM roofline of the dominant kernel (the M2L stream, k_m2l_hm, one
@@ -224,12 +226,12 @@ def main():
     full_stats = op.stats()
     perm = torch.tensor(op.tree_perm(), device="cuda", dtype=torch.int64)
     if world > 1:
-        ranges = adist.shard_ranges(op, world)
+        # sharded apply: own subtrees + halo up pass, one all-gather
+        # of the tier-0 root multipoles mid-apply, one halo all-to-all per iterate
         op.set_shard(rank, world)
-        L = adist.pad_len(ranges)
-        slab = torch.zeros(nb, L, dtype=torch.float64, device="cuda")
-        gathered = torch.zeros(world * nb * L, dtype=torch.float64, device="cuda")
-        gidx = torch.tensor(adist.block_gather_index(ranges, L, nb), device="cuda")
+        xchg = adist.ShardExchange(op, rank, world, nb, "cuda", args.backend)
+        xchg0 = adist.ShardExchange(op, rank, world, 1, "cuda", args.backend) if block else xchg
+        ob, oe = xchg.own
     op.setCoeff(ss, st)
     modes = list(range(2 * ks - 1))
     t0 = time.time()
@@ -254,14 +256,18 @@ def main():
         if world == 1:
             local_apply(x, y)
             return
-        local_apply(x, slab)  # writes the owned entries of every block
-        if args.backend == "nccl":
-            dist.all_gather_into_tensor(gathered, slab.view(-1))
-        else:  # gloo rehearsal: stage through host memory
-            parts = [torch.zeros(nb * L, dtype=torch.float64) for _ in range(world)]
-            dist.all_gather(parts, slab.view(-1).cpu())
-            gathered.copy_(torch.cat(parts))
-        torch.index_select(gathered, 0, gidx, out=y.view(-1))
+        # phase 1 (own + halo up tasks, near field), the root all-gather, phase 2
+        # (upper tiers, M2L, down pass into the owned slice of y), the halo of y
+        if block:
+            yo = y[:, ob:oe]
+            op.block_op_begin_dev(2, x, yo, xchg.roots_send)
+            xchg.roots_allgather()
+            op.block_op_end_dev(2, x, yo, xchg.roots_recv, world)
+        else:
+            op.forward_tree_begin_dev(x[0], y[0, ob:oe], xchg.roots_send)
+            xchg.roots_allgather()
+            op.forward_tree_end_dev(x[0], y[0, ob:oe], xchg.roots_recv, world)
+        xchg.halo(y)
 
     def timed(fn, steps, warmup):
         nonlocal v, w
@@ -373,20 +379,19 @@ def main():
         "cache_build_s": round(t_cache, 3),
         "roofline": roofline,
     }
+    if world > 1:
+        line["exchange"] = {"root_allgather_bytes_per_rank": 8 * xchg.C * xchg.R,
+                            "halo_bytes_received": xchg.halo_bytes(), "backend": args.backend}
     if block:
         # main.cpp's mode-0 matvec on the same operator (secondary number)
         def mode0(x, y):
             if world == 1:
                 op.forward_tree_dev(x[0], y[0])
                 return
-            op.forward_tree_dev(x[0], slab[0])
-            if args.backend == "nccl":
-                dist.all_gather_into_tensor(gathered, slab.view(-1))
-            else:
-                parts = [torch.zeros(nb * L, dtype=torch.float64) for _ in range(world)]
-                dist.all_gather(parts, slab.view(-1).cpu())
-                gathered.copy_(torch.cat(parts))
-            torch.index_select(gathered, 0, gidx, out=y.view(-1))
+            op.forward_tree_begin_dev(x[0], y[0, ob:oe], xchg0.roots_send)
+            xchg0.roots_allgather()
+            op.forward_tree_end_dev(x[0], y[0, ob:oe], xchg0.roots_recv, world)
+            xchg0.halo(y[0:1])
 
         el0, t0s = timed(mode0, args.steps, 2)
         line["mode0_matvec_per_s"] = round(args.steps / el0, 3)
@@ -408,7 +413,19 @@ def main():
             ref_op.forward_dev(U[0], ref[0])
         torch.cuda.synchronize()
         ref = ref[:, perm]
-        line["verify_rel_err_vs_unsharded"] = float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref))
+        b_, e_ = (ob, oe) if world > 1 else (0, N)
+        # owned slice of every rank (and its halo, filled by the exchange) vs the unsharded operator
+        sq = torch.tensor([float(torch.sum((got[:, b_:e_] - ref[:, b_:e_]) ** 2)),
+                           float(torch.sum(ref[:, b_:e_] ** 2))], dtype=torch.float64)
+        if world > 1:
+            hal = [torch.arange(lo, hi, device="cuda") for lo, hi in xchg.halos[rank]]
+            if hal:
+                hi_ = torch.cat(hal)
+                line["verify_halo_rel_err"] = float(torch.linalg.norm(got[:, hi_] - ref[:, hi_])
+                                                    / torch.linalg.norm(ref[:, hi_]))
+            sq = sq.to("cuda") if args.backend == "nccl" else sq
+            dist.all_reduce(sq)
+        line["verify_rel_err_vs_unsharded"] = float((sq[0] / sq[1]) ** 0.5)
         del ref_op
     if rank == 0 and world == 1 and not args.no_cpu:
         def block_check(sz):

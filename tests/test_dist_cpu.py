@@ -1,8 +1,24 @@
-"""The N>1 path's composition on CPU with gloo (world_size 2 and 3): every rank
-owns an FMM-subtree shard (a contiguous tree-order range), computes its targets,
-and one all-gather of the tree-ordered slices + a permutation rebuilds the full
-vector.  The per-rank compute is played by the oracle here (no GPU on CPU); on
-the GPU box the same composition runs over RCCL with the HIP apply (bench.py)."""
+"""The N>1 path on CPU with gloo (world sizes 2 and 3): the host-side exchange plan
+of the sharded apply (aniso_amd/dist.py) and the claim it rests on.
+
+Every rank owns an FMM-subtree shard (a contiguous tree-order range).  Per apply it
+runs the up pass only over the tier-0 subtrees its kernels read (own + halo), and
+receives every other tier-0 root multipole through one all-gather; per iterate one
+all-to-all refreshes its halo.  Here, per rank:
+
+* the halo all-to-all (ShardExchange.halo over gloo) delivers exactly the owners'
+  values at the rank's halo positions and touches nothing else;
+* the root all-gather lands every rank's roots in the slots of aniso_shard_roots'
+  receive map;
+* the claim, checked with the CPU oracle (the reference algorithm): the rank's owned
+  outputs depend on the input outside its own range and halo ONLY through the tier-0
+  root multipoles.  A perturbation supported outside own + halo and in the null
+  space of every skipped subtree's root P2M (bbfmm.h:737-748: S_x(i) S_y(j) w_p per
+  point) leaves the owned outputs unchanged to rounding, while it does change other
+  ranks' outputs.
+
+The handle is host-only here (plans need no GPU); on the GPU box the same plan runs
+the HIP apply over RCCL (bench.py, tests/test_gpu_parity.py)."""
 import os
 import socket
 
@@ -21,6 +37,45 @@ def _free_port():
     return p
 
 
+def cheb_s(u, npc=4):
+    """S(u, c_i) of bbfmm.h:653-655 for u in [-1, 1] (rows: points, columns: i)."""
+    c = -np.cos((np.arange(npc) + 0.5) * np.pi / npc)
+    Tu = np.stack([np.cos(l * np.arccos(np.clip(u, -1, 1))) for l in range(npc)], axis=1)
+    Tc = np.stack([np.cos(l * np.arccos(c)) for l in range(npc)], axis=0)
+    return (2.0 * Tu @ Tc - 1.0) / npc
+
+
+def null_perturbation(op, rank_valid, rng):
+    """delta (tree order): zero on the rank's valid positions and on the tier-0
+    subtrees it runs; on every other tier-0 subtree a random vector in the null space
+    of that root's P2M (16 x n_points: S_x(i) S_y(j) w_p)."""
+    ints, geom = op.tree_nodes()
+    ex = op.shard_exchange()
+    L0 = ex["t0_level"]
+    _, _, run = op.shard_roots()
+    run = set(run.tolist())
+    perm = op.tree_perm()
+    xy = op.getNodes()
+    w = op.getWeights()
+    delta = np.zeros(op.N)
+    skipped = 0
+    for n in np.nonzero((ints[:, 5] == L0) & (ints[:, 8] == 0))[0]:
+        if n in run:
+            continue
+        b, c = int(ints[n, 10]), int(ints[n, 9])
+        pos = np.arange(b, b + c)
+        assert not rank_valid[pos].any(), "a skipped subtree overlaps the rank's own range or halo"
+        pts = perm[pos]
+        cx, cy, rx, ry = geom[n]
+        A = (cheb_s((xy[pts, 0] - cx) / rx)[:, None, :] * cheb_s((xy[pts, 1] - cy) / ry)[:, :, None]).reshape(c, 16)
+        A = (A * w[pts, None]).T  # 16 x c
+        d = rng.uniform(-1, 1, c)
+        d -= A.T @ np.linalg.solve(A @ A.T, A @ d)
+        delta[pos] = d
+        skipped += 1
+    return delta, skipped
+
+
 def _worker(rank, world, port, result_q):
     import sys
 
@@ -34,48 +89,99 @@ def _worker(rank, world, port, result_q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        sz, d = 12, 2
-        a = aniso_amd.Aniso(sz, d, 2, 0.5, 8, 4, 20)
-        ranges = adist.shard_ranges(a, world)
-        a.set_shard(rank, world)
-        assert a.shard() == ranges[rank]
-        perm = a.tree_perm()
-        o = Oracle(sz, d, 2, 0.5, 8, 4, 20)
+        sz, d, ks, nb = 128, 1, 2, 2
+        op = aniso_amd.Aniso(sz, d, ks, 0.5, 6, 4, 20)
+        N = op.N
+        op.set_shard(rank, world)
+        x = adist.ShardExchange(op, rank, world, nb, "cpu", "gloo")
+        b, e = x.own
+        assert (b, e) == op.shard()
+        valid = np.zeros(N, dtype=bool)
+        valid[b:e] = True
+        for lo, hi in x.halos[rank]:
+            assert not valid[lo:hi].any(), "halo overlaps the own range"
+            valid[lo:hi] = True
+        # -- halo all-to-all: owners' values at the halo, nothing else touched
+        y = torch.zeros(nb, N, dtype=torch.float64)
+        ref = torch.arange(nb * N, dtype=torch.float64).reshape(nb, N) + 1.0
+        y[:, b:e] = ref[:, b:e]
+        x.halo(y)
+        vm = torch.from_numpy(valid)
+        halo_ok = bool(torch.equal(y[:, vm], ref[:, vm])) and bool((y[:, ~vm] == 0).all())
+        # -- root all-gather: every rank's roots land in their receive slots
+        send, recv, _ = op.shard_roots()
+        rs = x.roots_send[: x.C * x.R].view(x.C, x.R)
+        rs.zero_()
+        rs[: len(send)] = torch.from_numpy(send.astype(np.float64))[:, None]
+        x.roots_allgather()
+        got = x.roots_recv[: world * x.C * x.R].view(world * x.C, x.R)
+        slots = recv >= 0
+        roots_ok = bool(torch.equal(got[torch.from_numpy(slots)][:, 0], torch.from_numpy(recv[slots].astype(np.float64))))
+        roots_ok &= bool((got[torch.from_numpy(slots)] == got[torch.from_numpy(slots)][:, :1]).all())
+        all_roots = set()
+        for r in range(world):
+            all_roots |= set(recv[r * x.C:(r + 1) * x.C][recv[r * x.C:(r + 1) * x.C] >= 0].tolist())
+        roots_ok &= len(all_roots) == int(slots.sum())  # each root sent by exactly one rank
+        # -- the claim, with the oracle: perturbations the rank never sees leave its outputs alone
+        rng = np.random.default_rng(11 + rank)
+        delta, skipped = null_perturbation(op, valid, rng)
+        perm = op.tree_perm()
+        o = Oracle(sz, d, ks, 0.5, 6, 4, 20)
         xy = o.getNodes()
-        rng = np.random.default_rng(7)
-        o.setCoeff(rng.uniform(1, 2, o.N), rng.uniform(2, 3, o.N))
-        o.cache(1)
-        q = rng.uniform(-1, 1, o.N)
-        full = o.mapping(q, 1)  # every rank can compute it: stands in for the shard's apply
-        L = adist.pad_len(ranges)
-        mine = torch.from_numpy(adist.local_slice(full, perm, ranges[rank], L))
-        parts = [torch.zeros(L, dtype=torch.float64) for _ in range(world)]
-        dist.all_gather(parts, mine)
-        gathered = torch.stack(parts)
-        out = adist.assemble_from_gathered(gathered.numpy(), ranges, perm)
-        result_q.put((rank, float(np.abs(out - full).max()), xy.shape[0]))
-    except Exception as e:  # surface worker failures instead of hanging the queue
-        result_q.put((rank, repr(e), -1))
+        o.setCoeff(np.full(N, 2.0), 2.5 + np.sin(3 * xy[:, 0]))
+        q = rng.uniform(-1, 1, N)
+        dq = np.zeros(N)
+        dq[perm] = delta
+        errs, ctrl = [], []
+        for m in (0, 1):
+            o.cache(m)
+            y0 = o.mapping(q, m)[perm]
+            y1 = o.mapping(q + dq, m)[perm]
+            o.uncache(m)
+            errs.append(float(np.abs(y1[b:e] - y0[b:e]).max() / np.abs(y0[b:e]).max()))
+            ctrl.append(float(np.abs(y1 - y0).max() / np.abs(y0).max()))
+        o.close()
+        result_q.put((rank, dict(halo_ok=halo_ok, roots_ok=roots_ok, skipped=skipped, errs=errs, ctrl=ctrl,
+                                 halo_points=int(valid.sum() - (e - b)), own=e - b)))
+    except Exception as ex:  # surface worker failures instead of hanging the queue
+        result_q.put((rank, repr(ex)))
         raise
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_gloo_sharded_assembly(world):
+def test_gloo_sharded_exchange_plan(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
+    res = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for r, err, n in res:
-        assert n > 0, err
-        assert err == 0.0, (r, err)
+    for r, v in res:
+        assert isinstance(v, dict), v
+        assert v["halo_ok"] and v["roots_ok"], (r, v)
+        assert v["skipped"] > 0, (r, v)  # the test perturbs something
+        assert max(v["errs"]) < 1e-12, (r, v)  # owned outputs: unchanged to rounding
+        assert min(v["ctrl"]) > 1e-6, (r, v)  # ... while the perturbation is felt elsewhere
+        assert v["halo_points"] < v["own"], (r, v)
+
+
+def test_halo_plan_pairs_up():
+    """send[r] of rank a == recv[a] of rank r, for a hand-made plan."""
+    from aniso_amd import dist as adist
+
+    cuts = [0, 10, 20, 30]
+    halos = [[(10, 12)], [(8, 10), (20, 23)], [(15, 20), (29, 30)]]
+    plans = [adist.halo_plan(cuts, halos, r) for r in range(3)]
+    for a in range(3):
+        for r in range(3):
+            assert np.array_equal(plans[a][0][r], plans[r][1][a])
+    assert plans[1][0][0].tolist() == [10, 11] and plans[1][0][2].tolist() == [15, 16, 17, 18, 19]
 
 
 def test_block_gather_index_assembles_block_slices():

@@ -639,14 +639,92 @@ def test_block_matvec_knobs_agree(knob, monkeypatch):
     assert _rel(outs[0], outs[1]) <= 1e-12
 
 
-def test_block_matvec_eight_shards_at_config3_size():
-    """The driver's 8-GPU bench path at full size, on one GPU: BASELINE's 1M-point
-    block matvec (config 3) sharded by FMM subtree over 8 ranks (each rank: its own
-    handle, tree-order input, owned slice out, assembled through the bench's
-    all-gather index) equals the unsharded matvec."""
+def _two_phase_shards(sz, d, ks, ml, coef, world, X, ref, g=0.8, ns=10):
+    """Every rank's sharded apply in two phases, the root all-gather
+    played by concatenating the ranks' send buffers: rank r's input holds X at its
+    own range and halo and NaN everywhere else, so any read outside them poisons
+    its output.  ks > 1: x - mforward(x) (aniso_block_op_*_dev, which = 2); ks = 1:
+    main.cpp's forward operator (aniso_forward_tree_*_dev).  Returns (rel err of
+    the assembled owned slices vs ref, NaN count, halo points / N)."""
     torch = _torch()
     import aniso_amd
-    from aniso_amd import dist as adist
+
+    nb = X.shape[0]
+    hs, outs, sends, halo = [], [], [], 0
+    for r in range(world):
+        sh = aniso_amd.Aniso(sz, d, ks, g, ns, 4, ml)
+        sh.set_shard(r, world)
+        sh.setCoeff(*coef)
+        for m in range(2 * ks - 1):
+            sh.cache(m)
+        b, e = sh.shard()
+        ex = sh.shard_exchange(nb)
+        xr = torch.full_like(X, float("nan"))
+        xr[:, b:e] = X[:, b:e]
+        for lo, hi in sh.shard_halo():
+            xr[:, lo:hi] = X[:, lo:hi]
+            halo += hi - lo
+        y = torch.zeros(nb, max(e - b, 1), dtype=torch.float64, device="cuda")
+        rs = torch.zeros(max(ex["root_chunk"] * ex["root_record"], 1), dtype=torch.float64, device="cuda")
+        if ks > 1:
+            sh.block_op_begin_dev(2, xr, y, rs)
+        else:
+            sh.forward_tree_begin_dev(xr[0], y[0], rs)
+        hs.append((sh, xr, (b, e), ex))
+        outs.append(y)
+        sends.append(rs[: ex["root_chunk"] * ex["root_record"]])
+    recv = torch.cat(sends) if sends[0].numel() else torch.zeros(1, dtype=torch.float64, device="cuda")
+    got = torch.zeros_like(X)
+    for (sh, xr, (b, e), ex), y in zip(hs, outs):
+        if ks > 1:
+            sh.block_op_end_dev(2, xr, y, recv, world)
+        else:
+            sh.forward_tree_end_dev(xr[0], y[0], recv, world)
+        got[:, b:e] = y[:, : e - b]
+    torch.cuda.synchronize()
+    nans = int(torch.isnan(got).sum())
+    return float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref)), nans, halo / X.shape[1]
+
+
+@pytest.mark.parametrize("sz,d,ks,ml,coeffs,world", [
+    (64, 1, 5, 20, "main", 2), (64, 1, 5, 20, "rough", 8), (48, 2, 3, 20, "rough", 3), (30, 3, 1, 20, "main", 4),
+    (40, 1, 2, 3, "rough", 3), (16, 1, 5, 20, "main", 3), (11, 3, 1, 20, "rough", 2), (1, 3, 1, 20, "main", 2)])
+def test_two_phase_sharded_apply_reads_only_own_and_halo(sz, d, ks, ml, coeffs, world):
+    """The multi-GPU apply (own + halo up pass, tier-0 root all-gather, owned slice
+    out) on NaN-poisoned inputs equals the unsharded tree-order operator: the
+    exchange plan covers everything each rank's kernels read (uniform, odd-sized,
+    maxLevel-limited and single-leaf trees; 1, 2, 3 (padded to 4) and 5 right-hand
+    sides; even and odd world sizes)."""
+    torch = _torch()
+    import aniso_amd
+
+    full = aniso_amd.Aniso(sz, d, ks, 0.8, 10, 4, ml)
+    xy = full.getNodes()
+    coef = main_coeffs(xy) if coeffs == "main" else rough_coeffs(xy, 3)
+    full.setCoeff(*coef)
+    for m in range(2 * ks - 1):
+        full.cache(m)
+    X = torch.tensor(np.random.default_rng(sz).uniform(-1, 1, (ks, full.N)), device="cuda")
+    ref = torch.zeros_like(X)
+    if ks > 1:
+        full.block_op_dev(2, X, ref, tree=True)
+    else:
+        full.forward_tree_dev(X[0], ref[0])
+    torch.cuda.synchronize()
+    del full
+    err, nans, _ = _two_phase_shards(sz, d, ks, ml, coef, world, X, ref)
+    assert nans == 0
+    assert err <= 1e-13, err
+
+
+def test_block_matvec_eight_shards_at_config3_size():
+    """The driver's 8-GPU bench path at full size, on one GPU: BASELINE's 1M-point
+    block matvec (config 3) sharded by FMM subtree over 8 ranks -- each rank its own
+    handle, input valid only at its own range and halo (NaN elsewhere), up pass over
+    its own and halo subtrees, the tier-0 root multipoles exchanged, owned slice out
+    -- equals the unsharded matvec."""
+    torch = _torch()
+    import aniso_amd
 
     sz, d, ks, g = 1024, 1, 5, 0.8
     full = aniso_amd.Aniso(sz, d, ks, g, 10, 4, 20)
@@ -660,25 +738,11 @@ def test_block_matvec_eight_shards_at_config3_size():
     ref = torch.zeros_like(U)
     full.block_op_dev(2, U, ref, tree=True)
     torch.cuda.synchronize()
-    world = 8
-    ranges = adist.shard_ranges(full, world)
     del full
-    L = adist.pad_len(ranges)
-    gathered = torch.zeros(world, ks, L, dtype=torch.float64, device="cuda")
-    for r in range(world):
-        sh = aniso_amd.Aniso(sz, d, ks, g, 10, 4, 20)
-        sh.set_shard(r, world)
-        sh.setCoeff(*coef)
-        for m in range(2 * ks - 1):
-            sh.cache(m)
-        b, e = sh.shard()
-        assert (b, e) == ranges[r]
-        sh.block_op_dev(2, U, gathered[r], tree=True)
-        torch.cuda.synchronize()
-        del sh
-    gidx = torch.tensor(adist.block_gather_index(ranges, L, ks), device="cuda")
-    got = torch.index_select(gathered.view(-1), 0, gidx).view(ks, -1)
-    assert float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref)) <= 1e-13
+    err, nans, halo = _two_phase_shards(sz, d, ks, 20, coef, 8, U, ref, g=g)
+    assert nans == 0
+    assert err <= 1e-13, err
+    assert halo < 0.2  # halo points per rank / own points (1 ring of 16 x 16-point subtrees)
 
 
 @pytest.mark.parametrize("sz", [256, 1024])
