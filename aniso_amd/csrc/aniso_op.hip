@@ -291,6 +291,9 @@ void Operator::uploadPlan() {
     up(dNearPts, plan.nearPts);
     up(dXT0Tasks, plan.xT0Tasks);
     up(dXRootRecv, plan.xRootRecv);
+    up(dNsPtr, plan.nsPtr);
+    up(dNsPts, plan.nsPts);
+    up(dNearLoc, plan.nearLoc);
     up(dXRootSlot, plan.xRootSlot);
     up(dXSendSlot, plan.xSendSlot);
     up(dUpTaskPtr, plan.upTaskPtr);
@@ -694,7 +697,9 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
                            dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(), dNearKOff.as<int64_t>(),
                            dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dSigDiag.as<double>(), hw,
-                           dFT.as<double>(), operm, obase, ldo, mask, scale, out, sn);
+                           dFT.as<double>(), operm, obase, ldo, mask, scale, out,
+                           dNearLoc.as<uint16_t>(), dNsPtr.as<int64_t>(), dNsPts.as<int>(),
+                           plan.nsMax, sn);
         } else if (plan.nearPartTotal > 0) {
             // symmetric U storage (K = 1 handles): one launch per term; the transposed
             // products go to partials summed over the terms

@@ -192,6 +192,7 @@ private:
     DevBuf dUpTaskPtr, dUpGrpPtr, dUpGrp, dUpNode, dUpCode, dUpDesc, dUpGrpFix, dUpGeom, dUpLeaf;                       // up-pass tiers
     DevBuf dDnTaskPtr, dDnGrpPtr, dDnGrp, dDnNode, dDnLeafPtr, dDnLeafSlot, dDnLeafIdx, dDnLeafPts, dDnPtsRange, dDnDesc, dDnGrpFix, dDnLeafGeom;  // down
     DevBuf dLeafInfo, dNearPtsPtr, dNearPts;
+    DevBuf dNsPtr, dNsPts, dNearLoc;  // near field sources staged per workgroup (k_near_hs)
     DevBuf dXT0Tasks, dXRootRecv, dXRootSlot, dXSendSlot;  // sharded up pass (plan.buildExchange)
     DevBuf dM2LNDir, dM2LCanonBase, dM2LInPtr, dM2LOutSlot, dM2LPart;  // symmetric M2L
     DevBuf dNearSym, dNearPart, dDnLeafNear, dDnNearPtr, dDnNearOff, dDnChainPtr, dDnChain;              // symmetric near field

@@ -510,6 +510,124 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
     }
 }
 
+// The same near field (leaves <= 16 points) with the sources staged in LDS: one
+// workgroup = 16 consecutive leaves (a 4 x 4 leaf block on a uniform grid) whose
+// U/W source points form one table (Plan::nsPts: their union, ~36 leaves instead
+// of 16 x 9 per-column gathers); the table rows (x, y, charges) are loaded once,
+// coalesced, and every column then reads its source from LDS by its 16-bit row
+// (nearLoc).  Only the E stream stays in HBM.  Same lane layout as k_near_hm<G=16>.
+template <int K, int U, int NR>
+__global__ void __launch_bounds__(256) k_near_hs(int nl, const int4* __restrict__ leafInfo,
+                                                 const int64_t* __restrict__ nearPtsPtr,
+                                                 const uint16_t* __restrict__ nearLoc, const int64_t* __restrict__ nsPtr,
+                                                 const int* __restrict__ nsPts, const int64_t* __restrict__ nearKOff,
+                                                 const double* __restrict__ E, const double* __restrict__ pxT,
+                                                 const double* __restrict__ pyT, const double* __restrict__ sigDiag,
+                                                 HarmWeights hw, const double* __restrict__ fT,
+                                                 const int* __restrict__ operm, int64_t obase, int64_t ldo, int flags,
+                                                 double scale, double* __restrict__ out) {
+    constexpr int KS = kStride<K>;
+    constexpr int RW = KS + 2;  // table row: x, y, the charges
+    extern __shared__ double tab[];
+    const bool nearOn = (flags & kStageNear) != 0;
+    const int g = (int)blockIdx.x;
+    if (nearOn) {
+        const int64_t r0 = nsPtr[g];
+        const int nr = (int)(nsPtr[g + 1] - r0);
+        for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+            const int64_t p = nsPts[r0 + i];
+            double* row = tab + (size_t)i * RW;
+            row[0] = pxT[p];
+            row[1] = pyT[p];
+#pragma unroll
+            for (int v = 0; v < KS; ++v) row[2 + v] = fT[(size_t)p * KS + v];
+        }
+    }
+    __syncthreads();
+    const int gl = threadIdx.x & 15;
+    const int li = g * 16 + (int)(threadIdx.x >> 4);
+    const bool active = li < nl;
+    int4 info = make_int4(0, 0, 0, 0);
+    int64_t pb = 0, koff = 0;
+    if (active) {
+        info = leafInfo[li];
+        pb = nearPtsPtr[li];
+        koff = nearKOff[li];
+    }
+    const int nT = info.z, S = nearOn ? info.w : 0;
+    const int64_t tb = info.y;
+    const int nq = (nT + 3) >> 2;
+    const int cstr = 2 * nq;
+    const int rq = gl & 3, cph = gl >> 2;  // 4 lanes per column, 4 column phases
+    const bool rowOk = active && rq < nq;
+    double tx[4], ty[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int t = min(4 * rq + j, max(nT - 1, 0));  // padded rows: E is zero there
+        tx[j] = rowOk ? pxT[tb + t] : 0.0;
+        ty[j] = rowOk ? pyT[tb + t] : 0.0;
+    }
+    double a[4][K];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < K; ++i) a[j][i] = 0.0;
+    if (rowOk) {
+        const dbl2* kc = reinterpret_cast<const dbl2*>(E + koff) + 2 * rq;
+        for (int c0 = cph; c0 < S; c0 += U * 4) {
+            dbl2 kk[U][2];
+            int ix[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int sc = c0 + u * 4;
+                const bool ok = sc < S;
+                const dbl2* p = kc + (size_t)min(sc, S - 1) * cstr;
+                kk[u][0] = ok ? __builtin_nontemporal_load(p) : dbl2{0.0, 0.0};
+                kk[u][1] = ok ? __builtin_nontemporal_load(p + 1) : dbl2{0.0, 0.0};
+                ix[u] = nearLoc[pb + min(sc, S - 1)];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const double* row = tab + (size_t)ix[u] * RW;
+                const double sx = row[0], sy = row[1];
+                double xw[K];
+#pragma unroll
+                for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * row[2 + b];
+                const double e4[4] = {kk[u][0].x, kk[u][0].y, kk[u][1].x, kk[u][1].y};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const double dy = sy - ty[j];
+                    hm_entry<K, true, NR>(e4[j], sx - tx[j], dy * dy, xw, a[j]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)  // sum over the column phases
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            double v = a[j][i];
+            v += dpp_f64<0x124>(v);  // row_ror:4
+            v += dpp_f64<0x128>(v);  // row_ror:8
+            a[j][i] = v;
+        }
+    if (rowOk) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = 4 * rq + j;
+            if (cph != j || t >= nT) continue;
+            const int64_t k = tb + t;
+            double f[K];
+            load_charges<K>(fT + (size_t)k * KS, f);
+            const double sd = nearOn ? sigDiag[k] : 0.0;
+            const int64_t oi = out_index(operm, obase, k);
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                out[(size_t)i * ldo + oi] = hw.om[i] * scale * __builtin_fma(hw.dw[i] * sd, f[i], a[j][i]);
+        }
+    }
+}
+
 
 // ----------------------------------------------------------------- launchers
 
@@ -564,8 +682,20 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, 
 void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
                     const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
                     const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
-                    int64_t ldo, int flags, double scale, double* out, hipStream_t s) {
+                    int64_t ldo, int flags, double scale, double* out, const uint16_t* nearLoc, const int64_t* nsPtr,
+                    const int* nsPts, int nsMax, hipStream_t s) {
     if (nl <= 0) return;
+    const size_t tabBytes = (size_t)nsMax * (kStride<8> + 2) * sizeof(double);
+    if (maxLeaf <= 16 && nsMax > 0 && nearLoc && tabBytes <= 64 * 1024) {  // sources staged in LDS (k_near_hs)
+        const unsigned ng = (unsigned)((nl + 15) / 16);
+        ANISO_HM_DISPATCH_K(K, ({
+            const size_t shm = (size_t)nsMax * (kStride<KK> + 2) * sizeof(double);
+            k_near_hs<KK, 4, 2><<<ng, 256, shm, s>>>(nl, leafInfo, nearPtsPtr, nearLoc, nsPtr, nsPts, nearKOff, E,
+                                                     pxT, pyT, sigDiag, hw, fT, operm, obase, ldo, flags, scale, out);
+        }));
+        HIP_LAUNCH_CHECK();
+        return;
+    }
 #define ANISO_NEAR_HM(G)                                                                                      \
     ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, G, 4, 2><<<blocks_for((int64_t)nl * G, 256), 256, 0, s>>>(           \
                                nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm, \

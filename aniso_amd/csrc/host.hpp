@@ -88,6 +88,14 @@ struct Plan {
     std::vector<int> nearInPtr, nearInOff;     // per leaf: offsets of the partial blocks addressed to it
     std::vector<int64_t> nearPtsPtr;           // per leaf: its S source points (tree positions)
     std::vector<int> nearPts;
+    // near field staged per workgroup (k_near_hs): 16 consecutive
+    // leaves (<= 16 points each) share one LDS table of the union of their source
+    // points; nearLoc[j] = nearPts[j]'s row in its group's table, nsPtr = CSR of the
+    // tables (tree positions).  Empty when the leaves do not fit the scheme.
+    std::vector<int64_t> nsPtr;
+    std::vector<int> nsPts;
+    std::vector<uint16_t> nearLoc;
+    int nsMax = 0;  // largest table (points)
     int64_t nearKTotal = 0;
     std::vector<int> m2lTgt;                   // active target nodes with M2L work
     std::vector<int64_t> m2lPtr;               // CSR over m2lTgt -> source nodes
