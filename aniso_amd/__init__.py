@@ -77,6 +77,8 @@ def lib():
             "aniso_block_op": [P, I, dp, dp],
             "aniso_apply_block": [P, dp, dp, D, dp],
             "aniso_shard_cuts": [P, I, lp],
+            "aniso_forward_f32_dev": [P, P, P, P],
+            "aniso_forward_f32_stages_dev": [P, P, I, P, P],
             "aniso_shard_exchange": [P, I, lp],
             "aniso_shard_halo": [P, lp],
             "aniso_shard_roots": [P, ip, ip, ip],
@@ -250,6 +252,24 @@ class Aniso:
         s = torch.cuda.current_stream().cuda_stream if stream is None else stream
         _check(lib().aniso_forward_tree_dev(self.address, px, py, ctypes.c_void_p(s)))
         return y_slice
+
+    def forward_f32_dev(self, X, Y, stream=None, mask=STAGE_ALL):
+        """Config 5's fp32 operator: Y = X - K_0(sigma_s .* X) for 16 right-hand sides on
+        MFMA.  X, Y: (N, 16) contiguous float32 CUDA tensors, point-major, tree order."""
+        import torch
+
+        for t, nm in ((X, "X"), (Y, "Y")):
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+                    and tuple(t.shape) == (self.N, 16)):
+                raise AnisoError(1, f"{nm} must be a contiguous ({self.N}, 16) float32 CUDA tensor")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        if mask == STAGE_ALL:
+            _check(lib().aniso_forward_f32_dev(self.address, ctypes.c_void_p(X.data_ptr()),
+                                               ctypes.c_void_p(Y.data_ptr()), ctypes.c_void_p(s)))
+        else:
+            _check(lib().aniso_forward_f32_stages_dev(self.address, ctypes.c_void_p(X.data_ptr()), int(mask),
+                                                      ctypes.c_void_p(Y.data_ptr()), ctypes.c_void_p(s)))
+        return Y
 
     # ---- the block operator of aniso.m (aniso.m:121-157)
     def apply_block_dev(self, x, ids, mixes, out, use_sigma=False, tree=False, stream=None):
@@ -445,7 +465,7 @@ class Aniso:
         _check(lib().aniso_stats(self.address, s.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
         keys = ["near_entries", "m2l_entries", "m2l_pairs", "leaves", "m2l_targets", "tree_nodes", "max_leaf", "N",
                 "stored_near", "stored_m2l", "m2l_canon", "near_partial", "harmonic", "att_m2l_blocks",
-                "hm_clusters", "hm_dual_pairs", "hm_block_reads", "near_clusters", "near_dual_pairs"]
+                "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "reserved"]
         return dict(zip(keys, (int(v) for v in s)))
 
     def set_timing(self, on):

@@ -210,6 +210,7 @@ void Operator::ensureDevice() {
     for (size_t i = 0; i < ct.legB.size(); ++i) P.legB[i] = ct.legB[i];
     for (int i = 0; i < d2; ++i) P.coefScale[i] = ct.coefScale[i];
     dParams.upload(&P, sizeof(P));
+    hostP = P;
     // work arrays
     dCharge.alloc(geo.N * sizeof(double));
     dOut.alloc(geo.N * sizeof(double));
@@ -945,6 +946,176 @@ void Operator::lineIntegrals(const double* seg, int n, double* out) {
     launch_line_integrals(n, ds.as<double>(), dStCoef.as<double>(), dParams.as<Params>(), dout.as<double>(), own);
     HIP_CHECK(hipStreamSynchronize(own));
     HIP_CHECK(hipMemcpy(out, dout.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost));
+}
+
+// ---------------------------------------------------------------- fp32 operator
+// (f32op.hip).  The plan is the unsharded tree's: every non-empty
+// leaf with its directed U then W sources (bbfmm.h:1081-1099), M2M levels bottom-up
+// (bbfmm.h:855-859), every non-empty node's V then X pairs (bbfmm.h:1051-1065), L2L
+// levels top-down (bbfmm.h:1070-1071).  The caches are the fp64 mode-0 operators
+// (k_cache_m2l / k_cache_near on these directed lists) rounded to fp32.
+void Operator::buildF32() {
+    if (plan.nranks != 1) throw std::logic_error("fp32 operator on a sharded handle");
+    if (!modeCached(0)) throw std::runtime_error("fp32 operator before cache(0)");
+    ensureDevice();
+    F32Plan& f = f32;
+    f = F32Plan();
+    const Tree& t = tree;
+    std::vector<int> lv;
+    for (int i = 0; i < t.nn; ++i)
+        if (t.isLeaf[i] && !t.isEmpty[i]) lv.push_back(i);
+    std::sort(lv.begin(), lv.end(), [&](int a, int b) { return t.begin[a] < t.begin[b]; });
+    f.nearPtr.push_back(0);
+    f.srcPtr.push_back(0);
+    int maxSrc = 1;
+    for (int n : lv) {
+        int64_t S = 0;
+        const int64_t s0 = (int64_t)f.srcNodes.size();
+        for (int64_t k = t.uPtr[n]; k < t.uPtr[n + 1]; ++k)
+            if (!t.isEmpty[t.uIdx[k]]) f.srcNodes.push_back(t.uIdx[k]);
+        for (int64_t k = t.wPtr[n]; k < t.wPtr[n + 1]; ++k)
+            if (!t.isEmpty[t.wIdx[k]]) f.srcNodes.push_back(t.wIdx[k]);
+        for (size_t k = s0; k < f.srcNodes.size(); ++k) {
+            const int b = f.srcNodes[k];
+            for (int64_t q = 0; q < t.count[b]; ++q) f.nearPts.push_back((int)(t.begin[b] + q));
+            S += t.count[b];
+        }
+        maxSrc = std::max<int>(maxSrc, (int)(f.srcNodes.size() - s0));
+        const int64_t Sp = (S + 15) & ~(int64_t)15;
+        for (int64_t q = S; q < Sp; ++q) f.nearPts.push_back((int)t.begin[n]);  // zero columns
+        const int nT = (int)t.count[n];
+        f.leaves.push_back(n);
+        f.leafInfo.push_back({n, (int)t.begin[n], nT, (int)Sp});
+        f.srcCount.push_back((int)S);
+        f.koff.push_back(f.nearTiles);
+        f.koffD.push_back(f.nearD);
+        f.nearTiles += (int64_t)((nT + 15) / 16) * (Sp / 16) * 64;
+        f.nearD += S * ((nT + 3) & ~3);
+        f.nearPtr.push_back((int64_t)f.nearPts.size());
+        f.srcPtr.push_back((int64_t)f.srcNodes.size());
+    }
+    const int D = t.maxLevel;
+    f.m2m.assign(std::max(D, 1), {});
+    f.l2l.assign(D + 1, {});
+    for (int i = 0; i < t.nn; ++i) {
+        if (t.isEmpty[i] || t.parent[i] < 0) continue;
+        if (!t.isLeaf[i]) f.m2m[t.level[i]].push_back(i);
+        if (t.level[i] >= 2) f.l2l[t.level[i]].push_back(i);
+        f.m2lTgt.push_back(i);
+    }
+    f.m2lPtr.push_back(0);
+    for (int n : f.m2lTgt) {
+        for (int64_t k = t.vPtr[n]; k < t.vPtr[n + 1]; ++k)
+            if (!t.isEmpty[t.vIdx[k]]) f.m2lSrc.push_back(t.vIdx[k]);
+        for (int64_t k = t.xPtr[n]; k < t.xPtr[n + 1]; ++k)
+            if (!t.isEmpty[t.xIdx[k]]) f.m2lSrc.push_back(t.xIdx[k]);
+        f.m2lPtr.push_back((int64_t)f.m2lSrc.size());
+        for (int64_t p = f.m2lPtr[f.m2lPtr.size() - 2]; p < f.m2lPtr.back(); ++p) f.m2lPairTgt.push_back(n);
+    }
+    // device lists
+    up(d32Leaves, f.leaves);
+    std::vector<int4> li(f.leafInfo.size());
+    for (size_t i = 0; i < li.size(); ++i)
+        li[i] = make_int4(f.leafInfo[i][0], f.leafInfo[i][1], f.leafInfo[i][2], f.leafInfo[i][3]);
+    up(d32LeafInfo, li);
+    up(d32NearPtr, f.nearPtr);
+    up(d32NearPts, f.nearPts);
+    up(d32Koff, f.koff);
+    up(d32Tgt, f.m2lTgt);
+    up(d32Ptr, f.m2lPtr);
+    up(d32Src, f.m2lSrc);
+    up(d32Level, t.level);
+    d32LevelNodes.clear();
+    d32LevelNodes.resize(f.m2m.size() + f.l2l.size());
+    for (size_t l = 0; l < f.m2m.size(); ++l) up(d32LevelNodes[l], f.m2m[l]);
+    for (size_t l = 0; l < f.l2l.size(); ++l) up(d32LevelNodes[f.m2m.size() + l], f.l2l[l]);
+    // transfer operators in A order: Rup = R_q^T (M2M), Rdn = R_q (L2L)
+    std::vector<float> rup(4 * 256), rdn(4 * 256);
+    for (int q = 0; q < 4; ++q)
+        for (int l = 0; l < 64; ++l)
+            for (int e = 0; e < 4; ++e) {
+                const int i = l & 15, k = 4 * (l >> 4) + e;
+                rup[q * 256 + l * 4 + e] = (float)hostP.R[q][k + i * 16];
+                rdn[q * 256 + l * 4 + e] = (float)hostP.R[q][i + k * 16];
+            }
+    up(d32Rup, rup);
+    up(d32Rdn, rdn);
+    d32Mult.alloc((size_t)t.nn * 256 * sizeof(float));
+    d32Local.alloc((size_t)t.nn * 256 * sizeof(float));
+    d32FT.alloc((size_t)geo.N * 16 * sizeof(float));
+    d32CT.alloc((size_t)geo.N * 16 * sizeof(float));
+    // caches: fp64 mode-0 blocks on the directed lists, rounded to fp32
+    const Params* P = dParams.as<Params>();
+    {
+        const int64_t np_ = (int64_t)f.m2lSrc.size();
+        DevBuf pt, tmp;
+        up(pt, f.m2lPairTgt);
+        tmp.alloc((size_t)std::max<int64_t>(np_, 1) * 256 * sizeof(double));
+        d32Km2l.alloc((size_t)std::max<int64_t>(np_, 1) * 256 * sizeof(float));
+        launch_cache_m2l(np_, pt.as<int>(), d32Src.as<int>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
+                         dNry.as<double>(), dStCoef.as<double>(), P, 0, tmp.as<double>(), own);
+        launch32_conv_m2l(np_, tmp.as<double>(), d32Km2l.p, own);
+        HIP_CHECK(hipStreamSynchronize(own));
+    }
+    {
+        DevBuf sp, sn, kd, tmp, sc;
+        up(sp, f.srcPtr);
+        up(sn, f.srcNodes);
+        up(kd, f.koffD);
+        up(sc, f.srcCount);
+        tmp.alloc((size_t)std::max<int64_t>(f.nearD, 1) * sizeof(double));
+        d32Knear.alloc((size_t)std::max<int64_t>(f.nearTiles, 1) * 4 * sizeof(float));
+        launch_cache_near((int)f.leaves.size(), d32Leaves.as<int>(), sp.as<int64_t>(), sn.as<int>(), kd.as<int64_t>(),
+                          dBegin.as<int64_t>(), dCount.as<int64_t>(), dPxT.as<double>(), dPyT.as<double>(),
+                          dStCoef.as<double>(), P, 0, maxSrc, tmp.as<double>(), own);
+        launch32_conv_near((int)f.leaves.size(), d32LeafInfo.as<int4>(), kd.as<int64_t>(), d32Koff.as<int64_t>(),
+                           sc.as<int>(), tmp.as<double>(), d32Knear.p, own);
+        HIP_CHECK(hipStreamSynchronize(own));
+    }
+    f32Ready = true;
+}
+
+void Operator::forwardF32Dev(const float* X, float* Y, hipStream_t s, int mask) {
+    if (!f32Ready) buildF32();
+    ensureDevice();
+    const Params* P = dParams.as<Params>();
+    const F32Plan& f = f32;
+    const float scale = (float)(M_1_PI / 2.0);  // AnisoWrapper.cpp:129-130
+    const bool tm = timeStages;
+    const int e0 = tm ? mark(s) : -1;
+    launch32_p2m((int)f.leaves.size(), d32Leaves.as<int>(), dBegin.as<int64_t>(), dCount.as<int64_t>(),
+                 dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(),
+                 dPyT.as<double>(), X, dSigmaT.as<double>(), dWT.as<double>(), P, d32Mult.p, d32FT.as<float>(),
+                 d32CT.as<float>(), s);
+    for (int l = (int)f.m2m.size() - 1; l >= 1; --l)
+        launch32_m2m((int)f.m2m[l].size(), d32LevelNodes[l].as<int>(), dChild.as<int4>(), dCount.as<int64_t>(),
+                     d32Rup.p, d32Mult.p, s);
+    const int e1 = tm ? mark(s) : -1;
+    if (tm) spans.push_back({1, e0, e1});
+    if (mask & kStageFar) {
+        launch32_m2l((int)f.m2lTgt.size(), d32Tgt.as<int>(), d32Ptr.as<int64_t>(), d32Src.as<int>(), d32Km2l.p,
+                     d32Mult.p, d32Local.p, s);
+        const int e2 = tm ? mark(s) : -1;
+        if (tm) spans.push_back({2, e1, e2});
+        for (size_t l = 2; l < f.l2l.size(); ++l)
+            launch32_l2l((int)f.l2l[l].size(), d32LevelNodes[f.m2m.size() + l].as<int>(), dParent.as<int>(),
+                         dSlot.as<int>(), d32Rdn.p, d32Local.p, s);
+    }
+    const int e3 = tm ? mark(s) : -1;
+    launch32_leaf((int)f.leaves.size(), d32LeafInfo.as<int4>(), d32NearPtr.as<int64_t>(), d32NearPts.as<int>(),
+                  d32Koff.as<int64_t>(), d32Knear.p, d32Level.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
+                  dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(), P, d32Local.p,
+                  d32FT.as<float>(), X, scale, mask, Y, s);
+    const int e4 = tm ? mark(s) : -1;
+    if (tm) spans.push_back({4, e3, e4});
+    launch32_corr(geo.d, geo.N, dPerm.as<int>(), dIperm.as<int>(), d32CT.as<float>(), d32FT.as<float>(),
+                  modes[0].C.as<double>(), modes[0].mu.as<double>(), P, mask, scale, Y, s);
+    if (tm) {
+        const int e5 = mark(s);
+        spans.push_back({6, e4, e5});
+        spans.push_back({7, e0, e5});
+        ++applies;
+    }
 }
 
 void Operator::permuteToTree(const double* orig, double* treeOut, hipStream_t s) {

@@ -109,6 +109,12 @@ public:
     void forwardDev(const double* u, double* out, hipStream_t s);
     int gmresHost(const double* q, double* x, int m, int maxit, double tol, double* hist, int maxhist,
                   double* finalResid);
+    // config 5's fp32 operator (f32op.hip): Y = X - K_0(sigma_s .* X)
+    // for 16 right-hand sides, X and Y point-major (N x 16 floats, tree order), every
+    // FMM translation a 16 x 16 x 16 MFMA product on fp32 caches (built from the
+    // fp64 mode-0 operators at the first call).  Unsharded handles only.
+    void forwardF32Dev(const float* X, float* Y, hipStream_t s, int mask = kStageAll);
+    int64_t f32Bytes() const { return f32Ready ? (int64_t)(d32Km2l.bytes + d32Knear.bytes) : 0; }
     hipStream_t stream() const { return own; }
     bool harmonicReady() const { return useAtt && attReady; }
     bool clustersOn() const { return useClusters; }
@@ -202,6 +208,24 @@ private:
     DevBuf dPadIn, dPadOut, dBlk;       // block operator: padded right-hand sides, x - mforward(x)
     DevBuf dHostIn, dHostOut, dSigAlt;  // host-pointer block operator: staging, sigma_s override
     std::vector<ModeCache> modes;
+    Params hostP{};  // the parameter block uploaded to dParams
+    // fp32 operator (buildF32): leaves with their directed U/W sources (padded to 16
+    // columns), M2M / L2L levels, directed M2L pairs
+    void buildF32();
+    bool f32Ready = false;
+    struct F32Plan {
+        std::vector<int> leaves;
+        std::vector<std::array<int, 4>> leafInfo;  // node, begin, count, padded sources
+        std::vector<int64_t> nearPtr, koff, koffD, srcPtr;
+        std::vector<int> nearPts, srcNodes, srcCount;
+        std::vector<std::vector<int>> m2m, l2l;  // per level: M2M bottom-up, L2L top-down
+        std::vector<int> m2lTgt, m2lSrc, m2lPairTgt;
+        std::vector<int64_t> m2lPtr;
+        int64_t nearTiles = 0, nearD = 0;
+    } f32;
+    DevBuf d32Leaves, d32LeafInfo, d32NearPtr, d32NearPts, d32Koff, d32Tgt, d32Ptr, d32Src;
+    DevBuf d32Km2l, d32Knear, d32Rup, d32Rdn, d32Mult, d32Local, d32FT, d32CT, d32Level;
+    std::vector<DevBuf> d32LevelNodes;  // m2m levels then l2l levels
 };
 
 }  // namespace aniso

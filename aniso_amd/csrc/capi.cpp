@@ -226,6 +226,25 @@ int aniso_forward_tree_end_dev(aniso_handle h, const double* x_tree, double* y_s
     });
 }
 
+int aniso_forward_f32_dev(aniso_handle h, const float* x, float* y, void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(x);
+        CHECK_PTR(y);
+        get(h).forwardF32Dev(x, y, (hipStream_t)stream);
+    });
+}
+
+int aniso_forward_f32_stages_dev(aniso_handle h, const float* x, int mask, float* y, void* stream) {
+    CHECK_HANDLE(h);
+    return guarded([&] {
+        CHECK_PTR(x);
+        CHECK_PTR(y);
+        if (mask < 0 || mask > aniso::kStageAll) throw std::invalid_argument("bad stage mask");
+        get(h).forwardF32Dev(x, y, (hipStream_t)stream, mask);
+    });
+}
+
 int aniso_apply_block_dev(aniso_handle h, int nrhs, const double* x, int64_t ldx, int use_sigma, int nterm,
                           const int* ids, const double* mixes, double* out, int64_t ldo, int tree, void* stream) {
     CHECK_HANDLE(h);
@@ -462,7 +481,7 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[14] = cl ? (int64_t)op.plan.hmClPtr.size() - 1 : 0;
         s[15] = cl ? op.plan.hmDual : 0;
         s[16] = cl ? (int64_t)op.plan.hmSrc.size() : (int64_t)op.plan.attSrc.size();
-        s[17] = 0;  // reserved (near-field clusters, removed in round 2)
+        s[17] = op.f32Bytes();  // config 5's fp32 operator caches (0 before its first apply)
         s[18] = 0;
     });
 }

@@ -86,6 +86,28 @@ void launch_up_tier(int K, int ntask, int taskBase, const int* taskList, int max
                     const double* pxT, const double* pyT, const double* xin, int64_t ldi, int treeIn, const int* perm,
                     const double* sigT, const double* wT, double* fT, double* cT, const Params* P, double* mult,
                     const int* rootSlot, const double* recv, const int* sendSlot, double* send, hipStream_t s);
+// config 5's fp32 operator (f32op.hip): node expansions as 64 lanes x float4
+// (void* below), vectors point-major N x 16 floats
+void launch32_p2m(int nleaf, const int* leaves, const int64_t* begin, const int64_t* count, const double* ncx,
+                  const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
+                  const float* X, const double* sigT, const double* wT, const Params* P, void* mult, float* fT,
+                  float* cT, hipStream_t s);
+void launch32_m2m(int nn, const int* nodes, const int4* child, const int64_t* count, const void* Rup, void* mult,
+                  hipStream_t s);
+void launch32_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* src, const void* K32, const void* mult,
+                  void* local, hipStream_t s);
+void launch32_l2l(int nn, const int* nodes, const int* parent, const int* slot, const void* Rdn, void* local,
+                  hipStream_t s);
+void launch32_leaf(int nleaf, const int4* leafInfo, const int64_t* nearPtr, const int* nearPts, const int64_t* koff,
+                   const void* Knear, const int* level, const double* ncx, const double* ncy, const double* nrx,
+                   const double* nry, const double* pxT, const double* pyT, const Params* P, const void* local,
+                   const float* fT, const float* X, float scale, int flags, float* Y, hipStream_t s);
+void launch32_corr(int d, int64_t N, const int* perm, const int* iperm, const float* cT, const float* fT,
+                   const double* C, const double* mu, const Params* P, int flags, float scale, float* Y,
+                   hipStream_t s);
+void launch32_conv_m2l(int64_t npairs, const double* Kd, void* K32, hipStream_t s);
+void launch32_conv_near(int nl, const int4* info, const int64_t* koffD, const int64_t* koff, const int* srcCount,
+                        const double* Kd, void* K32, hipStream_t s);
 // the tier-0 root records of a sharded apply without upper tiers, scattered back
 // from the all-gather (mult[nodes[j]] = recv[j] where nodes[j] >= 0)
 void launch_roots_unpack(int K, int nslots, const int* nodes, const double* recv, double* mult, hipStream_t s);

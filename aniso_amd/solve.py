@@ -13,9 +13,13 @@ for k right-hand sides at once).
 * Outer loop: iterative refinement in fp64, r = b - A x, x += inner(r), until
   ||r|| / ||b|| <= tol for every right-hand side.
 
+* Inner operator for 16 right-hand sides: the fp32 MFMA operator
+  (`Aniso.forward_f32_dev`: fp32 caches, every FMM translation a 16 x 16 x 16
+  v_mfma_f32_16x16x4_f32 product) on tree-order, point-major
+  vectors.  The outer residuals use the fp64 operator.
+
 This is host orchestration over torch tensors (device memory and BLAS-1 plumbing);
-the operator it calls is the HIP path.  The fp32 *caches* of config 5 are not built:
-the operator stays fp64.
+the operators it calls are the HIP path.
 """
 import numpy as np
 
@@ -91,41 +95,48 @@ def rhs_block(op, Q):
     return R
 
 
-def _inner_gmres(op, R, m, tol, max_cycles):
-    """Approximately solve A D = R (rows independent) with an fp32 Krylov basis."""
+def _inner_gmres(apply, R, m, tol, max_cycles, rd=1):
+    """Approximately solve A D = R (right-hand sides independent) with an fp32 Krylov
+    basis.  rd: the axis of R that runs over the points (1: R is (k, n), the fp64
+    operator's row layout; 0: (n, k), the fp32 operator's point-major layout).
+    apply(X, W): W = A X in R's layout (X may be fp32 or fp64, W fp64)."""
     import torch
 
-    k, n = R.shape
+    k = R.shape[1 - rd]
+
+    def col(v):  # per-right-hand-side scalars broadcast along the points
+        return v[:, None] if rd == 1 else v[None, :]
+
     D = torch.zeros_like(R)
-    r0 = torch.linalg.norm(R, dim=1).cpu().numpy()
+    r0 = torch.linalg.norm(R, dim=rd).cpu().numpy()
     W = torch.empty_like(R)
     its = 0
     for _ in range(max_cycles):
         Rc = R.clone()
         if its:
-            forward_block(op, D, W)
+            apply(D, W)
             Rc -= W
-        beta = torch.linalg.norm(Rc, dim=1).cpu().numpy()
+        beta = torch.linalg.norm(Rc, dim=rd).cpu().numpy()
         done = beta <= tol * r0
         if done.all():
             break
-        V = torch.zeros(m + 1, k, n, dtype=torch.float32, device=R.device)
-        V[0] = (Rc / torch.tensor(np.where(beta > 0, beta, 1.0), device=R.device)[:, None]).float()
+        V = torch.zeros((m + 1,) + tuple(R.shape), dtype=torch.float32, device=R.device)
+        V[0] = (Rc / col(torch.tensor(np.where(beta > 0, beta, 1.0), device=R.device))).float()
         H = np.zeros((k, m + 1, m))
         cs, sn = np.zeros((k, m)), np.zeros((k, m))
         g = np.zeros((k, m + 1))
         g[:, 0] = beta
         j_used = 0
         for j in range(m):
-            forward_block(op, V[j].double(), W)
+            apply(V[j], W)
             w = W
             for i in range(j + 1):  # modified Gram-Schmidt, fp64 accumulation of fp32 vectors
-                h = (V[i].double() * w).sum(1)
-                w = w - h[:, None] * V[i].double()
+                h = (V[i].double() * w).sum(rd)
+                w = w - col(h) * V[i].double()
                 H[:, i, j] = h.cpu().numpy()
-            hn = torch.linalg.norm(w, dim=1)
+            hn = torch.linalg.norm(w, dim=rd)
             H[:, j + 1, j] = hn.cpu().numpy()
-            V[j + 1] = (w / torch.where(hn > 0, hn, torch.ones_like(hn))[:, None]).float()
+            V[j + 1] = (w / col(torch.where(hn > 0, hn, torch.ones_like(hn)))).float()
             for r in range(k):  # Givens (gmres.cpp:120-150) per right-hand side
                 for i in range(j):
                     t = cs[r, i] * H[r, i, j] + sn[r, i] * H[r, i + 1, j]
@@ -152,26 +163,49 @@ def _inner_gmres(op, R, m, tol, max_cycles):
             except np.linalg.LinAlgError:  # breakdown: least squares on the rotated system
                 Y[r] = np.linalg.lstsq(Hr, g[r, :j_used], rcond=None)[0]
         Yt = torch.tensor(Y, device=R.device)
-        D += torch.einsum("kj,jkn->kn", Yt, V[:j_used].double())
+        if rd == 1:
+            D += torch.einsum("kj,jkn->kn", Yt, V[:j_used].double())
+        else:
+            D += torch.einsum("kj,jnk->nk", Yt, V[:j_used].double())
     return D, its
 
 
-def gmres_mixed(op, B, tol=1e-12, m=40, inner_tol=1e-6, max_outer=30, max_cycles=20):
+def gmres_mixed(op, B, tol=1e-12, m=40, inner_tol=1e-6, max_outer=30, max_cycles=20, fp32_op=None):
     """Solve A X = B (rows) to ||B - A X|| / ||B|| <= tol per row.  Returns
-    (X, outer iterations, inner iterations, final relative residuals)."""
+    (X, outer iterations, inner iterations, final relative residuals).
+
+    fp32_op (default: when B has 16 rows): the inner solves run on the fp32 MFMA
+    operator (Aniso.forward_f32_dev, fp32 caches) in tree order, point-major; the
+    outer residuals stay on the fp64 operator, so the solution is fp64-accurate."""
     import torch
 
+    if fp32_op is None:
+        fp32_op = B.shape[0] == 16
     X = torch.zeros_like(B)
     W = torch.empty_like(B)
     bn = torch.linalg.norm(B, dim=1)
     inner = 0
+    if fp32_op:
+        perm = torch.tensor(op.tree_perm(), device=B.device, dtype=torch.int64)
+        X32 = torch.empty((B.shape[1], 16), dtype=torch.float32, device=B.device)
+        W32 = torch.empty_like(X32)
+
+        def apply32(Xin, Wout):
+            X32.copy_(Xin)
+            op.forward_f32_dev(X32, W32)
+            Wout.copy_(W32)
+
     for outer in range(max_outer + 1):
         forward_block(op, X, W)
         R = B - W
         rel = (torch.linalg.norm(R, dim=1) / bn).cpu().numpy()
         if (rel <= tol).all() or outer == max_outer:
             return X, outer, inner, rel
-        D, its = _inner_gmres(op, R, m, inner_tol, max_cycles)
+        if fp32_op:
+            D, its = _inner_gmres(apply32, R[:, perm].t().contiguous(), m, inner_tol, max_cycles, rd=0)
+            X[:, perm] += D.t()
+        else:
+            D, its = _inner_gmres(lambda a, b: forward_block(op, a.double(), b), R, m, inner_tol, max_cycles)
+            X += D
         inner += its
-        X += D
     return X, max_outer, inner, rel

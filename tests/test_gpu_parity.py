@@ -749,9 +749,11 @@ def test_block_matvec_eight_shards_at_config3_size():
 def test_config5_mixed_precision_16_rhs_matches_fp64_gmres(sz):
     """the config-3 geometry (sz = 1024 is the full 1M
     points), mode 0, 16 right-hand sides q_k (Gaussian bumps centred by
-    mt19937_64(seed = k)), solved with an fp32 Krylov basis and fp64 refinement over
-    the batched device apply (8 right-hand sides per apply); each solution matches the
-    fp64 single-RHS device GMRES (main.cpp:121-141) to 1e-10."""
+    mt19937_64(seed = k)), solved with an fp32 Krylov basis and the fp32 MFMA
+    operator (fp32 caches, 16 right-hand sides per apply) in the inner solves and
+    fp64 refinement over the fp64 batched device apply; each solution matches the
+    fp64 single-RHS device GMRES (main.cpp:121-141) to 1e-10 (that GMRES is checked
+    against the oracle's in test_config5_fp64_gmres_matches_oracle)."""
     torch = _torch()
     import aniso_amd
     from aniso_amd.solve import config5_charges, gmres_mixed, rhs_block
@@ -771,6 +773,32 @@ def test_config5_mixed_precision_16_rhs_matches_fp64_gmres(sz):
         its, x, hist, fr = a.gmres(Q[s], m=80, maxit=400, tol=1e-12)
         assert its > 0
         assert _rel(Xh[s], x) <= 1e-10, (s, _rel(Xh[s], x))
+
+
+def test_config5_fp64_gmres_matches_oracle():
+    """The fp64 reference solve of config 5 (the device GMRES, main.cpp:121-141) against
+    the oracle's GMRES (gmres.cpp:53-169 restated) at sz = 256 (N = 65,536) for the
+    first config-5 right-hand side: same iteration count, solutions within 1e-10."""
+    _torch()
+    import aniso_amd
+    from aniso_amd.solve import config5_charges
+    from oracle.oracle_py import Oracle
+
+    sz = 256
+    a = aniso_amd.Aniso(sz, 1, 1, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    ss, st = main_coeffs(xy)
+    a.setCoeff(ss, st)
+    a.cache(0)
+    q = config5_charges(xy, 0)
+    j, x, hist, fr = a.gmres(q, m=80, maxit=400, tol=1e-12)
+    o = Oracle(sz, 1, 1, 0.8, 10, 4, 20)
+    o.setCoeff(ss, st)
+    o.cache(0)
+    jo, xo, ho, fro = o.gmres_main(q, 80, 400, 1e-12)
+    o.close()
+    assert j > 0 and jo == j, (j, jo)
+    assert _rel(x, xo) <= 1e-10
 
 
 def test_config2_full_size_matches_oracle():
@@ -830,3 +858,34 @@ def test_config4_four_million_points_properties_and_shard():
     torch.cuda.synchronize()
     ref = full[b:e]
     assert float(torch.linalg.norm(part - ref) / torch.linalg.norm(ref)) <= 1e-14
+
+
+@pytest.mark.parametrize("sz,d,ml,coeffs", [(64, 1, 20, "main"), (30, 3, 20, "rough"), (24, 1, 2, "rough"),
+                                            (11, 3, 20, "main"), (13, 2, 20, "rough"), (1, 3, 20, "main")])
+def test_fp32_mfma_operator_matches_fp64(sz, d, ml, coeffs):
+    """Config 5's fp32 operator (16 right-hand sides, every FMM translation on
+    v_mfma_f32_16x16x4_f32, fp32 caches) against the fp64 forward operator
+    (main.cpp:125-136) column by column: fp32 agreement (<= 2e-6 relative, the
+    inner solver's operator; the outer refinement keeps the fp64 one).  Uniform,
+    d = 3 (9-point squares), maxLevel-limited (36-point leaves), odd sz, and the
+    single-leaf tree."""
+    torch = _torch()
+    import aniso_amd
+
+    a = aniso_amd.Aniso(sz, d, 1, 0.8, 8, 4, ml)
+    xy = a.getNodes()
+    a.setCoeff(*(main_coeffs(xy) if coeffs == "main" else rough_coeffs(xy, 5)))
+    a.cache(0)
+    rng = np.random.default_rng(sz + d)
+    X = torch.tensor(rng.uniform(-1, 1, (a.N, 16)), device="cuda", dtype=torch.float32)
+    Y = torch.zeros_like(X)
+    a.forward_f32_dev(X, Y)
+    Xd = X.double().t().contiguous()
+    ref = torch.zeros_like(Xd)
+    for j in range(16):
+        a.forward_tree_dev(Xd[j], ref[j])
+    torch.cuda.synchronize()
+    err = float(torch.linalg.norm(Y.double().t() - ref) / torch.linalg.norm(ref))
+    # the operator part alone (X - Y vs X - ref): fp32 relative accuracy of K_0
+    kerr = float(torch.linalg.norm((Xd - Y.double().t()) - (Xd - ref)) / torch.linalg.norm(Xd - ref))
+    assert err <= 2e-6 and kerr <= 2e-5, (err, kerr)

@@ -14,10 +14,20 @@ class DenseOp:
         rng = np.random.default_rng(seed)
         self.K = torch.tensor(rng.uniform(-1, 1, (n, n)) / (2.5 * np.sqrt(n)))
         self.sig = torch.tensor(rng.uniform(0.5, 1.0, n))
+        self.perm = rng.permutation(n).astype(np.int32)
 
     def apply_block_dev(self, x, ids, mixes, out, use_sigma=False):
         y = (x * self.sig if use_sigma else x) @ self.K.T
         out.copy_(torch.tensor(mixes[0]) @ y)
+
+    def tree_perm(self):
+        return self.perm
+
+    def forward_f32_dev(self, X, Y):
+        """The fp32 operator's call shape: (n, 16) float32, tree order, point-major."""
+        K = self.K[self.perm][:, self.perm].float()
+        s = self.sig[self.perm].float()
+        Y.copy_(X - K @ (s[:, None] * X))
 
 
 def test_mt19937_64_reference_value():
@@ -36,12 +46,18 @@ def test_config5_charges_are_gaussian_bumps_in_the_box():
         assert 0.1 <= c[0] <= 0.9 and 0.1 <= c[1] <= 0.9
 
 
-def test_mixed_gmres_matches_dense_solve_for_16_rhs():
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("fp32_op", [True, False])
+def test_mixed_gmres_matches_dense_solve_for_16_rhs(fp32_op):
+    """Both inner operators: the fp32 one (tree order, point-major, as
+    Aniso.forward_f32_dev) and the fp64 row-layout one."""
     n, k = 300, 16
     op = DenseOp(n, 1)
     A = np.eye(n) - op.K.numpy() * op.sig.numpy()[None, :]
     B = torch.tensor(np.random.default_rng(2).uniform(-1, 1, (k, n)))
-    X, outer, inner, rel = gmres_mixed(op, B, tol=1e-12, m=30, inner_tol=1e-6)
+    X, outer, inner, rel = gmres_mixed(op, B, tol=1e-12, m=30, inner_tol=1e-6, fp32_op=fp32_op)
     ref = np.linalg.solve(A, B.numpy().T).T
     assert (rel <= 1e-12).all() and outer >= 2  # fp32 inner solves need refinement
     assert np.linalg.norm(X.numpy() - ref) / np.linalg.norm(ref) <= 1e-10
