@@ -79,6 +79,7 @@ def lib():
             "aniso_shard_cuts": [P, I, lp],
             "aniso_forward_f32_dev": [P, P, P, P],
             "aniso_forward_f32_stages_dev": [P, P, I, P, P],
+            "aniso_set_deterministic": [P, I],
             "aniso_shard_exchange": [P, I, lp],
             "aniso_shard_halo": [P, lp],
             "aniso_shard_roots": [P, ip, ip, ip],
@@ -467,6 +468,10 @@ class Aniso:
                 "stored_near", "stored_m2l", "m2l_canon", "near_partial", "harmonic", "att_m2l_blocks",
                 "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "reserved"]
         return dict(zip(keys, (int(v) for v in s)))
+
+    def set_deterministic(self, on):
+        """Bitwise-reproducible block applies (per-target M2L waves) on / off."""
+        _check(lib().aniso_set_deterministic(self.address, int(bool(on))))
 
     def set_timing(self, on):
         _check(lib().aniso_set_timing(self.address, int(bool(on))))

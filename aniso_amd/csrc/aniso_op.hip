@@ -78,7 +78,6 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     // (DESIGN.md §3.9); ANISO_HARMONIC=0 keeps the per-mode operator stream
     useAtt = ks > 1 && !plan.nearSymmetric;
     if (const char* e = std::getenv("ANISO_HARMONIC")) useAtt = useAtt && e[0] != '0';
-    if (const char* e = std::getenv("ANISO_HM_CLUSTER")) useClusters = e[0] != '0';
     if (const char* e = std::getenv("ANISO_OVERLAP")) overlap = std::atoi(e);
     if (const char* e = std::getenv("ANISO_FUSE_SUB")) fuseSub = e[0] != '0';
     sigma_s.assign(geo.N, 0.0);

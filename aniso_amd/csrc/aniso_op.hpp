@@ -118,6 +118,10 @@ public:
     hipStream_t stream() const { return own; }
     bool harmonicReady() const { return useAtt && attReady; }
     bool clustersOn() const { return useClusters; }
+    // bitwise-reproducible applies: the harmonic M2L as one wave per target (a fixed
+    // summation order) instead of the clustered kernel, whose LDS adds of the partner
+    // products land in run-dependent order (repeat applies agree to ~1e-15)
+    void setDeterministic(bool on) { useClusters = !on; }
     bool modeCached(int id) const { return id >= 0 && id < kernelSize && modes[id].ready; }
     int kernelSize = 0;
     // stage timing with HIP events recorded in-stream (no host sync per apply);

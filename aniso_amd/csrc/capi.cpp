@@ -341,6 +341,11 @@ int aniso_shard_cuts(aniso_handle h, int nranks, int64_t* cuts) {
     });
 }
 
+int aniso_set_deterministic(aniso_handle h, int on) {
+    CHECK_HANDLE(h);
+    return guarded([&] { get(h).setDeterministic(on != 0); });
+}
+
 int aniso_shard_exchange(aniso_handle h, int nrhs, int64_t* info) {
     CHECK_HANDLE(h);
     return guarded([&] {

@@ -396,6 +396,12 @@ def main():
         el0, t0s = timed(mode0, args.steps, 2)
         line["mode0_matvec_per_s"] = round(args.steps / el0, 3)
         line["mode0_stage_ms"] = {k: round(v_, 5) for k, v_ in t0s.items()}
+        # the bitwise-reproducible mode (aniso_set_deterministic: per-target M2L waves)
+        op.set_deterministic(True)
+        eld, tds = timed(matvec, args.steps, 2)
+        op.set_deterministic(False)
+        line["deterministic_matvec_per_s"] = round(args.steps / eld, 3)
+        line["deterministic_stage_ms"] = {k: round(v_, 5) for k, v_ in tds.items()}
     if args.verify:
         # one matvec of a fixed block vector through this (possibly sharded) path vs
         # an unsharded operator on the same device

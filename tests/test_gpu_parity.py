@@ -582,9 +582,9 @@ def test_harmonic_symmetric_blocks_match_directed(sz, d, ks, monkeypatch):
 def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatch):
     """The clustered harmonic M2L (in-cluster V pairs read once by
     the smaller id, both products, locals summed in LDS) against one wave per target
-    (ANISO_HM_CLUSTER=0); odd sz (non-uniform tree), directed storage, a
-    maxLevel-limited tree.  Also checks that in-cluster pairs exist and that the
-    cluster plan reads fewer E blocks."""
+    (aniso_set_deterministic); odd sz (non-uniform tree), directed storage, a
+    maxLevel-limited tree.  Also checks that in-cluster pairs exist, that the cluster
+    plan reads fewer E blocks, and that the deterministic mode repeats bitwise."""
     torch = _torch()
     import aniso_amd
 
@@ -593,9 +593,9 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatc
     # clusters, which small trees only reach with 4-target clusters: no in-cluster pairs)
     monkeypatch.setenv("ANISO_HM_CLDEPTH", "3")
     outs, st = [], []
-    for cl in ("1", "0"):
-        monkeypatch.setenv("ANISO_HM_CLUSTER", cl)
+    for det in (False, True):
         a = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, ml)
+        a.set_deterministic(det)
         xy = a.getNodes()
         a.setCoeff(*rough_coeffs(xy, 3))
         for m in range(2 * ks - 1):
@@ -604,11 +604,39 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatc
         U = torch.tensor(np.random.default_rng(5).uniform(-1, 1, (ks, a.N)), device="cuda")
         out = torch.zeros_like(U)
         a.block_op_dev(2, U, out)
+        if det:
+            again = torch.zeros_like(U)
+            a.block_op_dev(2, U, again)
+            torch.cuda.synchronize()
+            assert torch.equal(out, again)
         torch.cuda.synchronize()
         outs.append(out.cpu().numpy())
     assert st[0]["harmonic"] == 1 and st[0]["hm_clusters"] > 0 and st[1]["hm_clusters"] == 0
     assert st[0]["hm_dual_pairs"] > 0 and st[0]["hm_block_reads"] < st[1]["hm_block_reads"]
     assert _rel(outs[0], outs[1]) <= 1e-13
+
+
+def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
+    """aniso_set_deterministic at BASELINE's 1M-point block matvec: repeat applies
+    are bitwise identical, and equal the default (clustered) matvec to 1e-13."""
+    torch = _torch()
+    import aniso_amd
+
+    a = aniso_amd.Aniso(1024, 1, 5, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    a.setCoeff(*rough_coeffs(xy, 2))
+    for m in range(9):
+        a.cache(m)
+    U = torch.tensor(np.random.default_rng(8).uniform(-1, 1, (5, a.N)), device="cuda")
+    ref = torch.zeros_like(U)
+    a.block_op_dev(2, U, ref, tree=True)
+    a.set_deterministic(True)
+    o1, o2 = torch.zeros_like(U), torch.zeros_like(U)
+    a.block_op_dev(2, U, o1, tree=True)
+    a.block_op_dev(2, U, o2, tree=True)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert float(torch.linalg.norm(o1 - ref) / torch.linalg.norm(ref)) <= 1e-13
 
 
 @pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0"])
