@@ -343,11 +343,13 @@ def main():
         near_ms = times["near"]
         near_bytes = 8.0 * my_stats["stored_near"]
         near_gbs = near_bytes / (near_ms * 1e-3) / 1e9 if near_ms > 0 else 0.0
-        ntraffic, _ = pmc_traffic(f"void aniso::k_near_hm<{nb},") if world == 1 and args.sz == 1024 and args.d == 1 \
+        # leaves <= 16 points (this geometry) run k_near_hs (sources staged in LDS)
+        nkern = "k_near_hs" if my_stats["max_leaf"] <= 16 else "k_near_hm"
+        ntraffic, _ = pmc_traffic(f"void aniso::{nkern}<{nb},") if world == 1 and args.sz == 1024 and args.d == 1 \
             else (None, None)
         roofline["near"] = {"bound": "hbm", "achieved": round(near_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(near_gbs / HBM_PEAK_GBS, 4), "traffic": ntraffic,
-                            "kernel": f"k_near_hm<{nb}>", "kernel_ms": round(near_ms, 5),
+                            "kernel": f"{nkern}<{nb}>", "kernel_ms": round(near_ms, 5),
                             "algorithmic_bytes": int(near_bytes), "overlapped_with": roofline["kernel"]}
         roofline["m2l_rsqrt"] = "v_rsq_f64 + 1 Newton step (~1e-13 relative per entry); near field 2 steps (full fp64)"
     applies = ks * (2 * ks - 1) if block else 1  # the reference's mapping calls per matvec
