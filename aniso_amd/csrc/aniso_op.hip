@@ -779,7 +779,10 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     int ep = tm ? mark(s) : -1;
     span(1, e0, ep);
     if (phase == 2) e0 = pend.e0;
-    if (!nearDone) nearStage();
+    if (!nearDone) {
+        nearStage();
+        if (tm && sn == s) ep = mark(s);  // serial (ANISO_OVERLAP=0): the M2L span starts after the near field
+    }
     if (mask & kStageFar) {
         if (clustered) {
             m2lClusters(0, ncl, s);
