@@ -48,10 +48,11 @@ for rank in ranks:
     steps = 20
     for _ in range(steps):
         step()
+    host_ms = 1e3 * (time.perf_counter() - t0) / steps  # enqueue time: close to ms = host-bound
     torch.cuda.synchronize()
     ms = 1e3 * (time.perf_counter() - t0) / steps
     st = op.stats()
-    print(json.dumps({"world": world, "rank": rank, "ms_per_apply": round(ms, 4),
+    print(json.dumps({"world": world, "rank": rank, "ms_per_apply": round(ms, 4), "host_ms_per_apply": round(host_ms, 4),
                       "stage_ms": {k: round(v, 4) for k, v in op.stage_times().items()},
                       "t0_tasks_run": ex["t0_run"], "t0_tasks": ex["t0_tasks"], "halo_points": ex["halo_points"],
                       "m2l_clusters": st["hm_clusters"], "m2l_targets": st["m2l_targets"], "leaves": st["leaves"]}),
