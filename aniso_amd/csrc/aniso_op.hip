@@ -259,8 +259,11 @@ void Operator::uploadPlan() {
         up(dAttPtr, plan.attPtr);
         up(dAttSrc, plan.attSrc);
         up(dAttBlk, plan.attBlk);
-        up(dAttOwner, plan.attOwner);
-        up(dAttOther, plan.attOther);
+        std::vector<int> own(plan.attOwner), oth(plan.attOther);  // stored blocks, then the cluster plan's copies
+        own.insert(own.end(), plan.hmCopyOwner.begin(), plan.hmCopyOwner.end());
+        oth.insert(oth.end(), plan.hmCopyOther.begin(), plan.hmCopyOther.end());
+        up(dAttOwner, own);
+        up(dAttOther, oth);
         up(dHmClPtr, plan.hmClPtr);
         up(dHmTgt, plan.hmTgt);
         up(dHmPtr, plan.hmPtr);
@@ -391,7 +394,7 @@ void Operator::cache(int id) {
 // every point (the mode-0 diagonal).  Built once per setCoeff on a block handle.
 void Operator::buildAttCache() {
     const Params* P = dParams.as<Params>();
-    const int64_t npairs = (int64_t)plan.attOwner.size();  // stored blocks
+    const int64_t npairs = (int64_t)(plan.attOwner.size() + plan.hmCopyOwner.size());  // stored blocks + copies
     dAttM2L.alloc((size_t)npairs * 256 * sizeof(double));
     dAttNear.alloc((size_t)plan.nearKTotal * sizeof(double));
     dSigDiag.alloc((size_t)geo.N * sizeof(double));

@@ -274,7 +274,9 @@ k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64
 #pragma unroll
             for (int i = 0; i < K; ++i) c[j][i] = 0.0;
         const int64_t p0 = ptr[c0 + ti], pd = p0 + ndir[c0 + ti], p1 = ptr[c0 + ti + 1];
-            // directed entries: PG blocks in flight, forward product only
+            // directed entries: PG blocks in flight, forward product only; every block
+            // is read in its stored orientation (the plan gives a transposed read a
+            // directed copy, Plan::hmCopyOwner): two 16-B loads per lane
             for (int64_t cb = p0; cb < pd; cb += kWave) {
                 const int cnt = (int)min<int64_t>(kWave, pd - cb);
                 const int mySrc = lane < cnt ? src[cb + lane] : 0;
@@ -286,11 +288,13 @@ k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64
     #pragma unroll
                     for (int g = 0; g < PG; ++g) {
                         const int b = __builtin_amdgcn_readlane(myBlk, min(j0 + g, cnt - 1));
-                        const bool tr = b < 0;
-                        const double* p = E + (size_t)(tr ? ~b : b) * 256 + (tr ? 64 * q + s : 16 * s + 4 * q);
-                        const int st = tr ? 16 : 1;
-    #pragma unroll
-                        for (int j = 0; j < 4; ++j) e4[g][j] = j0 + g < cnt ? p[j * st] : 0.0;
+                        const dbl2* p = reinterpret_cast<const dbl2*>(E + (size_t)b * 256 + 16 * s + 4 * q);
+                        const dbl2 k0 = p[0], k1 = p[1];
+                        const bool ok = j0 + g < cnt;  // a skipped slot re-reads a valid block
+                        e4[g][0] = ok ? k0.x : 0.0;
+                        e4[g][1] = ok ? k0.y : 0.0;
+                        e4[g][2] = ok ? k1.x : 0.0;
+                        e4[g][3] = ok ? k1.y : 0.0;
                     }
     #pragma unroll
                     for (int g = 0; g < PG; ++g) {  // a skipped block's source is a valid clamp; its E is zero

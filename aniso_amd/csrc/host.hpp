@@ -119,6 +119,10 @@ struct Plan {
     int hmMaxCl = 0;
     int hmDepth = 0;  // cluster depth chosen (ancestor levels up)
     int64_t hmDual = 0;
+    // cross-cluster pairs read by the non-storing end: a directed copy of the stored
+    // block (E of the reversed pair), appended after the stored blocks in the cache,
+    // so that k_m2l_hc reads every block in the stored orientation (16-B lane loads)
+    std::vector<int> hmCopyOwner, hmCopyOther;
     // tiered up / down passes: tier k has root level
     // tierRootLevel[k] and bottom level tierBottomLevel[k] (k = 0 is the deepest).
     std::vector<int> tierRootLevel, tierBottomLevel;

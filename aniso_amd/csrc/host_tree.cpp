@@ -670,6 +670,8 @@ void Plan::buildClusters(const Tree& t) {
     hmSlot.clear();
     hmMaxCl = 0;
     hmDual = 0;
+    hmCopyOwner.clear();
+    hmCopyOther.clear();
     const int nt = (int)m2lTgt.size();
     if (nt == 0) return;
     // cluster key: (level, ancestor kClusterDepth levels up); targets keep id order
@@ -734,7 +736,13 @@ void Plan::buildClusters(const Tree& t) {
             }
             if (same && b < n) continue;  // applied by b's wave (dual)
             hmSrc.push_back(b);
-            hmBlk.push_back(attBlk[e]);
+            if (attBlk[e] < 0) {  // a transposed read: read a directed copy of the block instead
+                hmBlk.push_back((int)(attOwner.size() + hmCopyOwner.size()));
+                hmCopyOwner.push_back(n);
+                hmCopyOther.push_back(b);
+            } else {
+                hmBlk.push_back(attBlk[e]);
+            }
             hmSlot.push_back(-1);
         }
         hmNDir.push_back((int)(hmSrc.size() - hmPtr.back()));
