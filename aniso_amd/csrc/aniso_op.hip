@@ -297,6 +297,7 @@ void Operator::uploadPlan() {
     up(dNsPtr, plan.nsPtr);
     up(dNsPts, plan.nsPts);
     up(dNearLoc, plan.nearLoc);
+    up(dNearCorrRow, plan.nearCorrRow);
     up(dXRootSlot, plan.xRootSlot);
     up(dXSendSlot, plan.xSendSlot);
     up(dUpTaskPtr, plan.upTaskPtr);
@@ -696,13 +697,18 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     auto nearStage = [&] {
         if (fork) HIP_CHECK(hipStreamWaitEvent(side, evFork, 0));
         const int en = tm ? mark(sn) : -1;
+        bool corrFused = false;
         if (harmonic) {
-            launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
+            // the corrections ride in the staged near kernel (d = 1, its table holds
+            // every stencil neighbour; Plan::nearCorrRow)
+            const NearCorr nc{dNearCorrRow.as<uint16_t>(), dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
+                              cf.Wc.as<double>(), cf.Wm.as<double>(), P};
+            corrFused = launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
                            dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(), dNearKOff.as<int64_t>(),
                            dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dSigDiag.as<double>(), hw,
                            dFT.as<double>(), operm, obase, ldo, mask, scale, out,
                            dNearLoc.as<uint16_t>(), dNsPtr.as<int64_t>(), dNsPts.as<int>(),
-                           plan.nsMax, sn);
+                           plan.nsMax, plan.nearCorrOk ? &nc : nullptr, sn);
         } else if (plan.nearPartTotal > 0) {
             // symmetric U storage (K = 1 handles): one launch per term; the transposed
             // products go to partials summed over the terms
@@ -722,8 +728,9 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         }
         const int e1 = tm ? mark(sn) : -1;
         span(4, en, e1);
-        launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
-                    dFT.as<double>(), cf.Wc.as<double>(), cf.Wm.as<double>(), P, mask, scale, treeOut, ldo, out, sn);
+        if (!corrFused)
+            launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
+                        dFT.as<double>(), cf.Wc.as<double>(), cf.Wm.as<double>(), P, mask, scale, treeOut, ldo, out, sn);
         const int e2 = tm ? mark(sn) : -1;
         span(6, e1, e2);
         if (fork) HIP_CHECK(hipEventRecord(evJoin, side));

@@ -30,6 +30,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "corr_point.hpp"
 #include "device_common.hpp"
 
 namespace aniso {
@@ -520,7 +521,8 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
 // of 16 x 9 per-column gathers); the table rows (x, y, charges) are loaded once,
 // coalesced, and every column then reads its source from LDS by its 16-bit row
 // (nearLoc).  Only the E stream stays in HBM.  Same lane layout as k_near_hm<G=16>.
-template <int K, int U, int NR>
+
+template <int K, int U, int NR, bool FUSE>
 __global__ void __launch_bounds__(256) k_near_hs(int nl, const int4* __restrict__ leafInfo,
                                                  const int64_t* __restrict__ nearPtsPtr,
                                                  const uint16_t* __restrict__ nearLoc, const int64_t* __restrict__ nsPtr,
@@ -529,7 +531,7 @@ __global__ void __launch_bounds__(256) k_near_hs(int nl, const int4* __restrict_
                                                  const double* __restrict__ pyT, const double* __restrict__ sigDiag,
                                                  HarmWeights hw, const double* __restrict__ fT,
                                                  const int* __restrict__ operm, int64_t obase, int64_t ldo, int flags,
-                                                 double scale, double* __restrict__ out) {
+                                                 double scale, double* __restrict__ out, NearCorr nc) {
     constexpr int KS = kStride<K>;
     constexpr int RW = KS + 2;  // table row: x, y, the charges
     extern __shared__ double tab[];
@@ -615,19 +617,35 @@ __global__ void __launch_bounds__(256) k_near_hs(int nl, const int4* __restrict_
             v += dpp_f64<0x128>(v);  // row_ror:8
             a[j][i] = v;
         }
-    if (rowOk) {
+    if (rowOk) {  // lane (rq, cph) finishes row 4 rq + cph: one pass with every lane active
+        const int t = 4 * rq + cph;
+        double av[K];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int t = 4 * rq + j;
-            if (cph != j || t >= nT) continue;
+        for (int i = 0; i < K; ++i) av[i] = cph == 0 ? a[0][i] : cph == 1 ? a[1][i] : cph == 2 ? a[2][i] : a[3][i];
+        if (t < nT) {
             const int64_t k = tb + t;
             double f[K];
             load_charges<K>(fT + (size_t)k * KS, f);
             const double sd = nearOn ? sigDiag[k] : 0.0;
             const int64_t oi = out_index(operm, obase, k);
+            double cr[K];  // FUSE: k_corr's contribution (d = 1), its neighbour charges from the table
+            if constexpr (FUSE) {
+                const uint16_t* rw = nc.rows + ((size_t)li * 16 + t) * 9;
+                corr_point<1, K>(nc.perm[k], nc.P, nc.iperm, nc.cT, nc.Wc, nc.Wm, flags,
+                                 [&](int q9, int, int, double (&fc)[K]) {
+                                     const double* row = tab + (size_t)rw[q9] * RW + 2;
+#pragma unroll
+                                     for (int b = 0; b < K; ++b) fc[b] = row[b];
+                                 },
+                                 cr);
+            } else {
+#pragma unroll
+                for (int i = 0; i < K; ++i) cr[i] = 0.0;
+            }
 #pragma unroll
             for (int i = 0; i < K; ++i)
-                out[(size_t)i * ldo + oi] = hw.om[i] * scale * __builtin_fma(hw.dw[i] * sd, f[i], a[j][i]);
+                out[(size_t)i * ldo + oi] =
+                    __builtin_fma(hw.om[i] * scale, __builtin_fma(hw.dw[i] * sd, f[i], av[i]), cr[i] * scale);
         }
     }
 }
@@ -683,22 +701,31 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, 
 // near field: 16 lanes per leaf for leaves <= 16 points (4 leaves per wave), a wave
 // per leaf otherwise; 4 source columns in flight per lane (2 and 8, XCD-contiguous
 // leaves and leaf clusters measured slower, r01h); 1/r to full fp64 (two Newton steps)
-void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
+bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
                     const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
                     const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
                     int64_t ldo, int flags, double scale, double* out, const uint16_t* nearLoc, const int64_t* nsPtr,
-                    const int* nsPts, int nsMax, hipStream_t s) {
-    if (nl <= 0) return;
+                    const int* nsPts, int nsMax, const NearCorr* corr, hipStream_t s) {
+    if (nl <= 0) return false;
     const size_t tabBytes = (size_t)nsMax * (kStride<8> + 2) * sizeof(double);
     if (maxLeaf <= 16 && nsMax > 0 && nearLoc && tabBytes <= 64 * 1024) {  // sources staged in LDS (k_near_hs)
         const unsigned ng = (unsigned)((nl + 15) / 16);
+        // the corrections ride along when the table is loaded (near field on)
+        const bool fuse = corr && corr->rows && (flags & kStageNear);
+        const NearCorr nc = fuse ? *corr : NearCorr{};
         ANISO_HM_DISPATCH_K(K, ({
             const size_t shm = (size_t)nsMax * (kStride<KK> + 2) * sizeof(double);
-            k_near_hs<KK, 4, 2><<<ng, 256, shm, s>>>(nl, leafInfo, nearPtsPtr, nearLoc, nsPtr, nsPts, nearKOff, E,
-                                                     pxT, pyT, sigDiag, hw, fT, operm, obase, ldo, flags, scale, out);
+            if (fuse)
+                k_near_hs<KK, 4, 2, true><<<ng, 256, shm, s>>>(nl, leafInfo, nearPtsPtr, nearLoc, nsPtr, nsPts, nearKOff,
+                                                               E, pxT, pyT, sigDiag, hw, fT, operm, obase, ldo, flags,
+                                                               scale, out, nc);
+            else
+                k_near_hs<KK, 4, 2, false><<<ng, 256, shm, s>>>(nl, leafInfo, nearPtsPtr, nearLoc, nsPtr, nsPts,
+                                                                nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm, obase,
+                                                                ldo, flags, scale, out, nc);
         }));
         HIP_LAUNCH_CHECK();
-        return;
+        return fuse;
     }
 #define ANISO_NEAR_HM(G)                                                                                      \
     ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, G, 4, 2><<<blocks_for((int64_t)nl * G, 256), 256, 0, s>>>(           \
@@ -711,6 +738,7 @@ void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
     }
 #undef ANISO_NEAR_HM
     HIP_LAUNCH_CHECK();
+    return false;
 }
 
 }  // namespace aniso

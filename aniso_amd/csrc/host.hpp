@@ -96,6 +96,10 @@ struct Plan {
     std::vector<int> nsPts;
     std::vector<uint16_t> nearLoc;
     int nsMax = 0;  // largest table (points)
+    // d = 1: per (leaf, target row) the table rows of the 3x3 stencil's 9 points
+    // (0xFFFF outside the grid), so k_near_hs applies the corrections from its table
+    std::vector<uint16_t> nearCorrRow;
+    bool nearCorrOk = false;
     int64_t nearKTotal = 0;
     std::vector<int> m2lTgt;                   // active target nodes with M2L work
     std::vector<int64_t> m2lPtr;               // CSR over m2lTgt -> source nodes

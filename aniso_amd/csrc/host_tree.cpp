@@ -764,6 +764,36 @@ void Plan::buildClusters(const Tree& t) {
 // from their owners (the rank holding the root's first point).
 void Plan::buildExchange(const Tree& t, int sz, int d2) {
     const int64_t N = t.count[0];
+    // the fused corrections of the staged near field (d = 1: a square is one point)
+    nearCorrRow.clear();
+    nearCorrOk = false;
+    if (d2 == 1 && sz > 0 && nsMax > 0 && !leaves.empty()) {
+        std::vector<int> ip(N), rowTmp(N, -1);
+        for (int64_t k = 0; k < N; ++k) ip[t.perm[k]] = (int)k;
+        nearCorrRow.assign(leaves.size() * 16 * 9, 0xFFFF);
+        bool ok = true;
+        for (size_t g0 = 0; g0 < leaves.size() && ok; g0 += 16) {
+            const int64_t r0 = nsPtr[g0 / 16], r1 = nsPtr[g0 / 16 + 1];
+            for (int64_t r = r0; r < r1; ++r) rowTmp[nsPts[r]] = (int)(r - r0);
+            for (size_t l = g0; l < std::min(leaves.size(), g0 + 16) && ok; ++l)
+                for (int64_t r = 0; r < t.count[leaves[l]] && ok; ++r) {
+                    const int tt = t.perm[t.begin[leaves[l]] + r], i = tt / sz, j = tt % sz;
+                    for (int q9 = 0; q9 < 9; ++q9) {
+                        const int di = q9 / 3 - 1, dj = q9 % 3 - 1;
+                        if (i + di < 0 || i + di >= sz || j + dj < 0 || j + dj >= sz) continue;
+                        const int row = rowTmp[ip[tt + di * sz + dj]];
+                        if (row < 0) {
+                            ok = false;
+                            break;
+                        }
+                        nearCorrRow[(l * 16 + r) * 9 + q9] = (uint16_t)row;
+                    }
+                }
+            for (int64_t r = r0; r < r1; ++r) rowTmp[nsPts[r]] = -1;
+        }
+        nearCorrOk = ok;
+        if (!ok) nearCorrRow.clear();
+    }
     xT0Tasks.clear();
     xRootSend.clear();
     xRootRecv.clear();

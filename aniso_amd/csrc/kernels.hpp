@@ -151,11 +151,22 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, 
                    const int* src, const int* blk, const int* slot, const double* E, const double* ncx, const double* ncy,
                    const double* nrx, const double* nry, const Params* P, const HarmWeights& hw, const double* mult,
                    double* local, hipStream_t s);
-void launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
+// the fused corrections of the staged near field (d = 1; harmonic.hip k_near_hs)
+struct NearCorr {  // the fused corrections of k_near_hs (d = 1), or ignored when rows == nullptr
+    const uint16_t* rows;
+    const int* perm;
+    const int* iperm;
+    const double* cT;
+    const double* Wc;
+    const double* Wm;
+    const Params* P;
+};
+// returns true when the corrections were fused (the caller skips launch_corr)
+bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
                     const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
                     const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
                     int64_t ldo, int flags, double scale, double* out, const uint16_t* nearLoc, const int64_t* nsPtr,
-                    const int* nsPts, int nsMax, hipStream_t s);
+                    const int* nsPts, int nsMax, const NearCorr* corr, hipStream_t s);
 void launch_sub_slice(int64_t n, int nrhs, const double* x, int64_t ldx, const double* a, int64_t lda, double* y,
                       int64_t ldy, hipStream_t s);
 
