@@ -85,6 +85,24 @@ __device__ __forceinline__ double xor16_f64(double v, bool r4) {
     }
 }
 
+// Reduce-scatter steps across lane ^ 16 / lane ^ 32 (gfx950 v_permlane16/32_swap with
+// x in VDST and y in SRC0): one lane of each pair ends with x + x', the other with
+// y + y' -- which one is measured by the caller (probe with x = 1, y = 0), not assumed.
+__device__ __forceinline__ double swap_add16_f64(double x, double y) {
+    const unsigned long long bx = __builtin_bit_cast(unsigned long long, x), by = __builtin_bit_cast(unsigned long long, y);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)bx, (unsigned)by, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(bx >> 32), (unsigned)(by >> 32), false, false);
+    return __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]) +
+           __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
+}
+__device__ __forceinline__ double swap_add32_f64(double x, double y) {
+    const unsigned long long bx = __builtin_bit_cast(unsigned long long, x), by = __builtin_bit_cast(unsigned long long, y);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)bx, (unsigned)by, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(bx >> 32), (unsigned)(by >> 32), false, false);
+    return __builtin_bit_cast(double, ((unsigned long long)hi[0] << 32) | lo[0]) +
+           __builtin_bit_cast(double, ((unsigned long long)hi[1] << 32) | lo[1]);
+}
+
 // v(lane) + v(lane ^ 16) and v(lane) + v(lane ^ 32) through gfx950's
 // v_permlane16/32_swap (row exchange on the VALU; the sum of both swap outputs is
 // the pair sum whichever row each output holds).

@@ -355,26 +355,60 @@ k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64
                     }
                 }
             }
-        {  // sum over the 16 columns (lane bits 2..5) on the VALU: DPP in-row, permlane swaps across rows
+        if constexpr (K == 5) {
+            // sum over the 16 columns (lane bits 2..5) as a reduce-scatter of the lane's
+            // 20 row sums (rows 4q + j, entries i; v = 5 j + i): 20 -> 10 (lane ^ 32),
+            // 10 -> 5 (lane ^ 16), 5 -> 3 (lane ^ 8), 3 -> 2 (lane ^ 4); each of the 16
+            // column lanes then adds its <= 2 finished sums -- ~90 VALU ops, not ~360
             const bool r4 = xor16_r4(lane);
+            const int k32 = swap_add32_f64(1.0, 0.0) > 1.5 ? 0 : 10;  // this lane keeps the first / second half
+            const int k16 = swap_add16_f64(1.0, 0.0) > 1.5 ? 0 : 5;
+            double v10[10];
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int k = 0; k < 10; ++k) v10[k] = swap_add32_f64(c[k / 5][k % 5], c[(k + 10) / 5][(k + 10) % 5]);
+            double v5[5];
 #pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    double v = c[j][i];
-                    v += xor16_f64<4>(v, r4);
-                    v += xor16_f64<8>(v, r4);
-                    v = xsum16_f64(v);
-                    c[j][i] = xsum32_f64(v);
+            for (int k = 0; k < 5; ++k) v5[k] = swap_add16_f64(v10[k], v10[k + 5]);
+            const bool h1 = (lane >> 3) & 1, h0 = (lane >> 2) & 1;
+            double v3[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {  // lane ^ 8: h1 = 0 keeps k, h1 = 1 keeps k + 3
+                const double x = v5[k], y = k + 3 < 5 ? v5[k + 3] : 0.0;
+                v3[k] = (h1 ? y : x) + dpp_f64<0x128>(h1 ? x : y);
+            }
+            double* d = acc + (size_t)ti * kRank * K;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {  // lane ^ 4: h0 = 0 keeps u, h0 = 1 keeps u + 2
+                const double x = v3[u], y = u + 2 < 3 ? v3[u + 2] : 0.0;
+                const double sum = (h0 ? y : x) + xor16_f64<4>(h0 ? x : y, r4);
+                const int w = u + 2 * h0, v2 = w + 3 * h1;
+                if (w <= 2 && v2 <= 4) {
+                    const int v0 = v2 + k16 + k32, j = v0 / 5, i = v0 - 5 * j;
+                    atomicAdd(d + (4 * q + j) * K + i, sum);
                 }
-        }
-        const int jr = s & 3, srcLane = 4 * s + (s >> 2);
-        double* d = acc + ((size_t)ti * kRank + s) * K;
+            }
+        } else {
+            {  // sum over the 16 columns (lane bits 2..5) on the VALU: DPP in-row, permlane swaps across rows
+                const bool r4 = xor16_r4(lane);
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const double sel = jr == 0 ? c[0][i] : jr == 1 ? c[1][i] : jr == 2 ? c[2][i] : c[3][i];
-            const double v = __shfl(sel, srcLane);
-            if ((i & 3) == q) atomicAdd(d + i, v);
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        double v = c[j][i];
+                        v += xor16_f64<4>(v, r4);
+                        v += xor16_f64<8>(v, r4);
+                        v = xsum16_f64(v);
+                        c[j][i] = xsum32_f64(v);
+                    }
+            }
+            const int jr = s & 3, srcLane = 4 * s + (s >> 2);
+            double* d = acc + ((size_t)ti * kRank + s) * K;
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const double sel = jr == 0 ? c[0][i] : jr == 1 ? c[1][i] : jr == 2 ? c[2][i] : c[3][i];
+                const double v = __shfl(sel, srcLane);
+                if ((i & 3) == q) atomicAdd(d + i, v);
+            }
         }
     }
     __syncthreads();
