@@ -922,6 +922,12 @@ void Operator::setTiming(bool on) {
         evUsed = 0;
         spans.clear();
         applies = 0;
+        ensureDevice();
+        while (evPool.size() < 512) {  // events for ~50 applies created here, not inside a timed region
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreate(&e));
+            evPool.push_back(e);
+        }
     }
 }
 
