@@ -704,6 +704,23 @@ void Plan::buildClusters(const Tree& t) {
     std::vector<int> order(nt);
     for (int w = 0; w < nt; ++w) order[w] = w;
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
+    {
+        // launch order: heaviest cluster first (its att pairs), so the workgroups
+        // dispatched last are short ones and the tail of the launch stays full
+        std::vector<std::array<int64_t, 3>> seg;  // -weight, begin, end in `order`
+        for (int k = 0; k < nt;) {
+            int e = k;
+            int64_t wgt = 0;
+            for (; e < nt && key[order[e]] == key[order[k]]; ++e) wgt += attPtr[order[e] + 1] - attPtr[order[e]];
+            seg.push_back({-wgt, k, e});
+            k = e;
+        }
+        std::stable_sort(seg.begin(), seg.end(), [](const auto& a, const auto& b) { return a[0] < b[0]; });
+        std::vector<int> o2;
+        o2.reserve(nt);
+        for (const auto& g : seg) o2.insert(o2.end(), order.begin() + g[1], order.begin() + g[2]);
+        order.swap(o2);
+    }
     std::vector<int> clOf(t.nn, -1), slotOf(t.nn, -1);
     int nc = 0;
     for (int k = 0; k < nt; ++k) {
