@@ -556,6 +556,12 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
 // coalesced, and every column then reads its source from LDS by its 16-bit row
 // (nearLoc).  Only the E stream stays in HBM.  Same lane layout as k_near_hm<G=16>.
 
+// Table row stride: x, y, the charges, rounded up to an odd number of doubles, so the
+// up to 16 different rows one wave reads at a time fall on different LDS banks (an
+// even stride of 8 doubles put every 4th row on the same banks).
+template <int K>
+constexpr int kTabRow = (kStride<K> + 2) | 1;
+
 template <int K, int U, int NR, bool FUSE>
 __global__ void __launch_bounds__(256) k_near_hs(int nl, const int4* __restrict__ leafInfo,
                                                  const int64_t* __restrict__ nearPtsPtr,
@@ -567,7 +573,7 @@ __global__ void __launch_bounds__(256) k_near_hs(int nl, const int4* __restrict_
                                                  const int* __restrict__ operm, int64_t obase, int64_t ldo, int flags,
                                                  double scale, double* __restrict__ out, NearCorr nc) {
     constexpr int KS = kStride<K>;
-    constexpr int RW = KS + 2;  // table row: x, y, the charges
+    constexpr int RW = kTabRow<K>;  // table row: x, y, the charges (padded)
     extern __shared__ double tab[];
     const bool nearOn = (flags & kStageNear) != 0;
     const int g = (int)blockIdx.x;
@@ -741,14 +747,14 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
                     int64_t ldo, int flags, double scale, double* out, const uint16_t* nearLoc, const int64_t* nsPtr,
                     const int* nsPts, int nsMax, const NearCorr* corr, hipStream_t s) {
     if (nl <= 0) return false;
-    const size_t tabBytes = (size_t)nsMax * (kStride<8> + 2) * sizeof(double);
+    const size_t tabBytes = (size_t)nsMax * kTabRow<8> * sizeof(double);
     if (maxLeaf <= 16 && nsMax > 0 && nearLoc && tabBytes <= 64 * 1024) {  // sources staged in LDS (k_near_hs)
         const unsigned ng = (unsigned)((nl + 15) / 16);
         // the corrections ride along when the table is loaded (near field on)
         const bool fuse = corr && corr->rows && (flags & kStageNear);
         const NearCorr nc = fuse ? *corr : NearCorr{};
         ANISO_HM_DISPATCH_K(K, ({
-            const size_t shm = (size_t)nsMax * (kStride<KK> + 2) * sizeof(double);
+            const size_t shm = (size_t)nsMax * kTabRow<KK> * sizeof(double);
             if (fuse)
                 k_near_hs<KK, 4, 2, true><<<ng, 256, shm, s>>>(nl, leafInfo, nearPtsPtr, nearLoc, nsPtr, nsPts, nearKOff,
                                                                E, pxT, pyT, sigDiag, hw, fT, operm, obase, ldo, flags,
