@@ -74,6 +74,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     plan.maxCanon = ks == 1 ? kMaxCanon : kMaxCanonBlock;
     plan.build(tree, np, 0, 1);
     plan.buildExchange(tree, geo.sz, geo.d2);
+    plan.buildTopWait(tree);
     // block handles apply aniso.m's operator through the mode-shared E caches
     // (DESIGN.md §3.9); ANISO_HARMONIC=0 keeps the per-mode operator stream
     useAtt = ks > 1 && !plan.nearSymmetric;
@@ -109,6 +110,7 @@ void Operator::getNodes(double* xy) const {
 void Operator::setShard(int rank, int nranks) {
     plan.build(tree, np, rank, nranks);
     plan.buildExchange(tree, geo.sz, geo.d2);
+    plan.buildTopWait(tree);
     pend = Pending();
     for (auto& m : modes) {
         m.Knear.alloc(0);
@@ -271,6 +273,8 @@ void Operator::uploadPlan() {
         up(dHmBlk, plan.hmBlk);
         up(dHmSlot, plan.hmSlot);
         up(dHmNDir, plan.hmNDir);
+        up(dHmClWait, plan.hmClWait);
+        dTopCnt.alloc((kMaxTopTiers + 1) * sizeof(unsigned));
         attReady = false;
     }
     up(dM2LCanonBase, plan.m2lCanonBase);
@@ -681,7 +685,10 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     // bottom tier it starved the latency-bound upper tiers the M2L waits on (up pass
     // 0.25 -> 0.14 ms, 644 -> 660 block matvec/s); a sharded apply starts it in
     // phase 1, beside the root exchange (8 shards: 0.317 vs 0.327 ms per rank)
-    const int forkTier = phase == 0 ? std::max(ntier - 1, 0) : plan.upLastLeafTier;
+    // the upper tiers ride in the M2L launch (k_top_m2l_hc) when every leaf is in the
+    // bottom tier: the near field then forks after it
+    const bool topFused = harmonic && (mask & kStageFar) && topFusedOn();
+    const int forkTier = phase == 0 && !topFused ? std::max(ntier - 1, 0) : plan.upLastLeafTier;
     // one up tier; a sharded apply's bottom tier runs this rank's tasks only (list)
     // and stores its tier-0 roots into send, its next tier reads the gathered ones
     auto upTier = [&](int k, const int* list, int ntask, const double* recv, double* send) {
@@ -689,7 +696,8 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                        dUpNode.as<int>(), dUpCode.as<int4>(), dUpGeom.as<double4>(), dUpLeaf.as<int2>(),
                        dPxT.as<double>(), dPyT.as<double>(), x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT,
                        dWT.as<double>(), dFT.as<double>(), dCT.as<double>(), P, dMult.as<double>(),
-                       recv ? dXRootSlot.as<int>() : nullptr, recv, send ? dXSendSlot.as<int>() : nullptr, send, s);
+                       recv ? dXRootSlot.as<int>() : nullptr, recv, send ? dXSendSlot.as<int>() : nullptr, send, s,
+                       topFused && k == 0 ? dTopCnt.as<unsigned>() : nullptr);
         if (fork && k == forkTier) HIP_CHECK(hipEventRecord(evFork, s));
     };
     auto tierTasks = [&](int k) { return plan.upTierTask[k + 1] - plan.upTierTask[k]; };
@@ -756,7 +764,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         }
         if (phase == 1 && ntier >= 1)
             upTier(0, dXT0Tasks.as<int>(), (int)plan.xT0Tasks.size(), nullptr, rootsSend);
-        for (int k = 0; k < ntier && phase == 0; ++k) upTier(k, nullptr, tierTasks(k), nullptr, nullptr);
+        for (int k = 0; k < (topFused ? 1 : ntier) && phase == 0; ++k) upTier(k, nullptr, tierTasks(k), nullptr, nullptr);
         if (phase == 1) {
             const int ep = tm ? mark(s) : -1;
             span(1, e0, ep);
@@ -777,7 +785,8 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         pend.active = false;
         const int ex = tm ? mark(s) : -1;
         span(0, pend.ePack, ex);  // the caller's root exchange
-        if (ntier >= 2) {  // the first upper tier reads the gathered roots (and stores them for the M2L)
+        if (topFused) {  // the upper tiers run inside the M2L launch below
+        } else if (ntier >= 2) {  // the first upper tier reads the gathered roots (and stores them for the M2L)
             upTier(1, nullptr, tierTasks(1), rootsRecv, nullptr);
             for (int k = 2; k < ntier; ++k) upTier(k, nullptr, tierTasks(k), nullptr, nullptr);
         } else {
@@ -794,7 +803,27 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         if (tm && sn == s) ep = mark(s);  // serial (ANISO_OVERLAP=0): the M2L span starts after the near field
     }
     if (mask & kStageFar) {
-        if (clustered) {
+        if (topFused) {
+            const UpArgs ua{plan.upMaxTask, dUpDesc.as<int4>(), dUpGrpFix.as<int>(), dUpNode.as<int>(),
+                            dUpCode.as<int4>(), dUpGeom.as<double4>(), dUpLeaf.as<int2>(), dPxT.as<double>(),
+                            dPyT.as<double>(), x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(),
+                            dFT.as<double>(), dCT.as<double>(), P, dMult.as<double>(),
+                            phase == 2 ? dXRootSlot.as<int>() : nullptr};
+            TopArgs ta{};
+            const int u1 = plan.upTierTask[1];
+            ta.nUp = plan.upTierTask[ntier] - u1;
+            ta.ntier = ntier;
+            for (int k = 1; k <= ntier; ++k) ta.blk0[k] = plan.upTierTask[k] - u1;
+            for (int k = 1; k < ntier; ++k) ta.task0[k] = plan.upTierTask[k];
+            ta.clWait = dHmClWait.as<int>();
+            ta.cnt = dTopCnt.as<unsigned>();
+            ta.recv1 = phase == 2 ? rootsRecv : nullptr;
+            const HcArgs ha{dHmClPtr.as<int>(), dHmTgt.as<int>(), dHmPtr.as<int64_t>(), dHmNDir.as<int>(),
+                            dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(), dAttM2L.as<double>(),
+                            dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), P, hw,
+                            dMult.as<double>(), dLocal.as<double>()};
+            launch_top_m2l_hc(K, ncl, plan.hmMaxCl, ua, ta, ha, s);
+        } else if (clustered) {
             m2lClusters(0, ncl, s);
         } else if (harmonic) {
             launch_m2l_hm(K, (int)plan.m2lTgt.size(), dM2LTgt.as<int>(), dAttPtr.as<int64_t>(), dAttSrc.as<int>(),

@@ -118,6 +118,12 @@ public:
     hipStream_t stream() const { return own; }
     bool harmonicReady() const { return useAtt && attReady; }
     bool clustersOn() const { return useClusters; }
+    // the block apply's upper up tiers ride in the clustered M2L launch (k_top_m2l_hc)
+    bool topFusedOn() const {
+        const int ntier = (int)plan.upTierTask.size() - 1;
+        return useClusters && top_fused_enabled() && ntier >= 2 && ntier <= kMaxTopTiers &&
+               plan.upLastLeafTier == 0 && plan.hmClWait.size() + 1 == plan.hmClPtr.size();
+    }
     // bitwise-reproducible applies: the harmonic M2L as one wave per target (a fixed
     // summation order) instead of the clustered kernel, whose LDS adds of the partner
     // products land in run-dependent order (repeat applies agree to ~1e-15)
@@ -164,6 +170,7 @@ private:
     bool useAtt = false, attReady = false;
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
+    DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
     bool useClusters = true;
     std::map<std::string, DevBuf> modeTabs;
     const CorrFold& corrTable(int K, int nterm, const int* ids, const double* mixes);

@@ -487,7 +487,7 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[15] = cl ? op.plan.hmDual : 0;
         s[16] = cl ? (int64_t)op.plan.hmSrc.size() : (int64_t)op.plan.attSrc.size();
         s[17] = op.f32Bytes();  // config 5's fp32 operator caches (0 before its first apply)
-        s[18] = 0;
+        s[18] = cl && op.topFusedOn() ? 1 : 0;
     });
 }
 

@@ -32,6 +32,7 @@
 
 #include "corr_point.hpp"
 #include "device_common.hpp"
+#include "up_task.hpp"
 
 namespace aniso {
 
@@ -234,17 +235,26 @@ __device__ __forceinline__ void hm_entry2(double e, double dx, double dy2, const
 // (ds_add_f64).  The block stream drops by the in-cluster share (0.65 of the V
 // pairs at 64 targets per cluster, tools/vfrac.py); the summation order of the LDS
 // adds is not fixed (results repeat to rounding, not bitwise).
-template <int K, int NR, int WPE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
-k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64_t* __restrict__ ptr,
-         const int* __restrict__ ndir, const int* __restrict__ src, const int* __restrict__ blk,
-         const int* __restrict__ slot, const double* __restrict__ E, const double* __restrict__ ncx, const double* __restrict__ ncy,
-         const double* __restrict__ nrx, const double* __restrict__ nry, const Params* __restrict__ P,
-         HarmWeights hw, const double* __restrict__ mult, double* __restrict__ local) {
+template <int K, int NR>
+__device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, double* sm) {
+    const int* __restrict__ clPtr = a.clPtr;
+    const int* __restrict__ tgt = a.tgt;
+    const int64_t* __restrict__ ptr = a.ptr;
+    const int* __restrict__ ndir = a.ndir;
+    const int* __restrict__ src = a.src;
+    const int* __restrict__ blk = a.blk;
+    const int* __restrict__ slot = a.slot;
+    const double* __restrict__ E = a.E;
+    const double* __restrict__ ncx = a.ncx;
+    const double* __restrict__ ncy = a.ncy;
+    const double* __restrict__ nrx = a.nrx;
+    const double* __restrict__ nry = a.nry;
+    const Params* __restrict__ P = a.P;
+    const HarmWeights& hw = a.hw;
+    const double* __restrict__ mult = a.mult;
+    double* __restrict__ local = a.local;
     constexpr int RK = kRank * K;
     constexpr int PG = 2;
-    extern __shared__ double sm[];
-    const int cid = (int)blockIdx.x;
     const int c0 = clPtr[cid], nt = clPtr[cid + 1] - c0;
     const int nw = (int)(blockDim.x / kWave);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
@@ -416,6 +426,82 @@ k_m2l_hc(const int* __restrict__ clPtr, const int* __restrict__ tgt, const int64
         const int k = e / RK, r = e - k * RK;
         local[(size_t)tgt[c0 + k] * RK + r] = hw.om[r % K] * acc[e];
     }
+}
+
+template <int K, int NR, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_m2l_hc(HcArgs a) {
+    extern __shared__ double sm[];
+    m2l_hc_cluster<K, NR>((int)blockIdx.x, a, sm);
+}
+
+// ----------------------------------------------------------------- fused top of tree + M2L
+//
+// The upper up tiers are a few hundred small, latency-bound tasks; as launches of
+// their own they sit between the bottom tier and the M2L on every apply (and on every
+// rank of a sharded one, where they do not shrink with the rank count).  Here they
+// run as the first blocks of the M2L launch: the clusters that need none of their
+// multipoles (the finest levels: all but a few percent of the work) stream from the
+// start, and the rest wait for the tier they read (TopArgs.clWait, Plan::hmClWait).
+// Hand-off per tier: a counter of finished tasks, published after an agent-scope
+// release by each task and polled (relaxed, agent scope) by one lane of a waiting
+// block, which then acquires before its block reads (MI355X_MICROARCH.md, cross-
+// workgroup visibility).  Waiting blocks have higher ids than every block they wait
+// for and the up blocks (a few hundred) all fit on the chip at once, so the
+// producers are always resident; a bounded spin counts a time-out in cnt[0] rather
+// than hanging.
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__device__ __forceinline__ void top_wait(unsigned* cnt, int k, unsigned target) {
+    if (threadIdx.x == 0) {
+        gu32* c = (gu32*)(cnt + k);
+        for (unsigned spins = 0; __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins == (1u << 24)) {
+                __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+__device__ __forceinline__ void top_publish(unsigned* cnt, int k) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: the fence's own wait can be dropped
+        __hip_atomic_fetch_add((gu32*)(cnt + k), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <int K, int NR, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a) {
+    extern __shared__ double sm[];
+    const int b = (int)blockIdx.x;
+    if (b < t.nUp) {
+        int k = 1;
+        while (b >= t.blk0[k + 1]) ++k;
+        if (k >= 2) top_wait(t.cnt, k - 1, (unsigned)(t.blk0[k] - t.blk0[k - 1]));
+        up_task<K>(t.task0[k] + (b - t.blk0[k]), u.maxTask, u.desc, u.grpFix, u.node, u.code, u.geom, u.leafRange,
+                   u.pxT, u.pyT, u.xin, u.ldi, u.treeIn, u.perm, u.sigT, u.wT, u.fT, u.cT, u.P, u.mult, u.rootSlot,
+                   k == 1 ? t.recv1 : nullptr, nullptr, nullptr, sm);
+        top_publish(t.cnt, k);
+        return;
+    }
+    const int cid = b - t.nUp;
+    const int w = t.clWait[cid];
+    if (w > 0) {  // its own copy: behind the wait's fence the source boxes load through the vector path
+        top_wait(t.cnt, w, (unsigned)(t.blk0[w + 1] - t.blk0[w]));
+        m2l_hc_cluster<K, NR>(cid, a, sm);
+        return;
+    }
+    // no store or fence on the way here, so the compiler keeps the wave-uniform
+    // source-box reads (ncx[B] ...) on scalar loads as in k_m2l_hc
+    m2l_hc_cluster<K, NR>(cid, a, sm);
 }
 
 // ----------------------------------------------------------------- near field
@@ -733,7 +819,33 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, 
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
             if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
         }
-        f<<<ncl, 256, shm, s>>>(clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry, P, hw, mult, local);
+        f<<<ncl, 256, shm, s>>>(HcArgs{clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry, P, hw, mult, local});
+    }));
+    HIP_LAUNCH_CHECK();
+}
+
+bool top_fused_enabled() {
+#ifdef ANISO_NO_TOP_FUSED
+    return false;
+#else
+    return true;
+#endif
+}
+
+void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs& t, const HcArgs& a, hipStream_t s) {
+    if (maxCl > 64) throw std::invalid_argument("harmonic M2L cluster larger than 64 targets");
+    if (t.ntier < 2 || t.ntier > kMaxTopTiers || t.blk0[t.ntier] != t.nUp)
+        throw std::invalid_argument("fused top-of-tree launch: bad tier layout");
+    const size_t shm = std::max((size_t)(maxCl + 256 / kWave) * kRank * K * sizeof(double), up_tier_lds(u.maxTask, K));
+    const unsigned nb = (unsigned)(t.nUp + ncl);
+    ANISO_HM_DISPATCH_K(K, ({
+        auto f = k_top_m2l_hc<KK, 1, 3>;
+        if (shm > 65536) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(f),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+            if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
+        }
+        f<<<nb, 256, shm, s>>>(u, t, a);
     }));
     HIP_LAUNCH_CHECK();
 }

@@ -122,6 +122,7 @@ struct Plan {
     std::vector<int64_t> hmPtr;
     int hmMaxCl = 0;
     int hmDepth = 0;  // cluster depth chosen (ancestor levels up)
+    std::vector<int> hmClWait;  // per cluster: the upper up tier whose multipoles it reads (0: none)
     int64_t hmDual = 0;
     // cross-cluster pairs read by the non-storing end: a directed copy of the stored
     // block (E of the reversed pair), appended after the stored blocks in the cache,
@@ -182,6 +183,8 @@ struct Plan {
     void build(const Tree& t, int np, int rank, int nranks);
     // the exchange plan above; sz / d2: the square grid of the correction stencil
     void buildExchange(const Tree& t, int sz, int d2);
+    // hmClWait (after build and buildExchange)
+    void buildTopWait(const Tree& t);
 
   private:
     void buildUpTasks(const Tree& t);

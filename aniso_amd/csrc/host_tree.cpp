@@ -695,10 +695,17 @@ void Plan::buildClusters(const Tree& t) {
     if (const char* e = std::getenv("ANISO_HM_CLDEPTH"))  // tuning/experiments only (1..kClusterDepth)
         depth = std::max(1, std::min(kClusterDepth, std::atoi(e)));
     hmDepth = depth;
+    // targets above the bottom up tier (at or above it on a shard: its roots arrive
+    // by the all-gather) read multipoles the upper tiers produce; in the fused launch
+    // their clusters may wait for them, so they form small clusters (<= 16 targets)
+    // that go last
+    const int upperBelow = tierRootLevel.empty() ? 0 : tierRootLevel[0] + (nranks > 1 ? 1 : 0);
+    auto upper = [&](int w) { return t.level[m2lTgt[w]] < upperBelow; };
     std::vector<int64_t> key(nt);
     for (int w = 0; w < nt; ++w) {
         int a = m2lTgt[w];
-        for (int k = 0; k < depth && t.parent[a] != -1; ++k) a = t.parent[a];
+        const int dp = upper(w) ? std::min(depth, 2) : depth;
+        for (int k = 0; k < dp && t.parent[a] != -1; ++k) a = t.parent[a];
         key[w] = ((int64_t)t.level[m2lTgt[w]] << 32) | (uint32_t)a;
     }
     std::vector<int> order(nt);
@@ -706,19 +713,22 @@ void Plan::buildClusters(const Tree& t) {
     std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key[x] < key[y]; });
     {
         // launch order: heaviest cluster first (its att pairs), so the workgroups
-        // dispatched last are short ones and the tail of the launch stays full
-        std::vector<std::array<int64_t, 3>> seg;  // -weight, begin, end in `order`
+        // dispatched last are short ones and the tail of the launch stays full; the
+        // upper-level clusters after all others
+        std::vector<std::array<int64_t, 4>> seg;  // upper, -weight, begin, end in `order`
         for (int k = 0; k < nt;) {
             int e = k;
             int64_t wgt = 0;
             for (; e < nt && key[order[e]] == key[order[k]]; ++e) wgt += attPtr[order[e] + 1] - attPtr[order[e]];
-            seg.push_back({-wgt, k, e});
+            seg.push_back({upper(order[k]) ? 1 : 0, -wgt, k, e});
             k = e;
         }
-        std::stable_sort(seg.begin(), seg.end(), [](const auto& a, const auto& b) { return a[0] < b[0]; });
+        std::stable_sort(seg.begin(), seg.end(), [](const auto& a, const auto& b) {
+            return a[0] != b[0] ? a[0] < b[0] : a[1] < b[1];
+        });
         std::vector<int> o2;
         o2.reserve(nt);
-        for (const auto& g : seg) o2.insert(o2.end(), order.begin() + g[1], order.begin() + g[2]);
+        for (const auto& g : seg) o2.insert(o2.end(), order.begin() + g[2], order.begin() + g[3]);
         order.swap(o2);
     }
     std::vector<int> clOf(t.nn, -1), slotOf(t.nn, -1);
@@ -779,6 +789,30 @@ void Plan::buildClusters(const Tree& t) {
 // points -- lives in a few tier-0 subtrees around its range; it runs those tasks.
 // Everything at or above L0 comes from the tier-0 roots, which each rank receives
 // from their owners (the rank holding the root's first point).
+// Fused top-of-tree launch (harmonic.hip k_top_m2l_hc): the upper up tier whose
+// multipoles each cluster reads, its targets' own (the in-cluster dual products)
+// included.  Tier k >= 1 writes its tasks' nodes; a sharded apply's tier 1 also
+// stores the gathered tier-0 roots (up_task's recv copy), so those count as tier 1.
+void Plan::buildTopWait(const Tree& t) {
+    hmClWait.assign(hmClPtr.empty() ? 0 : hmClPtr.size() - 1, 0);
+    const int ntier = (int)upTierTask.size() - 1;
+    if (ntier < 2 || hmClWait.empty()) return;
+    std::vector<int> prod(t.nn, 0);
+    for (int k = 1; k < ntier; ++k)
+        for (int task = upTierTask[k]; task < upTierTask[k + 1]; ++task)
+            for (int i = upDesc[task][0]; i < upDesc[task][0] + upDesc[task][1]; ++i) prod[upNode[i]] = k;
+    if (nranks > 1)
+        for (int task = upTierTask[0]; task < upTierTask[1]; ++task) prod[upTaskRoot[task]] = 1;
+    for (size_t c = 0; c + 1 < hmClPtr.size(); ++c) {
+        int w = 0;
+        for (int k = hmClPtr[c]; k < hmClPtr[c + 1]; ++k) {
+            w = std::max(w, prod[hmTgt[k]]);
+            for (int64_t e = hmPtr[k]; e < hmPtr[k + 1]; ++e) w = std::max(w, prod[hmSrc[e]]);
+        }
+        hmClWait[c] = w;
+    }
+}
+
 void Plan::buildExchange(const Tree& t, int sz, int d2) {
     const int64_t N = t.count[0];
     // the fused corrections of the staged near field (d = 1: a square is one point)

@@ -85,7 +85,8 @@ void launch_up_tier(int K, int ntask, int taskBase, const int* taskList, int max
                     const int* grpFix, const int* node, const int4* code, const double4* geom, const int2* leafRange,
                     const double* pxT, const double* pyT, const double* xin, int64_t ldi, int treeIn, const int* perm,
                     const double* sigT, const double* wT, double* fT, double* cT, const Params* P, double* mult,
-                    const int* rootSlot, const double* recv, const int* sendSlot, double* send, hipStream_t s);
+                    const int* rootSlot, const double* recv, const int* sendSlot, double* send, hipStream_t s,
+                    unsigned* zeroCnt = nullptr);
 // config 5's fp32 operator (f32op.hip): node expansions as 64 lanes x float4
 // (void* below), vectors point-major N x 16 floats
 void launch32_p2m(int nleaf, const int* leaves, const int64_t* begin, const int64_t* count, const double* ncx,
@@ -147,6 +148,63 @@ void launch_corr(int K, int d, int64_t b, int64_t e, const int* perm, const int*
 void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* src, const int* blk, const double* E,
                    const double* ncx, const double* ncy, const double* nrx, const double* nry, const Params* P,
                    const HarmWeights& hw, const double* mult, double* local, hipStream_t s);
+// the clustered M2L's arguments (harmonic.hip k_m2l_hc, k_top_m2l_hc)
+struct HcArgs {
+    const int* clPtr;
+    const int* tgt;
+    const int64_t* ptr;
+    const int* ndir;
+    const int* src;
+    const int* blk;
+    const int* slot;
+    const double* E;
+    const double* ncx;
+    const double* ncy;
+    const double* nrx;
+    const double* nry;
+    const Params* P;
+    HarmWeights hw;
+    const double* mult;
+    double* local;
+};
+// The fused top-of-tree + clustered M2L launch (harmonic.hip k_top_m2l_hc, DESIGN.md
+// §3.10): blocks 0 .. nUp - 1 run the up tasks of tiers 1 .. ntier - 1 (tier k's
+// tasks wait until tier k - 1 has finished), the other blocks are the clusters, a
+// cluster whose sources include upper-tier multipoles waiting for that tier.
+constexpr int kMaxTopTiers = 8;
+struct UpArgs {  // one up task's inputs (up_task.hpp)
+    int maxTask;
+    const int4* desc;
+    const int* grpFix;
+    const int* node;
+    const int4* code;
+    const double4* geom;
+    const int2* leafRange;
+    const double* pxT;
+    const double* pyT;
+    const double* xin;
+    int64_t ldi;
+    int treeIn;
+    const int* perm;
+    const double* sigT;
+    const double* wT;
+    double* fT;
+    double* cT;
+    const Params* P;
+    double* mult;
+    const int* rootSlot;
+};
+struct TopArgs {
+    int nUp;                      // up-task blocks
+    int ntier;                    // tiers 1 .. ntier - 1 run in the launch
+    int blk0[kMaxTopTiers + 1];   // first block of tier k; blk0[ntier] = nUp
+    int task0[kMaxTopTiers];      // first task of tier k
+    const int* clWait;            // per cluster: the upper tier it waits for (0: none)
+    unsigned* cnt;                // finished tasks per tier; cnt[0] = spin time-outs (zeroed by tier 0)
+    const double* recv1;          // sharded phase 2: the gathered tier-0 roots tier 1 reads
+};
+bool top_fused_enabled();
+void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs& t, const HcArgs& a, hipStream_t s);
 void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, const int64_t* ptr, const int* ndir,
                    const int* src, const int* blk, const int* slot, const double* E, const double* ncx, const double* ncy,
                    const double* nrx, const double* nry, const Params* P, const HarmWeights& hw, const double* mult,

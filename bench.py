@@ -23,8 +23,9 @@ mid-apply, computes its targets into its slice of the next iterate, and one halo
 all-to-all refreshes the points its neighbours read (aniso_amd/dist.py).
 
 Also reported on the same JSON line:
-  roofline      HBM roofline of the dominant kernel (the clustered M2L k_m2l_hc, one
-                launch per matvec) and of the near-field sweep, timed with HIP events
+  roofline      HBM roofline of the dominant kernel (the clustered M2L with the upper up
+                tiers, k_top_m2l_hc, one launch per matvec) and of the near-field sweep,
+                timed with HIP events
                 on the streams they run on over the timed region;
   cpu_baseline  the CPU oracle (a faithful port of the reference apply) on this
                 host's cores at the full workload size (modes 0 and 1);
@@ -335,7 +336,10 @@ def main():
     harmonic = block and my_stats["harmonic"] == 1
     if harmonic and my_stats["hm_clusters"] > 0:
         m2l_bytes = 2048.0 * my_stats["att_m2l_blocks"] + 2.0 * 128.0 * nb * my_stats["m2l_targets"]
-        kname, pmc_name = f"k_m2l_hc<{nb}>", f"void aniso::k_m2l_hc<{nb},"
+        # the upper up tiers ride in the same launch (k_top_m2l_hc, §3.10); their
+        # bytes (~1,400 small nodes) are not counted
+        kn = "k_top_m2l_hc" if my_stats["top_fused"] else "k_m2l_hc"
+        kname, pmc_name = f"{kn}<{nb}>", f"void aniso::{kn}<{nb},"
     elif harmonic:
         m2l_bytes = 2048.0 * my_stats["att_m2l_blocks"] + 2.0 * 128.0 * nb * my_stats["m2l_targets"]
         kname, pmc_name = f"k_m2l_hm<{nb}>", f"void aniso::k_m2l_hm<{nb},"

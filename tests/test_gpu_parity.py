@@ -618,7 +618,9 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatc
 
 def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
     """aniso_set_deterministic at BASELINE's 1M-point block matvec: repeat applies
-    are bitwise identical, and equal the default (clustered) matvec to 1e-13."""
+    are bitwise identical, and equal the default (clustered) matvec to 1e-13.  The
+    default runs the upper up tiers inside the M2L launch (k_top_m2l_hc), so this
+    also checks its in-launch hand-offs against the plain tier launches."""
     torch = _torch()
     import aniso_amd
 
@@ -627,6 +629,7 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
     a.setCoeff(*rough_coeffs(xy, 2))
     for m in range(9):
         a.cache(m)
+    assert a.stats()["top_fused"] == 1
     U = torch.tensor(np.random.default_rng(8).uniform(-1, 1, (5, a.N)), device="cuda")
     ref = torch.zeros_like(U)
     a.block_op_dev(2, U, ref, tree=True)
