@@ -154,6 +154,20 @@ __device__ __forceinline__ int64_t out_index(const int* __restrict__ operm, int6
     return operm ? (int64_t)operm[k] : k - obase;
 }
 
+// Store the K charges of one tree position as whole 16-B vectors (the pad entry of
+// an odd K is written as 0): one lane's row is contiguous, so a wave's consecutive
+// points write whole lines instead of K strided 8-B stores.
+template <int K>
+__device__ __forceinline__ void store_charges(double* __restrict__ p, const double (&c)[K]) {
+    if constexpr (K == 1) {
+        p[0] = c[0];
+    } else {
+#pragma unroll
+        for (int v = 0; v < kStride<K> / 2; ++v)
+            reinterpret_cast<dbl2*>(p)[v] = dbl2{c[2 * v], 2 * v + 1 < K ? c[2 * v + 1] : 0.0};
+    }
+}
+
 // Load the K charges of one tree position (row of fT / cT, stride kStride<K>).
 template <int K>
 __device__ __forceinline__ void load_charges(const double* __restrict__ p, double (&c)[K]) {

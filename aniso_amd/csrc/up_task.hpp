@@ -105,15 +105,19 @@ __device__ __forceinline__ void up_task(
                 cheb_weights(P, (pxT[kp] - cx) * irx, Sx);
                 cheb_weights(P, (pyT[kp] - cy) * iry, Sy);
                 const double w = wT[kp];
-#pragma unroll
-                for (int b = 0; b < K; ++b) cb[b] = input_charge(xin, ldi, b, treeIn, perm, sigT, kp);
+                double fb[K];
 #pragma unroll
                 for (int b = 0; b < K; ++b) {
-                    const double f = on ? cb[b] * w : 0.0;
-                    if (on) {
-                        fT[kp * kStride<K> + b] = f;  // for k_near and the corrections
-                        cT[kp * kStride<K> + b] = cb[b];
-                    }
+                    cb[b] = input_charge(xin, ldi, b, treeIn, perm, sigT, kp);
+                    fb[b] = on ? cb[b] * w : 0.0;
+                }
+                if (on) {  // for the near field and the corrections
+                    store_charges<K>(fT + kp * kStride<K>, fb);
+                    store_charges<K>(cT + kp * kStride<K>, cb);
+                }
+#pragma unroll
+                for (int b = 0; b < K; ++b) {
+                    const double f = fb[b];
                     double acc[kRank];
 #pragma unroll
                     for (int j = 0; j < kNP; ++j) {
