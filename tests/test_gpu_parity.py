@@ -920,3 +920,29 @@ def test_fp32_mfma_operator_matches_fp64(sz, d, ml, coeffs):
     # the operator part alone (X - Y vs X - ref): fp32 relative accuracy of K_0
     kerr = float(torch.linalg.norm((Xd - Y.double().t()) - (Xd - ref)) / torch.linalg.norm(Xd - ref))
     assert err <= 2e-6 and kerr <= 2e-5, (err, kerr)
+
+
+@pytest.mark.parametrize("ks", [2, 3, 5])
+def test_fused_top_of_tree_launch_matches_tier_launches(ks):
+    """The block operator's upper up tiers inside the clustered M2L launch
+    (k_top_m2l_hc: in-launch per-tier counters, waiting clusters) against the
+    bitwise-deterministic path, which runs every tier as a launch of its own, for
+    every compiled right-hand-side count the harmonic path uses (2, 4 = 3 padded, 5)."""
+    torch = _torch()
+    import aniso_amd
+
+    a = aniso_amd.Aniso(256, 1, ks, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    a.setCoeff(*rough_coeffs(xy, 6))
+    for m in range(2 * ks - 1):
+        a.cache(m)
+    assert a.stats()["top_fused"] == 1
+    U = torch.tensor(np.random.default_rng(9).uniform(-1, 1, (ks, a.N)), device="cuda")
+    outs = []
+    for det in (False, True, False):
+        a.set_deterministic(det)
+        out = torch.zeros_like(U)
+        a.block_op_dev(2, U, out)
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy())
+    assert _rel(outs[0], outs[1]) <= 1e-13 and _rel(outs[2], outs[1]) <= 1e-13
