@@ -274,6 +274,20 @@ def test_bench_sharded_path_rehearsal_two_ranks():
     assert res["verify_rel_err_vs_unsharded"] <= 1e-13
 
 
+def test_rccl_shard_exchange_collectives_one_rank():
+    """ShardExchange's all-gather and halo all-to-all through RCCL (backend "nccl"),
+    one rank on the box's GPU (tools/rccl_check.py): the calls bench.py makes at N > 1."""
+    import subprocess
+    import sys
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", "--master-port=29537", os.path.join(ROOT, "tools", "rccl_check.py")]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["allgather_equal"] and res["halo_equal"] and res["empty_halo_untouched"]
+
+
 @pytest.mark.parametrize("sz,d,ks,ml", [(32, 1, 2, 20), (11, 3, 2, 20), (15, 3, 2, 2)])
 def test_symmetric_storage_matches_directed(sz, d, ks, ml, monkeypatch):
     """Symmetric M2L / U-pair storage against the fully directed
