@@ -48,6 +48,8 @@ def lib():
             "aniso_create": [I, I, I, D, I, I, I, ctypes.POINTER(P)],
             "aniso_destroy": [P],
             "aniso_num_nodes": [P, lp],
+            "aniso_num_blocks": [P, ip],
+            "aniso_sync": [P],
             "aniso_get_nodes": [P, dp],
             "aniso_get_weights": [P, dp],
             "aniso_set_coeff": [P, dp, dp],
@@ -468,6 +470,15 @@ class Aniso:
                 "stored_near", "stored_m2l", "m2l_canon", "near_partial", "harmonic", "att_m2l_blocks",
                 "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "top_fused"]
         return dict(zip(keys, (int(v) for v in s)))
+
+    def sync(self):
+        """Wait for this handle's applies and raise if any reported a device-side failure."""
+        _check(lib().aniso_sync(self.address))
+
+    def num_blocks(self):
+        k = ctypes.c_int()
+        _check(lib().aniso_num_blocks(self.address, ctypes.byref(k)))
+        return k.value
 
     def set_deterministic(self, on):
         """Bitwise-reproducible block applies (per-target M2L waves) on / off."""

@@ -81,6 +81,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_HARMONIC")) useAtt = useAtt && e[0] != '0';
     if (const char* e = std::getenv("ANISO_OVERLAP")) overlap = std::atoi(e);
     if (const char* e = std::getenv("ANISO_FUSE_SUB")) fuseSub = e[0] != '0';
+    if (const char* e = std::getenv("ANISO_TOP_SPIN_LIMIT")) topSpinLimit = (unsigned)std::strtoul(e, nullptr, 10);
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
     modes.resize(kernelSize);
@@ -96,6 +97,7 @@ Operator::~Operator() {
         if (evJoin) (void)hipEventDestroy(evJoin);
         if (side) (void)hipStreamDestroy(side);
         if (own) (void)hipStreamDestroy(own);
+        if (topErr) (void)hipHostFree(topErr);
         if (prev >= 0) (void)hipSetDevice(prev);
     }
 }
@@ -131,6 +133,8 @@ void Operator::ensureDevice() {
     HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&evFork, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
+    HIP_CHECK(hipHostMalloc((void**)&topErr, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+    *(volatile unsigned*)topErr = 0;
     // tree-order coordinates
     std::vector<double> pxT(geo.N), pyT(geo.N);
     for (int64_t k = 0; k < geo.N; ++k) {
@@ -358,6 +362,7 @@ void Operator::setCoeff(const double* ss, const double* st) {
     up(dSigmaT, sT);
     for (auto& m : modes) m.ready = false;
     attReady = false;
+    f32Ready = false;  // config 5's fp32 caches are rounded from the mode-0 operators of sigma_t
     coeffSet = true;
 }
 
@@ -370,6 +375,7 @@ void Operator::cache(int id) {
     if (!coeffSet) throw std::runtime_error("cache called before setCoeff");
     ensureDevice();
     ModeCache& mc = modes[id];
+    if (id == 0) f32Ready = false;  // rebuilt from the new mode-0 operators at the next fp32 apply
     mc.Knear.alloc((size_t)plan.nearKTotal * sizeof(double));
     mc.Km2l.alloc((size_t)plan.storedM2L * 256 * sizeof(double));
     const Params* P = dParams.as<Params>();
@@ -463,6 +469,7 @@ void Operator::mappingHost(const double* charge, int id, double* out) {
     mappingDev(dCharge.as<double>(), id, dOut.as<double>(), own, kStageAll);
     HIP_CHECK(hipMemcpyAsync(out, dOut.p, geo.N * sizeof(double), hipMemcpyDeviceToHost, own));
     HIP_CHECK(hipStreamSynchronize(own));
+    checkDeviceErrors();
 }
 
 // k right-hand sides of one mode, up to 8 per batched apply (identity mix)
@@ -485,6 +492,7 @@ void Operator::mappingBatchedHost(const double* Q, int k, int id, double* Out) {
         HIP_CHECK(hipMemcpyAsync(Out + (size_t)j0 * N, dout.p, (size_t)nb * N * sizeof(double), hipMemcpyDeviceToHost,
                                  own));
         HIP_CHECK(hipStreamSynchronize(own));
+        checkDeviceErrors();
     }
 }
 
@@ -511,6 +519,7 @@ void Operator::forwardTreePhase(int phase, const double* xTree, double* ySlice, 
                                 const double* rootsRecv, hipStream_t s) {
     if (!modeCached(0)) throw std::runtime_error("forward operator before cache(0)");
     ensureDevice();
+    pendingCall(phase, PendingCall{0, 0, xTree, ySlice, dSigmaT.p, geo.N, 0, 0.0});
     const double one = 1.0;
     const int id = 0;
     applyBlock(1, xTree, geo.N, true, dSigmaT.as<double>(), 1, &id, &one, dTmpS.as<double>(), geo.N, true, s,
@@ -625,6 +634,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                           const int* ids, const double* mixes, double* out, int64_t ldo, bool treeOut, hipStream_t s,
                           int mask, int phase, double* rootsSend, const double* rootsRecv) {
     if (K < 1 || K > 8) throw std::invalid_argument("block apply supports 1..8 right-hand sides, got " + std::to_string(K));
+    checkDeviceErrors();
     if (nterm < 1) throw std::invalid_argument("block apply needs at least one mode term");
     for (int t = 0; t < nterm; ++t) {
         if (ids[t] < 0 || ids[t] >= kernelSize) throw std::out_of_range("kernel id out of range");
@@ -818,6 +828,8 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             ta.clWait = dHmClWait.as<int>();
             ta.cnt = dTopCnt.as<unsigned>();
             ta.recv1 = phase == 2 ? rootsRecv : nullptr;
+            ta.spinLimit = topSpinLimit;
+            HIP_CHECK(hipHostGetDevicePointer((void**)&ta.err, topErr, 0));
             const HcArgs ha{dHmClPtr.as<int>(), dHmTgt.as<int>(), dHmPtr.as<int64_t>(), dHmNDir.as<int>(),
                             dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(), dAttM2L.as<double>(),
                             dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), P, hw,
@@ -892,6 +904,7 @@ void Operator::blockOpDev(int which, const double* x, int64_t ldx, double* out, 
     const int nb = ks, nm = 2 * ks - 1;
     const auto mix = blockMixes(nb, std::isnan(gval) ? g : gval, which != 0);
     const double* sig = sigT ? sigT : dSigmaT.as<double>();
+    pendingCall(phase, PendingCall{1, which, x, out, sig, ldx, ldo, std::isnan(gval) ? g : gval});
     std::vector<int> ids(nm);
     for (int m = 0; m < nm; ++m) ids[m] = m;
     if (which < 2) {
@@ -943,6 +956,7 @@ void Operator::blockOpHost(int which, const double* u, const double* sigmaS, dou
     blockOpDev(which, dHostIn.as<double>(), N, dHostOut.as<double>(), N, false, own, gval, sigT);
     HIP_CHECK(hipMemcpyAsync(out, dHostOut.p, bytes, hipMemcpyDeviceToHost, own));
     HIP_CHECK(hipStreamSynchronize(own));
+    checkDeviceErrors();
 }
 
 void Operator::setTiming(bool on) {
@@ -1162,6 +1176,35 @@ void Operator::forwardF32Dev(const float* X, float* Y, hipStream_t s, int mask) 
         spans.push_back({6, e4, e5});
         spans.push_back({7, e0, e5});
         ++applies;
+    }
+}
+
+void Operator::checkDeviceErrors() {
+    if (!topErr) return;
+    if (*(volatile unsigned*)topErr == 0) return;
+    *(volatile unsigned*)topErr = 0;
+    throw std::runtime_error(
+        "hand-off time-out in the fused top-of-tree M2L launch (k_top_m2l_hc): a cluster gave up waiting for the "
+        "upper up tiers, so the output of an apply enqueued earlier on this handle is invalid");
+}
+
+void Operator::sync() {
+    if (device < 0) return;
+    HIP_CHECK(hipSetDevice(device));
+    HIP_CHECK(hipDeviceSynchronize());
+    checkDeviceErrors();
+}
+
+// The two phases of a sharded apply must come from the same public call: an _end
+// that does not repeat its _begin (another operation, block-operator kind, vectors,
+// strides or coefficients) would run on the other call's weighted charges.
+void Operator::pendingCall(int phase, const PendingCall& c) {
+    if (phase == 1) {
+        pendCall = c;
+    } else if (phase == 2) {
+        if (!pend.active || !(pendCall == c))
+            throw std::logic_error("sharded apply: end does not match the pending begin (operation, which, x, out, "
+                                   "strides and coefficients must repeat)");
     }
 }
 

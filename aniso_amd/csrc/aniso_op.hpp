@@ -116,6 +116,11 @@ public:
     void forwardF32Dev(const float* X, float* Y, hipStream_t s, int mask = kStageAll);
     int64_t f32Bytes() const { return f32Ready ? (int64_t)(d32Km2l.bytes + d32Knear.bytes) : 0; }
     hipStream_t stream() const { return own; }
+    // raise (ANISO_ERR_RUNTIME) if a fused top-of-tree launch gave up waiting for its
+    // producers since the last check: its locals, and so the apply's output, are invalid
+    void checkDeviceErrors();
+    // wait for every apply enqueued by this handle (both streams), then check
+    void sync();
     bool harmonicReady() const { return useAtt && attReady; }
     bool clustersOn() const { return useClusters; }
     // the block apply's upper up tiers ride in the clustered M2L launch (k_top_m2l_hc)
@@ -161,6 +166,19 @@ private:
         bool active = false, nearDone = false;
         int K = 0, e0 = -1, ePack = -1;
     } pend;
+    // the public call that started a pending sharded apply: its _end must repeat it
+    // (operation, which, vectors, strides, sigma_s, g)
+    struct PendingCall {
+        int kind = -1, which = -1;
+        const void *x = nullptr, *out = nullptr, *sig = nullptr;
+        int64_t ldx = 0, ldo = 0;
+        double g = 0;
+        bool operator==(const PendingCall& o) const {
+            return kind == o.kind && which == o.which && x == o.x && out == o.out && sig == o.sig && ldx == o.ldx &&
+                   ldo == o.ldo && (g == o.g || (std::isnan(g) && std::isnan(o.g)));
+        }
+    } pendCall;
+    void pendingCall(int phase, const PendingCall& c);
     void ensureWork(int K);  // work arrays for K right-hand sides
     const ModeArgs* modeTable(int K, int nterm, const int* ids, const double* mixes);
     // harmonic (mode-shared) block apply, DESIGN.md §3.9: the E caches of every
@@ -171,6 +189,11 @@ private:
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
     DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
+    // sticky time-out flag of the fused launch's in-kernel hand-offs, in host-visible
+    // memory (the kernel stores 1 there when a wait gives up; checked at every API
+    // entry and by sync(), never read on the device)
+    unsigned* topErr = nullptr;
+    unsigned topSpinLimit = 1u << 24;  // ANISO_TOP_SPIN_LIMIT (tests: 0 forces the time-out path)
     bool useClusters = true;
     std::map<std::string, DevBuf> modeTabs;
     const CorrFold& corrTable(int K, int nterm, const int* ids, const double* mixes);

@@ -66,12 +66,20 @@ aniso::Operator& get(aniso_handle h) {
     return h->op;
 }
 
+// validates the handle (returns ANISO_ERR_HANDLE from the calling entry point)
 #define CHECK_HANDLE(h)                              \
-    if (!h || h->magic != 0xA2150A2150ULL) {         \
-        g_err = "invalid aniso handle";              \
-        return ANISO_ERR_HANDLE;                     \
-    }                                                \
-    DeviceRestore restore_device__(h)
+    do {                                             \
+        if (!(h) || (h)->magic != 0xA2150A2150ULL) { \
+            g_err = "invalid aniso handle";          \
+            return ANISO_ERR_HANDLE;                 \
+        }                                            \
+    } while (0)
+// restores the caller's current HIP device when the entry point returns
+#define DEVICE_GUARD(h) DeviceRestore device_guard_((h))
+// the two above, at the top of every entry point that takes a handle
+#define ENTER(h)     \
+    CHECK_HANDLE(h); \
+    DEVICE_GUARD(h)
 
 #define CHECK_PTR(p)                                                         \
     do {                                                                     \
@@ -90,7 +98,7 @@ int aniso_create(int sz, int d, int ks, double g, int ns, int np, int maxLevel, 
 }
 
 int aniso_destroy(aniso_handle h) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         h->magic = 0;
         delete h;
@@ -98,15 +106,28 @@ int aniso_destroy(aniso_handle h) {
 }
 
 int aniso_num_nodes(aniso_handle h, int64_t* n) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(n);
         *n = get(h).numNodes();
     });
 }
 
+int aniso_num_blocks(aniso_handle h, int* ks) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(ks);
+        *ks = get(h).ks;
+    });
+}
+
+int aniso_sync(aniso_handle h) {
+    ENTER(h);
+    return guarded([&] { get(h).sync(); });
+}
+
 int aniso_get_nodes(aniso_handle h, double* xy) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(xy);
         get(h).getNodes(xy);
@@ -114,7 +135,7 @@ int aniso_get_nodes(aniso_handle h, double* xy) {
 }
 
 int aniso_get_weights(aniso_handle h, double* w) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(w);
         auto& op = get(h);
@@ -123,7 +144,7 @@ int aniso_get_weights(aniso_handle h, double* w) {
 }
 
 int aniso_set_coeff(aniso_handle h, const double* ss, const double* st) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(ss);
         CHECK_PTR(st);
@@ -132,12 +153,12 @@ int aniso_set_coeff(aniso_handle h, const double* ss, const double* st) {
 }
 
 int aniso_cache(aniso_handle h, int id) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] { get(h).cache(id); });
 }
 
 int aniso_mapping(aniso_handle h, const double* charge, int id, double* out) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(charge);
         CHECK_PTR(out);
@@ -146,7 +167,7 @@ int aniso_mapping(aniso_handle h, const double* charge, int id, double* out) {
 }
 
 int aniso_mapping_dev(aniso_handle h, const double* charge, int id, double* out, void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(charge);
         CHECK_PTR(out);
@@ -155,7 +176,7 @@ int aniso_mapping_dev(aniso_handle h, const double* charge, int id, double* out,
 }
 
 int aniso_mapping_stages_dev(aniso_handle h, const double* charge, int id, int mask, double* out, void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(charge);
         CHECK_PTR(out);
@@ -165,7 +186,7 @@ int aniso_mapping_stages_dev(aniso_handle h, const double* charge, int id, int m
 }
 
 int aniso_mapping_batched(aniso_handle h, const double* Q, int k, int id, double* Out) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(Q);
         CHECK_PTR(Out);
@@ -176,7 +197,7 @@ int aniso_mapping_batched(aniso_handle h, const double* Q, int k, int id, double
 }
 
 int aniso_forward_dev(aniso_handle h, const double* u, double* out, void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(u);
         CHECK_PTR(out);
@@ -187,7 +208,7 @@ int aniso_forward_dev(aniso_handle h, const double* u, double* out, void* stream
 }
 
 int aniso_mapping_tree_dev(aniso_handle h, const double* q_tree, int id, double* out_slice, void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(q_tree);
         CHECK_PTR(out_slice);
@@ -196,7 +217,7 @@ int aniso_mapping_tree_dev(aniso_handle h, const double* q_tree, int id, double*
 }
 
 int aniso_forward_tree_dev(aniso_handle h, const double* x_tree, double* y_slice, void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(x_tree);
         CHECK_PTR(y_slice);
@@ -208,7 +229,7 @@ int aniso_forward_tree_dev(aniso_handle h, const double* x_tree, double* y_slice
 
 int aniso_forward_tree_begin_dev(aniso_handle h, const double* x_tree, double* y_slice, double* roots_send,
                                  void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(x_tree);
         CHECK_PTR(y_slice);
@@ -218,7 +239,7 @@ int aniso_forward_tree_begin_dev(aniso_handle h, const double* x_tree, double* y
 
 int aniso_forward_tree_end_dev(aniso_handle h, const double* x_tree, double* y_slice, const double* roots_recv,
                                void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(x_tree);
         CHECK_PTR(y_slice);
@@ -227,7 +248,7 @@ int aniso_forward_tree_end_dev(aniso_handle h, const double* x_tree, double* y_s
 }
 
 int aniso_forward_f32_dev(aniso_handle h, const float* x, float* y, void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(x);
         CHECK_PTR(y);
@@ -236,7 +257,7 @@ int aniso_forward_f32_dev(aniso_handle h, const float* x, float* y, void* stream
 }
 
 int aniso_forward_f32_stages_dev(aniso_handle h, const float* x, int mask, float* y, void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(x);
         CHECK_PTR(y);
@@ -247,7 +268,7 @@ int aniso_forward_f32_stages_dev(aniso_handle h, const float* x, int mask, float
 
 int aniso_apply_block_dev(aniso_handle h, int nrhs, const double* x, int64_t ldx, int use_sigma, int nterm,
                           const int* ids, const double* mixes, double* out, int64_t ldo, int tree, void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(x);
         CHECK_PTR(out);
@@ -260,7 +281,7 @@ int aniso_apply_block_dev(aniso_handle h, int nrhs, const double* x, int64_t ldx
 
 int aniso_block_op_dev(aniso_handle h, int which, const double* x, int64_t ldx, double* out, int64_t ldo, int tree,
                        void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(x);
         CHECK_PTR(out);
@@ -270,7 +291,7 @@ int aniso_block_op_dev(aniso_handle h, int which, const double* x, int64_t ldx, 
 
 int aniso_block_op_begin_dev(aniso_handle h, int which, const double* x, int64_t ldx, double* out, int64_t ldo,
                              double* roots_send, void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(x);
         CHECK_PTR(out);
@@ -280,7 +301,7 @@ int aniso_block_op_begin_dev(aniso_handle h, int which, const double* x, int64_t
 
 int aniso_block_op_end_dev(aniso_handle h, int which, const double* x, int64_t ldx, double* out, int64_t ldo,
                            const double* roots_recv, void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(x);
         CHECK_PTR(out);
@@ -289,7 +310,7 @@ int aniso_block_op_end_dev(aniso_handle h, int which, const double* x, int64_t l
 }
 
 int aniso_block_op(aniso_handle h, int which, const double* u, double* out) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(u);
         CHECK_PTR(out);
@@ -298,7 +319,7 @@ int aniso_block_op(aniso_handle h, int which, const double* u, double* out) {
 }
 
 int aniso_apply_block(aniso_handle h, const double* u, const double* sigma_s, double g, double* out) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(u);
         CHECK_PTR(sigma_s);
@@ -318,7 +339,7 @@ int aniso_block_mixes(int nb, double g, int chi, double* mixes) {
 
 int aniso_gmres(aniso_handle h, const double* q, double* x, int m, int maxit, double tol, double* hist, int maxhist,
                 int* iters, double* final_resid) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(q);
         CHECK_PTR(x);
@@ -328,12 +349,12 @@ int aniso_gmres(aniso_handle h, const double* q, double* x, int m, int maxit, do
 }
 
 int aniso_set_shard(aniso_handle h, int rank, int nranks) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] { get(h).setShard(rank, nranks); });
 }
 
 int aniso_shard_cuts(aniso_handle h, int nranks, int64_t* cuts) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(cuts);
         const auto c = aniso::shard_cuts(get(h).tree, nranks);
@@ -342,12 +363,12 @@ int aniso_shard_cuts(aniso_handle h, int nranks, int64_t* cuts) {
 }
 
 int aniso_set_deterministic(aniso_handle h, int on) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] { get(h).setDeterministic(on != 0); });
 }
 
 int aniso_shard_exchange(aniso_handle h, int nrhs, int64_t* info) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(info);
         if (nrhs < 1 || nrhs > 8) throw std::invalid_argument("nrhs must be in 1..8");
@@ -365,7 +386,7 @@ int aniso_shard_exchange(aniso_handle h, int nrhs, int64_t* info) {
 }
 
 int aniso_shard_halo(aniso_handle h, int64_t* ranges) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(ranges);
         const auto& p = get(h).plan;
@@ -374,7 +395,7 @@ int aniso_shard_halo(aniso_handle h, int64_t* ranges) {
 }
 
 int aniso_shard_roots(aniso_handle h, int* send_nodes, int* recv_nodes, int* t0_roots) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         const auto& p = get(h).plan;
         if (send_nodes) std::copy(p.xRootSend.begin(), p.xRootSend.end(), send_nodes);
@@ -385,7 +406,7 @@ int aniso_shard_roots(aniso_handle h, int* send_nodes, int* recv_nodes, int* t0_
 }
 
 int aniso_get_shard(aniso_handle h, int64_t* b, int64_t* e) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(b);
         CHECK_PTR(e);
@@ -394,7 +415,7 @@ int aniso_get_shard(aniso_handle h, int64_t* b, int64_t* e) {
 }
 
 int aniso_tree_perm(aniso_handle h, int* perm) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(perm);
         auto& t = get(h).tree;
@@ -403,7 +424,7 @@ int aniso_tree_perm(aniso_handle h, int* perm) {
 }
 
 int aniso_permute_to_tree_dev(aniso_handle h, const double* orig, double* tree, void* stream) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(orig);
         CHECK_PTR(tree);
@@ -412,7 +433,7 @@ int aniso_permute_to_tree_dev(aniso_handle h, const double* orig, double* tree, 
 }
 
 int aniso_tree_size(aniso_handle h, int* nnodes, int* max_level) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         auto& t = get(h).tree;
         if (nnodes) *nnodes = t.nn;
@@ -421,7 +442,7 @@ int aniso_tree_size(aniso_handle h, int* nnodes, int* max_level) {
 }
 
 int aniso_tree_nodes(aniso_handle h, int* ints, double* geom) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         auto& t = get(h).tree;
         for (int i = 0; i < t.nn; ++i) {
@@ -448,7 +469,7 @@ int aniso_tree_nodes(aniso_handle h, int* ints, double* geom) {
 }
 
 int aniso_tree_list(aniso_handle h, int which, int64_t* ptr, int* idx) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         auto& t = get(h).tree;
         const std::vector<int64_t>* P[4] = {&t.uPtr, &t.vPtr, &t.wPtr, &t.xPtr};
@@ -461,7 +482,7 @@ int aniso_tree_list(aniso_handle h, int which, int64_t* ptr, int* idx) {
 }
 
 int aniso_stats(aniso_handle h, int64_t* s) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(s);
         auto& op = get(h);
@@ -492,12 +513,12 @@ int aniso_stats(aniso_handle h, int64_t* s) {
 }
 
 int aniso_set_timing(aniso_handle h, int on) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] { get(h).setTiming(on != 0); });
 }
 
 int aniso_stage_times(aniso_handle h, float* t) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(t);
         auto s = get(h).stageTimes();
@@ -507,7 +528,7 @@ int aniso_stage_times(aniso_handle h, float* t) {
 }
 
 int aniso_line_integrals(aniso_handle h, const double* seg, int n, double* out) {
-    CHECK_HANDLE(h);
+    ENTER(h);
     return guarded([&] {
         CHECK_PTR(seg);
         CHECK_PTR(out);

@@ -447,19 +447,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 // block, which then acquires before its block reads (MI355X_MICROARCH.md, cross-
 // workgroup visibility).  Waiting blocks have higher ids than every block they wait
 // for and the up blocks (a few hundred) all fit on the chip at once, so the
-// producers are always resident; a bounded spin counts a time-out in cnt[0] rather
-// than hanging.
+// producers are always resident.  The spin is still bounded: a wait that gives up
+// counts in cnt[0] and stores 1 into the host-visible flag err, which the host turns
+// into ANISO_ERR_RUNTIME at its next entry / sync (Operator::checkDeviceErrors) --
+// the apply's output is then invalid, never silently accepted.
 typedef __attribute__((address_space(1))) unsigned gu32;
 
-__device__ __forceinline__ void top_wait(unsigned* cnt, int k, unsigned target) {
+__device__ __forceinline__ void top_wait(const TopArgs& t, int k, unsigned target) {
     if (threadIdx.x == 0) {
-        gu32* c = (gu32*)(cnt + k);
-        for (unsigned spins = 0; __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target;) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins == (1u << 24)) {
-                __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gu32* c = (gu32*)(t.cnt + k);
+        for (unsigned spins = 0;; ++spins) {
+            if (spins >= t.spinLimit) {
+                __hip_atomic_fetch_add((gu32*)t.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(t.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
             }
+            if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+            __builtin_amdgcn_s_sleep(2);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
@@ -485,7 +489,7 @@ k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a) {
     if (b < t.nUp) {
         int k = 1;
         while (b >= t.blk0[k + 1]) ++k;
-        if (k >= 2) top_wait(t.cnt, k - 1, (unsigned)(t.blk0[k] - t.blk0[k - 1]));
+        if (k >= 2) top_wait(t, k - 1, (unsigned)(t.blk0[k] - t.blk0[k - 1]));
         up_task<K>(t.task0[k] + (b - t.blk0[k]), u.maxTask, u.desc, u.grpFix, u.node, u.code, u.geom, u.leafRange,
                    u.pxT, u.pyT, u.xin, u.ldi, u.treeIn, u.perm, u.sigT, u.wT, u.fT, u.cT, u.P, u.mult, u.rootSlot,
                    k == 1 ? t.recv1 : nullptr, nullptr, nullptr, sm);
@@ -495,7 +499,7 @@ k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a) {
     const int cid = b - t.nUp;
     const int w = t.clWait[cid];
     if (w > 0) {  // its own copy: behind the wait's fence the source boxes load through the vector path
-        top_wait(t.cnt, w, (unsigned)(t.blk0[w + 1] - t.blk0[w]));
+        top_wait(t, w, (unsigned)(t.blk0[w + 1] - t.blk0[w]));
         m2l_hc_cluster<K, NR>(cid, a, sm);
         return;
     }
@@ -836,6 +840,7 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
     if (maxCl > 64) throw std::invalid_argument("harmonic M2L cluster larger than 64 targets");
     if (t.ntier < 2 || t.ntier > kMaxTopTiers || t.blk0[t.ntier] != t.nUp)
         throw std::invalid_argument("fused top-of-tree launch: bad tier layout");
+    if (!t.err) throw std::invalid_argument("fused top-of-tree launch: no time-out flag");
     const size_t shm = std::max((size_t)(maxCl + 256 / kWave) * kRank * K * sizeof(double), up_tier_lds(u.maxTask, K));
     const unsigned nb = (unsigned)(t.nUp + ncl);
     ANISO_HM_DISPATCH_K(K, ({

@@ -202,6 +202,8 @@ struct TopArgs {
     const int* clWait;            // per cluster: the upper tier it waits for (0: none)
     unsigned* cnt;                // finished tasks per tier; cnt[0] = spin time-outs (zeroed by tier 0)
     const double* recv1;          // sharded phase 2: the gathered tier-0 roots tier 1 reads
+    unsigned spinLimit;           // polls before a wait gives up (0: give up at once -- tests only)
+    unsigned* err;                // host-visible sticky flag: set to 1 when a wait gave up
 };
 bool top_fused_enabled();
 void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs& t, const HcArgs& a, hipStream_t s);

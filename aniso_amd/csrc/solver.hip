@@ -188,6 +188,7 @@ done:
     if (finalResid) *finalResid = resid;
     HIP_CHECK(hipMemcpyAsync(xh, x, N * sizeof(double), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    checkDeviceErrors();
     return ret;
 }
 

@@ -53,6 +53,12 @@ static int64_t num_nodes(aniso_handle h) {
     return n;
 }
 
+static int64_t num_blocks(aniso_handle h) {
+    int ks = 0;
+    CALL(aniso_num_blocks(h, &ks));
+    return ks;
+}
+
 /* a real double vector of exactly n entries (the reference's asserts were compiled
  * out, AnisoWrapper.cpp:55-56; this shim checks) */
 static const double* column(const mxArray* a, int64_t n, const char* what) {
@@ -108,15 +114,16 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         /* aniso.m:121-136 forward, :138-157 mforward, :155 x - mforward(x); the
          * argument is the stacked column [u_0; ...; u_{ks-1}] of ks * N entries */
         aniso_handle h;
-        int64_t n, len;
+        int64_t len;
+        const double* u;
         const int which = !strcmp(op, "forward") ? 0 : !strcmp(op, "mforward") ? 1 : 2;
         need(nrhs, 3, op);
         h = handle_of(prhs[1]);
-        n = num_nodes(h);
-        len = (int64_t)mxGetNumberOfElements(prhs[2]);
-        if (n <= 0 || len % n) mexErrMsgIdAndTxt("mexplus:arguments:error", "%s: length must be ks * N", op);
+        /* the library reads and writes exactly ks * N doubles */
+        len = num_blocks(h) * num_nodes(h);
+        u = column(prhs[2], len, "u"); /* the stacked column [u_0; ...; u_{ks-1}], exactly ks * N */
         plhs[0] = mxCreateDoubleMatrix((size_t)len, 1, mxREAL);
-        CALL(aniso_block_op(h, which, column(prhs[2], len, "u"), mxGetPr(plhs[0])));
+        CALL(aniso_block_op(h, which, u, mxGetPr(plhs[0])));
     } else {
         mexErrMsgIdAndTxt("mexplus:dispatch:argumentError", "Unknown operation %s", op);
     }

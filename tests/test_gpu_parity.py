@@ -957,6 +957,179 @@ def test_fused_top_of_tree_launch_matches_tier_launches(ks):
         a.set_deterministic(det)
         out = torch.zeros_like(U)
         a.block_op_dev(2, U, out)
-        torch.cuda.synchronize()
+        a.sync()  # raises if an in-launch hand-off timed out (its output would be invalid)
         outs.append(out.cpu().numpy())
     assert _rel(outs[0], outs[1]) <= 1e-13 and _rel(outs[2], outs[1]) <= 1e-13
+
+
+def test_fused_top_of_tree_time_out_is_an_error(monkeypatch):
+    """A hand-off wait of k_top_m2l_hc that gives up (forced here: ANISO_TOP_SPIN_LIMIT=0
+    makes every waiting block give up at its first poll) must surface as
+    ANISO_ERR_RUNTIME -- from aniso_sync, and from a host-pointer call, which
+    synchronises itself -- never as a silently wrong matvec; the flag is reported once.
+    A default handle reports nothing."""
+    torch = _torch()
+    import aniso_amd
+
+    monkeypatch.setenv("ANISO_TOP_SPIN_LIMIT", "0")
+    ks = 5
+    a = aniso_amd.Aniso(256, 1, ks, 0.8, 10, 4, 20)
+    monkeypatch.delenv("ANISO_TOP_SPIN_LIMIT")
+    xy = a.getNodes()
+    a.setCoeff(*main_coeffs(xy))
+    for m in range(2 * ks - 1):
+        a.cache(m)
+    assert a.stats()["top_fused"] == 1
+    U = torch.tensor(np.random.default_rng(1).uniform(-1, 1, (ks, a.N)), device="cuda")
+    out = torch.zeros_like(U)
+    a.block_op_dev(2, U, out)
+    with pytest.raises(aniso_amd.AnisoError) as ei:
+        a.sync()
+    assert ei.value.code == 2 and "time-out" in str(ei.value)
+    a.sync()  # reported once
+    with pytest.raises(aniso_amd.AnisoError) as ei:
+        a.block_op(2, U.cpu().numpy())
+    assert ei.value.code == 2
+    b = aniso_amd.Aniso(256, 1, ks, 0.8, 10, 4, 20)
+    b.setCoeff(*main_coeffs(xy))
+    for m in range(2 * ks - 1):
+        b.cache(m)
+    b.block_op_dev(2, U, out)
+    b.sync()
+
+
+def test_set_coeff_rebuilds_fp32_caches():
+    """Config 5's fp32 operator after a second setCoeff + cache(0) runs on the new
+    sigma_t's caches (they are rounded from the mode-0 operators), and before that
+    cache(0) it fails as a state error instead of using the old ones."""
+    torch = _torch()
+    import aniso_amd
+
+    a = aniso_amd.Aniso(64, 1, 1, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    X = torch.tensor(np.random.default_rng(2).uniform(-1, 1, (a.N, 16)), device="cuda", dtype=torch.float32)
+    Y = torch.zeros_like(X)
+    a.setCoeff(*main_coeffs(xy))
+    a.cache(0)
+    a.forward_f32_dev(X, Y)
+    a.setCoeff(*rough_coeffs(xy, 8))
+    with pytest.raises(aniso_amd.AnisoError) as ei:
+        a.forward_f32_dev(X, Y)
+    assert ei.value.code == 3
+    a.cache(0)
+    a.forward_f32_dev(X, Y)
+    Xd = X.double().t().contiguous()
+    ref = torch.zeros_like(Xd)
+    for j in range(16):
+        a.forward_tree_dev(Xd[j], ref[j])
+    torch.cuda.synchronize()
+    err = float(torch.linalg.norm(Y.double().t() - ref) / torch.linalg.norm(ref))
+    assert err <= 2e-6, err
+
+
+def test_sharded_end_must_repeat_its_begin():
+    """Phase 2 of a sharded apply checks that it repeats its phase 1 (operation, which,
+    vectors, strides): a mismatched _end is a state error and leaves the begun apply
+    pending, and the matching _end then completes it correctly."""
+    torch = _torch()
+    import aniso_amd
+
+    sz, ks, world = 32, 5, 2
+    full = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
+    xy = full.getNodes()
+    coef = main_coeffs(xy)
+    full.setCoeff(*coef)
+    for m in range(2 * ks - 1):
+        full.cache(m)
+    X = torch.tensor(np.random.default_rng(4).uniform(-1, 1, (ks, full.N)), device="cuda")
+    ref = torch.zeros_like(X)
+    full.block_op_dev(2, X, ref, tree=True)
+    hs = []
+    for r in range(world):
+        sh = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
+        sh.set_shard(r, world)
+        sh.setCoeff(*coef)
+        for m in range(2 * ks - 1):
+            sh.cache(m)
+        ex = sh.shard_exchange(ks)
+        rs = torch.zeros(max(ex["root_chunk"] * ex["root_record"], 1), dtype=torch.float64, device="cuda")
+        y = torch.zeros(ks, sh.n_owned(), dtype=torch.float64, device="cuda")
+        sh.block_op_begin_dev(2, X, y, rs)
+        hs.append((sh, y, rs[: ex["root_chunk"] * ex["root_record"]]))
+    recv = torch.cat([h[2] for h in hs])
+    sh, y, _ = hs[0]
+    y2 = torch.zeros_like(y)
+    for bad in (lambda: sh.block_op_end_dev(1, X, y, recv, world), lambda: sh.block_op_end_dev(2, X, y2, recv, world),
+                lambda: sh.forward_tree_end_dev(X[0], y[0], recv, world)):
+        with pytest.raises(aniso_amd.AnisoError) as ei:
+            bad()
+        assert ei.value.code == 3
+    got = []
+    for sh, y, _ in hs:
+        sh.block_op_end_dev(2, X, y, recv, world)
+        got.append(y)
+    torch.cuda.synchronize()
+    got = torch.cat(got, 1)
+    assert float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref)) <= 1e-13
+
+
+def _block_ref_per_mode(o, U, g, ss):
+    """x - mforward(x) (aniso.m:138-157, 155) composed from oracle mode applies, the
+    oracle holding one mode's caches at a time (its 9-mode cache would not fit at
+    full size): for every mode m, each input block b the mixes use is applied once."""
+    import aniso_amd
+
+    nb = U.shape[0]
+    mix = aniso_amd.block_mixes(nb, g, True)
+    out = U.copy()
+    for m in range(2 * nb - 1):
+        o.cache(m)
+        for b in range(nb):
+            if np.any(mix[m, :, b]):
+                y = o.mapping(U[b] * ss, m)
+                for i in range(nb):
+                    if mix[m, i, b]:
+                        out[i] -= mix[m, i, b] * y
+        o.uncache(m)
+    return out
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+def test_config3_full_size_odd_mode_matches_oracle():
+    """BASELINE's headline geometry at its FULL size (config 3: sz = 1024, d = 1,
+    ns = 10, N = 1,048,576) against the oracle apply (AnisoWrapper.cpp:92-136
+    restated) for an odd mode (m = 5) with varying sigma: <= 1e-10 relative.  The
+    oracle's one-mode cache takes ~40 s on the box's cores."""
+    a, o, xy = _pair(1024, 1, 5, 10, 20, "main")
+    m = 5
+    a.cache(m)
+    o.cache(m)
+    q = gaussian_charge(xy) + np.random.default_rng(1024).uniform(-0.1, 0.1, a.N)
+    err = _rel(a.mapping(q, m), o.mapping(q, m))
+    o.close()
+    assert err <= TOL, err
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+def test_block_matvec_sz512_matches_oracle_composition():
+    """aniso.m's GMRES matvec x - mforward(x) on the harmonic block path (all 9 modes x
+    5 blocks in one apply, the bench's operator) at sz = 512 (N = 262,144) against the
+    oracle's per-mode composition (45 mapping calls in aniso.m's loop): <= 1e-10."""
+    torch = _torch()
+    a, o, xy = _pair(512, 1, 5, 10, 20, "main")
+    ks, ss = 5, main_coeffs(xy)[0]
+    for m in range(2 * ks - 1):
+        a.cache(m)
+    assert a.stats()["harmonic"] == 1
+    U = np.random.default_rng(512).uniform(-1, 1, (ks, a.N))
+    U[0] += gaussian_charge(xy)
+    Ud = torch.tensor(U, device="cuda")
+    out = torch.zeros_like(Ud)
+    a.block_op_dev(2, Ud, out)
+    a.sync()
+    got = out.cpu().numpy()
+    ref = _block_ref_per_mode(o, U, a.g, ss)
+    o.close()
+    assert _rel(got, ref) <= TOL, _rel(got, ref)
