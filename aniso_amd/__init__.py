@@ -73,6 +73,8 @@ def lib():
             "aniso_mapping_tree_dev": [P, P, I, P, P],
             "aniso_forward_tree_dev": [P, P, P, P],
             "aniso_gmres": [P, dp, dp, I, I, D, dp, I, ip, dp],
+            "aniso_block_solve": [P, dp, dp, I, D, I, dp, I, ip, dp],
+            "aniso_block_solve_dev": [P, P, P, I, D, I, dp, I, ip, dp, P],
             "aniso_apply_block_dev": [P, I, P, I64, I, I, ip, dp, P, I64, I, P],
             "aniso_block_op_dev": [P, I, P, I64, P, I64, I, P],
             "aniso_block_mixes": [I, D, I, dp],
@@ -393,6 +395,29 @@ class Aniso:
         n = abs(it.value) + 1 if it.value != 0 else 1
         return it.value, x, hist[:n], fr.value
 
+    def block_solve(self, rhs, restart=400, tol=1e-11, maxit=400, x0=None):
+        """aniso.m:159-173 on the device: u = gmres(A, rhs, restart, tol, maxit), A = u - mforward(u).
+        rhs: (ks, N) or the stacked ks*N column; returns (iters, u (ks, N), residual history, relres)."""
+        rhs = _f64(rhs, self.ks * self.N, "rhs")
+        x = np.zeros(self.ks * self.N) if x0 is None else _f64(x0, self.ks * self.N, "x0").copy()
+        hist = np.zeros(restart * maxit if restart * maxit < 100000 else 100000)
+        it, rr = ctypes.c_int(), ctypes.c_double()
+        _check(lib().aniso_block_solve(self.address, _dp(rhs), _dp(x), int(restart), float(tol), int(maxit), _dp(hist),
+                                       len(hist), ctypes.byref(it), ctypes.byref(rr)))
+        return it.value, x.reshape(self.ks, self.N), hist[: min(abs(it.value), len(hist))], rr.value
+
+    def block_solve_dev(self, rhs, x, restart=400, tol=1e-11, maxit=400, stream=None):
+        """The same on (ks, N) float64 CUDA tensors (original order); x: guess in, solution out."""
+        import torch
+
+        pr, px = _dev_vec(rhs, self.ks * self.N, "rhs"), _dev_vec(x, self.ks * self.N, "x")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        hist = np.zeros(min(restart * maxit, 100000))
+        it, rr = ctypes.c_int(), ctypes.c_double()
+        _check(lib().aniso_block_solve_dev(self.address, pr, px, int(restart), float(tol), int(maxit), _dp(hist),
+                                           len(hist), ctypes.byref(it), ctypes.byref(rr), ctypes.c_void_p(s)))
+        return it.value, hist[: min(abs(it.value), len(hist))], rr.value
+
     def set_shard(self, rank, nranks):
         _check(lib().aniso_set_shard(self.address, int(rank), int(nranks)))
 
@@ -464,11 +489,11 @@ class Aniso:
         return ptr, idx
 
     def stats(self):
-        s = np.zeros(19, dtype=np.int64)
+        s = np.zeros(20, dtype=np.int64)
         _check(lib().aniso_stats(self.address, s.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
         keys = ["near_entries", "m2l_entries", "m2l_pairs", "leaves", "m2l_targets", "tree_nodes", "max_leaf", "N",
                 "stored_near", "stored_m2l", "m2l_canon", "near_partial", "harmonic", "att_m2l_blocks",
-                "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "top_fused"]
+                "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "top_fused", "staged_m2l"]
         return dict(zip(keys, (int(v) for v in s)))
 
     def sync(self):

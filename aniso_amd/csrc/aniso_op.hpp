@@ -109,6 +109,12 @@ public:
     void forwardDev(const double* u, double* out, hipStream_t s);
     int gmresHost(const double* q, double* x, int m, int maxit, double tol, double* hist, int maxhist,
                   double* finalResid);
+    // aniso.m:159-173: gmres(A, rhs, restart, tol, maxit), A = x - mforward(x), on the
+    // ks stacked blocks (original order, block b at b * N); device / host pointers
+    int blockSolveDev(const double* rhs, double* x, int restart, double tol, int maxit, double* hist, int maxhist,
+                      double* relres, hipStream_t s);
+    int blockSolveHost(const double* rhs, double* x, int restart, double tol, int maxit, double* hist, int maxhist,
+                       double* relres);
     // config 5's fp32 operator (f32op.hip): Y = X - K_0(sigma_s .* X)
     // for 16 right-hand sides, X and Y point-major (N x 16 floats, tree order), every
     // FMM translation a 16 x 16 x 16 MFMA product on fp32 caches (built from the
@@ -189,6 +195,14 @@ private:
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
     DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
+    DevBuf dCsRow, dCsSelf, dCsRowPtr, dCsRowNode, dCsCut;  // staged-source clusters (k_m2l_cs)
+    bool useStaged = true;  // ANISO_HM_STAGED=0: the clustered M2L without staged sources (k_m2l_hc)
+  public:
+    // the block apply of K right-hand sides runs the staged-source M2L (k_m2l_cs)
+    bool stagedOn(int K) const {
+        return useAtt && useStaged && useClusters && m2l_cs_lds(K, plan.hmMaxCl, plan.csMaxRows) > 0;
+    }
+  private:
     // sticky time-out flag of the fused launch's in-kernel hand-offs, in host-visible
     // memory (the kernel stores 1 there when a wait gives up; checked at every API
     // entry and by sync(), never read on the device)

@@ -348,6 +348,30 @@ int aniso_gmres(aniso_handle h, const double* q, double* x, int m, int maxit, do
     });
 }
 
+int aniso_block_solve(aniso_handle h, const double* rhs, double* x, int restart, double tol, int maxit, double* hist,
+                      int maxhist, int* iters, double* relres) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(rhs);
+        CHECK_PTR(x);
+        const int it = get(h).blockSolveHost(rhs, x, restart, tol, maxit, hist, hist ? maxhist : 0, relres);
+        if (iters) *iters = it;
+    });
+}
+
+int aniso_block_solve_dev(aniso_handle h, const double* rhs, double* x, int restart, double tol, int maxit,
+                          double* hist, int maxhist, int* iters, double* relres, void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(rhs);
+        CHECK_PTR(x);
+        auto& op = get(h);
+        hipStream_t s = stream ? (hipStream_t)stream : op.stream();
+        const int it = op.blockSolveDev(rhs, x, restart, tol, maxit, hist, hist ? maxhist : 0, relres, s);
+        if (iters) *iters = it;
+    });
+}
+
 int aniso_set_shard(aniso_handle h, int rank, int nranks) {
     ENTER(h);
     return guarded([&] { get(h).setShard(rank, nranks); });
@@ -509,6 +533,7 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[16] = cl ? (int64_t)op.plan.hmSrc.size() : (int64_t)op.plan.attSrc.size();
         s[17] = op.f32Bytes();  // config 5's fp32 operator caches (0 before its first apply)
         s[18] = cl && op.topFusedOn() ? 1 : 0;
+        s[19] = cl && op.stagedOn(aniso::Operator::rootRhs(op.ks)) ? 1 : 0;
     });
 }
 

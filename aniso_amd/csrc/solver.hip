@@ -63,6 +63,110 @@ __global__ void __launch_bounds__(256) k_dot_final(int nb, const double* __restr
 
 static unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
 
+// ---- Krylov kernels of the block solve (aniso.m:159-173): classical Gram-Schmidt
+// with one reorthogonalisation (CGS2) on device-resident bases.  Every reduction
+// has a fixed order (per-block partials, then one block per output), so a solve is
+// bitwise reproducible; no host round trip sits inside a step except reading the
+// Hessenberg column for the Givens rotations.
+constexpr int kDotGroup = 8;  // basis vectors reduced together per pass over w
+
+// part[k * gridDim.x + blk] = sum over this block's chunk of V[k][j] w[j], k < nv
+__global__ void __launch_bounds__(256) k_mdot_partial(int64_t n, int nv, const double* __restrict__ V, int64_t ldv,
+                                                      const double* __restrict__ w, double* __restrict__ part) {
+    __shared__ double red[kDotGroup][256];
+    const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t j0 = (int64_t)blockIdx.x * chunk, j1 = min(n, j0 + chunk);
+    for (int k0 = 0; k0 < nv; k0 += kDotGroup) {
+        double acc[kDotGroup];
+#pragma unroll
+        for (int g = 0; g < kDotGroup; ++g) acc[g] = 0.0;
+        for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
+            const double wj = w[j];
+#pragma unroll
+            for (int g = 0; g < kDotGroup; ++g)
+                if (k0 + g < nv) acc[g] = __builtin_fma(V[(size_t)(k0 + g) * ldv + j], wj, acc[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < kDotGroup; ++g) red[g][threadIdx.x] = acc[g];
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o)
+#pragma unroll
+                for (int g = 0; g < kDotGroup; ++g) red[g][threadIdx.x] += red[g][threadIdx.x + o];
+            __syncthreads();
+        }
+        if ((int)threadIdx.x < kDotGroup && k0 + (int)threadIdx.x < nv)
+            part[(size_t)(k0 + threadIdx.x) * gridDim.x + blockIdx.x] = red[threadIdx.x][0];
+        __syncthreads();
+    }
+}
+
+// out[k] (+)= sum_b part[k * nb + b]: one block per k, a fixed order
+__global__ void __launch_bounds__(256) k_mdot_final(int nb, const double* __restrict__ part, int accumulate,
+                                                    double* __restrict__ out) {
+    __shared__ double r[256];
+    const int k = blockIdx.x;
+    double a = 0.0;
+    for (int b = threadIdx.x; b < nb; b += 256) a += part[(size_t)k * nb + b];
+    r[threadIdx.x] = a;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) r[threadIdx.x] += r[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[k] = accumulate ? out[k] + r[0] : r[0];
+}
+
+// w[j] += sign * sum_{k < nv} c[k] V[k][j]
+__global__ void __launch_bounds__(256) k_maxpy(int64_t n, int nv, const double* __restrict__ V, int64_t ldv,
+                                               const double* __restrict__ c, double sign, double* __restrict__ w) {
+    extern __shared__ double cs[];
+    for (int k = threadIdx.x; k < nv; k += 256) cs[k] = sign * c[k];
+    __syncthreads();
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    double a = w[j];
+    for (int k = 0; k < nv; ++k) a = __builtin_fma(cs[k], V[(size_t)k * ldv + j], a);
+    w[j] = a;
+}
+
+// y = a x
+__global__ void k_scale(int64_t n, double a, const double* __restrict__ x, double* __restrict__ y) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) y[j] = a * x[j];
+}
+
+// y = x / sqrt(*nrm2) (a norm computed on the device; 0 stays 0)
+__global__ void k_scale_rsqrt(int64_t n, const double* __restrict__ x, const double* __restrict__ nrm2,
+                              double* __restrict__ y) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const double s = *nrm2 > 0.0 ? 1.0 / sqrt(*nrm2) : 0.0;
+    if (j < n) y[j] = x[j] * s;
+}
+
+// orig[perm[k]] = tree[k] (the inverse of launch_permute)
+__global__ void k_unpermute(int64_t n, const int* __restrict__ perm, const double* __restrict__ tree,
+                            double* __restrict__ orig) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) orig[perm[k]] = tree[k];
+}
+
+constexpr int kMdotBlocks = 1024;
+
+struct Krylov {
+    int64_t n;
+    hipStream_t s;
+    double* part;  // kMdotBlocks x (restart + 1)
+    // out[0 .. nv) (+)= V[0 .. nv)^T w
+    void mdot(int nv, const double* V, int64_t ldv, const double* w, double* out, bool accumulate) {
+        k_mdot_partial<<<kMdotBlocks, 256, 0, s>>>(n, nv, V, ldv, w, part);
+        k_mdot_final<<<nv, 256, 0, s>>>(kMdotBlocks, part, accumulate ? 1 : 0, out);
+    }
+    void maxpy(int nv, const double* V, int64_t ldv, const double* c, double sign, double* w) {
+        k_maxpy<<<nblk(n), 256, (size_t)nv * sizeof(double), s>>>(n, nv, V, ldv, c, sign, w);
+    }
+};
+
 struct DeviceBlas {
     int64_t n;
     hipStream_t s;
@@ -190,6 +294,146 @@ done:
     HIP_CHECK(hipStreamSynchronize(s));
     checkDeviceErrors();
     return ret;
+}
+
+// aniso.m:159-173: u = gmres(A, rhs, restart, tol, maxit) with A(x) = x - mforward(x)
+// (aniso.m:155) on the nb = ks stacked blocks.  MATLAB's restarted GMRES semantics:
+// x0 = the given guess, at most maxit cycles of at most `restart` steps, converged
+// when ||rhs - A x|| / ||rhs|| <= tol (the estimate inside a cycle, confirmed by the
+// explicit residual at its end).  The vectors are permuted once into tree order and
+// every Krylov vector ((restart + 1) x ks x N doubles) stays in HBM; orthogonalisation
+// is CGS2 on the device.  rhs / x: device, original order, block b at b * N.
+// Returns the total step count (negative if not converged); hist gets the relative
+// residual estimate after every step.
+int Operator::blockSolveDev(const double* rhs, double* x, int restart, double tol, int maxit, double* hist,
+                            int maxhist, double* relresOut, hipStream_t s) {
+    if (plan.nranks != 1) throw std::logic_error("block solve on a sharded handle");
+    if (!coeffSet) throw std::runtime_error("block solve before setCoeff");
+    for (int m = 0; m < kernelSize; ++m)
+        if (!modes[m].ready) throw std::runtime_error("block solve before cache(" + std::to_string(m) + ")");
+    if (restart < 1 || maxit < 1 || !(tol > 0.0)) throw std::invalid_argument("block solve needs restart >= 1, maxit >= 1, tol > 0");
+    ensureDevice();
+    checkDeviceErrors();
+    const int64_t N = geo.N, L = (int64_t)ks * N;
+    const int m = restart;
+    DevBuf bB, bX, bW, bR, bV, bPart, bH, bY;
+    bB.alloc(L * sizeof(double));
+    bX.alloc(L * sizeof(double));
+    bW.alloc(L * sizeof(double));
+    bR.alloc(L * sizeof(double));
+    bV.alloc((size_t)(m + 1) * L * sizeof(double));
+    bPart.alloc((size_t)kMdotBlocks * (m + 2) * sizeof(double));
+    bH.alloc((size_t)(m + 2) * sizeof(double));  // Hessenberg column (m + 1 entries), then ||w||^2
+    bY.alloc((size_t)(m + 1) * sizeof(double));
+    double *b = bB.as<double>(), *xt = bX.as<double>(), *w = bW.as<double>(), *r = bR.as<double>();
+    double* V = bV.as<double>();
+    double* hd = bH.as<double>();
+    const int* perm = dPerm.as<int>();
+    for (int k = 0; k < ks; ++k) {  // tree order: the operator needs no permutation gathers
+        launch_permute(N, perm, rhs + (size_t)k * N, b + (size_t)k * N, s);
+        launch_permute(N, perm, x + (size_t)k * N, xt + (size_t)k * N, s);
+    }
+    Krylov kr{L, s, bPart.as<double>()};
+    auto norm2 = [&](const double* v) {  // ||v||^2 into hd[m + 1], returned on the host
+        kr.mdot(1, v, L, v, hd + m + 1, false);
+        double h = 0;
+        HIP_CHECK(hipMemcpyAsync(&h, hd + m + 1, sizeof(double), hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        return h;
+    };
+    auto residual = [&] {  // r = b - A x
+        blockOpDev(2, xt, N, w, N, true, s);
+        k_sub<<<nblk(L), 256, 0, s>>>(L, b, w, r);
+        return std::sqrt(norm2(r));
+    };
+    const double normb = std::sqrt(norm2(b));
+    int nh = 0, total = 0;
+    double relres = 0.0;
+    bool conv = false;
+    if (normb == 0.0) {
+        HIP_CHECK(hipMemsetAsync(xt, 0, L * sizeof(double), s));
+        conv = true;
+    } else {
+        double beta = residual();
+        relres = beta / normb;
+        conv = relres <= tol;
+        const int ld = m + 1;
+        std::vector<double> H((size_t)ld * m, 0.0), g(ld, 0.0), cs(m, 0.0), sn(m, 0.0), hc(m + 2), y(m);
+        for (int cyc = 0; cyc < maxit && !conv; ++cyc) {
+            if (beta == 0.0) break;
+            k_scale<<<nblk(L), 256, 0, s>>>(L, 1.0 / beta, r, V);
+            std::fill(g.begin(), g.end(), 0.0);
+            g[0] = beta;
+            int used = 0;
+            for (int i = 0; i < m; ++i) {
+                double* vi = V + (size_t)i * L;
+                blockOpDev(2, vi, N, w, N, true, s);
+                // CGS2: h = V^T w, w -= V h, twice (the second pass adds its correction)
+                kr.mdot(i + 1, V, L, w, hd, false);
+                kr.maxpy(i + 1, V, L, hd, -1.0, w);
+                kr.mdot(i + 1, V, L, w, bY.as<double>(), false);
+                kr.maxpy(i + 1, V, L, bY.as<double>(), -1.0, w);
+                k_axpby<<<nblk(i + 1), 256, 0, s>>>(i + 1, 1.0, bY.as<double>(), 1.0, hd);
+                kr.mdot(1, w, L, w, hd + m + 1, false);
+                k_scale_rsqrt<<<nblk(L), 256, 0, s>>>(L, w, hd + m + 1, V + (size_t)(i + 1) * L);
+                HIP_CHECK(hipMemcpyAsync(hc.data(), hd, (size_t)(m + 2) * sizeof(double), hipMemcpyDeviceToHost, s));
+                HIP_CHECK(hipStreamSynchronize(s));
+                double* Hc = H.data() + (size_t)i * ld;
+                for (int k = 0; k <= i; ++k) Hc[k] = hc[k];
+                Hc[i + 1] = std::sqrt(std::max(hc[m + 1], 0.0));
+                for (int k = 0; k < i; ++k) {  // the previous rotations
+                    const double t = cs[k] * Hc[k] + sn[k] * Hc[k + 1];
+                    Hc[k + 1] = -sn[k] * Hc[k] + cs[k] * Hc[k + 1];
+                    Hc[k] = t;
+                }
+                const double den = std::hypot(Hc[i], Hc[i + 1]);
+                cs[i] = den == 0.0 ? 1.0 : Hc[i] / den;
+                sn[i] = den == 0.0 ? 0.0 : Hc[i + 1] / den;
+                Hc[i] = den;
+                Hc[i + 1] = 0.0;
+                g[i + 1] = -sn[i] * g[i];
+                g[i] = cs[i] * g[i];
+                ++total;
+                used = i + 1;
+                relres = std::fabs(g[i + 1]) / normb;
+                if (hist && nh < maxhist) hist[nh++] = relres;
+                if (relres <= tol || hc[m + 1] <= 0.0) break;  // converged (estimate) or lucky breakdown
+            }
+            // x += V y, H y = g (upper triangular)
+            for (int k = used - 1; k >= 0; --k) {
+                double t = g[k];
+                for (int j = k + 1; j < used; ++j) t -= H[(size_t)j * ld + k] * y[j];
+                y[k] = H[(size_t)k * ld + k] != 0.0 ? t / H[(size_t)k * ld + k] : 0.0;
+            }
+            HIP_CHECK(hipMemcpyAsync(bY.p, y.data(), (size_t)used * sizeof(double), hipMemcpyHostToDevice, s));
+            kr.maxpy(used, V, L, bY.as<double>(), 1.0, xt);
+            beta = residual();
+            relres = beta / normb;
+            conv = relres <= tol;
+        }
+    }
+    for (int k = 0; k < ks; ++k)
+        k_unpermute<<<nblk(N), 256, 0, s>>>(N, perm, xt + (size_t)k * N, x + (size_t)k * N);
+    HIP_CHECK(hipStreamSynchronize(s));
+    checkDeviceErrors();
+    if (relresOut) *relresOut = relres;
+    return conv ? total : -std::max(total, 1);
+}
+
+// the same on host pointers (the MEX shim's 'solve' op): one staging copy each way
+int Operator::blockSolveHost(const double* rhs, double* x, int restart, double tol, int maxit, double* hist,
+                             int maxhist, double* relres) {
+    ensureDevice();
+    const size_t bytes = (size_t)ks * geo.N * sizeof(double);
+    DevBuf db, dx;
+    db.alloc(bytes);
+    dx.alloc(bytes);
+    HIP_CHECK(hipMemcpyAsync(db.p, rhs, bytes, hipMemcpyHostToDevice, own));
+    HIP_CHECK(hipMemcpyAsync(dx.p, x, bytes, hipMemcpyHostToDevice, own));
+    const int it = blockSolveDev(db.as<double>(), dx.as<double>(), restart, tol, maxit, hist, maxhist, relres, own);
+    HIP_CHECK(hipMemcpyAsync(x, dx.p, bytes, hipMemcpyDeviceToHost, own));
+    HIP_CHECK(hipStreamSynchronize(own));
+    return it;
 }
 
 }  // namespace aniso

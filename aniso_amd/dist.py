@@ -13,19 +13,10 @@ targets.  Per apply (ShardExchange, the multi-GPU GMRES matvec of bench.py):
    M2L and the down pass, writing the owned slice of the next iterate in place;
 4. ONE all-to-all sends every rank the halo of the next iterate from its owners.
 
-The older replicated scheme (whole input on every rank, full up pass, all-gather of
-the output slices: gather_index / block_gather_index / assemble_from_gathered) is
-kept for the original-order and single-phase tests.
+GMRES over the shards (aniso_amd.solve.gmres_dist) adds two all-reduces of its
+inner products per Arnoldi step (ShardExchange.allreduce).
 """
 import numpy as np
-
-
-def _is_torch(x):
-    try:
-        import torch
-    except ImportError:
-        return False
-    return isinstance(x, torch.Tensor)
 
 
 def shard_ranges(op, nranks):
@@ -33,57 +24,6 @@ def shard_ranges(op, nranks):
     changing the handle's shard or caches (aniso_shard_cuts)."""
     c = op.shard_cuts(nranks)
     return [(int(c[r]), int(c[r + 1])) for r in range(nranks)]
-
-
-def pad_len(ranges):
-    return max(e - b for b, e in ranges) if ranges else 0
-
-
-def assemble_from_gathered(gathered, ranges, perm, out=None):
-    """gathered: (nranks, L) tree-ordered slices (numpy or torch); returns the
-    original-order vector out[perm[k]] = tree[k]."""
-    if _is_torch(gathered):
-        import torch
-
-        parts = [gathered[r, : e - b] for r, (b, e) in enumerate(ranges)]
-        tree = torch.cat(parts)
-        if out is None:
-            out = torch.empty_like(tree)
-        out[perm] = tree
-        return out
-    tree = np.concatenate([gathered[r, : e - b] for r, (b, e) in enumerate(ranges)])
-    if out is None:
-        out = np.empty_like(tree)
-    out[perm] = tree
-    return out
-
-
-def local_slice(full_orig, perm, rng, L):
-    """Tree-order slice of this rank's owned targets, padded to length L."""
-    b, e = rng
-    if _is_torch(full_orig):
-        import torch
-
-        buf = torch.zeros(L, dtype=full_orig.dtype, device=full_orig.device)
-        buf[: e - b] = full_orig[perm[b:e]]
-        return buf
-    buf = np.zeros(L, dtype=full_orig.dtype)
-    buf[: e - b] = full_orig[perm[b:e]]
-    return buf
-
-
-def gather_index(ranges, L):
-    """Positions in the flattened (nranks, L) all-gather buffer of tree positions
-    0 .. N-1: tree[k] = gathered.reshape(-1)[idx[k]]."""
-    return np.concatenate([r * L + np.arange(e - b, dtype=np.int64) for r, (b, e) in enumerate(ranges)])
-
-
-def block_gather_index(ranges, L, nb):
-    """Positions in the flattened (nranks, nb, L) all-gather buffer of the block
-    vector (nb, N) in tree order: y.reshape(-1)[b * N + k] = gathered.reshape(-1)[idx]."""
-    g = gather_index(ranges, L)
-    r, off = g // L, g % L
-    return np.concatenate([r * nb * L + b * L + off for b in range(nb)])
 
 
 def _intersect(ranges, b, e):
@@ -169,3 +109,34 @@ class ShardExchange:
 
     def halo_bytes(self):
         return 8 * sum(self.out_splits)
+
+    def allreduce(self, t):
+        """Sum a small float64 tensor over the ranks in place (GMRES inner products,
+        aniso_amd.solve.gmres_dist: two per Arnoldi step)."""
+        if self.backend == "nccl":
+            self.dist.all_reduce(t)
+            return t
+        c = t.cpu()
+        self.dist.all_reduce(c)
+        t.copy_(c)
+        return t
+
+
+def sharded_block_matvec(op, xchg, which=2):
+    """apply(x, y) for aniso_amd.solve.gmres_dist on one rank's owned slices: x, y
+    are (nb, n_own) tree-order slices of the iterate.  The slice is placed into a
+    full-length work vector whose halo the all-to-all then fills from its owners;
+    phase 1, the root all-gather and phase 2 write y (x - mforward(x) for which = 2)."""
+    import torch
+
+    ob, oe = xchg.own
+    full = torch.zeros(xchg.nb, op.N, dtype=torch.float64, device=xchg.roots_send.device)
+
+    def apply(x, y):
+        full[:, ob:oe] = x
+        xchg.halo(full)
+        op.block_op_begin_dev(which, full, y, xchg.roots_send)
+        xchg.roots_allgather()
+        op.block_op_end_dev(which, full, y, xchg.roots_recv, xchg.world)
+
+    return apply

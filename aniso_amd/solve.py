@@ -209,3 +209,94 @@ def gmres_mixed(op, B, tol=1e-12, m=40, inner_tol=1e-6, max_outer=30, max_cycles
             X += D
         inner += its
     return X, max_outer, inner, rel
+
+
+def gmres_dist(apply, b, restart=400, tol=1e-11, maxit=400, x0=None, allreduce=None, hist=None):
+    """Restarted GMRES with MATLAB's semantics (aniso.m:159-173: gmres(A, rhs, restart,
+    tol, maxit); the Arnoldi/Givens structure of gmres.cpp:53-169) on vectors that may
+    be row slices of a sharded problem.
+
+    apply(x, y): y = A x on this rank's slice (the caller's operator does its own
+    exchanges: the sharded block matvec's halo all-to-all and root all-gather).
+    allreduce(t): sums a small float64 tensor over the ranks in place (None: one rank).
+    Orthogonalisation is classical Gram-Schmidt with one reorthogonalisation (CGS2):
+    each Arnoldi step reduces its inner products in TWO all-reduces -- [V^T w] and
+    [V^T w', w'.w'] -- instead of the j + 1 dependent reductions of modified
+    Gram-Schmidt (gmres.cpp:116-120), which would put j latency-bound collectives
+    on every step.  Converged when ||b - A x|| / ||b|| <= tol (the estimate inside a
+    cycle, confirmed by the explicit residual at its end).
+
+    Returns (x, total steps (negative if not converged), final relative residual).
+    hist (a list) receives the estimate after every step."""
+    import torch
+
+    red = allreduce or (lambda t: t)
+    x = torch.zeros_like(b) if x0 is None else x0.clone()
+    w = torch.empty_like(b)
+    n = b.numel()
+
+    def nrm(v):
+        t = (v.reshape(-1) @ v.reshape(-1)).reshape(1)
+        red(t)
+        return float(t.sqrt())
+
+    def residual():
+        apply(x, w)
+        return b - w
+
+    normb = nrm(b)
+    if normb == 0.0:
+        return torch.zeros_like(b), 0, 0.0
+    r = residual()
+    beta = nrm(r)
+    relres = beta / normb
+    total = 0
+    m = restart
+    V = torch.empty((m + 1, n), dtype=b.dtype, device=b.device)
+    for _ in range(maxit):
+        if relres <= tol or beta == 0.0:
+            break
+        V[0] = r.reshape(-1) / beta
+        H = np.zeros((m + 1, m))
+        cs, sn, g = np.zeros(m), np.zeros(m), np.zeros(m + 1)
+        g[0] = beta
+        used = 0
+        for i in range(m):
+            apply(V[i].view_as(b), w)
+            wv = w.reshape(-1).clone()
+            Vi = V[: i + 1]
+            h = Vi @ wv
+            red(h)
+            wv -= Vi.t() @ h
+            h2 = torch.cat([Vi @ wv, (wv @ wv).reshape(1)])
+            red(h2)
+            wv -= Vi.t() @ h2[: i + 1]
+            h = (h + h2[: i + 1]).cpu().numpy()
+            hn = float(max(h2[i + 1] - h2[: i + 1] @ h2[: i + 1], 0.0)) ** 0.5
+            H[: i + 1, i] = h
+            H[i + 1, i] = hn
+            V[i + 1] = wv / hn if hn > 0 else 0.0
+            for k in range(i):  # the previous rotations (gmres.cpp:136-139)
+                t = cs[k] * H[k, i] + sn[k] * H[k + 1, i]
+                H[k + 1, i] = -sn[k] * H[k, i] + cs[k] * H[k + 1, i]
+                H[k, i] = t
+            den = np.hypot(H[i, i], H[i + 1, i])
+            cs[i], sn[i] = (1.0, 0.0) if den == 0 else (H[i, i] / den, H[i + 1, i] / den)
+            H[i, i], H[i + 1, i] = den, 0.0
+            g[i + 1] = -sn[i] * g[i]
+            g[i] = cs[i] * g[i]
+            total += 1
+            used = i + 1
+            relres = abs(g[i + 1]) / normb
+            if hist is not None:
+                hist.append(relres)
+            if relres <= tol or hn == 0.0:
+                break
+        y = np.zeros(used)
+        for k in range(used - 1, -1, -1):
+            y[k] = (g[k] - H[k, k + 1:used] @ y[k + 1:]) / H[k, k] if H[k, k] != 0 else 0.0
+        x += (V[:used].t() @ torch.tensor(y, dtype=b.dtype, device=b.device)).view_as(b)
+        r = residual()
+        beta = nrm(r)
+        relres = beta / normb
+    return x, (total if relres <= tol else -max(total, 1)), relres

@@ -27,8 +27,9 @@ Also reported on the same JSON line:
                 tiers, k_top_m2l_hc, one launch per matvec) and of the near-field sweep,
                 timed with HIP events
                 on the streams they run on over the timed region;
-  cpu_baseline  the CPU oracle (a faithful port of the reference apply) on this
-                host's cores at the full workload size (modes 0 and 1);
+  cpu_baseline  the CPU oracle (a faithful port of the reference apply, timed with
+                the reference's per-use heap traffic repeated) on this host's cores at
+                the full workload size (modes 0 and 1);
   rel_err_vs_cpu  GPU vs CPU oracle on those inputs, plus the 45-term block
                 composition at sz=256;
   mode0_matvec_per_s, deterministic_matvec_per_s  secondary legs on the same
@@ -129,10 +130,20 @@ def cpu_baseline(args, coeffs, op, block_check):
     per-apply tree rebuild) timed on this host at the FULL workload size: one mode
     cached at a time (the reference caches all 9: ~190 GB at 1M points), modes 0
     and 1 (an even and an odd mode; every mode streams the same caches), one warm-up
-    and >= 3 timed applies each.  One block matvec = ks (2 ks - 1) = 45 mode-applies
-    (aniso.m's loop).  The same inputs go through the HIP path (op.mapping, host
-    pointers) for rel_err per mode at full size.  block_check(sz) runs the 45-term
-    composition x - mforward(x) against the oracle at sz (default 256).
+    and --cpu-reps timed applies each in two timing modes on the same caches:
+      reference_alloc -- the oracle repeats the reference's per-use heap traffic
+        (oracle_set_reference_alloc: Vector load(d^2) + ddot per Duffy point,
+        KernelFactory.cpp:847-855; two Vectors per target and neighbour,
+        :684-685; the cached block deep-copied per use, bbfmm.h:1053).  On the d = 1
+        aniso.m geometry this reproduces the reference's recorded rate (sz = 256:
+        2.14 vs 2.19 mode-applies/s at 8 threads, profiles/r03_calibration_refalloc.log),
+        so it is the reported baseline;
+      port -- the same arithmetic without that heap traffic (5-8x faster than the
+        reference's record on d = 1; within 8 % of it on the d = 3 cases).
+    One block matvec = ks (2 ks - 1) = 45 mode-applies (aniso.m's loop).  The same
+    inputs go through the HIP path (op.mapping, host pointers) for rel_err per mode
+    at full size.  block_check(sz) runs the 45-term composition x - mforward(x)
+    against the oracle at sz (default 256).
     Returns (baseline dict, {"mode0": err, "mode1": err, "block_sz256": err})."""
     from oracle.oracle_py import Oracle
 
@@ -144,18 +155,22 @@ def cpu_baseline(args, coeffs, op, block_check):
     ss, st = coeffs(xy)
     o.setCoeff(ss, st)
     u = gaussian(xy) * ss + np.random.default_rng(3).uniform(-0.1, 0.1, o.N)
-    per_mode, t_cache, errs = {}, 0.0, {}
+    per_mode, port_mode, t_cache, errs = {}, {}, 0.0, {}
     for m in modes:
         t0 = time.time()
         o.cache(m)
         t_cache += time.time() - t0
+        o.set_reference_alloc(False)
         ref = o.mapping(u, m)  # warm-up (and the check's reference)
-        ts = []
-        while len(ts) < args.cpu_reps:
-            t1 = time.perf_counter()
-            o.mapping(u, m)
-            ts.append(time.perf_counter() - t1)
-        per_mode[m] = float(np.median(ts))
+        for alloc, dst in ((False, port_mode), (True, per_mode)):
+            o.set_reference_alloc(alloc)
+            ts = []
+            while len(ts) < args.cpu_reps:
+                t1 = time.perf_counter()
+                o.mapping(u, m)
+                ts.append(time.perf_counter() - t1)
+            dst[m] = float(np.median(ts))
+        o.set_reference_alloc(False)
         o.uncache(m)
         got = op.mapping(u, m)
         errs[f"mode{m}"] = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
@@ -163,6 +178,7 @@ def cpu_baseline(args, coeffs, op, block_check):
     if block:
         errs["block_sz256"] = block_check(args.cpu_check_sz)
     t_apply = float(np.mean(list(per_mode.values())))
+    t_port = float(np.mean(list(port_mode.values())))
     per_matvec = ks * (2 * ks - 1) if block else 1  # aniso.m's loop: ks x (2ks-1) mapping calls per mforward
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {
@@ -170,13 +186,17 @@ def cpu_baseline(args, coeffs, op, block_check):
         "unit": "matvec/s",
         "cores": cores,
         "kind": "port",
+        "timing_mode": "reference_alloc",
         "cpu_model": cpu_model(),
-        "sample": (f"oracle mode-apply at the full workload size N={o.N} (tree rebuilt per apply as in the reference), "
-                   f"modes {modes} one cached at a time, median of {args.cpu_reps} applies each after a warm-up: "
+        "sample": (f"oracle mode-apply at the full workload size N={o.N} (tree rebuilt per apply as in the reference, "
+                   f"the reference's per-use heap vectors and block copies repeated), modes {modes} one cached at a "
+                   f"time, median of {args.cpu_reps} applies each after a warm-up: "
                    + ", ".join(f"mode {m} {t * 1e3:.0f} ms" for m, t in per_mode.items())
                    + f"; one matvec = {per_matvec} mode-applies (the reference's loop); cache build {t_cache:.1f} s "
                    f"not timed; OMP threads={cores}"),
         "mode_apply_s": {str(m): round(t, 4) for m, t in per_mode.items()},
+        "port_value": 1.0 / (per_matvec * t_port),
+        "port_mode_apply_s": {str(m): round(t, 4) for m, t in port_mode.items()},
     }, errs
 
 
@@ -192,7 +212,8 @@ def main():
     ap.add_argument("--ks", type=int, default=5)
     ap.add_argument("--g", type=float, default=0.8)
     ap.add_argument("--max-level", type=int, default=20)
-    ap.add_argument("--cpu-reps", type=int, default=3, help="timed oracle applies per mode (after one warm-up)")
+    ap.add_argument("--cpu-reps", type=int, default=2,
+                    help="timed oracle applies per mode and timing mode (after one warm-up)")
     ap.add_argument("--cpu-check-sz", type=int, default=256, help="sz of the 45-term block composition check")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -200,6 +221,9 @@ def main():
     ap.add_argument("--same-device", action="store_true",
                     help="all ranks on cuda:0 (rehearse the sharded path on a one-GPU box; use --backend gloo)")
     ap.add_argument("--verify", action="store_true", help="check the sharded matvec against an unsharded operator")
+    ap.add_argument("--gmres", type=int, default=30,
+                    help="steps of the GMRES leg (aniso_amd.solve.gmres_dist over this run's matvec; 0: skip)")
+    ap.add_argument("--no-solve", action="store_true", help="skip the one-GPU aniso.m solve (aniso_block_solve)")
     args = ap.parse_args()
 
     import torch
@@ -414,6 +438,43 @@ def main():
         line["exchange"] = {"root_allgather_bytes_per_rank": 8 * xchg.C * xchg.R,
                             "halo_bytes_received": xchg.halo_bytes(), "backend": args.backend}
     line.update(sec)  # mode-0 operator and deterministic block matvec (measured before the headline leg)
+    if args.gmres > 0 and block:
+        # GMRES over this run's (possibly sharded) block matvec: aniso_amd.solve.gmres_dist,
+        # CGS2 with two all-reduces of its inner products per step, one cycle of exactly
+        # --gmres steps (tol 0); the initial and final residuals add two matvecs
+        from aniso_amd.solve import gmres_dist
+
+        rhs0 = torch.zeros(nb, N, dtype=torch.float64, device="cuda")
+        rhs0[0] = torch.tensor(gaussian(xy), device="cuda")[perm]
+        if world == 1:
+            gb = rhs0
+
+            def gapply(x, y):
+                op.block_op_dev(2, x, y, tree=True)
+            gred = None
+        else:
+            gb = rhs0[:, ob:oe].contiguous()
+            gapply = adist.sharded_block_matvec(op, xchg)
+            gred = xchg.allreduce
+        gmres_dist(gapply, gb, restart=2, tol=0.0, maxit=1, allreduce=gred)  # warm-up
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        _, _, grel = gmres_dist(gapply, gb, restart=args.gmres, tol=0.0, maxit=1, allreduce=gred)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        gel = time.perf_counter() - tg
+        if world > 1:
+            t = torch.tensor([gel], device="cuda", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            gel = float(t.item())
+        line["gmres"] = {"steps": args.gmres, "steps_per_s": round(args.gmres / gel, 3),
+                         "ms_per_step": round(1e3 * gel / args.gmres, 4), "matvecs": args.gmres + 2,
+                         "relres_after": grel,
+                         "method": "aniso_amd.solve.gmres_dist: restarted GMRES, CGS2 (2 all-reduces per step), "
+                                   "Krylov basis in HBM; tol 0 so exactly `steps` Arnoldi steps are timed"}
     if args.verify:
         # one matvec of a fixed block vector through this (possibly sharded) path vs
         # an unsharded operator on the same device
@@ -445,6 +506,22 @@ def main():
             dist.all_reduce(sq)
         line["verify_rel_err_vs_unsharded"] = float((sq[0] / sq[1]) ** 0.5)
         del ref_op
+    if world == 1 and block and not args.no_solve:
+        # aniso.m:159-173 as the MATLAB caller runs it: rhs = forward(charge), u = gmres(A,
+        # rhs, 400, 1e-11, 400), A(u) = u - mforward(u), through aniso_block_solve_dev
+        # (Krylov basis of 401 x 5 x N doubles in HBM; wall time incl. its allocation)
+        charge = torch.zeros(nb, N, dtype=torch.float64, device="cuda")
+        charge[0] = torch.tensor(gaussian(xy), device="cuda")
+        rhs = torch.zeros_like(charge)
+        op.block_op_dev(0, charge, rhs)
+        u = torch.zeros_like(charge)
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        its, shist, srel = op.block_solve_dev(rhs, u, 400, 1e-11, 400)
+        sel = time.perf_counter() - ts
+        line["block_solve"] = {"call": "gmres(A, rhs, 400, 1e-11, 400), A(u) = u - mforward(u) (aniso.m:159-173)",
+                               "iterations": its, "relres": srel, "seconds": round(sel, 4),
+                               "ms_per_iteration": round(1e3 * sel / max(abs(its), 1), 4)}
     if rank == 0 and world == 1 and not args.no_cpu:
         def block_check(sz):
             """x - mforward(x) (aniso.m:155) at sz: HIP harmonic block apply vs the

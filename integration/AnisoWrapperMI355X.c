@@ -13,6 +13,9 @@
  *   theta = AnisoWrapperMI355X('mapping', h, charge, id);
  * and aniso.m's GMRES operator (aniso.m:155) becomes one call per matvec:
  *   A = @(x) AnisoWrapperMI355X('blockMatvec', h, x);   % x - mforward(x), x = [u_0; ...; u_{ks-1}]
+ * and aniso.m:159-173's solve, gmres(A, rhs, 400, 1e-11, 400), as one call with the
+ * Krylov basis resident on the GPU:
+ *   [u, relres, iters] = AnisoWrapperMI355X('solve', h, rhs, 400, 1e-11, 400);
  *
  * MATLAB is absent from this image and from the GPU box: tests/test_integration.py
  * compiles this file for syntax against a declaration-only mex.h (tests/mex_stub).
@@ -70,7 +73,6 @@ static const double* column(const mxArray* a, int64_t n, const char* what) {
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     char op[32];
-    (void)nlhs;
     if (nrhs < 1 || mxGetString(prhs[0], op, sizeof op))
         mexErrMsgIdAndTxt("mexplus:dispatch:argumentError", "first argument must be the operation name");
     if (!strcmp(op, "new")) { /* AnisoWrapper.cpp:10-25: (sz, d, ks, g, ns, np, maxLevel) */
@@ -124,6 +126,24 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         u = column(prhs[2], len, "u"); /* the stacked column [u_0; ...; u_{ks-1}], exactly ks * N */
         plhs[0] = mxCreateDoubleMatrix((size_t)len, 1, mxREAL);
         CALL(aniso_block_op(h, which, u, mxGetPr(plhs[0])));
+    } else if (!strcmp(op, "solve")) {
+        /* aniso.m:159-173 in one call: [u, relres, iters] = ('solve', h, rhs, restart, tol, maxit)
+         * = gmres(@(x) x - mforward(x), rhs, restart, tol, maxit) with every Krylov
+         * vector in HBM (MATLAB's call: restart 400, tol 1e-11, maxit 400) */
+        aniso_handle h;
+        int64_t len;
+        const double* rhs;
+        int iters = 0;
+        double relres = 0.0;
+        need(nrhs, 6, op);
+        h = handle_of(prhs[1]);
+        len = num_blocks(h) * num_nodes(h);
+        rhs = column(prhs[2], len, "rhs");
+        plhs[0] = mxCreateDoubleMatrix((size_t)len, 1, mxREAL); /* zeros: MATLAB's default x0 */
+        CALL(aniso_block_solve(h, rhs, mxGetPr(plhs[0]), (int)mxGetScalar(prhs[3]), mxGetScalar(prhs[4]),
+                               (int)mxGetScalar(prhs[5]), NULL, 0, &iters, &relres));
+        if (nlhs > 1) plhs[1] = mxCreateDoubleScalar(relres);
+        if (nlhs > 2) plhs[2] = mxCreateDoubleScalar((double)iters);
     } else {
         mexErrMsgIdAndTxt("mexplus:dispatch:argumentError", "Unknown operation %s", op);
     }

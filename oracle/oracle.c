@@ -350,6 +350,7 @@ struct oracle {
     double **nearI; /* [mode] N*9*nref */
     double **singI; /* [mode] N*nsing */
     int faithful;
+    int refalloc; /* timing mode: the reference's per-use heap vectors (oracle_set_reference_alloc) */
 };
 
 /* makeLegendreMatrix (Geometry.cpp:129-154); K is rows x cols col-major */
@@ -496,6 +497,34 @@ void oracle_destroy(oracle_t *o) {
 int64_t oracle_num_nodes(oracle_t *o) { return o->N; }
 int oracle_refine_size(oracle_t *o) { return o->nref; }
 void oracle_set_faithful_rebuild(oracle_t *o, int on) { o->faithful = on; }
+/* Timing mode (results unchanged): repeat the reference's per-use heap traffic on the
+ * apply path -- the cached block deep-copied on every use (K = Cache[rootId][cnt],
+ * bbfmm.h:1053, Matrix::operator= linalg.h:213-237), the two Vectors per target and
+ * neighbour of refineAddOnFast (KernelFactory.cpp:684-685) and the Vector load(d^2) +
+ * ddot per Duffy point of singularAddFast (KernelFactory.cpp:847-855). */
+void oracle_set_reference_alloc(oracle_t *o, int on) { o->refalloc = on; }
+
+/* the reference's Vector(n): new scalar_t[n] + memset (linalg.h:20-27) */
+static double *ref_vector(int n) {
+    double *v = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    if (!v) { fprintf(stderr, "oracle: out of memory\n"); abort(); }
+    memset(v, 0, sizeof(double) * (size_t)n);
+    return v;
+}
+/* cblas_ddot as a call the compiler cannot inline into the loop (blas_wrapper.cpp) */
+__attribute__((noinline)) static double ref_ddot(int n, const double *x, const double *y) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += x[i] * y[i];
+    return s;
+}
+/* Matrix::operator= of a cached block (delete[] + new[] + memcpy, linalg.h:213-237) */
+static const double *ref_copy(double **held, const double *K, size_t n) {
+    free(*held);
+    *held = (double *)malloc(sizeof(double) * (n ? n : 1));
+    if (!*held) { fprintf(stderr, "oracle: out of memory\n"); abort(); }
+    memcpy(*held, K, sizeof(double) * n);
+    return *held;
+}
 
 void oracle_get_nodes(oracle_t *o, double *xy) {
     for (int i = 0; i < o->N; ++i) { xy[i] = o->px[i]; xy[i + o->N] = o->py[i]; }
@@ -873,19 +902,22 @@ static void fmm_down(oracle_t *o, fmm_t *f, const double *charge, double *potent
             if (n->level != L) continue;
             double *np_ = f->nodePotential + (size_t)id * rk;
             const double *K = f->cache[id];
+            double *held = NULL;
             for (int pass = 0; pass < 2; ++pass) {
                 ivec *lst = pass == 0 ? &n->V : &n->X;
                 for (int k = 0; k < lst->n; ++k) {
                     if (t->nd[lst->a[k]].isEmpty) continue;
                     const double *sc = f->nodeCharge + (size_t)lst->a[k] * rk;
+                    const double *Ku = o->refalloc ? ref_copy(&held, K, (size_t)rk * rk) : K;
                     for (int a = 0; a < rk; ++a) {
                         double s = 0.0;
-                        for (int b = 0; b < rk; ++b) s += K[a + (size_t)b * rk] * sc[b];
+                        for (int b = 0; b < rk; ++b) s += Ku[a + (size_t)b * rk] * sc[b];
                         np_[a] += s;
                     }
                     K += (size_t)rk * rk;
                 }
             }
+            free(held);
             const double *pp = f->nodePotential + (size_t)n->parent * rk;
             for (int a = 0; a < rk; ++a) {
                 double s = 0.0;
@@ -907,19 +939,22 @@ static void fmm_down(oracle_t *o, fmm_t *f, const double *charge, double *potent
         }
         int nT = n->nsrc;
         double *pot = (double *)xcalloc(nT, sizeof(double));
+        double *held = NULL;
         for (int pass = 0; pass < 2; ++pass) {
             ivec *lst = pass == 0 ? &n->U : &n->W;
             for (int k = 0; k < lst->n; ++k) {
                 onode *s = &t->nd[lst->a[k]];
                 if (s->isEmpty) continue;
+                const double *Ku = o->refalloc ? ref_copy(&held, K, (size_t)nT * s->nsrc) : K;
                 for (int a = 0; a < nT; ++a) {
                     double acc = 0.0;
-                    for (int b = 0; b < s->nsrc; ++b) acc += K[a + (size_t)b * nT] * charge[s->src[b]];
+                    for (int b = 0; b < s->nsrc; ++b) acc += Ku[a + (size_t)b * nT] * charge[s->src[b]];
                     pot[a] += acc;
                 }
                 K += (size_t)nT * s->nsrc;
             }
         }
+        free(held);
         /* L2T: pot += L * nodePotential (L built like R for targets) */
         double *L = (double *)xcalloc((size_t)nT * rk, sizeof(double));
         leaf_transfer(f, n, t->px, t->py, L);
@@ -1067,14 +1102,23 @@ static void refine_fast(oracle_t *o, int mode, const double *f, double *ret) {
                     if (nsq_ == tsq) continue;
                     if (!(dr + trow >= 0 && dr + trow < sz)) continue;
                     if (!(dc + tcol >= 0 && dc + tcol < sz)) continue;
-                    for (int q = 0; q < d2; ++q) oldv[q] = f[nsq_ * d2 + q] / o->sqrtW[q];
+                    double *ov = oldv, *nv = newv;
+                    if (o->refalloc) {  /* Vector oldValues(d^2), newValues(16 d^2) (KernelFactory.cpp:684-685) */
+                        ov = ref_vector(d2);
+                        nv = ref_vector(nref);
+                    }
+                    for (int q = 0; q < d2; ++q) ov[q] = f[nsq_ * d2 + q] / o->sqrtW[q];
                     for (int r = 0; r < nref; ++r) {
                         double s = 0.0;
-                        for (int c = 0; c < d2; ++c) s += o->nearMap[r + (size_t)c * nref] * oldv[c];
-                        newv[r] = s;
+                        for (int c = 0; c < d2; ++c) s += o->nearMap[r + (size_t)c * nref] * ov[c];
+                        nv[r] = s;
                     }
                     const double *row = C + ((size_t)tid * 9 + (dr + 1) * 3 + (dc + 1)) * nref;
-                    for (int r = 0; r < nref; ++r) ret[tid] += row[r] * newv[r];
+                    for (int r = 0; r < nref; ++r) ret[tid] += row[r] * nv[r];
+                    if (o->refalloc) {
+                        free(ov);
+                        free(nv);
+                    }
                 }
         }
 }
@@ -1094,8 +1138,16 @@ static void singular_fast(oracle_t *o, int mode, const double *coeff, double *re
                 double x = (0.5 + col) * dx + 0.5 * (o->singX[(size_t)tq * ns + p]) * dx;
                 double y = (0.5 + row) * dx + 0.5 * (o->singY[(size_t)tq * ns + p]) * dx;
                 double dot = 0.0;
-                for (int n = 0; n < d; ++n)
-                    for (int k = 0; k < d; ++k) dot += legendre(n, x) * legendre(k, y) / o->lnorm[n * d + k] * cf[n * d + k];
+                if (o->refalloc) {  /* Vector load(d^2), filled, then ddot (KernelFactory.cpp:847-855) */
+                    double *load = ref_vector(d2);
+                    for (int n = 0; n < d; ++n)
+                        for (int k = 0; k < d; ++k) load[n * d + k] = legendre(n, x) * legendre(k, y) / o->lnorm[n * d + k];
+                    dot = ref_ddot(d2, load, cf);
+                    free(load);
+                } else {
+                    for (int n = 0; n < d; ++n)
+                        for (int k = 0; k < d; ++k) dot += legendre(n, x) * legendre(k, y) / o->lnorm[n * d + k] * cf[n * d + k];
+                }
                 ret[tid] += dot * C[(size_t)tid * ns + p];
             }
         }

@@ -47,6 +47,8 @@ void oracle_mapping(oracle_t *o, const double *charge, int id, double *out);
 void oracle_mapping_stages(oracle_t *o, const double *charge, int id, double *stages);
 /* rebuild the FMM trees on every apply like the reference (default 1) */
 void oracle_set_faithful_rebuild(oracle_t *o, int on);
+/* timing mode: the reference's per-use heap vectors and block copies (results unchanged) */
+void oracle_set_reference_alloc(oracle_t *o, int on);
 /* main.cpp:125-141: GMRES(m, maxit, tol) on u - K_0(sigma_s .* u) = K_0 q.
  * x (N) in: initial guess, out: solution.  hist receives up to maxhist residuals.
  * returns the iteration count j at exit (negative if not converged). */

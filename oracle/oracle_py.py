@@ -33,6 +33,7 @@ def lib():
             "oracle_mapping": (None, [P, dp, I, dp]),
             "oracle_mapping_stages": (None, [P, dp, I, dp]),
             "oracle_set_faithful_rebuild": (None, [P, I]),
+            "oracle_set_reference_alloc": (None, [P, I]),
             "oracle_gmres_main": (I, [P, dp, dp, I, I, D, dp, I, dp]),
             "oracle_refine_size": (I, [P]),
             "oracle_get_matrices": (None, [P, dp, dp, dp, dp]),
@@ -113,6 +114,10 @@ class Oracle:
 
     def set_faithful(self, on):
         lib().oracle_set_faithful_rebuild(self.h, int(on))
+
+    def set_reference_alloc(self, on):
+        """Timing mode: the reference's per-use heap Vectors / block copies (same results)."""
+        lib().oracle_set_reference_alloc(self.h, int(on))
 
     def gmres_main(self, q, m=80, maxit=400, tol=1e-12, x0=None):
         q = np.ascontiguousarray(q, dtype=np.float64)

@@ -21,4 +21,5 @@ int mxIsDouble(const mxArray* a);
 int mxIsComplex(const mxArray* a);
 mxArray* mxCreateNumericMatrix(size_t m, size_t n, mxClassID c, mxComplexity f);
 mxArray* mxCreateDoubleMatrix(size_t m, size_t n, mxComplexity f);
+mxArray* mxCreateDoubleScalar(double v);
 #endif

@@ -180,18 +180,17 @@ def test_sharded_apply_composes_to_full(nranks):
     full.mapping_dev(q, 1, ref)
     ranges = adist.shard_ranges(full, nranks)
     perm = torch.tensor(full.tree_perm(), device="cuda", dtype=torch.int64)
-    L = adist.pad_len(ranges)
-    gathered = torch.zeros(nranks, L, dtype=torch.float64, device="cuda")
+    got = torch.zeros_like(q)
     for r in range(nranks):
         sh = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, 20)
         sh.set_shard(r, nranks)
         sh.setCoeff(*coef)
         sh.cache(1)
-        out = torch.zeros_like(q)
-        sh.mapping_dev(q, 1, out)
-        gathered[r] = adist.local_slice(out, perm, ranges[r], L)
+        out = torch.full_like(q, float("nan"))
+        sh.mapping_dev(q, 1, out)  # writes only the shard's own targets (original order)
+        own = perm[ranges[r][0]:ranges[r][1]]
+        got[own] = out[own]
     torch.cuda.synchronize()
-    got = adist.assemble_from_gathered(gathered, ranges, perm)
     assert float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref)) <= 1e-14
 
 
@@ -319,7 +318,7 @@ def test_symmetric_storage_matches_directed(sz, d, ks, ml, monkeypatch):
 def test_tree_order_paths_match_original_order(nranks):
     """aniso_mapping_tree_dev / aniso_forward_tree_dev (tree-order vectors, owned
     slices) against the original-order apply and forward operator, unsharded and
-    composed over shards by the index gather of the padded all-gather buffer."""
+    composed over shards by concatenating their owned tree-order slices."""
     torch = _torch()
     import aniso_amd
     from aniso_amd import dist as adist
@@ -338,22 +337,22 @@ def test_tree_order_paths_match_original_order(nranks):
     reff = torch.zeros_like(q)
     full.forward_dev(q, reff)
     ranges = adist.shard_ranges(full, nranks)
-    L = adist.pad_len(ranges)
-    gidx = torch.tensor(adist.gather_index(ranges, L), device="cuda")
-    g1 = torch.zeros(nranks, L, dtype=torch.float64, device="cuda")
-    gf = torch.zeros(nranks, L, dtype=torch.float64, device="cuda")
     qt = q[perm].contiguous()
+    s1, sf = [], []
     for r in range(nranks):
         sh = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, 20)
         sh.set_shard(r, nranks)
         sh.setCoeff(*coef)
         sh.cache(0)
         sh.cache(1)
-        sh.mapping_tree_dev(qt, 1, g1[r])
-        sh.forward_tree_dev(qt, gf[r])
+        n = ranges[r][1] - ranges[r][0]
+        s1.append(torch.zeros(n, dtype=torch.float64, device="cuda"))
+        sf.append(torch.zeros(n, dtype=torch.float64, device="cuda"))
+        sh.mapping_tree_dev(qt, 1, s1[-1])
+        sh.forward_tree_dev(qt, sf[-1])
         torch.cuda.synchronize()
-    got1 = g1.view(-1)[gidx]
-    gotf = gf.view(-1)[gidx]
+    got1 = torch.cat(s1)
+    gotf = torch.cat(sf)
     assert float(torch.linalg.norm(got1 - ref1[perm]) / torch.linalg.norm(ref1)) <= 1e-14
     assert float(torch.linalg.norm(gotf - reff[perm]) / torch.linalg.norm(reff)) <= 1e-14
 
@@ -595,7 +594,9 @@ def test_harmonic_symmetric_blocks_match_directed(sz, d, ks, monkeypatch):
                                             (40, 1, 5, 3, "1")])
 def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatch):
     """The clustered harmonic M2L (in-cluster V pairs read once by
-    the smaller id, both products, locals summed in LDS) against one wave per target
+    the smaller id, both products, locals summed in LDS) -- with its sources staged in
+    LDS and entries split over 12 waves (k_m2l_cs, the default) and without
+    (k_m2l_hc, ANISO_HM_STAGED=0) -- against one wave per target
     (aniso_set_deterministic); odd sz (non-uniform tree), directed storage, a
     maxLevel-limited tree.  Also checks that in-cluster pairs exist, that the cluster
     plan reads fewer E blocks, and that the deterministic mode repeats bitwise."""
@@ -607,7 +608,8 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatc
     # clusters, which small trees only reach with 4-target clusters: no in-cluster pairs)
     monkeypatch.setenv("ANISO_HM_CLDEPTH", "3")
     outs, st = [], []
-    for det in (False, True):
+    for det, staged in ((False, "1"), (False, "0"), (True, "1")):
+        monkeypatch.setenv("ANISO_HM_STAGED", staged)
         a = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, ml)
         a.set_deterministic(det)
         xy = a.getNodes()
@@ -623,11 +625,37 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatc
             a.block_op_dev(2, U, again)
             torch.cuda.synchronize()
             assert torch.equal(out, again)
-        torch.cuda.synchronize()
+        a.sync()
         outs.append(out.cpu().numpy())
-    assert st[0]["harmonic"] == 1 and st[0]["hm_clusters"] > 0 and st[1]["hm_clusters"] == 0
-    assert st[0]["hm_dual_pairs"] > 0 and st[0]["hm_block_reads"] < st[1]["hm_block_reads"]
-    assert _rel(outs[0], outs[1]) <= 1e-13
+    assert st[0]["staged_m2l"] == 1 and st[1]["staged_m2l"] == 0 and st[2]["staged_m2l"] == 0
+    assert st[0]["harmonic"] == 1 and st[0]["hm_clusters"] > 0 and st[2]["hm_clusters"] == 0
+    assert st[0]["hm_dual_pairs"] > 0 and st[0]["hm_block_reads"] < st[2]["hm_block_reads"]
+    assert _rel(outs[0], outs[2]) <= 1e-13 and _rel(outs[1], outs[2]) <= 1e-13
+
+
+@pytest.mark.parametrize("ks,world", [(5, 8), (2, 4), (3, 3)])
+def test_staged_clusters_on_shards_match_unstaged(ks, world, monkeypatch):
+    """The staged-source M2L on the small clusters of an N-GPU shard (the adaptive
+    depth gives 16-target clusters there) and with padded block counts: every rank's
+    two-phase apply equals the unsharded operator."""
+    torch = _torch()
+    import aniso_amd
+
+    sz = 256
+    full = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
+    xy = full.getNodes()
+    coef = rough_coeffs(xy, 12)
+    full.setCoeff(*coef)
+    for m in range(2 * ks - 1):
+        full.cache(m)
+    X = torch.tensor(np.random.default_rng(ks).uniform(-1, 1, (ks, full.N)), device="cuda")
+    ref = torch.zeros_like(X)
+    full.block_op_dev(2, X, ref, tree=True)
+    torch.cuda.synchronize()
+    del full
+    err, nans, _ = _two_phase_shards(sz, 1, ks, 20, coef, world, X, ref)
+    assert nans == 0
+    assert err <= 1e-13, err
 
 
 def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
@@ -656,7 +684,7 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
     assert float(torch.linalg.norm(o1 - ref) / torch.linalg.norm(ref)) <= 1e-13
 
 
-@pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0"])
+@pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0", "ANISO_HM_STAGED=0"])
 def test_block_matvec_knobs_agree(knob, monkeypatch):
     """Every remaining environment knob of the block apply:
     the serial near/M2L order, the separate x - mforward(x) subtraction and the
@@ -1133,3 +1161,91 @@ def test_block_matvec_sz512_matches_oracle_composition():
     ref = _block_ref_per_mode(o, U, a.g, ss)
     o.close()
     assert _rel(got, ref) <= TOL, _rel(got, ref)
+
+
+def _gmres_matlab(apply, b, restart, tol, maxit):
+    """Restarted GMRES with MATLAB's stopping rule (relative residual <= tol, checked
+    per step on the estimate and confirmed explicitly at each cycle's end), modified
+    Gram-Schmidt, numpy on the host: the reference solve of aniso.m:159-173 over the
+    oracle's operator.  Returns (x, total steps, final relative residual)."""
+    x = np.zeros_like(b)
+    nb = np.linalg.norm(b)
+    r = b - apply(x)
+    beta = np.linalg.norm(r)
+    total = 0
+    for _ in range(maxit):
+        if beta / nb <= tol:
+            break
+        V = np.zeros((restart + 1, b.size))
+        H = np.zeros((restart + 1, restart))
+        V[0] = r / beta
+        g = np.zeros(restart + 1)
+        g[0] = beta
+        cs, sn = np.zeros(restart), np.zeros(restart)
+        used = 0
+        for i in range(restart):
+            w = apply(V[i])
+            for k in range(i + 1):
+                H[k, i] = V[k] @ w
+                w = w - H[k, i] * V[k]
+            H[i + 1, i] = np.linalg.norm(w)
+            V[i + 1] = w / H[i + 1, i]
+            for k in range(i):
+                t = cs[k] * H[k, i] + sn[k] * H[k + 1, i]
+                H[k + 1, i] = -sn[k] * H[k, i] + cs[k] * H[k + 1, i]
+                H[k, i] = t
+            den = np.hypot(H[i, i], H[i + 1, i])
+            cs[i], sn[i] = H[i, i] / den, H[i + 1, i] / den
+            H[i, i], H[i + 1, i] = den, 0.0
+            g[i + 1], g[i] = -sn[i] * g[i], cs[i] * g[i]
+            total += 1
+            used = i + 1
+            if abs(g[i + 1]) / nb <= tol:
+                break
+        y = np.linalg.solve(np.triu(H[:used, :used]), g[:used])
+        x = x + V[:used].T @ y
+        r = b - apply(x)
+        beta = np.linalg.norm(r)
+    return x, total, beta / nb
+
+
+@pytest.mark.parametrize("sz,restart", [(32, 400), (48, 8)])
+def test_block_solve_matches_gmres_over_oracle(sz, restart):
+    """aniso.m:159-173's solve -- rhs = forward(charge), u = gmres(A, rhs, restart,
+    1e-11, 400) with A(u) = u - mforward(u) -- through aniso_block_solve (every Krylov
+    vector in HBM, CGS2 on the device) against the same restarted GMRES over the
+    oracle's 45-call composition (a host MGS restatement with MATLAB's stopping rule)
+    and SciPy's gmres: the same step count as the restatement, solutions within 1e-10,
+    with a restart short enough to cycle (restart 8) and MATLAB's 400."""
+    from scipy.sparse.linalg import LinearOperator, gmres
+
+    _torch()
+    a, o, xy = _pair(sz, 1, 5, 10, 20, "main")
+    ks, ss = 5, main_coeffs(xy)[0]
+    for m in range(2 * ks - 1):
+        a.cache(m)
+        o.cache(m)
+    charge = np.zeros((ks, a.N))
+    charge[0] = gaussian_charge(xy)  # demo.m:24-29: the source in block 0
+    rhs = _block_ref(o, charge, a.g, ss, 0).reshape(-1)
+
+    def A(v):
+        return _block_ref(o, v.reshape(ks, a.N), a.g, ss, 2).reshape(-1)
+
+    tol = 1e-11
+    xr, its_ref, rr_ref = _gmres_matlab(A, rhs, restart, tol, 400)
+    its, u, hist, rr = a.block_solve(rhs, restart, tol, 400)
+    assert its > 0 and rr <= tol and rr_ref <= tol
+    assert its == its_ref, (its, its_ref)
+    assert _rel(u.reshape(-1), xr) <= 1e-10, _rel(u.reshape(-1), xr)
+    assert hist.size == its and hist[-1] <= tol
+    xs, info = gmres(LinearOperator((rhs.size, rhs.size), matvec=A), rhs, rtol=tol, restart=restart, maxiter=400)
+    assert info == 0
+    assert _rel(u.reshape(-1), xs) <= 1e-10, _rel(u.reshape(-1), xs)
+    # the device entry point on the same system, from a nonzero initial guess
+    torch = _torch()
+    rd = torch.tensor(rhs.reshape(ks, a.N), device="cuda")
+    xd = torch.tensor(0.5 * xr.reshape(ks, a.N), device="cuda")
+    its_d, _, rr_d = a.block_solve_dev(rd, xd, restart, tol, 400)
+    assert its_d > 0 and rr_d <= tol
+    assert _rel(xd.cpu().numpy().reshape(-1), xr) <= 1e-10

@@ -1,0 +1,87 @@
+"""Same-process A/B of environment knobs on the 1M-point block matvec (or one rank of
+an N-way shard): one handle per configuration (knobs are read at handle creation),
+timed in interleaved repetitions so box drift hits every configuration alike.
+usage: ab_handles.py [--world W] [--rank R] [--steps S] [--reps P] CFG [CFG ...]
+CFG = "" (defaults) or "ANISO_X=a,ANISO_Y=b"."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import aniso_amd  # noqa: E402
+from bench import demo_coeffs, gaussian  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--world", type=int, default=1)
+ap.add_argument("--rank", type=int, default=0)
+ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--sz", type=int, default=1024)
+ap.add_argument("cfgs", nargs="+")
+args = ap.parse_args()
+world, rank = args.world, args.rank
+runs = []
+for cfg in args.cfgs:
+    kv = [c.split("=", 1) for c in cfg.split(",") if c]
+    saved = {k: os.environ.get(k) for k, _ in kv}
+    for k, v in kv:
+        os.environ[k] = v
+    op = aniso_amd.Aniso(args.sz, 1, 5, 0.8, 10, 4, 20)
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    xy = op.getNodes()
+    perm = torch.tensor(op.tree_perm(), device="cuda", dtype=torch.int64)
+    if world > 1:
+        op.set_shard(rank, world)
+    op.setCoeff(*demo_coeffs(xy))
+    for m in range(9):
+        op.cache(m)
+    b, e = op.shard()
+    ex = op.shard_exchange(5)
+    C, R = ex["root_chunk"], ex["root_record"]
+    x = torch.zeros(5, op.N, dtype=torch.float64, device="cuda")
+    x[0] = torch.tensor(gaussian(xy), device="cuda")[perm]
+    y = torch.zeros_like(x)
+    send = torch.zeros(max(C * R, 1), dtype=torch.float64, device="cuda")
+    recv = torch.zeros(world * max(C * R, 1), dtype=torch.float64, device="cuda")
+    runs.append(dict(cfg=cfg or "default", op=op, x=x, y=y, send=send, recv=recv, b=b, e=e, C=C, R=R, ms=[], st=None))
+
+
+def step(r):
+    op, x, y = r["op"], r["x"], r["y"]
+    if world == 1:
+        op.block_op_dev(2, x, y, tree=True)
+        return
+    b, e, C, R = r["b"], r["e"], r["C"], r["R"]
+    op.block_op_begin_dev(2, x, y[:, b:e], r["send"])
+    r["recv"][rank * C * R:(rank + 1) * C * R].copy_(r["send"][: C * R])  # stands in for the all-gather
+    op.block_op_end_dev(2, x, y[:, b:e], r["recv"], world)
+
+
+for rep in range(args.reps):
+    for r in runs:
+        for _ in range(3):
+            step(r)
+        r["op"].set_timing(rep == args.reps - 1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(r)
+        torch.cuda.synchronize()
+        r["ms"].append(round(1e3 * (time.perf_counter() - t0) / args.steps, 4))
+        if rep == args.reps - 1:
+            r["st"] = {k: round(v, 4) for k, v in r["op"].stage_times().items()}
+            r["op"].set_timing(False)
+        r["op"].sync()
+for r in runs:
+    s = r["op"].stats()
+    print(json.dumps({"cfg": r["cfg"], "world": world, "rank": rank, "ms": r["ms"], "best_ms": min(r["ms"]),
+                      "stage_ms": r["st"], "staged": s["staged_m2l"], "clusters": s["hm_clusters"],
+                      "block_reads": s["hm_block_reads"]}), flush=True)

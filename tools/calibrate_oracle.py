@@ -4,7 +4,9 @@ build of the reference, OpenMP 8 threads on an 8-core Xeon VM, the class of host
 container is).  Times the oracle here with the same thread count on the same
 geometries and prints one JSON line per case with the ratio oracle rate / reference
 rate.  TEST INFRASTRUCTURE: loads oracle/ only.  usage: OMP_NUM_THREADS=8
-python tools/calibrate_oracle.py [--big]"""
+python tools/calibrate_oracle.py [--refalloc]
+(--refalloc: the oracle repeats the reference's per-use heap vectors and block copies,
+oracle_set_reference_alloc; the results are unchanged)"""
 import json
 import os
 import sys
@@ -30,8 +32,10 @@ CASES = [
 def main():
     reps = 3
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    refalloc = "--refalloc" in sys.argv  # the reference's per-use heap vectors (oracle_set_reference_alloc)
     for name, sz, d, ks, g, ns, ml, coeffs, modes, ref_rate, src in CASES:
         o = Oracle(sz, d, ks, g, ns, 4, ml)
+        o.set_reference_alloc(refalloc)
         xy = o.getNodes()
         ss, st = coeffs(xy)
         o.setCoeff(ss, st)
@@ -50,6 +54,7 @@ def main():
         o.close()
         rate = 1.0 / float(np.mean(list(per.values())))
         print(json.dumps({"case": name, "N": sz * sz * d * d, "modes": modes, "threads": threads,
+                          "timing_mode": "reference_alloc" if refalloc else "port",
                           "oracle_apply_s": {str(k): round(v, 4) for k, v in per.items()},
                           "oracle_applies_per_s": round(rate, 3), "reference_applies_per_s": ref_rate,
                           "ratio_oracle_over_reference": round(rate / ref_rate, 2), "reference_source": src,
