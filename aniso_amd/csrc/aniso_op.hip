@@ -72,7 +72,6 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     plan.nearSymmetric = ks == 1;
     if (const char* e = std::getenv("ANISO_NEAR_SYMMETRIC")) plan.nearSymmetric = e[0] == '1';
     plan.maxCanon = ks == 1 ? kMaxCanon : kMaxCanonBlock;
-    if (const char* e = std::getenv("ANISO_CS_WAVES")) plan.csWaves = std::atoi(e) == 4 ? 4 : 12;
     plan.build(tree, np, 0, 1);
     plan.buildExchange(tree, geo.sz, geo.d2);
     plan.buildTopWait(tree);
@@ -82,7 +81,6 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_HARMONIC")) useAtt = useAtt && e[0] != '0';
     if (const char* e = std::getenv("ANISO_OVERLAP")) overlap = std::atoi(e);
     if (const char* e = std::getenv("ANISO_FUSE_SUB")) fuseSub = e[0] != '0';
-    if (const char* e = std::getenv("ANISO_HM_STAGED")) useStaged = e[0] != '0';
     if (const char* e = std::getenv("ANISO_TOP_SPIN_LIMIT")) topSpinLimit = (unsigned)std::strtoul(e, nullptr, 10);
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
@@ -280,11 +278,6 @@ void Operator::uploadPlan() {
         up(dHmSlot, plan.hmSlot);
         up(dHmNDir, plan.hmNDir);
         up(dHmClWait, plan.hmClWait);
-        up(dCsRow, plan.csRow);
-        up(dCsSelf, plan.csSelf);
-        up(dCsRowPtr, plan.csRowPtr);
-        up(dCsRowNode, plan.csRowNode);
-        up(dCsCut, plan.csCut);
         dTopCnt.alloc((kMaxTopTiers + 1) * sizeof(unsigned));
         attReady = false;
     }
@@ -761,15 +754,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         if (fork) HIP_CHECK(hipEventRecord(evJoin, side));
     };
     const bool clustered = harmonic && useClusters;
-    const bool staged = clustered && stagedOn(K);
     const int ncl = (int)plan.hmClPtr.size() - 1;
-    auto csArgs = [&] {
-        return CsArgs{dHmClPtr.as<int>(), dHmTgt.as<int>(), dHmPtr.as<int64_t>(), dHmNDir.as<int>(),
-                      dHmBlk.as<int>(), dHmSlot.as<int>(), dCsRow.as<uint16_t>(), dCsSelf.as<uint16_t>(),
-                      dCsRowPtr.as<int>(), dCsRowNode.as<int>(), dCsCut.as<int64_t>(), plan.csWaves,
-                      dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
-                      dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>()};
-    };
     auto m2lClusters = [&](int c0, int c1, hipStream_t st) {
         launch_m2l_hc(K, c1 - c0, plan.hmMaxCl, dHmClPtr.as<int>() + c0, dHmTgt.as<int>(), dHmPtr.as<int64_t>(),
                       dHmNDir.as<int>(), dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(), dAttM2L.as<double>(),
@@ -845,17 +830,11 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             ta.recv1 = phase == 2 ? rootsRecv : nullptr;
             ta.spinLimit = topSpinLimit;
             HIP_CHECK(hipHostGetDevicePointer((void**)&ta.err, topErr, 0));
-            if (staged) {
-                launch_top_m2l_cs(K, ncl, plan.hmMaxCl, plan.csMaxRows, ua, ta, csArgs(), s);
-            } else {
-                const HcArgs ha{dHmClPtr.as<int>(), dHmTgt.as<int>(), dHmPtr.as<int64_t>(), dHmNDir.as<int>(),
-                                dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(), dAttM2L.as<double>(),
-                                dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), P, hw,
-                                dMult.as<double>(), dLocal.as<double>()};
-                launch_top_m2l_hc(K, ncl, plan.hmMaxCl, ua, ta, ha, s);
-            }
-        } else if (staged) {
-            launch_m2l_cs(K, ncl, plan.hmMaxCl, plan.csMaxRows, csArgs(), s);
+            const HcArgs ha{dHmClPtr.as<int>(), dHmTgt.as<int>(), dHmPtr.as<int64_t>(), dHmNDir.as<int>(),
+                            dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(), dAttM2L.as<double>(),
+                            dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), P, hw,
+                            dMult.as<double>(), dLocal.as<double>()};
+            launch_top_m2l_hc(K, ncl, plan.hmMaxCl, ua, ta, ha, s);
         } else if (clustered) {
             m2lClusters(0, ncl, s);
         } else if (harmonic) {

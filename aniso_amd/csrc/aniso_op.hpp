@@ -195,14 +195,6 @@ private:
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
     DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
-    DevBuf dCsRow, dCsSelf, dCsRowPtr, dCsRowNode, dCsCut;  // staged-source clusters (k_m2l_cs)
-    bool useStaged = true;  // ANISO_HM_STAGED=0: the clustered M2L without staged sources (k_m2l_hc)
-  public:
-    // the block apply of K right-hand sides runs the staged-source M2L (k_m2l_cs)
-    bool stagedOn(int K) const {
-        return useAtt && useStaged && useClusters && m2l_cs_lds(K, plan.hmMaxCl, plan.csMaxRows) > 0;
-    }
-  private:
     // sticky time-out flag of the fused launch's in-kernel hand-offs, in host-visible
     // memory (the kernel stores 1 there when a wait gives up; checked at every API
     // entry and by sync(), never read on the device)

@@ -533,7 +533,6 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[16] = cl ? (int64_t)op.plan.hmSrc.size() : (int64_t)op.plan.attSrc.size();
         s[17] = op.f32Bytes();  // config 5's fp32 operator caches (0 before its first apply)
         s[18] = cl && op.topFusedOn() ? 1 : 0;
-        s[19] = cl && op.stagedOn(aniso::Operator::rootRhs(op.ks)) ? 1 : 0;
     });
 }
 

@@ -434,249 +434,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     m2l_hc_cluster<K, NR>((int)blockIdx.x, a, sm);
 }
 
-// ----------------------------------------------------------------- staged-source clusters
-//
-// The clustered M2L with the cluster's sources staged in LDS: one
-// 12-wave workgroup per cluster (1 per CU: the VGPR file holds 12 such waves), whose
-// table holds the hw-weighted multipoles and boxes of the union of its entries'
-// sources and its own targets (a 64-target cluster reads ~144 nodes: 92 KB at K = 5,
-// loaded once, coalesced).  The per-pair 640-B multipole gathers of k_m2l_hc become
-// LDS reads, their registers go to E blocks in flight (4 per wave instead of 2, 2
-// instead of 1 on two-way pairs), and the cluster's entries are split over the 12
-// waves by weight instead of by target, so a wave's share does not depend on how
-// many targets a cluster has (shards of N-GPU runs have 16-target clusters).  A
-// target whose entries span two waves is flushed by both (LDS adds, as the partner
-// products are); the summation order is not fixed, as in k_m2l_hc.
-
-// The 16 column sums of one target's row sums c[4][K] (rows 4q + j of lane (s, q))
-// added to its LDS locals d[16][K] (the reduce-scatter of m2l_hc_cluster).
-template <int K>
-__device__ __forceinline__ void flush_target(double (&c)[4][K], double* d, int lane) {
-    const int s = lane >> 2, q = lane & 3;
-    if constexpr (K == 5) {
-        const bool r4 = xor16_r4(lane);
-        const int k32 = swap_add32_f64(1.0, 0.0) > 1.5 ? 0 : 10;
-        const int k16 = swap_add16_f64(1.0, 0.0) > 1.5 ? 0 : 5;
-        double v10[10];
-#pragma unroll
-        for (int k = 0; k < 10; ++k) v10[k] = swap_add32_f64(c[k / 5][k % 5], c[(k + 10) / 5][(k + 10) % 5]);
-        double v5[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) v5[k] = swap_add16_f64(v10[k], v10[k + 5]);
-        const bool h1 = (lane >> 3) & 1, h0 = (lane >> 2) & 1;
-        double v3[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const double x = v5[k], y = k + 3 < 5 ? v5[k + 3] : 0.0;
-            v3[k] = (h1 ? y : x) + dpp_f64<0x128>(h1 ? x : y);
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const double x = v3[u], y = u + 2 < 3 ? v3[u + 2] : 0.0;
-            const double sum = (h0 ? y : x) + xor16_f64<4>(h0 ? x : y, r4);
-            const int w = u + 2 * h0, v2 = w + 3 * h1;
-            if (w <= 2 && v2 <= 4) {
-                const int v0 = v2 + k16 + k32, j = v0 / 5, i = v0 - 5 * j;
-                atomicAdd(d + (4 * q + j) * K + i, sum);
-            }
-        }
-    } else {
-        const bool r4 = xor16_r4(lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int i = 0; i < K; ++i) {
-                double v = c[j][i];
-                v += xor16_f64<4>(v, r4);
-                v += xor16_f64<8>(v, r4);
-                v = xsum16_f64(v);
-                c[j][i] = xsum32_f64(v);
-            }
-        const int jr = s & 3, srcLane = 4 * s + (s >> 2);
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const double sel = jr == 0 ? c[0][i] : jr == 1 ? c[1][i] : jr == 2 ? c[2][i] : c[3][i];
-            const double v = __shfl(sel, srcLane);
-            if ((i & 3) == q) atomicAdd(d + s * K + i, v);
-        }
-    }
-}
-
-// One two-way entry (an in-cluster pair): the forward product o as hm_entry and the
-// partner's product ob[i] += T_i(c) (E/r) sum_b (-1)^b T_b(c) xa[b] (the reversed
-// direction has cos = -c; xa = the target's own hw-weighted multipole row).
-template <int K, int NR>
-__device__ __forceinline__ void hm_entry2s(double e, double dx, double dy2, const double (&xw)[K],
-                                           const double* __restrict__ xa, double (&o)[K], double (&ob)[K]) {
-    const double r2 = __builtin_fma(dx, dx, dy2);
-    const double ri = rsqrt_nr<NR>(r2);
-    const double c = dx * ri;
-    double T[K];
-    cheb_T<K>(c, T);
-    double v = xw[0], va = xa[0];
-#pragma unroll
-    for (int b = 1; b < K; ++b) {
-        v = __builtin_fma(T[b], xw[b], v);
-        va = __builtin_fma((b & 1) ? -T[b] : T[b], xa[b], va);
-    }
-    const double er = e * ri;
-    const double av = er * v, ava = er * va;
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        o[i] = __builtin_fma(T[i], av, o[i]);
-        ob[i] = __builtin_fma(T[i], ava, ob[i]);
-    }
-}
-
-template <int K, int NR>
-__device__ __forceinline__ void m2l_cs_cluster(const int cid, const CsArgs& a, double* sm) {
-    constexpr int RK = kRank * K;
-    constexpr int PG = 4;   // directed blocks in flight per wave
-    constexpr int PGD = 2;  // two-way blocks in flight per wave
-    const Params* __restrict__ P = a.P;
-    const int c0 = a.clPtr[cid], nt = a.clPtr[cid + 1] - c0;
-    const int r0 = a.rowPtr[cid], nr = a.rowPtr[cid + 1] - r0;
-    double* acc = sm;                     // nt x 16 x K: the cluster's locals
-    double* tab = acc + (size_t)nt * RK;  // nr x 16 x K: hw-weighted source multipoles
-    double* geo = tab + (size_t)nr * RK;  // nr x 4: source boxes (cx, cy, rx, ry)
-    for (int i = threadIdx.x; i < nt * RK; i += blockDim.x) acc[i] = 0.0;
-    for (int i = threadIdx.x; i < nr * kRank; i += blockDim.x) {
-        const int r = i >> 4, sr = i & (kRank - 1);
-        const double* m = a.mult + ((size_t)a.rowNode[r0 + r] * kRank + sr) * K;
-        double* t = tab + (size_t)i * K;
-#pragma unroll
-        for (int b = 0; b < K; ++b) t[b] = a.hw.hw[b] * m[b];
-    }
-    for (int i = threadIdx.x; i < nr; i += blockDim.x) {
-        const int n = a.rowNode[r0 + i];
-        geo[4 * i] = a.ncx[n];
-        geo[4 * i + 1] = a.ncy[n];
-        geo[4 * i + 2] = a.nrx[n];
-        geo[4 * i + 3] = a.nry[n];
-    }
-    __syncthreads();
-    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-    const int lane = threadIdx.x & (kWave - 1);
-    const int s = lane >> 2, q = lane & 3;
-    const double chx = P->cheb[s & 3], chy = P->cheb[s >> 2];
-    const int64_t* cutp = a.cut + (size_t)cid * (a.waves + 1);
-    int64_t e = cutp[w];
-    const int64_t eEnd = cutp[w + 1];
-    int k = 0;
-    while (k < nt - 1 && a.ptr[c0 + k + 1] <= e) ++k;
-    for (; e < eEnd && k < nt; ++k) {
-        const int64_t p1 = a.ptr[c0 + k + 1], pd = a.ptr[c0 + k] + a.ndir[c0 + k];
-        const int64_t se = min(eEnd, p1);
-        if (se <= e) continue;
-        const int n = a.tgt[c0 + k];
-        double bx[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bx[j] = a.ncx[n] + a.nrx[n] * P->cheb[j];
-        const double by = a.ncy[n] + a.nry[n] * P->cheb[q];
-        double c[4][K];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int i = 0; i < K; ++i) c[j][i] = 0.0;
-        // directed entries: PG blocks in flight, the source multipoles and boxes from LDS
-        const int64_t de = min(se, pd);
-        for (int64_t cb = e; cb < de; cb += kWave) {
-            const int cnt = (int)min<int64_t>(kWave, de - cb);
-            const int myBlk = lane < cnt ? a.blk[cb + lane] : 0;
-            const int myRow = lane < cnt ? (int)a.row[cb + lane] : 0;
-            for (int j0 = 0; j0 < cnt; j0 += PG) {
-                double e4[PG][4];
-#pragma unroll
-                for (int g = 0; g < PG; ++g) {
-                    const int b = __builtin_amdgcn_readlane(myBlk, min(j0 + g, cnt - 1));
-                    const dbl2* p = reinterpret_cast<const dbl2*>(a.E + (size_t)b * 256 + 16 * s + 4 * q);
-                    const dbl2 k0 = p[0], k1 = p[1];
-                    const bool ok = j0 + g < cnt;  // a skipped slot re-reads a valid block
-                    e4[g][0] = ok ? k0.x : 0.0;
-                    e4[g][1] = ok ? k0.y : 0.0;
-                    e4[g][2] = ok ? k1.x : 0.0;
-                    e4[g][3] = ok ? k1.y : 0.0;
-                }
-#pragma unroll
-                for (int g = 0; g < PG; ++g) {
-                    const int R = __builtin_amdgcn_readlane(myRow, min(j0 + g, cnt - 1));
-                    const double* gr = geo + 4 * R;
-                    const double ax = gr[0] + gr[2] * chx;
-                    const double dy = (gr[1] + gr[3] * chy) - by;
-                    const double dy2 = dy * dy;
-                    const double* xr = tab + (size_t)R * RK + s * K;
-                    double xw[K];
-#pragma unroll
-                    for (int b = 0; b < K; ++b) xw[b] = xr[b];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) hm_entry<K, false, NR>(e4[g][j], ax - bx[j], dy2, xw, c[j]);
-                }
-            }
-        }
-        // in-cluster (two-way) entries: both products from one read
-        const double* xa = tab + (size_t)a.self[c0 + k] * RK;
-        for (int64_t cb = max(e, pd); cb < se; cb += kWave) {
-            const int cnt = (int)min<int64_t>(kWave, se - cb);
-            const int myBlk = lane < cnt ? a.blk[cb + lane] : 0;
-            const int myRow = lane < cnt ? (int)a.row[cb + lane] : 0;
-            const int mySlot = lane < cnt ? a.slot[cb + lane] : 0;
-            for (int j0 = 0; j0 < cnt; j0 += PGD) {
-                double e4[PGD][4];
-#pragma unroll
-                for (int g = 0; g < PGD; ++g) {
-                    const int b = __builtin_amdgcn_readlane(myBlk, min(j0 + g, cnt - 1));
-                    const dbl2* p = reinterpret_cast<const dbl2*>(a.E + (size_t)b * 256 + 16 * s + 4 * q);
-                    const dbl2 k0 = p[0], k1 = p[1];
-                    e4[g][0] = k0.x;
-                    e4[g][1] = k0.y;
-                    e4[g][2] = k1.x;
-                    e4[g][3] = k1.y;
-                }
-#pragma unroll
-                for (int g = 0; g < PGD; ++g) {
-                    if (j0 + g >= cnt) break;  // wave-uniform: a two-way slot must not add twice
-                    const int R = __builtin_amdgcn_readlane(myRow, j0 + g);
-                    const int sl = __builtin_amdgcn_readlane(mySlot, j0 + g);
-                    const double* gr = geo + 4 * R;
-                    const double ax = gr[0] + gr[2] * chx;
-                    const double dy = (gr[1] + gr[3] * chy) - by;
-                    const double dy2 = dy * dy;
-                    const double* xr = tab + (size_t)R * RK + s * K;
-                    double xw[K], ob[K];
-#pragma unroll
-                    for (int b = 0; b < K; ++b) {
-                        xw[b] = xr[b];
-                        ob[b] = 0.0;
-                    }
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        hm_entry2s<K, NR>(e4[g][j], ax - bx[j], dy2, xw, xa + (4 * q + j) * K, c[j], ob);
-#pragma unroll
-                    for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // rows 4q'+j over the quad
-                    if (q == 0) {
-                        double* d = acc + ((size_t)sl * kRank + s) * K;
-#pragma unroll
-                        for (int i = 0; i < K; ++i) atomicAdd(d + i, (i & 1) ? -ob[i] : ob[i]);
-                    }
-                }
-            }
-        }
-        flush_target<K>(c, acc + (size_t)k * RK, lane);
-        e = se;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nt * RK; i += blockDim.x) {
-        const int kk = i / RK, r = i - kk * RK;
-        a.local[(size_t)a.tgt[c0 + kk] * RK + r] = a.hw.om[r % K] * acc[i];
-    }
-}
-
-template <int K, int NR, int W>
-__global__ void __launch_bounds__(W * kWave) __attribute__((amdgpu_waves_per_eu(3))) k_m2l_cs(CsArgs a) {
-    extern __shared__ double sm[];
-    m2l_cs_cluster<K, NR>((int)blockIdx.x, a, sm);
-}
-
 // ----------------------------------------------------------------- fused top of tree + M2L
 //
 // The upper up tiers are a few hundred small, latency-bound tasks; as launches of
@@ -749,32 +506,6 @@ k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a) {
     // no store or fence on the way here, so the compiler keeps the wave-uniform
     // source-box reads (ncx[B] ...) on scalar loads as in k_m2l_hc
     m2l_hc_cluster<K, NR>(cid, a, sm);
-}
-
-// the fused top-of-tree launch over staged-source clusters: blocks of kCsWaves waves
-// (up_task runs at any block size); the same hand-offs as k_top_m2l_hc
-template <int K, int NR, int W>
-__global__ void __launch_bounds__(W * kWave) __attribute__((amdgpu_waves_per_eu(3))) k_top_m2l_cs(UpArgs u, TopArgs t, CsArgs a) {
-    extern __shared__ double sm[];
-    const int b = (int)blockIdx.x;
-    if (b < t.nUp) {
-        int k = 1;
-        while (b >= t.blk0[k + 1]) ++k;
-        if (k >= 2) top_wait(t, k - 1, (unsigned)(t.blk0[k] - t.blk0[k - 1]));
-        up_task<K>(t.task0[k] + (b - t.blk0[k]), u.maxTask, u.desc, u.grpFix, u.node, u.code, u.geom, u.leafRange,
-                   u.pxT, u.pyT, u.xin, u.ldi, u.treeIn, u.perm, u.sigT, u.wT, u.fT, u.cT, u.P, u.mult, u.rootSlot,
-                   k == 1 ? t.recv1 : nullptr, nullptr, nullptr, sm);
-        top_publish(t.cnt, k);
-        return;
-    }
-    const int cid = b - t.nUp;
-    const int w = t.clWait[cid];
-    if (w > 0) {
-        top_wait(t, w, (unsigned)(t.blk0[w + 1] - t.blk0[w]));
-        m2l_cs_cluster<K, NR>(cid, a, sm);
-        return;
-    }
-    m2l_cs_cluster<K, NR>(cid, a, sm);
 }
 
 // ----------------------------------------------------------------- near field
@@ -1165,63 +896,6 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
 #undef ANISO_NEAR_HM
     HIP_LAUNCH_CHECK();
     return false;
-}
-
-
-// K = 8 does not fit (its table and locals exceed the LDS of one workgroup, and its
-// registers spill): block handles of 8 right-hand sides keep k_m2l_hc
-#define ANISO_CS_DISPATCH_K(k, CALL)                                                                    \
-    switch (k) {                                                                                        \
-        case 2: { constexpr int KK = 2; CALL; } break;                                                  \
-        case 4: { constexpr int KK = 4; CALL; } break;                                                  \
-        case 5: { constexpr int KK = 5; CALL; } break;                                                  \
-        default: throw std::invalid_argument("staged M2L: unsupported block count " + std::to_string(k)); \
-    }
-
-size_t m2l_cs_lds(int K, int maxCl, int maxRows) {
-    if (K != 2 && K != 4 && K != 5) return 0;
-    const size_t b = ((size_t)maxCl * kRank * K + (size_t)maxRows * (kRank * K + 4)) * sizeof(double);
-    return b <= 160 * 1024 ? b : 0;
-}
-
-// staged-source clusters: 12 waves per cluster, 1/r as k_m2l_hc (one Newton step)
-void launch_m2l_cs(int K, int ncl, int maxCl, int maxRows, const CsArgs& a, hipStream_t s) {
-    if (ncl <= 0) return;
-    if (a.waves != 4 && a.waves != 12) throw std::invalid_argument("staged M2L: 4 or 12 waves per cluster");
-    const size_t shm = m2l_cs_lds(K, maxCl, maxRows);
-    if (shm == 0) throw std::invalid_argument("staged M2L cluster exceeds one workgroup's LDS");
-    ANISO_CS_DISPATCH_K(K, ({
-        auto f = a.waves == 4 ? k_m2l_cs<KK, 1, 4> : k_m2l_cs<KK, 1, 12>;
-        if (shm > 65536) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(f),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-            if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
-        }
-        f<<<ncl, a.waves * kWave, shm, s>>>(a);
-    }));
-    HIP_LAUNCH_CHECK();
-}
-
-void launch_top_m2l_cs(int K, int ncl, int maxCl, int maxRows, const UpArgs& u, const TopArgs& t, const CsArgs& a,
-                       hipStream_t s) {
-    if (t.ntier < 2 || t.ntier > kMaxTopTiers || t.blk0[t.ntier] != t.nUp)
-        throw std::invalid_argument("fused top-of-tree launch: bad tier layout");
-    if (!t.err) throw std::invalid_argument("fused top-of-tree launch: no time-out flag");
-    const size_t cs = m2l_cs_lds(K, maxCl, maxRows);
-    if (cs == 0) throw std::invalid_argument("staged M2L cluster exceeds one workgroup's LDS");
-    const size_t shm = std::max(cs, up_tier_lds(u.maxTask, K));
-    if (shm > 160 * 1024) throw std::invalid_argument("fused top-of-tree launch exceeds one workgroup's LDS");
-    const unsigned nb = (unsigned)(t.nUp + ncl);
-    ANISO_CS_DISPATCH_K(K, ({
-        auto f = a.waves == 4 ? k_top_m2l_cs<KK, 1, 4> : k_top_m2l_cs<KK, 1, 12>;
-        if (shm > 65536) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(f),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-            if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
-        }
-        f<<<nb, a.waves * kWave, shm, s>>>(u, t, a);
-    }));
-    HIP_LAUNCH_CHECK();
 }
 
 }  // namespace aniso

@@ -128,17 +128,6 @@ struct Plan {
     // block (E of the reversed pair), appended after the stored blocks in the cache,
     // so that k_m2l_hc reads every block in the stored orientation (16-B lane loads)
     std::vector<int> hmCopyOwner, hmCopyOther;
-    // the same clusters with their sources staged in LDS (k_m2l_cs):
-    // per cluster a table of rows = the union of its targets and its entries'
-    // sources (csRowPtr CSR over csRowNode), each entry's source row (csRow), each
-    // target's own row (csSelf); the cluster's entries are split over csWaves waves
-    // by weight (csCut: csWaves + 1 absolute entry indices per cluster), so a wave's
-    // share does not depend on how many targets the cluster has
-    std::vector<int> csRowPtr, csRowNode;
-    std::vector<uint16_t> csRow, csSelf;
-    std::vector<int64_t> csCut;
-    int csMaxRows = 0;
-    int csWaves = 12;  // input: waves per staged cluster workgroup (4: 256 threads, or 12: 768)
     // tiered up / down passes: tier k has root level
     // tierRootLevel[k] and bottom level tierBottomLevel[k] (k = 0 is the deepest).
     std::vector<int> tierRootLevel, tierBottomLevel;
@@ -200,7 +189,6 @@ struct Plan {
   private:
     void buildUpTasks(const Tree& t);
     void buildClusters(const Tree& t);
-    void buildStagedClusters(const Tree& t);
     void buildDownTasks(const Tree& t);
 };
 

@@ -779,49 +779,6 @@ void Plan::buildClusters(const Tree& t) {
         hmDual += (int64_t)dSrc.size();
         hmPtr.push_back((int64_t)hmSrc.size());
     }
-    buildStagedClusters(t);
-}
-
-// The source tables and wave shares of the staged-source clusters (k_m2l_cs).
-void Plan::buildStagedClusters(const Tree& t) {
-    csRowPtr.assign(1, 0);
-    csRowNode.clear();
-    csRow.assign(hmSrc.size(), 0);
-    csSelf.assign(hmTgt.size(), 0);
-    csCut.clear();
-    csMaxRows = 0;
-    const int ncl = (int)hmClPtr.size() - 1;
-    std::vector<int> rowOf(t.nn, -1);
-    for (int c = 0; c < ncl; ++c) {
-        const int r0 = (int)csRowNode.size();
-        auto rowFor = [&](int n) {
-            if (rowOf[n] < 0) {
-                rowOf[n] = (int)csRowNode.size() - r0;
-                csRowNode.push_back(n);
-            }
-            return rowOf[n];
-        };
-        for (int k = hmClPtr[c]; k < hmClPtr[c + 1]; ++k) csSelf[k] = (uint16_t)rowFor(hmTgt[k]);
-        for (int k = hmClPtr[c]; k < hmClPtr[c + 1]; ++k)
-            for (int64_t e = hmPtr[k]; e < hmPtr[k + 1]; ++e) csRow[e] = (uint16_t)rowFor(hmSrc[e]);
-        for (size_t i = r0; i < csRowNode.size(); ++i) rowOf[csRowNode[i]] = -1;
-        csRowPtr.push_back((int)csRowNode.size());
-        csMaxRows = std::max(csMaxRows, (int)csRowNode.size() - r0);
-        if ((int)csRowNode.size() - r0 > 65535) throw std::logic_error("staged M2L cluster table exceeds 16-bit rows");
-        // wave shares by weight: a directed entry 2, an in-cluster (two-way) entry 3
-        const int64_t e0 = hmPtr[hmClPtr[c]], e1 = hmPtr[hmClPtr[c + 1]];
-        std::vector<int64_t> wsum(1, 0);
-        for (int k = hmClPtr[c]; k < hmClPtr[c + 1]; ++k)
-            for (int64_t e = hmPtr[k]; e < hmPtr[k + 1]; ++e)
-                wsum.push_back(wsum.back() + (e < hmPtr[k] + hmNDir[k] ? 2 : 3));
-        const int64_t W = wsum.back();
-        int64_t pos = 0;
-        for (int w = 0; w <= csWaves; ++w) {
-            const int64_t goal = W * w / csWaves;
-            while (pos < e1 - e0 && wsum[pos] < goal) ++pos;
-            csCut.push_back(e0 + (w == csWaves ? e1 - e0 : pos));
-        }
-    }
 }
 
 // Exchange plan of the sharded up pass (the reference

@@ -211,37 +211,6 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, 
                    const int* src, const int* blk, const int* slot, const double* E, const double* ncx, const double* ncy,
                    const double* nrx, const double* nry, const Params* P, const HarmWeights& hw, const double* mult,
                    double* local, hipStream_t s);
-// The staged-source clustered M2L (harmonic.hip k_m2l_cs): the
-// cluster plan above plus each cluster's LDS table of source rows and the waves'
-// shares of its entries (Plan::buildStagedClusters)
-struct CsArgs {
-    const int* clPtr;
-    const int* tgt;
-    const int64_t* ptr;
-    const int* ndir;
-    const int* blk;
-    const int* slot;
-    const uint16_t* row;   // per entry: its source's table row
-    const uint16_t* self;  // per target: its own table row
-    const int* rowPtr;     // per cluster: first table row (CSR over rowNode)
-    const int* rowNode;
-    const int64_t* cut;    // per cluster: waves + 1 entry boundaries
-    int waves;             // waves per cluster workgroup (Plan::csWaves)
-    const double* E;
-    const double* ncx;
-    const double* ncy;
-    const double* nrx;
-    const double* nry;
-    const Params* P;
-    HarmWeights hw;
-    const double* mult;
-    double* local;
-};
-// LDS bytes of a staged cluster launch (0: does not fit one workgroup's 160 KB)
-size_t m2l_cs_lds(int K, int maxCl, int maxRows);
-void launch_m2l_cs(int K, int ncl, int maxCl, int maxRows, const CsArgs& a, hipStream_t s);
-void launch_top_m2l_cs(int K, int ncl, int maxCl, int maxRows, const UpArgs& u, const TopArgs& t, const CsArgs& a,
-                       hipStream_t s);
 // the fused corrections of the staged near field (d = 1; harmonic.hip k_near_hs)
 struct NearCorr {  // the fused corrections of k_near_hs (d = 1), or ignored when rows == nullptr
     const uint16_t* rows;

@@ -594,9 +594,7 @@ def test_harmonic_symmetric_blocks_match_directed(sz, d, ks, monkeypatch):
                                             (40, 1, 5, 3, "1")])
 def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatch):
     """The clustered harmonic M2L (in-cluster V pairs read once by
-    the smaller id, both products, locals summed in LDS) -- with its sources staged in
-    LDS and entries split over 12 waves (k_m2l_cs, the default) and without
-    (k_m2l_hc, ANISO_HM_STAGED=0) -- against one wave per target
+    the smaller id, both products, locals summed in LDS) against one wave per target
     (aniso_set_deterministic); odd sz (non-uniform tree), directed storage, a
     maxLevel-limited tree.  Also checks that in-cluster pairs exist, that the cluster
     plan reads fewer E blocks, and that the deterministic mode repeats bitwise."""
@@ -608,8 +606,7 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatc
     # clusters, which small trees only reach with 4-target clusters: no in-cluster pairs)
     monkeypatch.setenv("ANISO_HM_CLDEPTH", "3")
     outs, st = [], []
-    for det, staged in ((False, "1"), (False, "0"), (True, "1")):
-        monkeypatch.setenv("ANISO_HM_STAGED", staged)
+    for det in (False, True):
         a = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, ml)
         a.set_deterministic(det)
         xy = a.getNodes()
@@ -627,16 +624,15 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatc
             assert torch.equal(out, again)
         a.sync()
         outs.append(out.cpu().numpy())
-    assert st[0]["staged_m2l"] == 1 and st[1]["staged_m2l"] == 0 and st[2]["staged_m2l"] == 0
-    assert st[0]["harmonic"] == 1 and st[0]["hm_clusters"] > 0 and st[2]["hm_clusters"] == 0
-    assert st[0]["hm_dual_pairs"] > 0 and st[0]["hm_block_reads"] < st[2]["hm_block_reads"]
-    assert _rel(outs[0], outs[2]) <= 1e-13 and _rel(outs[1], outs[2]) <= 1e-13
+    assert st[0]["harmonic"] == 1 and st[0]["hm_clusters"] > 0 and st[1]["hm_clusters"] == 0
+    assert st[0]["hm_dual_pairs"] > 0 and st[0]["hm_block_reads"] < st[1]["hm_block_reads"]
+    assert _rel(outs[0], outs[1]) <= 1e-13
 
 
 @pytest.mark.parametrize("ks,world", [(5, 8), (2, 4), (3, 3)])
-def test_staged_clusters_on_shards_match_unstaged(ks, world, monkeypatch):
-    """The staged-source M2L on the small clusters of an N-GPU shard (the adaptive
-    depth gives 16-target clusters there) and with padded block counts: every rank's
+def test_small_clusters_on_shards_match_unsharded(ks, world):
+    """The clustered M2L on the small clusters of an N-GPU shard (the adaptive depth
+    gives 16-target clusters there) with 2, 4 (3 padded) and 5 blocks: every rank's
     two-phase apply equals the unsharded operator."""
     torch = _torch()
     import aniso_amd
@@ -684,7 +680,7 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
     assert float(torch.linalg.norm(o1 - ref) / torch.linalg.norm(ref)) <= 1e-13
 
 
-@pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0", "ANISO_HM_STAGED=0"])
+@pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0"])
 def test_block_matvec_knobs_agree(knob, monkeypatch):
     """Every remaining environment knob of the block apply:
     the serial near/M2L order, the separate x - mforward(x) subtraction and the
@@ -1230,7 +1226,7 @@ def test_block_solve_matches_gmres_over_oracle(sz, restart):
     rhs = _block_ref(o, charge, a.g, ss, 0).reshape(-1)
 
     def A(v):
-        return _block_ref(o, v.reshape(ks, a.N), a.g, ss, 2).reshape(-1)
+        return _block_ref(o, np.asarray(v, dtype=np.float64).reshape(ks, a.N), a.g, ss, 2).reshape(-1)
 
     tol = 1e-11
     xr, its_ref, rr_ref = _gmres_matlab(A, rhs, restart, tol, 400)
@@ -1239,7 +1235,8 @@ def test_block_solve_matches_gmres_over_oracle(sz, restart):
     assert its == its_ref, (its, its_ref)
     assert _rel(u.reshape(-1), xr) <= 1e-10, _rel(u.reshape(-1), xr)
     assert hist.size == its and hist[-1] <= tol
-    xs, info = gmres(LinearOperator((rhs.size, rhs.size), matvec=A), rhs, rtol=tol, restart=restart, maxiter=400)
+    xs, info = gmres(LinearOperator((rhs.size, rhs.size), matvec=A, dtype=np.float64), rhs, rtol=tol,
+                     restart=restart, maxiter=400)
     assert info == 0
     assert _rel(u.reshape(-1), xs) <= 1e-10, _rel(u.reshape(-1), xs)
     # the device entry point on the same system, from a nonzero initial guess

@@ -83,5 +83,5 @@ for rep in range(args.reps):
 for r in runs:
     s = r["op"].stats()
     print(json.dumps({"cfg": r["cfg"], "world": world, "rank": rank, "ms": r["ms"], "best_ms": min(r["ms"]),
-                      "stage_ms": r["st"], "staged": s["staged_m2l"], "clusters": s["hm_clusters"],
+                      "stage_ms": r["st"], "clusters": s["hm_clusters"],
                       "block_reads": s["hm_block_reads"]}), flush=True)
