@@ -82,6 +82,8 @@ def lib():
             "aniso_apply_block": [P, dp, dp, D, dp],
             "aniso_shard_cuts": [P, I, lp],
             "aniso_forward_f32_dev": [P, P, P, P],
+            "aniso_forward16_f64_dev": [P, P, P, P],
+            "aniso_mapping16_f64_dev": [P, I, P, P, I, P],
             "aniso_forward_f32_stages_dev": [P, P, I, P, P],
             "aniso_set_deterministic": [P, I],
             "aniso_shard_exchange": [P, I, lp],
@@ -274,6 +276,33 @@ class Aniso:
         else:
             _check(lib().aniso_forward_f32_stages_dev(self.address, ctypes.c_void_p(X.data_ptr()), int(mask),
                                                       ctypes.c_void_p(Y.data_ptr()), ctypes.c_void_p(s)))
+        return Y
+
+    def forward16_f64_dev(self, X, Y, stream=None):
+        """The fp64 16-RHS operator on MFMA: Y = X - K_0(sigma_s .* X); X, Y (N, 16)
+        contiguous float64 CUDA tensors, point-major, tree order."""
+        import torch
+
+        for t, nm in ((X, "X"), (Y, "Y")):
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()
+                    and tuple(t.shape) == (self.N, 16)):
+                raise AnisoError(1, f"{nm} must be a contiguous ({self.N}, 16) float64 CUDA tensor")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_forward16_f64_dev(self.address, ctypes.c_void_p(X.data_ptr()), ctypes.c_void_p(Y.data_ptr()),
+                                             ctypes.c_void_p(s)))
+        return Y
+
+    def mapping16_f64_dev(self, id_, X, Y, mask=STAGE_ALL, stream=None):
+        """Y = K_id X for 16 right-hand sides on fp64 MFMA (shapes as forward16_f64_dev)."""
+        import torch
+
+        for t, nm in ((X, "X"), (Y, "Y")):
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()
+                    and tuple(t.shape) == (self.N, 16)):
+                raise AnisoError(1, f"{nm} must be a contiguous ({self.N}, 16) float64 CUDA tensor")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_mapping16_f64_dev(self.address, int(id_), ctypes.c_void_p(X.data_ptr()),
+                                             ctypes.c_void_p(Y.data_ptr()), int(mask), ctypes.c_void_p(s)))
         return Y
 
     # ---- the block operator of aniso.m (aniso.m:121-157)

@@ -119,6 +119,9 @@ void Operator::setShard(int rank, int nranks) {
         m.Km2l.alloc(0);
         m.ready = false;
     }
+    f32Ready = false;
+    mrhsPlanReady = false;
+    m64.clear();
     if (device >= 0) uploadPlan();
 }
 
@@ -363,6 +366,7 @@ void Operator::setCoeff(const double* ss, const double* st) {
     for (auto& m : modes) m.ready = false;
     attReady = false;
     f32Ready = false;  // config 5's fp32 caches are rounded from the mode-0 operators of sigma_t
+    m64.clear();       // ... and the fp64 16-RHS caches are the modes' operators
     coeffSet = true;
 }
 
@@ -376,6 +380,7 @@ void Operator::cache(int id) {
     ensureDevice();
     ModeCache& mc = modes[id];
     if (id == 0) f32Ready = false;  // rebuilt from the new mode-0 operators at the next fp32 apply
+    m64.erase(id);
     mc.Knear.alloc((size_t)plan.nearKTotal * sizeof(double));
     mc.Km2l.alloc((size_t)plan.storedM2L * 256 * sizeof(double));
     const Params* P = dParams.as<Params>();
@@ -472,11 +477,36 @@ void Operator::mappingHost(const double* charge, int id, double* out) {
     checkDeviceErrors();
 }
 
-// k right-hand sides of one mode, up to 8 per batched apply (identity mix)
+// k right-hand sides of one mode: up to 8 per batched apply (identity mix), or, for
+// more than 8 on an unsharded handle, 16 per apply of the fp64 MFMA operator
+// (f64op.hip; zero columns pad the last chunk)
 void Operator::mappingBatchedHost(const double* Q, int k, int id, double* Out) {
     if (k == 0) return;
     ensureDevice();
     const int64_t N = geo.N;
+    if (k > 8 && plan.nranks == 1) {
+        if (id < 0 || id >= kernelSize) throw std::out_of_range("kernel id out of range");
+        if (!modes[id].ready)
+            throw std::runtime_error("mapping on kernel id " + std::to_string(id) + " before cache(" + std::to_string(id) + ")");
+        DevBuf dq, dout, x16, y16;
+        dq.alloc((size_t)16 * N * sizeof(double));
+        dout.alloc((size_t)16 * N * sizeof(double));
+        x16.alloc((size_t)16 * N * sizeof(double));
+        y16.alloc((size_t)16 * N * sizeof(double));
+        for (int j0 = 0; j0 < k; j0 += 16) {
+            const int kc = std::min(16, k - j0);
+            HIP_CHECK(hipMemcpyAsync(dq.p, Q + (size_t)j0 * N, (size_t)kc * N * sizeof(double), hipMemcpyHostToDevice,
+                                     own));
+            launch64_gather16(N, kc, dPerm.as<int>(), dq.as<double>(), x16.as<double>(), own);
+            mrhs64Dev(id, false, x16.as<double>(), y16.as<double>(), own);
+            launch64_scatter16(N, kc, dPerm.as<int>(), y16.as<double>(), dout.as<double>(), own);
+            HIP_CHECK(hipMemcpyAsync(Out + (size_t)j0 * N, dout.p, (size_t)kc * N * sizeof(double),
+                                     hipMemcpyDeviceToHost, own));
+            HIP_CHECK(hipStreamSynchronize(own));
+        }
+        checkDeviceErrors();
+        return;
+    }
     const int kb = std::min(k, 8);
     DevBuf dq, dout;
     dq.alloc((size_t)kb * N * sizeof(double));
@@ -1015,9 +1045,9 @@ void Operator::lineIntegrals(const double* seg, int n, double* out) {
 // (bbfmm.h:855-859), every non-empty node's V then X pairs (bbfmm.h:1051-1065), L2L
 // levels top-down (bbfmm.h:1070-1071).  The caches are the fp64 mode-0 operators
 // (k_cache_m2l / k_cache_near on these directed lists) rounded to fp32.
-void Operator::buildF32() {
-    if (plan.nranks != 1) throw std::logic_error("fp32 operator on a sharded handle");
-    if (!modeCached(0)) throw std::runtime_error("fp32 operator before cache(0)");
+void Operator::buildMrhsPlan() {
+    if (plan.nranks != 1) throw std::logic_error("16-right-hand-side operator on a sharded handle");
+    if (mrhsPlanReady) return;
     ensureDevice();
     F32Plan& f = f32;
     f = F32Plan();
@@ -1028,7 +1058,6 @@ void Operator::buildF32() {
     std::sort(lv.begin(), lv.end(), [&](int a, int b) { return t.begin[a] < t.begin[b]; });
     f.nearPtr.push_back(0);
     f.srcPtr.push_back(0);
-    int maxSrc = 1;
     for (int n : lv) {
         int64_t S = 0;
         const int64_t s0 = (int64_t)f.srcNodes.size();
@@ -1041,7 +1070,7 @@ void Operator::buildF32() {
             for (int64_t q = 0; q < t.count[b]; ++q) f.nearPts.push_back((int)(t.begin[b] + q));
             S += t.count[b];
         }
-        maxSrc = std::max<int>(maxSrc, (int)(f.srcNodes.size() - s0));
+        f.maxSrc = std::max<int>(f.maxSrc, (int)(f.srcNodes.size() - s0));
         const int64_t Sp = (S + 15) & ~(int64_t)15;
         for (int64_t q = S; q < Sp; ++q) f.nearPts.push_back((int)t.begin[n]);  // zero columns
         const int nT = (int)t.count[n];
@@ -1086,57 +1115,153 @@ void Operator::buildF32() {
     up(d32Ptr, f.m2lPtr);
     up(d32Src, f.m2lSrc);
     up(d32Level, t.level);
+    up(d32PairTgt, f.m2lPairTgt);
+    up(d32SrcPtr, f.srcPtr);
+    up(d32SrcNodes, f.srcNodes);
+    up(d32KoffD, f.koffD);
+    up(d32SrcCount, f.srcCount);
     d32LevelNodes.clear();
     d32LevelNodes.resize(f.m2m.size() + f.l2l.size());
     for (size_t l = 0; l < f.m2m.size(); ++l) up(d32LevelNodes[l], f.m2m[l]);
     for (size_t l = 0; l < f.l2l.size(); ++l) up(d32LevelNodes[f.m2m.size() + l], f.l2l[l]);
-    // transfer operators in A order: Rup = R_q^T (M2M), Rdn = R_q (L2L)
+    // transfer operators in A order: Rup = R_q^T (M2M), Rdn = R_q (L2L); fp32 lane l,
+    // element e: k = 4 (l >> 4) + e; fp64: k = (l >> 4) + 4 e (each MFMA's own order)
     std::vector<float> rup(4 * 256), rdn(4 * 256);
+    std::vector<double> rup64(4 * 256), rdn64(4 * 256);
     for (int q = 0; q < 4; ++q)
         for (int l = 0; l < 64; ++l)
             for (int e = 0; e < 4; ++e) {
-                const int i = l & 15, k = 4 * (l >> 4) + e;
+                const int i = l & 15, k = 4 * (l >> 4) + e, k64 = (l >> 4) + 4 * e;
                 rup[q * 256 + l * 4 + e] = (float)hostP.R[q][k + i * 16];
                 rdn[q * 256 + l * 4 + e] = (float)hostP.R[q][i + k * 16];
+                rup64[q * 256 + l * 4 + e] = hostP.R[q][k64 + i * 16];
+                rdn64[q * 256 + l * 4 + e] = hostP.R[q][i + k64 * 16];
             }
     up(d32Rup, rup);
     up(d32Rdn, rdn);
+    up(d64Rup, rup64);
+    up(d64Rdn, rdn64);
+    mrhsPlanReady = true;
+}
+
+// config 5's fp32 caches: the fp64 mode-0 blocks on the directed lists, rounded
+void Operator::buildF32() {
+    if (!modeCached(0)) throw std::runtime_error("fp32 operator before cache(0)");
+    buildMrhsPlan();
+    const F32Plan& f = f32;
+    const Tree& t = tree;
     d32Mult.alloc((size_t)t.nn * 256 * sizeof(float));
     d32Local.alloc((size_t)t.nn * 256 * sizeof(float));
     d32FT.alloc((size_t)geo.N * 16 * sizeof(float));
     d32CT.alloc((size_t)geo.N * 16 * sizeof(float));
-    // caches: fp64 mode-0 blocks on the directed lists, rounded to fp32
     const Params* P = dParams.as<Params>();
     {
         const int64_t np_ = (int64_t)f.m2lSrc.size();
-        DevBuf pt, tmp;
-        up(pt, f.m2lPairTgt);
+        DevBuf tmp;
         tmp.alloc((size_t)std::max<int64_t>(np_, 1) * 256 * sizeof(double));
         d32Km2l.alloc((size_t)std::max<int64_t>(np_, 1) * 256 * sizeof(float));
-        launch_cache_m2l(np_, pt.as<int>(), d32Src.as<int>(), dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(),
-                         dNry.as<double>(), dStCoef.as<double>(), P, 0, tmp.as<double>(), own);
+        launch_cache_m2l(np_, d32PairTgt.as<int>(), d32Src.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
+                         dNrx.as<double>(), dNry.as<double>(), dStCoef.as<double>(), P, 0, tmp.as<double>(), own);
         launch32_conv_m2l(np_, tmp.as<double>(), d32Km2l.p, own);
         HIP_CHECK(hipStreamSynchronize(own));
     }
     {
-        DevBuf sp, sn, kd, tmp, sc;
-        up(sp, f.srcPtr);
-        up(sn, f.srcNodes);
-        up(kd, f.koffD);
-        up(sc, f.srcCount);
+        DevBuf tmp;
         tmp.alloc((size_t)std::max<int64_t>(f.nearD, 1) * sizeof(double));
         d32Knear.alloc((size_t)std::max<int64_t>(f.nearTiles, 1) * 4 * sizeof(float));
-        launch_cache_near((int)f.leaves.size(), d32Leaves.as<int>(), sp.as<int64_t>(), sn.as<int>(), kd.as<int64_t>(),
-                          dBegin.as<int64_t>(), dCount.as<int64_t>(), dPxT.as<double>(), dPyT.as<double>(),
-                          dStCoef.as<double>(), P, 0, maxSrc, tmp.as<double>(), own);
-        launch32_conv_near((int)f.leaves.size(), d32LeafInfo.as<int4>(), kd.as<int64_t>(), d32Koff.as<int64_t>(),
-                           sc.as<int>(), tmp.as<double>(), d32Knear.p, own);
+        launch_cache_near((int)f.leaves.size(), d32Leaves.as<int>(), d32SrcPtr.as<int64_t>(), d32SrcNodes.as<int>(),
+                          d32KoffD.as<int64_t>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dPxT.as<double>(),
+                          dPyT.as<double>(), dStCoef.as<double>(), P, 0, f.maxSrc, tmp.as<double>(), own);
+        launch32_conv_near((int)f.leaves.size(), d32LeafInfo.as<int4>(), d32KoffD.as<int64_t>(),
+                           d32Koff.as<int64_t>(), d32SrcCount.as<int>(), tmp.as<double>(), d32Knear.p, own);
         HIP_CHECK(hipStreamSynchronize(own));
     }
     f32Ready = true;
 }
 
+// the fp64 16-RHS caches of mode id (f64op.hip): the mode's blocks on the directed
+// lists, the M2L blocks rearranged in place into A order, the near blocks as tiles
+void Operator::buildMrhs64(int id) {
+    buildMrhsPlan();
+    const F32Plan& f = f32;
+    const Params* P = dParams.as<Params>();
+    Mrhs64Cache& c = m64[id];
+    const int64_t np_ = (int64_t)f.m2lSrc.size();
+    c.Km2l.alloc((size_t)std::max<int64_t>(np_, 1) * 256 * sizeof(double));
+    launch_cache_m2l(np_, d32PairTgt.as<int>(), d32Src.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
+                     dNrx.as<double>(), dNry.as<double>(), dStCoef.as<double>(), P, id, c.Km2l.as<double>(), own);
+    launch64_lane_major(np_, c.Km2l.as<double>(), own);
+    {
+        DevBuf tmp;
+        tmp.alloc((size_t)std::max<int64_t>(f.nearD, 1) * sizeof(double));
+        c.Knear.alloc((size_t)std::max<int64_t>(f.nearTiles, 1) * 4 * sizeof(double));
+        launch_cache_near((int)f.leaves.size(), d32Leaves.as<int>(), d32SrcPtr.as<int64_t>(), d32SrcNodes.as<int>(),
+                          d32KoffD.as<int64_t>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dPxT.as<double>(),
+                          dPyT.as<double>(), dStCoef.as<double>(), P, id, f.maxSrc, tmp.as<double>(), own);
+        launch64_conv_near((int)f.leaves.size(), d32LeafInfo.as<int4>(), d32KoffD.as<int64_t>(),
+                           d32Koff.as<int64_t>(), d32SrcCount.as<int>(), tmp.as<double>(), c.Knear.p, own);
+        HIP_CHECK(hipStreamSynchronize(own));
+    }
+    d64Mult.alloc((size_t)tree.nn * 256 * sizeof(double));
+    d64Local.alloc((size_t)tree.nn * 256 * sizeof(double));
+    d64FT.alloc((size_t)geo.N * 16 * sizeof(double));
+    d64CT.alloc((size_t)geo.N * 16 * sizeof(double));
+}
+
+void Operator::mrhs64Dev(int id, bool forward, const double* X, double* Y, hipStream_t s, int mask) {
+    if (plan.nranks != 1) throw std::logic_error("16-right-hand-side operator on a sharded handle");
+    if (id < 0 || id >= kernelSize) throw std::out_of_range("kernel id out of range");
+    if (forward && id != 0) throw std::invalid_argument("the forward operator is mode 0's (main.cpp:125-136)");
+    if (!modes[id].ready)
+        throw std::runtime_error("16-RHS fp64 operator on kernel id " + std::to_string(id) + " before cache(" +
+                                 std::to_string(id) + ")");
+    ensureDevice();
+    checkDeviceErrors();
+    if (!m64.count(id)) buildMrhs64(id);
+    const Mrhs64Cache& c = m64[id];
+    const Params* P = dParams.as<Params>();
+    const F32Plan& f = f32;
+    const double scale = M_1_PI / 2.0;  // AnisoWrapper.cpp:129-130
+    const bool tm = timeStages;
+    const int e0 = tm ? mark(s) : -1;
+    launch64_p2m((int)f.leaves.size(), d32Leaves.as<int>(), dBegin.as<int64_t>(), dCount.as<int64_t>(),
+                 dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(),
+                 dPyT.as<double>(), X, forward ? dSigmaT.as<double>() : nullptr, dWT.as<double>(), P, d64Mult.p,
+                 d64FT.as<double>(), d64CT.as<double>(), s);
+    for (int l = (int)f.m2m.size() - 1; l >= 1; --l)
+        launch64_m2m((int)f.m2m[l].size(), d32LevelNodes[l].as<int>(), dChild.as<int4>(), dCount.as<int64_t>(),
+                     d64Rup.p, d64Mult.p, s);
+    const int e1 = tm ? mark(s) : -1;
+    if (tm) spans.push_back({1, e0, e1});
+    if (mask & kStageFar) {
+        launch64_m2l((int)f.m2lTgt.size(), d32Tgt.as<int>(), d32Ptr.as<int64_t>(), d32Src.as<int>(), c.Km2l.p,
+                     d64Mult.p, d64Local.p, s);
+        const int e2 = tm ? mark(s) : -1;
+        if (tm) spans.push_back({2, e1, e2});
+        for (size_t l = 2; l < f.l2l.size(); ++l)
+            launch64_l2l((int)f.l2l[l].size(), d32LevelNodes[f.m2m.size() + l].as<int>(), dParent.as<int>(),
+                         dSlot.as<int>(), d64Rdn.p, d64Local.p, s);
+    }
+    const int e3 = tm ? mark(s) : -1;
+    launch64_leaf((int)f.leaves.size(), d32LeafInfo.as<int4>(), d32NearPtr.as<int64_t>(), d32NearPts.as<int>(),
+                  d32Koff.as<int64_t>(), c.Knear.p, d32Level.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
+                  dNrx.as<double>(), dNry.as<double>(), dPxT.as<double>(), dPyT.as<double>(), P, d64Local.p,
+                  d64FT.as<double>(), X, scale, (mask & kStageAll) | (forward ? kStageForward : 0), Y, s);
+    const int e4 = tm ? mark(s) : -1;
+    if (tm) spans.push_back({4, e3, e4});
+    // corrections: Y -= scale' corr with scale' = scale (forward: X - K x) or -scale (mapping: K x)
+    launch64_corr(geo.d, geo.N, dPerm.as<int>(), dIperm.as<int>(), d64CT.as<double>(), d64FT.as<double>(),
+                  modes[id].C.as<double>(), modes[id].mu.as<double>(), P, mask, forward ? scale : -scale, Y, s);
+    if (tm) {
+        const int e5 = mark(s);
+        spans.push_back({6, e4, e5});
+        spans.push_back({7, e0, e5});
+        ++applies;
+    }
+}
+
 void Operator::forwardF32Dev(const float* X, float* Y, hipStream_t s, int mask) {
+    if (plan.nranks != 1) throw std::logic_error("fp32 operator on a sharded handle");
     if (!f32Ready) buildF32();
     ensureDevice();
     const Params* P = dParams.as<Params>();

@@ -120,6 +120,11 @@ public:
     // FMM translation a 16 x 16 x 16 MFMA product on fp32 caches (built from the
     // fp64 mode-0 operators at the first call).  Unsharded handles only.
     void forwardF32Dev(const float* X, float* Y, hipStream_t s, int mask = kStageAll);
+    // the fp64 16-right-hand-side operator on MFMA (f64op.hip): Y = K_id X
+    // (forward = false) or main.cpp's Y = X - K_0(sigma_s .* X) (forward = true, id 0);
+    // X, Y point-major N x 16 doubles in tree order.  The mode's fp64 caches (directed
+    // lists, A order) are built from its operators at the first call.  Unsharded only.
+    void mrhs64Dev(int id, bool forward, const double* X, double* Y, hipStream_t s, int mask = kStageAll);
     int64_t f32Bytes() const { return f32Ready ? (int64_t)(d32Km2l.bytes + d32Knear.bytes) : 0; }
     hipStream_t stream() const { return own; }
     // raise (ANISO_ERR_RUNTIME) if a fused top-of-tree launch gave up waiting for its
@@ -254,6 +259,15 @@ private:
     // columns), M2M / L2L levels, directed M2L pairs
     void buildF32();
     bool f32Ready = false;
+    void buildMrhsPlan();  // the directed lists both 16-RHS operators share (f32 plan below)
+    bool mrhsPlanReady = false;
+    struct Mrhs64Cache {
+        DevBuf Km2l, Knear;
+    };
+    std::map<int, Mrhs64Cache> m64;  // fp64 16-RHS caches per mode id
+    void buildMrhs64(int id);
+    DevBuf d64Rup, d64Rdn, d64Mult, d64Local, d64FT, d64CT;
+    DevBuf d32PairTgt, d32SrcPtr, d32SrcNodes, d32KoffD, d32SrcCount;  // cache-build inputs of the 16-RHS plan
     struct F32Plan {
         std::vector<int> leaves;
         std::vector<std::array<int, 4>> leafInfo;  // node, begin, count, padded sources
@@ -263,6 +277,7 @@ private:
         std::vector<int> m2lTgt, m2lSrc, m2lPairTgt;
         std::vector<int64_t> m2lPtr;
         int64_t nearTiles = 0, nearD = 0;
+        int maxSrc = 1;
     } f32;
     DevBuf d32Leaves, d32LeafInfo, d32NearPtr, d32NearPts, d32Koff, d32Tgt, d32Ptr, d32Src;
     DevBuf d32Km2l, d32Knear, d32Rup, d32Rdn, d32Mult, d32Local, d32FT, d32CT, d32Level;

@@ -256,6 +256,25 @@ int aniso_forward_f32_dev(aniso_handle h, const float* x, float* y, void* stream
     });
 }
 
+int aniso_forward16_f64_dev(aniso_handle h, const double* x, double* y, void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(x);
+        CHECK_PTR(y);
+        get(h).mrhs64Dev(0, true, x, y, (hipStream_t)stream);
+    });
+}
+
+int aniso_mapping16_f64_dev(aniso_handle h, int id, const double* x, double* y, int mask, void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(x);
+        CHECK_PTR(y);
+        if (mask < 0 || mask > aniso::kStageAll) throw std::invalid_argument("bad stage mask");
+        get(h).mrhs64Dev(id, false, x, y, (hipStream_t)stream, mask);
+    });
+}
+
 int aniso_forward_f32_stages_dev(aniso_handle h, const float* x, int mask, float* y, void* stream) {
     ENTER(h);
     return guarded([&] {

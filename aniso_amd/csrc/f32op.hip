@@ -28,6 +28,7 @@
 #include <string>
 
 #include "device_common.hpp"
+#include "mrhs_corr.hpp"
 
 namespace aniso {
 
@@ -211,113 +212,6 @@ __global__ void __launch_bounds__(256) k32_leaf(int nleaf, const int4* __restric
     }
 }
 
-// Corrections of the forward operator (nearRemoval + refineAddOn + singularAdd,
-// KernelFactory.cpp:445-478, 662-709, 828-860) for the 16 right-hand sides: the
-// mode-0 stencil C (d2 x 9 x d2) and singular moments mu (d2 x d x d) as k_corr
-// (apply.hip), one thread per point (its 16 right-hand sides as 4 float4 rows),
-// fp64 arithmetic on the fp32 charges; Y -= scale corr.
-template <int D>
-__global__ void __launch_bounds__(256) k32_corr(int64_t N, const int* __restrict__ perm, const int* __restrict__ iperm,
-                                                const float* __restrict__ cT, const float* __restrict__ fT,
-                                                const double* __restrict__ C, const double* __restrict__ mu,
-                                                const Params* __restrict__ P, int flags, float scale,
-                                                float* __restrict__ Y) {
-    constexpr int D2 = D * D;
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= N) return;
-    const int t = perm[k];
-    const int sz = P->sz;
-    const int sq = t / D2, tq = t - sq * D2;
-    const int i = sq / sz, jj = sq - i * sz;
-    double acc[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] = 0.0;
-    if (flags & kStageStencil) {
-        for (int dr = -1; dr <= 1; ++dr) {
-            if (i + dr < 0 || i + dr >= sz) continue;
-            for (int dc = -1; dc <= 1; ++dc) {
-                if (jj + dc < 0 || jj + dc >= sz) continue;
-                const int q9 = (dr + 1) * 3 + (dc + 1);
-                const int* it = iperm + (size_t)(sq + dr * sz + dc) * D2;
-#pragma unroll
-                for (int c = 0; c < D2; ++c) {
-                    const double w = C[((size_t)tq * 9 + q9) * D2 + c];
-                    const float4* f = reinterpret_cast<const float4*>(fT + (size_t)it[c] * 16);
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        const float4 x = f[v];
-                        acc[4 * v] += w * x.x;
-                        acc[4 * v + 1] += w * x.y;
-                        acc[4 * v + 2] += w * x.z;
-                        acc[4 * v + 3] += w * x.w;
-                    }
-                }
-            }
-        }
-    }
-    if (flags & kStageSing) {
-        const double Xc = (0.5 + i) * P->dx, Yc = (0.5 + jj) * P->dx;
-        double bx[D][D], by[D][D];
-#pragma unroll
-        for (int nn = 0; nn < D; ++nn)
-#pragma unroll
-            for (int a = 0; a < D; ++a) {
-                double sx = 0.0, sy = 0.0, px = 1.0, py = 1.0;
-#pragma unroll
-                for (int e2 = 0; e2 < D; ++e2) {
-                    const double cb = P->legB[(nn * D + a) * D + e2];
-                    sx += cb * px;
-                    sy += cb * py;
-                    px *= Xc;
-                    py *= Yc;
-                }
-                bx[nn][a] = sx;
-                by[nn][a] = sy;
-            }
-        // g[q] = sum_ab (basis products of coefficient nk) . mu: the singular term is
-        // linear in the square's charges, sing_j = sum_q g[q] cT[q][j]
-        double g[D2];
-#pragma unroll
-        for (int q = 0; q < D2; ++q) g[q] = 0.0;
-#pragma unroll
-        for (int nk = 0; nk < D2; ++nk) {
-            const int nn = nk / D, kk = nk % D;
-            double m = 0.0;  // sum over a <= nn, bb <= kk of bx by mu
-#pragma unroll
-            for (int a = 0; a < D; ++a)
-#pragma unroll
-                for (int bb = 0; bb < D; ++bb)
-                    if (a <= nn && bb <= kk) m += bx[nn][a] * by[kk][bb] * mu[(size_t)tq * D2 + a * D + bb];
-            m *= P->coefScale[nk];
-#pragma unroll
-            for (int q = 0; q < D2; ++q) g[q] += m * P->interp[nk + q * D2] * P->sqrtW[q];
-        }
-        const int* itS = iperm + (size_t)sq * D2;
-#pragma unroll
-        for (int q = 0; q < D2; ++q) {
-            const float4* c4 = reinterpret_cast<const float4*>(cT + (size_t)itS[q] * 16);
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const float4 x = c4[v];
-                acc[4 * v] += g[q] * x.x;
-                acc[4 * v + 1] += g[q] * x.y;
-                acc[4 * v + 2] += g[q] * x.z;
-                acc[4 * v + 3] += g[q] * x.w;
-            }
-        }
-    }
-    float4* y = reinterpret_cast<float4*>(Y + (size_t)k * 16);
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        float4 o = y[v];
-        o.x -= scale * (float)acc[4 * v];
-        o.y -= scale * (float)acc[4 * v + 1];
-        o.z -= scale * (float)acc[4 * v + 2];
-        o.w -= scale * (float)acc[4 * v + 3];
-        y[v] = o;
-    }
-}
-
 // fp64 column-major M2L blocks (k_cache_m2l: pair*256 + s*16 + t) -> fp32 A order
 // (lane l, element e = K[t = l&15][s = 4(l>>4) + e])
 __global__ void k32_conv_m2l(int64_t n, const double* __restrict__ Kd, float* __restrict__ K32) {
@@ -407,12 +301,12 @@ void launch32_corr(int d, int64_t N, const int* perm, const int* iperm, const fl
     if (N <= 0) return;
     const unsigned nb = blocks_for(N, 256);
     switch (d) {
-        case 1: k32_corr<1><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
-        case 2: k32_corr<2><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
-        case 3: k32_corr<3><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
-        case 4: k32_corr<4><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
-        case 5: k32_corr<5><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
-        case 6: k32_corr<6><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
+        case 1: k16_corr<float, 1><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
+        case 2: k16_corr<float, 2><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
+        case 3: k16_corr<float, 3><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
+        case 4: k16_corr<float, 4><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
+        case 5: k16_corr<float, 5><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
+        case 6: k16_corr<float, 6><<<nb, 256, 0, s>>>(N, perm, iperm, cT, fT, C, mu, P, flags, scale, Y); break;
         default: throw std::invalid_argument("quadRule out of range");
     }
     HIP_LAUNCH_CHECK();

@@ -56,6 +56,7 @@ enum StageMask : int {
     kStageStencil = 4,  // nearRemoval + refineAddOn
     kStageSing = 8,     // singularAddOn
     kStageAll = 15,
+    kStageForward = 16,  // 16-RHS fp64 operator (f64op.hip): Y = X - K (sigma_s X) instead of Y = K X
 };
 
 constexpr int kTierThreads = 256;  // workgroup of the down pass tasks
@@ -109,6 +110,30 @@ void launch32_corr(int d, int64_t N, const int* perm, const int* iperm, const fl
 void launch32_conv_m2l(int64_t npairs, const double* Kd, void* K32, hipStream_t s);
 void launch32_conv_near(int nl, const int4* info, const int64_t* koffD, const int64_t* koff, const int* srcCount,
                         const double* Kd, void* K32, hipStream_t s);
+// the fp64 16-right-hand-side operator on MFMA (f64op.hip): the same plan and
+// layouts as the fp32 one, expansions as 64 lanes x 4 doubles
+void launch64_p2m(int nleaf, const int* leaves, const int64_t* begin, const int64_t* count, const double* ncx,
+                  const double* ncy, const double* nrx, const double* nry, const double* pxT, const double* pyT,
+                  const double* X, const double* sigT, const double* wT, const Params* P, void* mult, double* fT,
+                  double* cT, hipStream_t s);
+void launch64_m2m(int nn, const int* nodes, const int4* child, const int64_t* count, const void* Rup, void* mult,
+                  hipStream_t s);
+void launch64_m2l(int ntgt, const int* tgt, const int64_t* ptr, const int* src, const void* K64, const void* mult,
+                  void* local, hipStream_t s);
+void launch64_l2l(int nn, const int* nodes, const int* parent, const int* slot, const void* Rdn, void* local,
+                  hipStream_t s);
+void launch64_leaf(int nleaf, const int4* leafInfo, const int64_t* nearPtr, const int* nearPts, const int64_t* koff,
+                   const void* Knear, const int* level, const double* ncx, const double* ncy, const double* nrx,
+                   const double* nry, const double* pxT, const double* pyT, const Params* P, const void* local,
+                   const double* fT, const double* X, double scale, int flags, double* Y, hipStream_t s);
+void launch64_corr(int d, int64_t N, const int* perm, const int* iperm, const double* cT, const double* fT,
+                   const double* C, const double* mu, const Params* P, int flags, double scale, double* Y,
+                   hipStream_t s);
+void launch64_lane_major(int64_t npairs, double* K, hipStream_t s);
+void launch64_conv_near(int nl, const int4* info, const int64_t* koffD, const int64_t* koff, const int* srcCount,
+                        const double* Kd, void* K64, hipStream_t s);
+void launch64_gather16(int64_t N, int k, const int* perm, const double* Q, double* X16, hipStream_t s);
+void launch64_scatter16(int64_t N, int k, const int* perm, const double* Y16, double* Out, hipStream_t s);
 // the tier-0 root records of a sharded apply without upper tiers, scattered back
 // from the all-gather (mult[nodes[j]] = recv[j] where nodes[j] >= 0)
 void launch_roots_unpack(int K, int nslots, const int* nodes, const double* recv, double* mult, hipStream_t s);

@@ -84,6 +84,18 @@ def forward_block(op, X, Y):
         ys.neg_().add_(xs)
 
 
+def forward16(op, X, W, perm):
+    """W = X - K_0(sigma_s .* X) for 16 rows on the fp64 MFMA operator
+    (Aniso.forward16_f64_dev: tree order, point-major; every FMM translation a
+    16 x 16 x 16 v_mfma_f64_16x16x4_f64 product)."""
+    import torch
+
+    X16 = X[:, perm].t().contiguous()
+    Y16 = torch.empty_like(X16)
+    op.forward16_f64_dev(X16, Y16)
+    W[:, perm] = Y16.t()
+
+
 def rhs_block(op, Q):
     """rhs_k = K_0 q_k (main.cpp:121-124: the right-hand side is the mapping of q)."""
     import torch
@@ -170,17 +182,21 @@ def _inner_gmres(apply, R, m, tol, max_cycles, rd=1):
     return D, its
 
 
-def gmres_mixed(op, B, tol=1e-12, m=40, inner_tol=1e-6, max_outer=30, max_cycles=20, fp32_op=None):
+def gmres_mixed(op, B, tol=1e-12, m=40, inner_tol=1e-6, max_outer=30, max_cycles=20, fp32_op=None, fp64_mfma=None):
     """Solve A X = B (rows) to ||B - A X|| / ||B|| <= tol per row.  Returns
     (X, outer iterations, inner iterations, final relative residuals).
 
     fp32_op (default: when B has 16 rows): the inner solves run on the fp32 MFMA
     operator (Aniso.forward_f32_dev, fp32 caches) in tree order, point-major; the
-    outer residuals stay on the fp64 operator, so the solution is fp64-accurate."""
+    outer residuals stay in fp64, so the solution is fp64-accurate.
+    fp64_mfma (default: when B has 16 rows): the outer fp64 residuals run on the fp64
+    MFMA operator (Aniso.forward16_f64_dev) instead of two 8-row VALU batches."""
     import torch
 
     if fp32_op is None:
         fp32_op = B.shape[0] == 16
+    if fp64_mfma is None:
+        fp64_mfma = B.shape[0] == 16 and hasattr(op, "forward16_f64_dev")
     X = torch.zeros_like(B)
     W = torch.empty_like(B)
     bn = torch.linalg.norm(B, dim=1)
@@ -195,8 +211,13 @@ def gmres_mixed(op, B, tol=1e-12, m=40, inner_tol=1e-6, max_outer=30, max_cycles
             op.forward_f32_dev(X32, W32)
             Wout.copy_(W32)
 
+    if fp64_mfma:
+        perm64 = torch.tensor(op.tree_perm(), device=B.device, dtype=torch.int64)
     for outer in range(max_outer + 1):
-        forward_block(op, X, W)
+        if fp64_mfma:
+            forward16(op, X, W, perm64)
+        else:
+            forward_block(op, X, W)
         R = B - W
         rel = (torch.linalg.norm(R, dim=1) / bn).cpu().numpy()
         if (rel <= tol).all() or outer == max_outer:

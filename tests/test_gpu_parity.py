@@ -1246,3 +1246,41 @@ def test_block_solve_matches_gmres_over_oracle(sz, restart):
     its_d, _, rr_d = a.block_solve_dev(rd, xd, restart, tol, 400)
     assert its_d > 0 and rr_d <= tol
     assert _rel(xd.cpu().numpy().reshape(-1), xr) <= 1e-10
+
+
+@pytest.mark.parametrize("sz,d,ml,coeffs", [(64, 1, 20, "main"), (30, 3, 20, "rough"), (24, 1, 2, "rough"),
+                                            (11, 3, 20, "main"), (13, 2, 20, "rough"), (1, 3, 20, "main")])
+def test_fp64_mfma_operator_matches_vector_path(sz, d, ml, coeffs):
+    """The fp64 16-right-hand-side operator on v_mfma_f64_16x16x4_f64 (f64op.hip):
+    main.cpp's forward operator and the mapping of modes 1 and 2 against the VALU
+    path column by column (<= 1e-13: fp64 throughout, only the summation order
+    differs), and aniso_mapping_batched for 11 and 16 columns (which runs on it)
+    against per-column mapping and the oracle.  Uniform, d = 3, maxLevel-limited,
+    odd sz, d = 2, and the single-leaf tree."""
+    torch = _torch()
+    a, o, xy = _pair(sz, d, 2, 8, ml, coeffs, seed=4)
+    for m in range(3):
+        a.cache(m)
+    rng = np.random.default_rng(sz + d)
+    X = torch.tensor(rng.uniform(-1, 1, (a.N, 16)), device="cuda")
+    Y = torch.zeros_like(X)
+    a.forward16_f64_dev(X, Y)
+    Xc = X.t().contiguous()
+    ref = torch.zeros_like(Xc)
+    for j in range(16):
+        a.forward_tree_dev(Xc[j], ref[j])
+    torch.cuda.synchronize()
+    assert float(torch.linalg.norm(Y.t() - ref) / torch.linalg.norm(ref)) <= 1e-13
+    for m in (1, 2):
+        a.mapping16_f64_dev(m, X, Y)
+        for j in range(16):
+            a.mapping_tree_dev(Xc[j], m, ref[j])
+        torch.cuda.synchronize()
+        assert float(torch.linalg.norm(Y.t() - ref) / torch.linalg.norm(ref)) <= 1e-13, m
+    for k, m in ((11, 1), (16, 0)):
+        Q = rng.uniform(-1, 1, (a.N, k))
+        B = a.mapping_batched(Q, m)
+        o.cache(m)
+        for j in (0, k - 1):
+            assert _rel(B[:, j], a.mapping(Q[:, j], m)) <= 1e-13
+            assert _rel(B[:, j], o.mapping(Q[:, j], m)) <= TOL

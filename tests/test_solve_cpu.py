@@ -23,6 +23,12 @@ class DenseOp:
     def tree_perm(self):
         return self.perm
 
+    def forward16_f64_dev(self, X, Y):
+        """The fp64 MFMA operator's call shape: (n, 16) float64, tree order, point-major."""
+        K = self.K[self.perm][:, self.perm]
+        s = self.sig[self.perm]
+        Y.copy_(X - K @ (s[:, None] * X))
+
     def forward_f32_dev(self, X, Y):
         """The fp32 operator's call shape: (n, 16) float32, tree order, point-major."""
         K = self.K[self.perm][:, self.perm].float()
@@ -49,15 +55,16 @@ def test_config5_charges_are_gaussian_bumps_in_the_box():
 import pytest  # noqa: E402
 
 
-@pytest.mark.parametrize("fp32_op", [True, False])
-def test_mixed_gmres_matches_dense_solve_for_16_rhs(fp32_op):
+@pytest.mark.parametrize("fp32_op,fp64_mfma", [(True, True), (False, False), (True, False)])
+def test_mixed_gmres_matches_dense_solve_for_16_rhs(fp32_op, fp64_mfma):
     """Both inner operators: the fp32 one (tree order, point-major, as
-    Aniso.forward_f32_dev) and the fp64 row-layout one."""
+    Aniso.forward_f32_dev) and the fp64 row-layout one; the outer fp64 residual
+    through the 16-RHS operator's layout (Aniso.forward16_f64_dev) or the rows."""
     n, k = 300, 16
     op = DenseOp(n, 1)
     A = np.eye(n) - op.K.numpy() * op.sig.numpy()[None, :]
     B = torch.tensor(np.random.default_rng(2).uniform(-1, 1, (k, n)))
-    X, outer, inner, rel = gmres_mixed(op, B, tol=1e-12, m=30, inner_tol=1e-6, fp32_op=fp32_op)
+    X, outer, inner, rel = gmres_mixed(op, B, tol=1e-12, m=30, inner_tol=1e-6, fp32_op=fp32_op, fp64_mfma=fp64_mfma)
     ref = np.linalg.solve(A, B.numpy().T).T
     assert (rel <= 1e-12).all() and outer >= 2  # fp32 inner solves need refinement
     assert np.linalg.norm(X.numpy() - ref) / np.linalg.norm(ref) <= 1e-10
