@@ -19,6 +19,22 @@ _lib = None
 STAGE_FAR, STAGE_NEAR, STAGE_STENCIL, STAGE_SING, STAGE_ALL = 1, 2, 4, 8, 15
 
 
+# the caller-supplied collectives of the library's multi-GPU exchange (aniso_collectives)
+COLL_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                  ctypes.c_void_p)
+COLL_ALLTOALLV = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                  ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                  ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p)
+COLL_ALLREDUCE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+
+
+class Collectives(ctypes.Structure):
+    """aniso_collectives (include/aniso_mi355x.h)."""
+
+    _fields_ = [("ctx", ctypes.c_void_p), ("allgather", COLL_ALLGATHER), ("alltoallv", COLL_ALLTOALLV),
+                ("allreduce", COLL_ALLREDUCE)]
+
+
 class AnisoError(RuntimeError):
     """Raised for any non-zero status of the C ABI (mexErrMsgIdAndTxt analogue)."""
 
@@ -94,6 +110,11 @@ def lib():
             "aniso_block_op_begin_dev": [P, I, P, I64, P, I64, P, P],
             "aniso_block_op_end_dev": [P, I, P, I64, P, I64, P, P],
             "aniso_last_error": [ctypes.c_char_p, ctypes.c_size_t],
+            "aniso_comm_unique_id": [ctypes.c_char_p],
+            "aniso_comm_init_rccl": [P, ctypes.c_char_p],
+            "aniso_comm_init_callbacks": [P, ctypes.POINTER(Collectives)],
+            "aniso_block_op_sharded_dev": [P, I, P, I64, P, I64, P],
+            "aniso_memcpy": [P, P, ctypes.c_size_t],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -447,6 +468,29 @@ class Aniso:
                                            len(hist), ctypes.byref(it), ctypes.byref(rr), ctypes.c_void_p(s)))
         return it.value, hist[: min(abs(it.value), len(hist))], rr.value
 
+    # ---- the library's own multi-GPU exchange (aniso_comm_*)
+    def comm_init_rccl(self, unique_id):
+        """Attach an RCCL communicator (every rank together, after set_shard)."""
+        _check(lib().aniso_comm_init_rccl(self.address, bytes(unique_id)))
+
+    def comm_init_callbacks(self, coll):
+        """Attach caller-supplied collectives (a Collectives structure; kept alive here)."""
+        self._coll = coll
+        _check(lib().aniso_comm_init_callbacks(self.address, ctypes.byref(coll)))
+
+    def block_op_sharded_dev(self, which, x, y, stream=None):
+        """One call of the sharded aniso.m operator: x (ks, N) tree order holds this
+        rank's own range (its halo is filled here), y's owned slice receives the result."""
+        import torch
+
+        _dev_rows(x, self.ks, self.N, "x")
+        _dev_rows(y, self.ks, self.N, "y")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_block_op_sharded_dev(self.address, int(which), ctypes.c_void_p(x.data_ptr()),
+                                                int(x.stride(0)), ctypes.c_void_p(y.data_ptr()), int(y.stride(0)),
+                                                ctypes.c_void_p(s)))
+        return y
+
     def set_shard(self, rank, nranks):
         _check(lib().aniso_set_shard(self.address, int(rank), int(nranks)))
 
@@ -551,6 +595,18 @@ class Aniso:
         out = np.zeros(seg.shape[0])
         _check(lib().aniso_line_integrals(self.address, _dp(seg), seg.shape[0], _dp(out)))
         return out
+
+
+def comm_unique_id():
+    """A fresh RCCL unique id (128 bytes) for aniso_comm_init_rccl."""
+    b = ctypes.create_string_buffer(128)
+    _check(lib().aniso_comm_unique_id(b))
+    return b.raw
+
+
+def memcpy(dst, src, nbytes):
+    """aniso_memcpy: hipMemcpy between any two addresses (ints)."""
+    _check(lib().aniso_memcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), int(nbytes)))
 
 
 def block_mixes(nb, g, chi=True):

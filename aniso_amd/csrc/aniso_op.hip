@@ -110,6 +110,7 @@ void Operator::getNodes(double* xy) const {
 }
 
 void Operator::setShard(int rank, int nranks) {
+    comm.reset();  // a communicator belongs to one shard layout
     plan.build(tree, np, rank, nranks);
     plan.buildExchange(tree, geo.sz, geo.d2);
     plan.buildTopWait(tree);
@@ -1302,6 +1303,117 @@ void Operator::forwardF32Dev(const float* X, float* Y, hipStream_t s, int mask) 
         spans.push_back({7, e0, e5});
         ++applies;
     }
+}
+
+// Attach a communicator (every rank together) and build the halo exchange: each rank
+// receives, from the owner of each position of its halo (plan.xHalo), that position;
+// what it sends to peer p is p's halo inside its own range, so every rank's halo
+// ranges are exchanged once (one all-gather of the counts, one of the ranges).
+void Operator::commInit(std::unique_ptr<Collectives> c) {
+    if (!c) throw std::invalid_argument("null communicator");
+    if (c->nranks != plan.nranks || c->rank != plan.rank)
+        throw std::logic_error("communicator rank / size (" + std::to_string(c->rank) + " of " +
+                               std::to_string(c->nranks) + ") differ from the handle's shard (" +
+                               std::to_string(plan.rank) + " of " + std::to_string(plan.nranks) + ")");
+    ensureDevice();
+    comm.reset();
+    const int P = c->nranks, me = c->rank;
+    const int64_t nr = (int64_t)plan.xHalo.size() / 2;
+    DevBuf a, b;
+    a.alloc(sizeof(double));
+    b.alloc((size_t)P * sizeof(double));
+    double v = (double)nr;
+    HIP_CHECK(hipMemcpy(a.p, &v, sizeof(double), hipMemcpyHostToDevice));
+    c->allgather(a.as<double>(), b.as<double>(), 1, own);
+    HIP_CHECK(hipStreamSynchronize(own));
+    std::vector<double> counts(P);
+    HIP_CHECK(hipMemcpy(counts.data(), b.p, (size_t)P * sizeof(double), hipMemcpyDeviceToHost));
+    int64_t mx = 1;
+    for (double x : counts) mx = std::max<int64_t>(mx, (int64_t)x);
+    std::vector<double> mine((size_t)2 * mx, -1.0);
+    for (int64_t i = 0; i < 2 * nr; ++i) mine[i] = (double)plan.xHalo[i];
+    a.alloc((size_t)2 * mx * sizeof(double));
+    b.alloc((size_t)P * 2 * mx * sizeof(double));
+    HIP_CHECK(hipMemcpy(a.p, mine.data(), (size_t)2 * mx * sizeof(double), hipMemcpyHostToDevice));
+    c->allgather(a.as<double>(), b.as<double>(), (size_t)2 * mx, own);
+    HIP_CHECK(hipStreamSynchronize(own));
+    std::vector<double> all((size_t)P * 2 * mx);
+    HIP_CHECK(hipMemcpy(all.data(), b.p, all.size() * sizeof(double), hipMemcpyDeviceToHost));
+    const auto cuts = shard_cuts(tree, P);
+    if (cuts[me] != plan.ownBegin || cuts[me + 1] != plan.ownEnd) throw std::logic_error("shard cuts disagree with the plan");
+    const int nb = ks;
+    auto ranges = [&](int r) {  // rank r's halo ranges
+        std::vector<std::pair<int64_t, int64_t>> v;
+        for (int64_t i = 0; i < (int64_t)counts[r]; ++i)
+            v.push_back({(int64_t)all[((size_t)r * mx + i) * 2], (int64_t)all[((size_t)r * mx + i) * 2 + 1]});
+        return v;
+    };
+    auto intersect = [](const std::vector<std::pair<int64_t, int64_t>>& rs, int64_t lo, int64_t hi,
+                        std::vector<int64_t>& out) {
+        for (const auto& r : rs)
+            for (int64_t k = std::max(r.first, lo); k < std::min(r.second, hi); ++k) out.push_back(k);
+    };
+    std::vector<int64_t> spos, sbase, sstr, rpos, rbase, rstr;
+    hxScount.assign(P, 0);
+    hxSoff.assign(P, 0);
+    hxRcount.assign(P, 0);
+    hxRoff.assign(P, 0);
+    const auto myHalo = ranges(me);
+    for (int p = 0; p < P; ++p) {
+        hxSoff[p] = (int64_t)spos.size() * nb;
+        hxRoff[p] = (int64_t)rpos.size() * nb;
+        if (p == me) continue;
+        std::vector<int64_t> sp, rp;
+        intersect(ranges(p), plan.ownBegin, plan.ownEnd, sp);  // p's halo inside my range
+        intersect(myHalo, cuts[p], cuts[p + 1], rp);           // my halo inside p's range
+        for (size_t i = 0; i < sp.size(); ++i) {
+            spos.push_back(sp[i]);
+            sbase.push_back(hxSoff[p] + (int64_t)i);
+            sstr.push_back((int64_t)sp.size());
+        }
+        for (size_t i = 0; i < rp.size(); ++i) {
+            rpos.push_back(rp[i]);
+            rbase.push_back(hxRoff[p] + (int64_t)i);
+            rstr.push_back((int64_t)rp.size());
+        }
+        hxScount[p] = (int64_t)sp.size() * nb;
+        hxRcount[p] = (int64_t)rp.size() * nb;
+    }
+    hxNsend = (int64_t)spos.size();
+    hxNrecv = (int64_t)rpos.size();
+    up(dHxSendPos, spos);
+    up(dHxSendBase, sbase);
+    up(dHxSendStride, sstr);
+    up(dHxRecvPos, rpos);
+    up(dHxRecvBase, rbase);
+    up(dHxRecvStride, rstr);
+    dHxSendBuf.alloc((size_t)std::max<int64_t>(hxNsend * nb, 1) * sizeof(double));
+    dHxRecvBuf.alloc((size_t)std::max<int64_t>(hxNrecv * nb, 1) * sizeof(double));
+    const int64_t rec = (int64_t)plan.xRootChunk * kRank * rootRhs(nb);
+    dXRootsSend.alloc((size_t)std::max<int64_t>(rec, 1) * sizeof(double));
+    dXRootsRecv.alloc((size_t)std::max<int64_t>(rec * P, 1) * sizeof(double));
+    HIP_CHECK(hipMemset(dXRootsSend.p, 0, dXRootsSend.bytes));
+    comm = std::move(c);
+}
+
+void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, int64_t ldy, hipStream_t s) {
+    if (!comm) throw std::logic_error("sharded block operator before aniso_comm_init");
+    if (ldx < geo.N || ldy < geo.N) throw std::invalid_argument("sharded block operator: leading dimension below N");
+    ensureDevice();
+    const int nb = ks;
+    // the input's halo from its owners
+    launch_halo_pack(hxNsend, nb, dHxSendPos.as<int64_t>(), dHxSendBase.as<int64_t>(), dHxSendStride.as<int64_t>(),
+                     x, ldx, dHxSendBuf.as<double>(), s);
+    comm->alltoallv(dHxSendBuf.as<double>(), hxScount.data(), hxSoff.data(), dHxRecvBuf.as<double>(),
+                    hxRcount.data(), hxRoff.data(), s);
+    launch_halo_unpack(hxNrecv, nb, dHxRecvPos.as<int64_t>(), dHxRecvBase.as<int64_t>(), dHxRecvStride.as<int64_t>(),
+                       dHxRecvBuf.as<double>(), x, ldx, s);
+    // phase 1, the tier-0 root all-gather, phase 2 (the owned slice of y)
+    double* yo = y + plan.ownBegin;
+    blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 1, dXRootsSend.as<double>(), nullptr);
+    const int64_t rec = (int64_t)plan.xRootChunk * kRank * rootRhs(nb);
+    if (rec > 0) comm->allgather(dXRootsSend.as<double>(), dXRootsRecv.as<double>(), (size_t)rec, s);
+    blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 2, nullptr, dXRootsRecv.as<double>());
 }
 
 void Operator::checkDeviceErrors() {

@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "comm.hpp"
 #include "host.hpp"
 #include "kernels.hpp"
 
@@ -101,6 +102,12 @@ public:
 
     // --- extensions
     void setShard(int rank, int nranks);
+    // the library's own multi-GPU exchange (comm.hpp): attach a
+    // communicator of this shard's rank / nranks, then blockOpShardedDev runs the
+    // input's halo all-to-all, phase 1, the root all-gather and phase 2 in one call
+    void commInit(std::unique_ptr<Collectives> c);
+    void blockOpShardedDev(int which, double* x, int64_t ldx, double* y, int64_t ldy, hipStream_t s);
+    bool commReady() const { return comm != nullptr; }
     void getShard(int64_t* ownBegin, int64_t* ownEnd) const { *ownBegin = plan.ownBegin; *ownEnd = plan.ownEnd; }
     // sharded apply: writes only owned targets of out (original order), others untouched
     void permuteToTree(const double* orig, double* tree, hipStream_t s);
@@ -200,6 +207,14 @@ private:
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
     DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
+    // the attached communicator and its halo exchange plan (commInit): per element of
+    // the send / receive position lists its tree position and its place in the
+    // peer-major buffers (base + b * stride for block b); doubles per peer
+    std::unique_ptr<Collectives> comm;
+    DevBuf dHxSendPos, dHxSendBase, dHxSendStride, dHxRecvPos, dHxRecvBase, dHxRecvStride, dHxSendBuf, dHxRecvBuf;
+    DevBuf dXRootsSend, dXRootsRecv;
+    std::vector<int64_t> hxScount, hxSoff, hxRcount, hxRoff;
+    int64_t hxNsend = 0, hxNrecv = 0;
     // sticky time-out flag of the fused launch's in-kernel hand-offs, in host-visible
     // memory (the kernel stores 1 there when a wait gives up; checked at every API
     // entry and by sync(), never read on the device)

@@ -11,6 +11,10 @@
 #include "aniso_op.hpp"
 #include "kernels.hpp"
 
+namespace aniso {
+[[noreturn]] void throw_hip(hipError_t e, const char* file, int line);
+}  // namespace aniso
+
 struct aniso_op_s {
     uint64_t magic = 0xA2150A2150ULL;
     aniso::Operator op;
@@ -576,6 +580,52 @@ int aniso_line_integrals(aniso_handle h, const double* seg, int n, double* out) 
         CHECK_PTR(seg);
         CHECK_PTR(out);
         get(h).lineIntegrals(seg, n, out);
+    });
+}
+
+int aniso_comm_unique_id(unsigned char* id) {
+    return guarded([&] {
+        CHECK_PTR(id);
+        aniso::rccl_unique_id(id);
+    });
+}
+
+int aniso_comm_init_rccl(aniso_handle h, const unsigned char* id) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(id);
+        auto& op = get(h);
+        op.commInit(aniso::make_rccl_collectives(id, op.plan.nranks, op.plan.rank));
+    });
+}
+
+int aniso_comm_init_callbacks(aniso_handle h, const aniso_collectives* c) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(c);
+        auto& op = get(h);
+        op.commInit(aniso::make_callback_collectives(*c, op.plan.nranks, op.plan.rank));
+    });
+}
+
+int aniso_block_op_sharded_dev(aniso_handle h, int which, double* x, int64_t ldx, double* y, int64_t ldy,
+                               void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(x);
+        CHECK_PTR(y);
+        auto& op = get(h);
+        op.blockOpShardedDev(which, x, ldx, y, ldy, stream ? (hipStream_t)stream : op.stream());
+    });
+}
+
+int aniso_memcpy(void* dst, const void* src, size_t bytes) {
+    return guarded([&] {
+        if (bytes == 0) return;
+        CHECK_PTR(dst);
+        CHECK_PTR(src);
+        const hipError_t e = hipMemcpy(dst, src, bytes, hipMemcpyDefault);
+        if (e != hipSuccess) aniso::throw_hip(e, __FILE__, __LINE__);
     });
 }
 

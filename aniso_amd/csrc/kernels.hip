@@ -303,4 +303,35 @@ void launch_line_integrals(int n, const double* seg, const double* stcoef, const
     HIP_LAUNCH_CHECK();
 }
 
+// ---- halo exchange of the sharded apply (comm.hpp)
+__global__ void k_halo_pack(int64_t n, int nb, const int64_t* __restrict__ pos, const int64_t* __restrict__ base,
+                            const int64_t* __restrict__ stride, const double* __restrict__ x, int64_t ldx,
+                            double* __restrict__ buf) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    for (int b = 0; b < nb; ++b) buf[base[j] + b * stride[j]] = x[(size_t)b * ldx + pos[j]];
+}
+
+__global__ void k_halo_unpack(int64_t n, int nb, const int64_t* __restrict__ pos, const int64_t* __restrict__ base,
+                              const int64_t* __restrict__ stride, const double* __restrict__ buf,
+                              double* __restrict__ x, int64_t ldx) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    for (int b = 0; b < nb; ++b) x[(size_t)b * ldx + pos[j]] = buf[base[j] + b * stride[j]];
+}
+
+void launch_halo_pack(int64_t n, int nb, const int64_t* pos, const int64_t* base, const int64_t* stride,
+                      const double* x, int64_t ldx, double* buf, hipStream_t s) {
+    if (n <= 0) return;
+    k_halo_pack<<<blocks_for(n, 256), 256, 0, s>>>(n, nb, pos, base, stride, x, ldx, buf);
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_halo_unpack(int64_t n, int nb, const int64_t* pos, const int64_t* base, const int64_t* stride,
+                        const double* buf, double* x, int64_t ldx, hipStream_t s) {
+    if (n <= 0) return;
+    k_halo_unpack<<<blocks_for(n, 256), 256, 0, s>>>(n, nb, pos, base, stride, buf, x, ldx);
+    HIP_LAUNCH_CHECK();
+}
+
 }  // namespace aniso

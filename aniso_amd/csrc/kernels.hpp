@@ -271,6 +271,12 @@ void launch_cache_att_m2l(int64_t npairs, const int* pairTgt, const int* src, co
 void launch_sigma_diag(int64_t N, const double* pxT, const double* pyT, const double* stcoef, const Params* P,
                        double* out, hipStream_t s);
 void launch_permute(int64_t N, const int* perm, const double* orig, double* tree, hipStream_t s);
+// halo exchange of an nb-block vector (comm.hpp): element j of a position list goes
+// to / comes from buf[base[j] + b * stride[j]] for block b, vector entry x[b * ldx + pos[j]]
+void launch_halo_pack(int64_t n, int nb, const int64_t* pos, const int64_t* base, const int64_t* stride,
+                      const double* x, int64_t ldx, double* buf, hipStream_t s);
+void launch_halo_unpack(int64_t n, int nb, const int64_t* pos, const int64_t* base, const int64_t* stride,
+                        const double* buf, double* x, int64_t ldx, hipStream_t s);
 
 // host-callable device helpers used by tests through the C ABI
 void launch_line_integrals(int n, const double* seg, const double* stcoef, const Params* P, double* out,

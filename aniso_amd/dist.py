@@ -140,3 +140,119 @@ def sharded_block_matvec(op, xchg, which=2):
         op.block_op_end_dev(which, full, y, xchg.roots_recv, xchg.world)
 
     return apply
+
+
+class HostCollectives:
+    """aniso_collectives over a torch.distributed group with host staging (gloo): the
+    library's own exchange (aniso_comm_init_callbacks) driven through CPU collectives,
+    so several ranks may share one GPU (RCCL refuses that).  copy(dst, src, nbytes)
+    moves bytes between device and host addresses (aniso_amd.memcpy; tests on the
+    CPU pass ctypes.memmove)."""
+
+    def __init__(self, world, copy=None):
+        import ctypes
+
+        import torch.distributed as dist
+
+        import aniso_amd
+
+        self.world, self.dist = world, dist
+        self.copy = copy or aniso_amd.memcpy
+        self.errors = []
+        self.struct = aniso_amd.Collectives(None, aniso_amd.COLL_ALLGATHER(self._allgather),
+                                            aniso_amd.COLL_ALLTOALLV(self._alltoallv),
+                                            aniso_amd.COLL_ALLREDUCE(self._allreduce))
+        self._ct = ctypes
+
+    def _host(self, ptr, n):
+        buf = np.empty(int(n), dtype=np.float64)
+        if n:
+            self.copy(buf.ctypes.data, ptr, 8 * int(n))
+        return buf
+
+    def _back(self, ptr, arr):
+        arr = np.ascontiguousarray(arr, dtype=np.float64)
+        if arr.size:
+            self.copy(ptr, arr.ctypes.data, 8 * arr.size)
+
+    def _guard(self, fn):
+        try:
+            fn()
+            return 0
+        except Exception as ex:  # a failure becomes the callback's status (the library raises)
+            self.errors.append(repr(ex))
+            return 1
+
+    def _allgather(self, ctx, send, recv, count, stream):
+        import torch
+
+        def run():
+            t = torch.from_numpy(self._host(send, count))
+            parts = [torch.empty(int(count), dtype=torch.float64) for _ in range(self.world)]
+            self.dist.all_gather(parts, t)
+            self._back(recv, torch.cat(parts).numpy())
+        return self._guard(run)
+
+    def _alltoallv(self, ctx, send, scount, soff, recv, rcount, roff, stream):
+        import torch
+
+        def run():
+            sc = [int(scount[p]) for p in range(self.world)]
+            rc = [int(rcount[p]) for p in range(self.world)]
+            so = [int(soff[p]) for p in range(self.world)]
+            ro = [int(roff[p]) for p in range(self.world)]
+            sbuf = self._host(send, max((o + c for o, c in zip(so, sc)), default=0))
+            st = torch.from_numpy(np.concatenate([sbuf[o:o + c] for o, c in zip(so, sc)]) if sum(sc) else np.zeros(0))
+            rt = torch.empty(sum(rc), dtype=torch.float64)
+            self.dist.all_to_all_single(rt, st, rc, sc)
+            r = rt.numpy()
+            pos = 0
+            for o, c in zip(ro, rc):
+                if c:
+                    self._back(recv + 8 * o, r[pos:pos + c])
+                pos += c
+        return self._guard(run)
+
+    def _allreduce(self, ctx, buf, count, stream):
+        import torch
+
+        def run():
+            t = torch.from_numpy(self._host(buf, count))
+            self.dist.all_reduce(t)
+            self._back(buf, t.numpy())
+        return self._guard(run)
+
+
+def native_comm_init(op, world, backend="nccl"):
+    """Attach the library's own communicator to a sharded handle (every rank together):
+    RCCL from a unique id broadcast over torch.distributed, or the host-staged
+    callbacks (gloo).  Returns the callbacks object (keep it alive) or None."""
+    import torch.distributed as dist
+
+    import aniso_amd
+
+    if backend == "nccl":
+        uid = [aniso_amd.comm_unique_id() if dist.get_rank() == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        op.comm_init_rccl(uid[0])
+        return None
+    coll = HostCollectives(world)
+    op.comm_init_callbacks(coll.struct)
+    return coll
+
+
+def native_block_matvec(op, nb, device, which=2):
+    """apply(x, y) for aniso_amd.solve.gmres_dist on this rank's owned slices over the
+    library's one-call sharded operator (aniso_block_op_sharded_dev)."""
+    import torch
+
+    b, e = op.shard()
+    fx = torch.zeros(nb, op.N, dtype=torch.float64, device=device)
+    fy = torch.zeros_like(fx)
+
+    def apply(x, y):
+        fx[:, b:e] = x
+        op.block_op_sharded_dev(which, fx, fy)
+        y.copy_(fy[:, b:e])
+
+    return apply

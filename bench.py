@@ -221,6 +221,9 @@ def main():
     ap.add_argument("--same-device", action="store_true",
                     help="all ranks on cuda:0 (rehearse the sharded path on a one-GPU box; use --backend gloo)")
     ap.add_argument("--verify", action="store_true", help="check the sharded matvec against an unsharded operator")
+    ap.add_argument("--comm", default="native", choices=["native", "python"],
+                    help="N>1 exchange: the library's own (one C call per matvec, RCCL or gloo callbacks) or "
+                         "aniso_amd.dist.ShardExchange between the two phases")
     ap.add_argument("--gmres", type=int, default=30,
                     help="steps of the GMRES leg (aniso_amd.solve.gmres_dist over this run's matvec; 0: skip)")
     ap.add_argument("--no-solve", action="store_true", help="skip the one-GPU aniso.m solve (aniso_block_solve)")
@@ -261,6 +264,8 @@ def main():
         xchg0 = adist.ShardExchange(op, rank, world, 1, "cuda", args.backend) if block else xchg
         ob, oe = xchg.own
     op.setCoeff(ss, st)
+    native = world > 1 and block and args.comm == "native"
+    coll = adist.native_comm_init(op, world, args.backend) if native else None  # noqa: F841 (kept alive)
     modes = list(range(2 * ks - 1))
     t0 = time.time()
     for m in modes:
@@ -283,6 +288,10 @@ def main():
     def matvec(x, y):
         if world == 1:
             local_apply(x, y)
+            return
+        if native:
+            # one library call: x's halo all-to-all, phase 1, the root all-gather, phase 2
+            op.block_op_sharded_dev(2, x, y)
             return
         # phase 1 (own + halo up tasks, near field), the root all-gather, phase 2
         # (upper tiers, M2L, down pass into the owned slice of y), the halo of y
@@ -436,7 +445,9 @@ def main():
     }
     if world > 1:
         line["exchange"] = {"root_allgather_bytes_per_rank": 8 * xchg.C * xchg.R,
-                            "halo_bytes_received": xchg.halo_bytes(), "backend": args.backend}
+                            "halo_bytes_received": xchg.halo_bytes(), "backend": args.backend,
+                            "comm": ("library (aniso_block_op_sharded_dev: halo all-to-all, phase 1, root all-gather, "
+                                     "phase 2 in one call)" if native else "aniso_amd.dist.ShardExchange")}
     line.update(sec)  # mode-0 operator and deterministic block matvec (measured before the headline leg)
     if args.gmres > 0 and block:
         # GMRES over this run's (possibly sharded) block matvec: aniso_amd.solve.gmres_dist,
@@ -454,7 +465,7 @@ def main():
             gred = None
         else:
             gb = rhs0[:, ob:oe].contiguous()
-            gapply = adist.sharded_block_matvec(op, xchg)
+            gapply = adist.native_block_matvec(op, nb, "cuda") if native else adist.sharded_block_matvec(op, xchg)
             gred = xchg.allreduce
         gmres_dist(gapply, gb, restart=2, tol=0.0, maxit=1, allreduce=gred)  # warm-up
         if world > 1:
@@ -480,7 +491,15 @@ def main():
         # an unsharded operator on the same device
         U = torch.tensor(np.random.default_rng(1).uniform(-1, 1, (nb, N)), device="cuda")
         got = torch.zeros_like(U)
-        matvec(U[:, perm].contiguous(), got)  # tree order in and out
+        Ut = U[:, perm].contiguous()
+        xin = Ut.clone()
+        if world > 1:  # the input holds the rank's own range only (NaN elsewhere)
+            xin.fill_(float("nan"))
+            xin[:, ob:oe] = Ut[:, ob:oe]
+            if not native:
+                for lo, hi in xchg.halos[rank]:
+                    xin[:, lo:hi] = Ut[:, lo:hi]
+        matvec(xin, got)  # tree order in and out
         ref_op = aniso_amd.Aniso(args.sz, args.d, ks, args.g, args.ns, 4, args.max_level)
         ref_op.setCoeff(ss, st)
         for m in modes:
@@ -493,15 +512,20 @@ def main():
         torch.cuda.synchronize()
         ref = ref[:, perm]
         b_, e_ = (ob, oe) if world > 1 else (0, N)
-        # owned slice of every rank (and its halo, filled by the exchange) vs the unsharded operator
+        # owned slice of every rank vs the unsharded operator; the halo the exchange filled
+        # (native: the input's, from the owners; python: the output's, after the matvec)
         sq = torch.tensor([float(torch.sum((got[:, b_:e_] - ref[:, b_:e_]) ** 2)),
                            float(torch.sum(ref[:, b_:e_] ** 2))], dtype=torch.float64)
         if world > 1:
             hal = [torch.arange(lo, hi, device="cuda") for lo, hi in xchg.halos[rank]]
             if hal:
                 hi_ = torch.cat(hal)
-                line["verify_halo_rel_err"] = float(torch.linalg.norm(got[:, hi_] - ref[:, hi_])
-                                                    / torch.linalg.norm(ref[:, hi_]))
+                if native:
+                    line["verify_halo_rel_err"] = float(torch.linalg.norm(xin[:, hi_] - Ut[:, hi_])
+                                                        / torch.linalg.norm(Ut[:, hi_]))
+                else:
+                    line["verify_halo_rel_err"] = float(torch.linalg.norm(got[:, hi_] - ref[:, hi_])
+                                                        / torch.linalg.norm(ref[:, hi_]))
             sq = sq.to("cuda") if args.backend == "nccl" else sq
             dist.all_reduce(sq)
         line["verify_rel_err_vs_unsharded"] = float((sq[0] / sq[1]) ** 0.5)

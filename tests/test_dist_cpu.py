@@ -266,3 +266,65 @@ def test_gloo_sharded_gmres_matches_one_rank(world):
         assert np.allclose(v["hist"], h1, rtol=1e-6, atol=1e-14)
         x[v["lo"]:v["hi"]] = v["x"]
     assert np.linalg.norm(x - x1.numpy()) / np.linalg.norm(x1.numpy()) <= 1e-10
+
+
+def _coll_worker(rank, world, port, result_q):
+    """The host-staged callbacks of the library's exchange (aniso_amd.dist.HostCollectives),
+    called through their C function pointers on host buffers (ctypes.memmove stands in
+    for the device copies)."""
+    import ctypes
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from aniso_amd.dist import HostCollectives
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = HostCollectives(world, copy=lambda d, s, n: ctypes.memmove(d, s, n))
+        st = c.struct
+        send = np.arange(3, dtype=np.float64) + 10 * rank
+        recv = np.zeros(3 * world)
+        rc1 = st.allgather(None, send.ctypes.data, recv.ctypes.data, 3, None)
+        # alltoallv: rank r sends (r + 1) * (p + 1) values r * 100 + p to peer p != r
+        sc = np.array([0 if p == rank else (rank + 1) * (p + 1) for p in range(world)], dtype=np.int64)
+        so = np.concatenate([[0], np.cumsum(sc)[:-1]]).astype(np.int64)
+        rcn = np.array([0 if p == rank else (p + 1) * (rank + 1) for p in range(world)], dtype=np.int64)
+        ro = np.concatenate([[0], np.cumsum(rcn)[:-1]]).astype(np.int64)
+        sbuf = np.concatenate([np.full(sc[p], rank * 100.0 + p) for p in range(world)])
+        rbuf = np.zeros(int(rcn.sum()) + 1)
+        P64 = ctypes.POINTER(ctypes.c_int64)
+        rc2 = st.alltoallv(None, sbuf.ctypes.data, sc.ctypes.data_as(P64), so.ctypes.data_as(P64), rbuf.ctypes.data,
+                           rcn.ctypes.data_as(P64), ro.ctypes.data_as(P64), None)
+        red = np.array([1.0 + rank, 2.0 * rank])
+        rc3 = st.allreduce(None, red.ctypes.data, 2, None)
+        result_q.put((rank, dict(rc=(rc1, rc2, rc3), recv=recv, rbuf=rbuf[:-1], rcn=rcn, red=red, errors=c.errors)))
+    except Exception as ex:
+        result_q.put((rank, repr(ex)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_host_collectives_of_the_native_exchange(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_coll_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        v = res[r]
+        assert isinstance(v, dict), v
+        assert v["rc"] == (0, 0, 0) and not v["errors"], v
+        assert np.array_equal(v["recv"], np.concatenate([np.arange(3) + 10 * p for p in range(world)]))
+        want = np.concatenate([np.full(v["rcn"][p], p * 100.0 + r) for p in range(world)])
+        assert np.array_equal(v["rbuf"], want)
+        assert np.allclose(v["red"], [sum(1.0 + p for p in range(world)), sum(2.0 * p for p in range(world))])

@@ -255,22 +255,29 @@ def test_uncached_mode_fails_loudly():
     assert e.value.code == 3
 
 
-def test_bench_sharded_path_rehearsal_two_ranks():
-    """bench.py's N>1 matvec (subtree shards + all-gather) with two ranks sharing
-    the one GPU of the box and gloo collectives; checked against the unsharded op."""
+@pytest.mark.parametrize("comm,port", [("native", 29533), ("python", 29534)])
+def test_bench_sharded_path_rehearsal_two_ranks(comm, port):
+    """bench.py's N>1 matvec (subtree shards, halo all-to-all, root all-gather) with
+    two ranks sharing the one GPU of the box over gloo: through the library's own
+    exchange (one C call per matvec, aniso_comm_init_callbacks) and through
+    aniso_amd.dist.ShardExchange; each rank's input holds only its own range (native)
+    or own range + halo (python), NaN elsewhere; checked against the unsharded op,
+    with the GMRES leg over the shards."""
     import subprocess
     import sys
 
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", "--master-port=29533", os.path.join(ROOT, "bench.py"),
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--sz", "128", "--backend", "gloo",
-           "--same-device", "--verify", "--no-cpu"]
+           "--same-device", "--verify", "--no-cpu", "--comm", comm, "--gmres", "6"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
     res = json.loads(line)
     assert res["n_gpus"] == 2
     assert res["verify_rel_err_vs_unsharded"] <= 1e-13
+    assert res["verify_halo_rel_err"] <= 1e-15
+    assert res["gmres"]["steps"] == 6 and res["gmres"]["relres_after"] < 1.0
 
 
 def test_rccl_shard_exchange_collectives_one_rank():
@@ -1284,3 +1291,49 @@ def test_fp64_mfma_operator_matches_vector_path(sz, d, ml, coeffs):
         for j in (0, k - 1):
             assert _rel(B[:, j], a.mapping(Q[:, j], m)) <= 1e-13
             assert _rel(B[:, j], o.mapping(Q[:, j], m)) <= TOL
+
+
+
+def test_native_exchange_one_rank_rccl_and_callbacks():
+    """The library's own exchange (aniso_comm_init_rccl / _callbacks +
+    aniso_block_op_sharded_dev: halo all-to-all, phase 1, root all-gather, phase 2 in
+    one call) on a one-rank shard: RCCL itself (a one-rank communicator; RCCL refuses
+    two ranks on one GPU) and caller-supplied callbacks equal the unsharded operator."""
+    torch = _torch()
+    import aniso_amd
+
+    ks = 5
+    full = aniso_amd.Aniso(64, 1, ks, 0.8, 10, 4, 20)
+    xy = full.getNodes()
+    coef = rough_coeffs(xy, 2)
+    full.setCoeff(*coef)
+    for m in range(2 * ks - 1):
+        full.cache(m)
+    X = torch.tensor(np.random.default_rng(6).uniform(-1, 1, (ks, full.N)), device="cuda")
+    ref = torch.zeros_like(X)
+    full.block_op_dev(2, X, ref, tree=True)
+    for kind in ("rccl", "callbacks"):
+        sh = aniso_amd.Aniso(64, 1, ks, 0.8, 10, 4, 20)
+        sh.set_shard(0, 1)
+        sh.setCoeff(*coef)
+        for m in range(2 * ks - 1):
+            sh.cache(m)
+        if kind == "rccl":
+            sh.comm_init_rccl(aniso_amd.comm_unique_id())
+        else:
+            def ag(ctx, send, recv, count, stream):
+                aniso_amd.memcpy(recv, send, 8 * count)
+                return 0
+
+            def a2a(ctx, send, sc, so, recv, rc, ro, stream):
+                return 0 if sc[0] == 0 and rc[0] == 0 else 1
+
+            def ar(ctx, buf, count, stream):
+                return 0
+
+            sh.comm_init_callbacks(aniso_amd.Collectives(None, aniso_amd.COLL_ALLGATHER(ag),
+                                                         aniso_amd.COLL_ALLTOALLV(a2a), aniso_amd.COLL_ALLREDUCE(ar)))
+        y = torch.zeros_like(X)
+        sh.block_op_sharded_dev(2, X.clone(), y)
+        sh.sync()
+        assert float(torch.linalg.norm(y - ref) / torch.linalg.norm(ref)) <= 1e-13, kind

@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import aniso_amd  # noqa: E402
-from bench import demo_coeffs, gaussian  # noqa: E402
+from bench import demo_coeffs, gaussian, main_coeffs  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--world", type=int, default=1)
@@ -21,6 +21,7 @@ ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--sz", type=int, default=1024)
+ap.add_argument("--ks", type=int, default=5, help="5: aniso.m block matvec; 1: main.cpp forward operator (mode 0)")
 ap.add_argument("cfgs", nargs="+")
 args = ap.parse_args()
 world, rank = args.world, args.rank
@@ -30,7 +31,7 @@ for cfg in args.cfgs:
     saved = {k: os.environ.get(k) for k, _ in kv}
     for k, v in kv:
         os.environ[k] = v
-    op = aniso_amd.Aniso(args.sz, 1, 5, 0.8, 10, 4, 20)
+    op = aniso_amd.Aniso(args.sz, 1, args.ks, 0.8, 10, 4, 20)
     for k, v in saved.items():
         if v is None:
             os.environ.pop(k, None)
@@ -40,13 +41,13 @@ for cfg in args.cfgs:
     perm = torch.tensor(op.tree_perm(), device="cuda", dtype=torch.int64)
     if world > 1:
         op.set_shard(rank, world)
-    op.setCoeff(*demo_coeffs(xy))
-    for m in range(9):
+    op.setCoeff(*(demo_coeffs(xy) if args.ks > 1 else main_coeffs(xy)))
+    for m in range(2 * args.ks - 1):
         op.cache(m)
     b, e = op.shard()
-    ex = op.shard_exchange(5)
+    ex = op.shard_exchange(args.ks)
     C, R = ex["root_chunk"], ex["root_record"]
-    x = torch.zeros(5, op.N, dtype=torch.float64, device="cuda")
+    x = torch.zeros(args.ks, op.N, dtype=torch.float64, device="cuda")
     x[0] = torch.tensor(gaussian(xy), device="cuda")[perm]
     y = torch.zeros_like(x)
     send = torch.zeros(max(C * R, 1), dtype=torch.float64, device="cuda")
@@ -56,13 +57,22 @@ for cfg in args.cfgs:
 
 def step(r):
     op, x, y = r["op"], r["x"], r["y"]
-    if world == 1:
-        op.block_op_dev(2, x, y, tree=True)
-        return
     b, e, C, R = r["b"], r["e"], r["C"], r["R"]
-    op.block_op_begin_dev(2, x, y[:, b:e], r["send"])
+    if world == 1:
+        if args.ks > 1:
+            op.block_op_dev(2, x, y, tree=True)
+        else:
+            op.forward_tree_dev(x[0], y[0])
+        return
+    if args.ks > 1:
+        op.block_op_begin_dev(2, x, y[:, b:e], r["send"])
+    else:
+        op.forward_tree_begin_dev(x[0], y[0, b:e], r["send"])
     r["recv"][rank * C * R:(rank + 1) * C * R].copy_(r["send"][: C * R])  # stands in for the all-gather
-    op.block_op_end_dev(2, x, y[:, b:e], r["recv"], world)
+    if args.ks > 1:
+        op.block_op_end_dev(2, x, y[:, b:e], r["recv"], world)
+    else:
+        op.forward_tree_end_dev(x[0], y[0, b:e], r["recv"], world)
 
 
 for rep in range(args.reps):
