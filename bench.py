@@ -227,6 +227,8 @@ def main():
     ap.add_argument("--gmres", type=int, default=30,
                     help="steps of the GMRES leg (aniso_amd.solve.gmres_dist over this run's matvec; 0: skip)")
     ap.add_argument("--no-solve", action="store_true", help="skip the one-GPU aniso.m solve (aniso_block_solve)")
+    ap.add_argument("--config4-sz", type=int, default=2048,
+                    help="secondary leg: BASELINE configs[3] (4M points, mode 0, sharded over the run's GPUs); 0 skips")
     args = ap.parse_args()
 
     import torch
@@ -486,6 +488,54 @@ def main():
                          "relres_after": grel,
                          "method": "aniso_amd.solve.gmres_dist: restarted GMRES, CGS2 (2 all-reduces per step), "
                                    "Krylov basis in HBM; tol 0 so exactly `steps` Arnoldi steps are timed"}
+    if args.config4_sz > 0 and block:
+        # BASELINE configs[3]: sz = 2048 (4,194,304 points), d = 1, mode 0 -- main.cpp's GMRES
+        # matvec u - K_0(sigma_s .* u), the configuration BASELINE names for 8 GPUs --
+        # sharded over this run's ranks like the headline (the library's one-call exchange at
+        # N > 1); its per-N rates give the strong scaling of the multi-GPU config
+        op4 = aniso_amd.Aniso(args.config4_sz, args.d, 1, args.g, args.ns, 4, args.max_level)
+        xy4 = op4.getNodes()
+        perm4 = torch.tensor(op4.tree_perm(), device="cuda", dtype=torch.int64)
+        if world > 1:
+            op4.set_shard(rank, world)
+        op4.setCoeff(*main_coeffs(xy4))
+        op4.cache(0)
+        if world > 1:
+            coll4 = adist.native_comm_init(op4, world, args.backend)  # noqa: F841 (kept alive)
+        x4 = torch.zeros(1, op4.N, dtype=torch.float64, device="cuda")
+        x4[0] = torch.tensor(gaussian(xy4), device="cuda")[perm4]
+        y4 = torch.zeros_like(x4)
+
+        def step4(a, b):
+            if world == 1:
+                op4.block_op_dev(2, a, b, tree=True)  # ks = 1: x - K_0(sigma_s x), main.cpp:125-136
+            else:
+                op4.block_op_sharded_dev(2, a, b)
+
+        for _ in range(2):
+            step4(x4, y4)
+            x4, y4 = y4, x4
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t4 = time.perf_counter()
+        for _ in range(args.steps):
+            step4(x4, y4)
+            x4, y4 = y4, x4
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el4 = time.perf_counter() - t4
+        if world > 1:
+            t = torch.tensor([el4], device="cuda", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el4 = float(t.item())
+        line["config4"] = {"workload": "configs[3]: sz=2048 (N=4194304), d=1, ns=10, mode 0: main.cpp GMRES matvec "
+                                       "u - K_0(sigma_s .* u), sharded by FMM subtree over the run's GPUs",
+                           "N": op4.N, "matvec_per_s": round(args.steps / el4, 3),
+                           "ms_per_step": round(1e3 * el4 / args.steps, 4), "steps": args.steps,
+                           "scaling": "strong", "n_gpus": world}
+        del op4
     if args.verify:
         # one matvec of a fixed block vector through this (possibly sharded) path vs
         # an unsharded operator on the same device

@@ -269,7 +269,7 @@ def test_bench_sharded_path_rehearsal_two_ranks(comm, port):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--sz", "128", "--backend", "gloo",
-           "--same-device", "--verify", "--no-cpu", "--comm", comm, "--gmres", "6"]
+           "--same-device", "--verify", "--no-cpu", "--comm", comm, "--gmres", "6", "--config4-sz", "256"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
@@ -278,6 +278,7 @@ def test_bench_sharded_path_rehearsal_two_ranks(comm, port):
     assert res["verify_rel_err_vs_unsharded"] <= 1e-13
     assert res["verify_halo_rel_err"] <= 1e-15
     assert res["gmres"]["steps"] == 6 and res["gmres"]["relres_after"] < 1.0
+    assert res["config4"]["N"] == 256 * 256 and res["config4"]["matvec_per_s"] > 0
 
 
 def test_rccl_shard_exchange_collectives_one_rank():
