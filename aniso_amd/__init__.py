@@ -85,6 +85,7 @@ def lib():
             "aniso_set_timing": [P, I],
             "aniso_stage_times": [P, fp],
             "aniso_line_integrals": [P, dp, I, dp],
+            "aniso_top_trace": [P, lp, I64, lp],
             "aniso_forward_dev": [P, P, P, P],
             "aniso_mapping_tree_dev": [P, P, I, P, P],
             "aniso_forward_tree_dev": [P, P, P, P],
@@ -589,6 +590,18 @@ class Aniso:
         t = (ctypes.c_float * 8)()
         _check(lib().aniso_stage_times(self.address, t))
         return dict(zip(["exchange", "up", "m2l", "gather", "near", "down", "corr", "total"], list(t)))
+
+    def top_trace(self):
+        """Per-block timeline of the last fused top-of-tree launch (ANISO_TOP_TRACE=1):
+        rows {start, waited, end (100 MHz ticks), hw id, kind (-k: up tier k, else the
+        cluster id), wait tier, targets, block reads}."""
+        n = ctypes.c_int64(0)
+        _check(lib().aniso_top_trace(self.address, None, 0, ctypes.byref(n)))
+        rec = np.zeros((n.value, 8), dtype=np.int64)
+        if n.value:
+            _check(lib().aniso_top_trace(self.address, rec.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n.value,
+                                         ctypes.byref(n)))
+        return rec
 
     def line_integrals(self, seg):
         seg = np.ascontiguousarray(np.asarray(seg, dtype=np.float64).reshape(-1, 4))

@@ -82,6 +82,8 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_OVERLAP")) overlap = std::atoi(e);
     if (const char* e = std::getenv("ANISO_FUSE_SUB")) fuseSub = e[0] != '0';
     if (const char* e = std::getenv("ANISO_TOP_SPIN_LIMIT")) topSpinLimit = (unsigned)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("ANISO_TOP_TRACE")) topTraceOn = std::atoi(e) != 0;
+    hmRing = hm_ring_depth();
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
     modes.resize(kernelSize);
@@ -159,6 +161,16 @@ void Operator::ensureDevice() {
     up(dNcy, tree.ncy);
     up(dNrx, tree.nrx);
     up(dNry, tree.nry);
+    {  // per node {cx, cy, rx, ry}: the source box one LDS-DMA lane pair fetches (k_m2l_hcr)
+        std::vector<double> g4((size_t)tree.nn * 4);
+        for (int i = 0; i < tree.nn; ++i) {
+            g4[4 * (size_t)i] = tree.ncx[i];
+            g4[4 * (size_t)i + 1] = tree.ncy[i];
+            g4[4 * (size_t)i + 2] = tree.nrx[i];
+            g4[4 * (size_t)i + 3] = tree.nry[i];
+        }
+        up(dNodeGeo, g4);
+    }
     up(dBegin, tree.begin);
     up(dCount, tree.count);
     up(dParent, tree.parent);
@@ -786,11 +798,19 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     };
     const bool clustered = harmonic && useClusters;
     const int ncl = (int)plan.hmClPtr.size() - 1;
+    HcArgs hca{dHmClPtr.as<int>(), dHmTgt.as<int>(), dHmPtr.as<int64_t>(), dHmNDir.as<int>(), dHmSrc.as<int>(),
+                     dHmBlk.as<int>(), dHmSlot.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(),
+                     dNrx.as<double>(), dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(),
+                     dNodeGeo.as<double>()};
+    if (hmRing > 0) {
+        const int xl = hm_ring_xl(K, plan.hmMaxCl, hmRing);
+        hca.ring = xl < 0 ? 0 : hmRing;
+        hca.ringXL = xl > 0;
+    }
     auto m2lClusters = [&](int c0, int c1, hipStream_t st) {
-        launch_m2l_hc(K, c1 - c0, plan.hmMaxCl, dHmClPtr.as<int>() + c0, dHmTgt.as<int>(), dHmPtr.as<int64_t>(),
-                      dHmNDir.as<int>(), dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(), dAttM2L.as<double>(),
-                      dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), P, hw,
-                      dMult.as<double>(), dLocal.as<double>(), st);
+        HcArgs a = hca;
+        a.clPtr += c0;
+        launch_m2l_hc(K, c1 - c0, plan.hmMaxCl, a, st);
     };
     int e0 = -1;
     bool nearDone = false;
@@ -861,11 +881,13 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             ta.recv1 = phase == 2 ? rootsRecv : nullptr;
             ta.spinLimit = topSpinLimit;
             HIP_CHECK(hipHostGetDevicePointer((void**)&ta.err, topErr, 0));
-            const HcArgs ha{dHmClPtr.as<int>(), dHmTgt.as<int>(), dHmPtr.as<int64_t>(), dHmNDir.as<int>(),
-                            dHmSrc.as<int>(), dHmBlk.as<int>(), dHmSlot.as<int>(), dAttM2L.as<double>(),
-                            dNcx.as<double>(), dNcy.as<double>(), dNrx.as<double>(), dNry.as<double>(), P, hw,
-                            dMult.as<double>(), dLocal.as<double>()};
-            launch_top_m2l_hc(K, ncl, plan.hmMaxCl, ua, ta, ha, s);
+            if (topTraceOn) {
+                topTraceBlocks = ta.nUp + ncl;
+                if (dTopTrace.bytes < (size_t)topTraceBlocks * 4 * sizeof(int64_t))
+                    dTopTrace.alloc((size_t)topTraceBlocks * 4 * sizeof(int64_t));
+                ta.trace = dTopTrace.as<int64_t>();
+            }
+            launch_top_m2l_hc(K, ncl, plan.hmMaxCl, ua, ta, hca, s);
         } else if (clustered) {
             m2lClusters(0, ncl, s);
         } else if (harmonic) {
@@ -1003,6 +1025,30 @@ void Operator::setTiming(bool on) {
             evPool.push_back(e);
         }
     }
+}
+
+std::vector<int64_t> Operator::topTrace() {
+    sync();
+    std::vector<int64_t> out;
+    if (!topTraceOn || topTraceBlocks == 0) return out;
+    std::vector<int64_t> raw((size_t)topTraceBlocks * 4);
+    HIP_CHECK(hipMemcpy(raw.data(), dTopTrace.p, raw.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
+    const int ntier = (int)plan.upTierTask.size() - 1;
+    const int u1 = plan.upTierTask[1], nUp = plan.upTierTask[ntier] - u1;
+    out.reserve((size_t)topTraceBlocks * 8);
+    for (int b = 0; b < topTraceBlocks; ++b) {
+        out.insert(out.end(), raw.begin() + 4 * b, raw.begin() + 4 * b + 4);
+        if (b < nUp) {
+            int k = 1;
+            while (k + 1 < ntier && b >= plan.upTierTask[k + 1] - u1) ++k;
+            out.insert(out.end(), {(int64_t)-k, (int64_t)(k - 1), 0, 0});
+        } else {
+            const int c = b - nUp, t0 = plan.hmClPtr[c], t1 = plan.hmClPtr[c + 1];
+            out.insert(out.end(), {(int64_t)c, (int64_t)plan.hmClWait[c], (int64_t)(t1 - t0),
+                                   (int64_t)(plan.hmPtr[t1] - plan.hmPtr[t0])});
+        }
+    }
+    return out;
 }
 
 StageTimes Operator::stageTimes() {

@@ -139,6 +139,10 @@ public:
     void checkDeviceErrors();
     // wait for every apply enqueued by this handle (both streams), then check
     void sync();
+    // development timeline of the last fused top-of-tree launch (ANISO_TOP_TRACE=1,
+    // tools/top_trace.py): per block 8 values {start, waited, end (100 MHz ticks), hw id,
+    // kind (-k: up tier k; else the cluster id), wait tier, targets, block reads}
+    std::vector<int64_t> topTrace();
     bool harmonicReady() const { return useAtt && attReady; }
     bool clustersOn() const { return useClusters; }
     // the block apply's upper up tiers ride in the clustered M2L launch (k_top_m2l_hc)
@@ -207,6 +211,10 @@ private:
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
     DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
+    DevBuf dTopTrace;           // ANISO_TOP_TRACE=1: the launch's per-block timeline
+    bool topTraceOn = false;
+    int hmRing = 0;  // the cluster M2L's LDS ring depth (ANISO_HM_RING; 0: the one-block-in-flight form)
+    int topTraceBlocks = 0;
     // the attached communicator and its halo exchange plan (commInit): per element of
     // the send / receive position lists its tree position and its place in the
     // peer-major buffers (base + b * stride for block b); doubles per peer
@@ -253,7 +261,7 @@ private:
     int mark(hipStream_t s);
     int maxNearS = 0;
     // geometry / tree on device
-    DevBuf dPxT, dPyT, dPerm, dW, dNcx, dNcy, dNrx, dNry, dBegin, dCount, dParent, dSlot, dChild, dIsLeaf;
+    DevBuf dPxT, dPyT, dPerm, dW, dNcx, dNcy, dNrx, dNry, dBegin, dCount, dParent, dSlot, dChild, dIsLeaf, dNodeGeo;
     DevBuf dLeaves, dNearPtr, dNearSrc, dNearKOff, dM2LTgt, dM2LPtr, dM2LSrc, dM2LPairTgt;
     DevBuf dUpTaskPtr, dUpGrpPtr, dUpGrp, dUpNode, dUpCode, dUpDesc, dUpGrpFix, dUpGeom, dUpLeaf;                       // up-pass tiers
     DevBuf dDnTaskPtr, dDnGrpPtr, dDnGrp, dDnNode, dDnLeafPtr, dDnLeafSlot, dDnLeafIdx, dDnLeafPts, dDnPtsRange, dDnDesc, dDnGrpFix, dDnLeafGeom;  // down

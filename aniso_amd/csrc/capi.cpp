@@ -574,6 +574,16 @@ int aniso_stage_times(aniso_handle h, float* t) {
     });
 }
 
+int aniso_top_trace(aniso_handle h, int64_t* rec, int64_t cap, int64_t* n) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(n);
+        const auto t = get(h).topTrace();
+        *n = (int64_t)t.size() / 8;
+        if (rec) std::copy(t.begin(), t.begin() + std::min<int64_t>(cap, *n) * 8, rec);
+    });
+}
+
 int aniso_line_integrals(aniso_handle h, const double* seg, int n, double* out) {
     ENTER(h);
     return guarded([&] {

@@ -225,6 +225,67 @@ __device__ __forceinline__ void hm_entry2(double e, double dx, double dy2, const
     }
 }
 
+// the end of a target in the cluster M2L: its 4 x K row sums per lane summed over the
+// 16 columns (lane bits 2..5) and added to its LDS locals at `at` (16 x K)
+template <int K>
+__device__ __forceinline__ void m2l_hc_store_target(double (&c)[4][K], double* at, int lane, int s, int q) {
+    if constexpr (K == 5) {
+        // sum over the 16 columns (lane bits 2..5) as a reduce-scatter of the lane's
+        // 20 row sums (rows 4q + j, entries i; v = 5 j + i): 20 -> 10 (lane ^ 32),
+        // 10 -> 5 (lane ^ 16), 5 -> 3 (lane ^ 8), 3 -> 2 (lane ^ 4); each of the 16
+        // column lanes then adds its <= 2 finished sums -- ~90 VALU ops, not ~360
+        const bool r4 = xor16_r4(lane);
+        const int k32 = swap_add32_f64(1.0, 0.0) > 1.5 ? 0 : 10;  // this lane keeps the first / second half
+        const int k16 = swap_add16_f64(1.0, 0.0) > 1.5 ? 0 : 5;
+        double v10[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) v10[k] = swap_add32_f64(c[k / 5][k % 5], c[(k + 10) / 5][(k + 10) % 5]);
+        double v5[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) v5[k] = swap_add16_f64(v10[k], v10[k + 5]);
+        const bool h1 = (lane >> 3) & 1, h0 = (lane >> 2) & 1;
+        double v3[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {  // lane ^ 8: h1 = 0 keeps k, h1 = 1 keeps k + 3
+            const double x = v5[k], y = k + 3 < 5 ? v5[k + 3] : 0.0;
+            v3[k] = (h1 ? y : x) + dpp_f64<0x128>(h1 ? x : y);
+        }
+        double* d = at;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {  // lane ^ 4: h0 = 0 keeps u, h0 = 1 keeps u + 2
+            const double x = v3[u], y = u + 2 < 3 ? v3[u + 2] : 0.0;
+            const double sum = (h0 ? y : x) + xor16_f64<4>(h0 ? x : y, r4);
+            const int w = u + 2 * h0, v2 = w + 3 * h1;
+            if (w <= 2 && v2 <= 4) {
+                const int v0 = v2 + k16 + k32, j = v0 / 5, i = v0 - 5 * j;
+                atomicAdd(d + (4 * q + j) * K + i, sum);
+            }
+        }
+    } else {
+        {  // sum over the 16 columns (lane bits 2..5) on the VALU: DPP in-row, permlane swaps across rows
+            const bool r4 = xor16_r4(lane);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    double v = c[j][i];
+                    v += xor16_f64<4>(v, r4);
+                    v += xor16_f64<8>(v, r4);
+                    v = xsum16_f64(v);
+                    c[j][i] = xsum32_f64(v);
+                }
+        }
+        const int jr = s & 3, srcLane = 4 * s + (s >> 2);
+        double* d = at + (size_t)s * K;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const double sel = jr == 0 ? c[0][i] : jr == 1 ? c[1][i] : jr == 2 ? c[2][i] : c[3][i];
+            const double v = __shfl(sel, srcLane);
+            if ((i & 3) == q) atomicAdd(d + i, v);
+        }
+    }
+}
+
 // The harmonic M2L in clusters: one 4-wave workgroup per
 // cluster (the active targets of one level under one ancestor kClusterDepth levels
 // up), the cluster's locals accumulated in LDS.  Each wave takes the cluster's
@@ -365,67 +426,271 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                     }
                 }
             }
-        if constexpr (K == 5) {
-            // sum over the 16 columns (lane bits 2..5) as a reduce-scatter of the lane's
-            // 20 row sums (rows 4q + j, entries i; v = 5 j + i): 20 -> 10 (lane ^ 32),
-            // 10 -> 5 (lane ^ 16), 5 -> 3 (lane ^ 8), 3 -> 2 (lane ^ 4); each of the 16
-            // column lanes then adds its <= 2 finished sums -- ~90 VALU ops, not ~360
-            const bool r4 = xor16_r4(lane);
-            const int k32 = swap_add32_f64(1.0, 0.0) > 1.5 ? 0 : 10;  // this lane keeps the first / second half
-            const int k16 = swap_add16_f64(1.0, 0.0) > 1.5 ? 0 : 5;
-            double v10[10];
-#pragma unroll
-            for (int k = 0; k < 10; ++k) v10[k] = swap_add32_f64(c[k / 5][k % 5], c[(k + 10) / 5][(k + 10) % 5]);
-            double v5[5];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) v5[k] = swap_add16_f64(v10[k], v10[k + 5]);
-            const bool h1 = (lane >> 3) & 1, h0 = (lane >> 2) & 1;
-            double v3[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {  // lane ^ 8: h1 = 0 keeps k, h1 = 1 keeps k + 3
-                const double x = v5[k], y = k + 3 < 5 ? v5[k + 3] : 0.0;
-                v3[k] = (h1 ? y : x) + dpp_f64<0x128>(h1 ? x : y);
-            }
-            double* d = acc + (size_t)ti * kRank * K;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {  // lane ^ 4: h0 = 0 keeps u, h0 = 1 keeps u + 2
-                const double x = v3[u], y = u + 2 < 3 ? v3[u + 2] : 0.0;
-                const double sum = (h0 ? y : x) + xor16_f64<4>(h0 ? x : y, r4);
-                const int w = u + 2 * h0, v2 = w + 3 * h1;
-                if (w <= 2 && v2 <= 4) {
-                    const int v0 = v2 + k16 + k32, j = v0 / 5, i = v0 - 5 * j;
-                    atomicAdd(d + (4 * q + j) * K + i, sum);
-                }
-            }
-        } else {
-            {  // sum over the 16 columns (lane bits 2..5) on the VALU: DPP in-row, permlane swaps across rows
-                const bool r4 = xor16_r4(lane);
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int i = 0; i < K; ++i) {
-                        double v = c[j][i];
-                        v += xor16_f64<4>(v, r4);
-                        v += xor16_f64<8>(v, r4);
-                        v = xsum16_f64(v);
-                        c[j][i] = xsum32_f64(v);
-                    }
-            }
-            const int jr = s & 3, srcLane = 4 * s + (s >> 2);
-            double* d = acc + ((size_t)ti * kRank + s) * K;
-#pragma unroll
-            for (int i = 0; i < K; ++i) {
-                const double sel = jr == 0 ? c[0][i] : jr == 1 ? c[1][i] : jr == 2 ? c[2][i] : c[3][i];
-                const double v = __shfl(sel, srcLane);
-                if ((i & 3) == q) atomicAdd(d + i, v);
-            }
-        }
+        m2l_hc_store_target<K>(c, acc + (size_t)ti * kRank * K, lane, s, q);
     }
     __syncthreads();
     for (int e = threadIdx.x; e < nt * RK; e += blockDim.x) {
         const int k = e / RK, r = e - k * RK;
         local[(size_t)tgt[c0 + k] * RK + r] = hw.om[r % K] * acc[e];
     }
+}
+
+// ---- the ring form of the cluster M2L ----
+//
+// m2l_hc_cluster keeps one block (two in the directed loop) in flight per wave:
+// every pair is a dependent HBM round trip (~1.7 us per block per wave at 1 and at 8
+// shards, tools/top_trace.py), and deeper register prefetch does not fit beside the
+// 40 accumulator VGPRs at 3 waves per SIMD.  Here each wave streams its pair list
+// through a private ring of D slots in LDS filled by LDS-DMA (global_load_lds_dwordx4:
+// no VGPR holds a block in flight): slot = the 2 KB E block, the source's 16 x K
+// multipole and its box (cx, cy, rx, ry).  The wave issues pair k + D - 1, waits with
+// a counted vmcnt for pair k and computes it from LDS, so D - 1 blocks stay in flight
+// across the compute.  The target's own weighted multipole (the dual products'
+// operand) lives in registers.
+//
+// The compiler's wait-count pass treats every LDS access as possibly reading an
+// LDS-DMA destination and would put vmcnt(0) before it, draining the ring.  So every
+// LDS access inside the stream is inline asm, which that pass does not see: the slot
+// reads (closed by one lgkmcnt(0) that re-defines their outputs) and the partner
+// products' ds_add_f64; the counted vmcnt waits are asm too.
+constexpr int kRingMaxK = 5;  // the ring forms compile without spills up to 5 blocks (hm_ring_xl)
+
+template <int K>
+struct Ring {
+    static_assert(K <= kRingMaxK, "the ring form spills above 5 blocks");
+    static constexpr int kMultB = kRank * K * 8;        // the multipole's bytes
+    static constexpr int kMultL = kMultB / 16;          // its 16-byte lanes
+    static constexpr bool kSplit = kMultL + 2 > kWave;  // the box in an instruction of its own (K = 8)
+    static constexpr int kNI = kSplit ? 4 : 3;          // LDS-DMA instructions per slot
+    static constexpr int kSlot = 2048 + kMultB + 32;    // bytes per slot
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ unsigned lds_offset(const void* p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+__device__ __forceinline__ void glds16(const double* g, unsigned lds) {
+    __builtin_amdgcn_global_load_lds(g, (lds_void*)(uintptr_t)lds, 16, 0, 0);
+}
+
+// no "memory" clobbers on the stream's asm: one would make every later global load of
+// the kernel a vector load (the wave-uniform pair indices must stay scalar loads, or
+// their vmcnt waits drain the ring); volatile asm keeps its order with the LDS-DMA
+// intrinsics and with each other
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N));
+}
+
+// wait until the slot issued `after` slots ago (0 .. 3) has landed
+template <int NI>
+__device__ __forceinline__ void ring_wait(int after) {
+    if (after >= 3) wait_vm<3 * NI>();
+    else if (after == 2) wait_vm<2 * NI>();
+    else if (after == 1) wait_vm<NI>();
+    else wait_vm<0>();
+}
+
+// fill a slot: block b of E, multipole and box of source node B (wave-uniform b, B)
+template <int K>
+__device__ __forceinline__ void ring_issue(const double* __restrict__ E, const double* __restrict__ mult,
+                                           const double* __restrict__ geo, int b, int B, unsigned slot, int lane) {
+    using R = Ring<K>;
+    const double* eg = E + (size_t)b * 256 + 2 * lane;
+    glds16(eg, slot);
+    glds16(eg + 128, slot + 1024);
+    const double* mg = mult + (size_t)B * (kRank * K) + 2 * lane;
+    const double* gg = geo + 4 * (size_t)B + 2 * (lane - (R::kSplit ? 0 : R::kMultL));
+    if constexpr (R::kSplit) {
+        glds16(mg, slot + 2048);
+        if (lane < 2) glds16(gg, slot + 2048 + R::kMultB);
+    } else {
+        if (lane < R::kMultL + 2) glds16(lane < R::kMultL ? mg : gg, slot + 2048);
+    }
+}
+
+// lane (s, q)'s operands from a landed slot: rows 4q .. 4q+3 of column s of the
+// block, the source multipole's row s, the source box
+template <int K>
+__device__ __forceinline__ void ring_read(unsigned slot, int lane, int s, double (&e4)[4], double (&xm)[K],
+                                          double (&g)[4]) {
+    using R = Ring<K>;
+    const unsigned eo = slot + 32 * lane, go = slot + 2048 + R::kMultB, mo = slot + 2048 + 8 * K * s;
+    dbl2 e01, e23, g01, g23;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(e01) : "v"(eo));
+    asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(e23) : "v"(eo));
+    asm volatile("ds_read_b128 %0, %1" : "=v"(g01) : "v"(go));
+    asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(g23) : "v"(go));
+#pragma unroll
+    for (int b = 0; b < K; ++b) asm volatile("ds_read_b64 %0, %1" : "=v"(xm[b]) : "v"(mo + 8 * b));
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(e01), "+v"(e23), "+v"(g01), "+v"(g23));
+#pragma unroll
+    for (int b = 0; b < K; ++b) asm volatile("" : "+v"(xm[b]));
+    e4[0] = e01.x;
+    e4[1] = e01.y;
+    e4[2] = e23.x;
+    e4[3] = e23.y;
+    g[0] = g01.x;
+    g[1] = g01.y;
+    g[2] = g23.x;
+    g[3] = g23.y;
+}
+
+// rows 4q .. 4q+3 of the wave's weighted target multipole (4K doubles from `off`)
+template <int K>
+__device__ __forceinline__ void ring_read_xa(unsigned off, double (&x)[4 * K]) {
+    dbl2 v[2 * K];
+#pragma unroll
+    for (int i = 0; i < 2 * K; ++i) asm volatile("ds_read_b128 %0, %1" : "=v"(v[i]) : "v"(off + 16 * i));
+    asm volatile("s_waitcnt lgkmcnt(0)");
+#pragma unroll
+    for (int i = 0; i < 2 * K; ++i) {
+        asm volatile("" : "+v"(v[i]));
+        x[2 * i] = v[i].x;
+        x[2 * i + 1] = v[i].y;
+    }
+}
+
+template <int K, int NR, int D, bool XL>
+__device__ __forceinline__ void m2l_hcr_cluster(const int cid, const HcArgs& a, double* sm) {
+    static_assert(D >= 2 && D <= 4, "ring depth");
+    using R = Ring<K>;
+    const int* __restrict__ clPtr = a.clPtr;
+    const int* __restrict__ tgt = a.tgt;
+    const int64_t* __restrict__ ptr = a.ptr;
+    const int* __restrict__ ndir = a.ndir;
+    const int* __restrict__ src = a.src;
+    const int* __restrict__ blk = a.blk;
+    const int* __restrict__ slot = a.slot;
+    const double* __restrict__ E = a.E;
+    const double* __restrict__ geo = a.geo;
+    const double* __restrict__ ncx = a.ncx;
+    const double* __restrict__ ncy = a.ncy;
+    const double* __restrict__ nrx = a.nrx;
+    const double* __restrict__ nry = a.nry;
+    const Params* __restrict__ P = a.P;
+    const HarmWeights& hw = a.hw;
+    const double* __restrict__ mult = a.mult;
+    double* __restrict__ local = a.local;
+    constexpr int RK = kRank * K;
+    const int c0 = clPtr[cid], nt = clPtr[cid + 1] - c0;
+    const int nw = (int)(blockDim.x / kWave);
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+    double* acc = sm;                                                       // nt x 16 x K: the cluster's locals
+    double* xl = sm + (size_t)nt * RK + (XL ? (size_t)w * RK : 0);          // XL: this wave's target multipole
+    const unsigned ring = lds_offset(sm + (size_t)nt * RK + (XL ? (size_t)nw * RK : 0)) + (unsigned)(w * D * R::kSlot);
+    const unsigned accOff = lds_offset(acc);
+    for (int i = threadIdx.x; i < nt * RK; i += blockDim.x) acc[i] = 0.0;
+    __syncthreads();
+    const int lane = threadIdx.x & (kWave - 1);
+    const int s = lane >> 2, q = lane & 3;
+    const double chx = P->cheb[s & 3], chy = P->cheb[s >> 2];
+    for (int ti = w; ti < nt; ti += nw) {
+        const int n = tgt[c0 + ti];
+        // the target's multipole rows 4q + j, (-1)^b hw_b weighted (the dual products):
+        // in registers (40 VGPRs at K = 5, 2 waves per SIMD), or (XL) in LDS, read per
+        // dual block (3 waves per SIMD)
+        double xa[XL ? 1 : 4][K];
+        if constexpr (XL) {
+            for (int e = lane; e < RK; e += kWave) {
+                const int b = e % K;
+                xl[e] = ((b & 1) ? -hw.hw[b] : hw.hw[b]) * mult[(size_t)n * RK + e];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // xl visible to every lane of the wave
+            __builtin_amdgcn_wave_barrier();
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int b = 0; b < K; ++b)
+                    xa[j][b] = ((b & 1) ? -hw.hw[b] : hw.hw[b]) * mult[(size_t)n * RK + (4 * q + j) * K + b];
+        }
+        double bx[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bx[j] = ncx[n] + nrx[n] * P->cheb[j];
+        const double by = ncy[n] + nry[n] * P->cheb[q];
+        double c[4][K];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < K; ++i) c[j][i] = 0.0;
+        const int64_t p0 = ptr[c0 + ti], pd = p0 + ndir[c0 + ti], p1 = ptr[c0 + ti + 1];
+        // the pair list in chunks of 64: its indices in lanes (one vector load each, while
+        // the ring is empty -- the compiler's wait for them would drain it), the ring
+        // filled and drained per chunk
+        for (int64_t cb = p0; cb < p1; cb += kWave) {
+            const int cnt = (int)min<int64_t>(kWave, p1 - cb);
+            const int mySrc = lane < cnt ? src[cb + lane] : 0;
+            const int myBlk = lane < cnt ? blk[cb + lane] : 0;
+            const int mySlot = lane < cnt && cb + lane >= pd ? slot[cb + lane] : 0;
+            const int nDir = (int)max<int64_t>(0, min<int64_t>(cnt, pd - cb));  // directed entries of the chunk
+            for (int k = 0; k < D - 1 && k < cnt; ++k)
+                ring_issue<K>(E, mult, geo, __builtin_amdgcn_readlane(myBlk, k), __builtin_amdgcn_readlane(mySrc, k),
+                              ring + k * R::kSlot, lane);
+            int cur = 0;  // the slot of pair k
+            for (int k = 0; k < cnt; ++k) {
+                int after = cnt - 1 - k;
+                if (k + D - 1 < cnt) {
+                    const int ns = cur == 0 ? D - 1 : cur - 1;  // the slot pair k - 1 used: free again
+                    ring_issue<K>(E, mult, geo, __builtin_amdgcn_readlane(myBlk, k + D - 1),
+                                  __builtin_amdgcn_readlane(mySrc, k + D - 1), ring + ns * R::kSlot, lane);
+                    after = D - 1;
+                }
+                ring_wait<R::kNI>(after);
+                double e4[4], xm[K], g[4];
+                ring_read<K>(ring + cur * R::kSlot, lane, s, e4, xm, g);
+                cur = cur == D - 1 ? 0 : cur + 1;
+                const double ax = g[0] + g[2] * chx;
+                const double dy = (g[1] + g[3] * chy) - by;
+                const double dy2 = dy * dy;
+                double xw[K];
+#pragma unroll
+                for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * xm[b];
+                if (k < nDir) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) hm_entry<K, false, NR>(e4[j], ax - bx[j], dy2, xw, c[j]);
+                } else {
+                    double ob[K];
+#pragma unroll
+                    for (int b = 0; b < K; ++b) ob[b] = 0.0;
+                    if constexpr (XL) {
+                        double xr[4 * K];
+                        ring_read_xa<K>(lds_offset(xl) + 32 * K * q, xr);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) hm_entry2<K, NR>(e4[j], ax - bx[j], dy2, xw, xr + j * K, c[j], ob);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) hm_entry2<K, NR>(e4[j], ax - bx[j], dy2, xw, xa[j], c[j], ob);
+                    }
+#pragma unroll
+                    for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // rows 4q'+j over the quad
+                    if (q == 0) {
+                        const int sl = __builtin_amdgcn_readlane(mySlot, k);
+                        const unsigned d = accOff + (unsigned)(((sl * kRank + s) * K) * 8);
+#pragma unroll
+                        for (int i = 0; i < K; ++i)
+                            asm volatile("ds_add_f64 %0, %1" ::"v"(d + 8 * i), "v"((i & 1) ? -ob[i] : ob[i]));
+                    }
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)");  // the partner adds, before the compiler's LDS ops
+        m2l_hc_store_target<K>(c, acc + (size_t)ti * RK, lane, s, q);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int e = threadIdx.x; e < nt * RK; e += blockDim.x) {
+        const int k = e / RK, r = e - k * RK;
+        local[(size_t)tgt[c0 + k] * RK + r] = hw.om[r % K] * acc[e];
+    }
+}
+
+template <int K, int NR, int D, bool XL, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_m2l_hcr(HcArgs a) {
+    extern __shared__ double sm[];
+    m2l_hcr_cluster<K, NR, D, XL>((int)blockIdx.x, a, sm);
 }
 
 template <int K, int NR, int WPE>
@@ -481,31 +746,60 @@ __device__ __forceinline__ void top_publish(unsigned* cnt, int k) {
     }
 }
 
-template <int K, int NR, int WPE>
+// development timeline of the fused launch (ANISO_TOP_TRACE=1, tools/top_trace.py):
+// per block the 100 MHz wall clock at its start, after its wait and at its end, and
+// the hardware slot it ran on (HW_ID: wave / SIMD / CU / SE bits; XCC_ID above)
+template <bool TRACE>
+__device__ __forceinline__ void top_mark(const TopArgs& t, int field) {
+    if constexpr (!TRACE) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t* r = t.trace + 4 * (int64_t)blockIdx.x;
+        r[field] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        if (field == 0)
+            r[3] = (int64_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)) |
+                   ((int64_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) << 32);
+    }
+}
+
+template <int K, int NR, int D, bool XL>
+__device__ __forceinline__ void m2l_cluster_form(int cid, const HcArgs& a, double* sm) {
+    if constexpr (D == 0) m2l_hc_cluster<K, NR>(cid, a, sm);
+    else m2l_hcr_cluster<K, NR, D, XL>(cid, a, sm);
+}
+
+template <int K, int NR, int WPE, int D, bool XL, bool TRACE = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a) {
     extern __shared__ double sm[];
     const int b = (int)blockIdx.x;
+    top_mark<TRACE>(t, 0);
     if (b < t.nUp) {
         int k = 1;
         while (b >= t.blk0[k + 1]) ++k;
         if (k >= 2) top_wait(t, k - 1, (unsigned)(t.blk0[k] - t.blk0[k - 1]));
+        top_mark<TRACE>(t, 1);
         up_task<K>(t.task0[k] + (b - t.blk0[k]), u.maxTask, u.desc, u.grpFix, u.node, u.code, u.geom, u.leafRange,
                    u.pxT, u.pyT, u.xin, u.ldi, u.treeIn, u.perm, u.sigT, u.wT, u.fT, u.cT, u.P, u.mult, u.rootSlot,
                    k == 1 ? t.recv1 : nullptr, nullptr, nullptr, sm);
         top_publish(t.cnt, k);
+        top_mark<TRACE>(t, 2);
         return;
     }
     const int cid = b - t.nUp;
     const int w = t.clWait[cid];
     if (w > 0) {  // its own copy: behind the wait's fence the source boxes load through the vector path
         top_wait(t, w, (unsigned)(t.blk0[w + 1] - t.blk0[w]));
-        m2l_hc_cluster<K, NR>(cid, a, sm);
+        top_mark<TRACE>(t, 1);
+        m2l_cluster_form<K, NR, D, XL>(cid, a, sm);
+        top_mark<TRACE>(t, 2);
         return;
     }
     // no store or fence on the way here, so the compiler keeps the wave-uniform
     // source-box reads (ncx[B] ...) on scalar loads as in k_m2l_hc
-    m2l_hc_cluster<K, NR>(cid, a, sm);
+    top_mark<TRACE>(t, 1);
+    m2l_cluster_form<K, NR, D, XL>(cid, a, sm);
+    top_mark<TRACE>(t, 2);
 }
 
 // ----------------------------------------------------------------- near field
@@ -809,22 +1103,78 @@ void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const in
 // XCD-contiguous cluster order all measured equal or slower, r01e-r01j), 3 waves per
 // SIMD; 1/r = v_rsq_f64 + ONE Newton step (~1e-13 relative per entry, 4 % faster
 // than two; the reduced-precision choice is tested at 1M points)
-void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, const int64_t* ptr, const int* ndir,
-                   const int* src, const int* blk, const int* slot, const double* E, const double* ncx, const double* ncy,
-                   const double* nrx, const double* nry, const Params* P, const HarmWeights& hw, const double* mult,
-                   double* local, hipStream_t s) {
+size_t m2l_hc_lds(int K, int maxCl, int depth, bool xl) {
+    size_t b = (size_t)maxCl * kRank * K * sizeof(double);
+    const int nw = 256 / kWave;
+    if (depth == 0 || xl) b += (size_t)nw * kRank * K * sizeof(double);  // each wave's weighted target multipole
+    if (depth == 0) return b;
+    const size_t slot = 2048 + (size_t)kRank * K * 8 + 32;
+    return b + (size_t)nw * depth * slot;
+}
+
+// the ring form (k_m2l_hcr, the default) and its depth: ANISO_HM_RING=0 restores the
+// one-block-in-flight form (A/B runs), ANISO_HM_RING=2..4 sets the depth
+int hm_ring_depth() {
+    const char* e = std::getenv("ANISO_HM_RING");
+    const int v = e ? std::atoi(e) : 0;
+    return v == 0 ? 0 : std::max(2, std::min(4, v));
+}
+
+// the ring form's target multipole: 1 in LDS (3 waves per SIMD), 0 in VGPRs (2 waves
+// per SIMD), -1 the ring form not used.  By default the LDS form where three
+// workgroups per CU fit in LDS with it (small clusters: shards); elsewhere the
+// one-block-in-flight form, which keeps 3 waves per SIMD there (r03m: at 64-target
+// clusters the ring's LDS allows 2 workgroups per CU and is 5-7 % slower).
+// ANISO_HM_RING_XL=0 / 1 forces the VGPR / LDS form.
+// K = 8 (aniso.m with more than 5 blocks) keeps the one-block-in-flight form: both
+// ring forms spill there, and a scratch store inside the stream would break the
+// counted vmcnt waits (stores retire out of order with the LDS-DMA loads).
+int hm_ring_xl(int K, int maxCl, int depth) {
+    if (K > kRingMaxK) return -1;
+    if (const char* e = std::getenv("ANISO_HM_RING_XL")) return std::atoi(e) != 0 ? 1 : 0;
+    return 3 * m2l_hc_lds(K, maxCl, depth, true) <= 160 * 1024 ? 1 : -1;
+}
+
+#define ANISO_HM_DISPATCH_RING(d, CALL)                                            \
+    switch (d) {                                                                   \
+        case 0: { constexpr int DD = 0; CALL; } break;                             \
+        case 2: { constexpr int DD = 2; CALL; } break;                             \
+        case 3: { constexpr int DD = 3; CALL; } break;                             \
+        case 4: { constexpr int DD = 4; CALL; } break;                             \
+        default: throw std::invalid_argument("harmonic M2L: bad ring depth");      \
+    }
+
+template <typename F>
+static void set_lds(F f, size_t shm) {
+    if (shm > 65536) {  // clusters of up to 64 targets need more than the default 64 KB
+        const hipError_t e =
+            hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
+    }
+}
+
+// clustered M2L (the default): 4 waves per cluster of <= 64 targets (512 / 768
+// threads, 2 waves per SIMD, 128-target clusters, a software-pipelined stream and an
+// XCD-contiguous cluster order all measured equal or slower, r01e-r01j), 3 waves per
+// SIMD; 1/r = v_rsq_f64 + ONE Newton step (~1e-13 relative per entry, 4 % faster
+// than two; the reduced-precision choice is tested at 1M points)
+void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s) {
     if (ncl <= 0) return;
     if (maxCl > 64) throw std::invalid_argument("harmonic M2L cluster larger than 64 targets");
-    const size_t shm = (size_t)(maxCl + 256 / kWave) * kRank * K * sizeof(double);
-    ANISO_HM_DISPATCH_K(K, ({
-        auto f = k_m2l_hc<KK, 1, 3>;
-        if (shm > 65536) {  // clusters of up to 64 targets at K = 8 need ~68 KB of the 160 KB LDS
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(f),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-            if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
+    const int depth = a.geo && K <= kRingMaxK ? a.ring : 0;
+    const bool xl = a.ringXL;
+    const size_t shm = m2l_hc_lds(K, maxCl, depth, xl);
+    ANISO_HM_DISPATCH_K(K, ANISO_HM_DISPATCH_RING(depth, ({
+        if constexpr (DD == 0 || KK > kRingMaxK) {
+            auto f = k_m2l_hc<KK, 1, 3>;
+            set_lds(f, shm);
+            f<<<ncl, 256, shm, s>>>(a);
+        } else {
+            auto f = xl ? k_m2l_hcr<KK, 1, DD, true, 3> : k_m2l_hcr<KK, 1, DD, false, 2>;
+            set_lds(f, shm);
+            f<<<ncl, 256, shm, s>>>(a);
         }
-        f<<<ncl, 256, shm, s>>>(HcArgs{clPtr, tgt, ptr, ndir, src, blk, slot, E, ncx, ncy, nrx, nry, P, hw, mult, local});
-    }));
+    })));
     HIP_LAUNCH_CHECK();
 }
 
@@ -841,17 +1191,23 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
     if (t.ntier < 2 || t.ntier > kMaxTopTiers || t.blk0[t.ntier] != t.nUp)
         throw std::invalid_argument("fused top-of-tree launch: bad tier layout");
     if (!t.err) throw std::invalid_argument("fused top-of-tree launch: no time-out flag");
-    const size_t shm = std::max((size_t)(maxCl + 256 / kWave) * kRank * K * sizeof(double), up_tier_lds(u.maxTask, K));
+    const int depth = a.geo && K <= kRingMaxK ? a.ring : 0;
+    const bool xl = a.ringXL;
+    const size_t shm = std::max(m2l_hc_lds(K, maxCl, depth, xl), up_tier_lds(u.maxTask, K));
     const unsigned nb = (unsigned)(t.nUp + ncl);
-    ANISO_HM_DISPATCH_K(K, ({
-        auto f = k_top_m2l_hc<KK, 1, 3>;
-        if (shm > 65536) {
-            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(f),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-            if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
+    ANISO_HM_DISPATCH_K(K, ANISO_HM_DISPATCH_RING(depth, ({
+        // the ring form with its target multipole in VGPRs needs ~216 of them at K = 5
+        if constexpr (DD == 0 || KK > kRingMaxK) {
+            auto f = t.trace ? k_top_m2l_hc<KK, 1, 3, 0, false, true> : k_top_m2l_hc<KK, 1, 3, 0, false>;
+            set_lds(f, shm);
+            f<<<nb, 256, shm, s>>>(u, t, a);
+        } else {
+            auto f = xl ? (t.trace ? k_top_m2l_hc<KK, 1, 3, DD, true, true> : k_top_m2l_hc<KK, 1, 3, DD, true>)
+                        : (t.trace ? k_top_m2l_hc<KK, 1, 2, DD, false, true> : k_top_m2l_hc<KK, 1, 2, DD, false>);
+            set_lds(f, shm);
+            f<<<nb, 256, shm, s>>>(u, t, a);
         }
-        f<<<nb, 256, shm, s>>>(u, t, a);
-    }));
+    })));
     HIP_LAUNCH_CHECK();
 }
 

@@ -191,6 +191,9 @@ struct HcArgs {
     HarmWeights hw;
     const double* mult;
     double* local;
+    const double* geo = nullptr;  // per node {cx, cy, rx, ry} (the ring form, k_m2l_hcr)
+    int ring = 0;                 // host: the ring form's depth (0: the one-block-in-flight form)
+    bool ringXL = false;          // host: the ring form keeps the target multipole in LDS (3 waves / SIMD)
 };
 // The fused top-of-tree + clustered M2L launch (harmonic.hip k_top_m2l_hc, DESIGN.md
 // §3.10): blocks 0 .. nUp - 1 run the up tasks of tiers 1 .. ntier - 1 (tier k's
@@ -229,13 +232,13 @@ struct TopArgs {
     const double* recv1;          // sharded phase 2: the gathered tier-0 roots tier 1 reads
     unsigned spinLimit;           // polls before a wait gives up (0: give up at once -- tests only)
     unsigned* err;                // host-visible sticky flag: set to 1 when a wait gave up
+    int64_t* trace;               // development (ANISO_TOP_TRACE=1): per block {start, waited, end, hw id}
 };
 bool top_fused_enabled();
 void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs& t, const HcArgs& a, hipStream_t s);
-void launch_m2l_hc(int K, int ncl, int maxCl, const int* clPtr, const int* tgt, const int64_t* ptr, const int* ndir,
-                   const int* src, const int* blk, const int* slot, const double* E, const double* ncx, const double* ncy,
-                   const double* nrx, const double* nry, const Params* P, const HarmWeights& hw, const double* mult,
-                   double* local, hipStream_t s);
+void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s);
+int hm_ring_depth();  // ANISO_HM_RING (read at handle creation): the cluster M2L's LDS ring depth
+int hm_ring_xl(int K, int maxCl, int depth);  // its target multipole in LDS / VGPRs / ring off (1, 0, -1)
 // the fused corrections of the staged near field (d = 1; harmonic.hip k_near_hs)
 struct NearCorr {  // the fused corrections of k_near_hs (d = 1), or ignored when rows == nullptr
     const uint16_t* rows;

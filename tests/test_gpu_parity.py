@@ -598,18 +598,28 @@ def test_harmonic_symmetric_blocks_match_directed(sz, d, ks, monkeypatch):
     assert _rel(outs[0], outs[1]) <= 1e-13
 
 
-@pytest.mark.parametrize("sz,d,ks,ml,sym", [(32, 1, 5, 20, "1"), (19, 2, 3, 20, "1"), (64, 1, 2, 20, "0"),
-                                            (40, 1, 5, 3, "1")])
-def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatch):
+@pytest.mark.parametrize("sz,d,ks,ml,sym,ring", [(32, 1, 5, 20, "1", "3x"), (19, 2, 3, 20, "1", "3x"),
+                                                 (64, 1, 2, 20, "0", "3x"), (40, 1, 5, 3, "1", "3x"),
+                                                 (32, 1, 5, 20, "1", "0"), (32, 1, 5, 20, "1", "2x"),
+                                                 (32, 1, 5, 20, "1", "4x"), (24, 1, 8, 20, "1", "3x"),
+                                                 (19, 2, 3, 20, "1", "0"), (32, 1, 5, 20, "1", "3v"),
+                                                 (24, 1, 8, 20, "1", "3v"), (32, 1, 5, 20, "1", "3")])
+def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, ring, monkeypatch):
     """The clustered harmonic M2L (in-cluster V pairs read once by
     the smaller id, both products, locals summed in LDS) against one wave per target
     (aniso_set_deterministic); odd sz (non-uniform tree), directed storage, a
-    maxLevel-limited tree.  Also checks that in-cluster pairs exist, that the cluster
-    plan reads fewer E blocks, and that the deterministic mode repeats bitwise."""
+    maxLevel-limited tree; the LDS-ring form at depths 2-4 with the target multipole
+    in LDS (x) or VGPRs (v), every block count it compiles for (2, 4, 5, 8), the
+    one-block-in-flight form (ANISO_HM_RING=0) and the default choice between them.
+    Also checks that in-cluster pairs exist, that the cluster plan reads fewer E
+    blocks, and that the deterministic mode repeats bitwise."""
     torch = _torch()
     import aniso_amd
 
     monkeypatch.setenv("ANISO_SYMMETRIC", sym)
+    monkeypatch.setenv("ANISO_HM_RING", ring[0])
+    if len(ring) > 1:
+        monkeypatch.setenv("ANISO_HM_RING_XL", "1" if ring[1] == "x" else "0")
     # 64-target clusters even at these sizes (the default depth keeps >= 512
     # clusters, which small trees only reach with 4-target clusters: no in-cluster pairs)
     monkeypatch.setenv("ANISO_HM_CLDEPTH", "3")
@@ -637,14 +647,16 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, monkeypatc
     assert _rel(outs[0], outs[1]) <= 1e-13
 
 
-@pytest.mark.parametrize("ks,world", [(5, 8), (2, 4), (3, 3)])
-def test_small_clusters_on_shards_match_unsharded(ks, world):
+@pytest.mark.parametrize("ks,world,ring", [(5, 8, "3"), (2, 4, "3"), (3, 3, "3"), (5, 8, "0")])
+def test_small_clusters_on_shards_match_unsharded(ks, world, ring, monkeypatch):
     """The clustered M2L on the small clusters of an N-GPU shard (the adaptive depth
     gives 16-target clusters there) with 2, 4 (3 padded) and 5 blocks: every rank's
-    two-phase apply equals the unsharded operator."""
+    two-phase apply equals the unsharded operator (the LDS-ring cluster form and the
+    one-block-in-flight form)."""
     torch = _torch()
     import aniso_amd
 
+    monkeypatch.setenv("ANISO_HM_RING", ring)
     sz = 256
     full = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
     xy = full.getNodes()
@@ -688,7 +700,7 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
     assert float(torch.linalg.norm(o1 - ref) / torch.linalg.norm(ref)) <= 1e-13
 
 
-@pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0"])
+@pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0", "ANISO_HM_RING=3"])
 def test_block_matvec_knobs_agree(knob, monkeypatch):
     """Every remaining environment knob of the block apply:
     the serial near/M2L order, the separate x - mforward(x) subtraction and the
@@ -992,6 +1004,34 @@ def test_fused_top_of_tree_launch_matches_tier_launches(ks):
         a.sync()  # raises if an in-launch hand-off timed out (its output would be invalid)
         outs.append(out.cpu().numpy())
     assert _rel(outs[0], outs[1]) <= 1e-13 and _rel(outs[2], outs[1]) <= 1e-13
+
+
+def test_fused_launch_timeline(monkeypatch):
+    """ANISO_TOP_TRACE=1 (development): aniso_top_trace returns one record per block of
+    the last fused top-of-tree launch -- the up tasks of tiers 1.. first, then every
+    cluster once -- with start <= end of wait <= end on the 100 MHz clock."""
+    torch = _torch()
+    import aniso_amd
+
+    monkeypatch.setenv("ANISO_TOP_TRACE", "1")
+    a = aniso_amd.Aniso(128, 1, 5, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    a.setCoeff(*rough_coeffs(xy, 4))
+    for m in range(9):
+        a.cache(m)
+    assert a.stats()["top_fused"] == 1
+    U = torch.tensor(np.random.default_rng(2).uniform(-1, 1, (5, a.N)), device="cuda")
+    out = torch.zeros_like(U)
+    a.block_op_dev(2, U, out, tree=True)
+    tr = a.top_trace()
+    st = a.stats()
+    assert tr.shape[1] == 8 and tr.shape[0] > st["hm_clusters"] > 0
+    up = tr[tr[:, 4] < 0]
+    cl = tr[tr[:, 4] >= 0]
+    assert len(cl) == st["hm_clusters"] and sorted(cl[:, 4].tolist()) == list(range(st["hm_clusters"]))
+    assert (np.diff(-up[:, 4]) >= 0).all()  # tiers in order
+    assert (tr[:, 0] <= tr[:, 1]).all() and (tr[:, 1] <= tr[:, 2]).all() and (tr[:, 0] > 0).all()
+    assert int(cl[:, 7].sum()) == st["hm_block_reads"]
 
 
 def test_fused_top_of_tree_time_out_is_an_error(monkeypatch):

@@ -13,8 +13,10 @@ import torch  # noqa: E402
 import aniso_amd  # noqa: E402
 from bench import demo_coeffs, gaussian  # noqa: E402
 
-world = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-ranks = [int(a) for a in sys.argv[2:]] or [0]
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+timing = "--no-timing" not in sys.argv  # --no-timing: no stage events (they add packets between the kernels)
+world = int(args[0]) if args else 8
+ranks = [int(a) for a in args[1:]] or [0]
 for rank in ranks:
     op = aniso_amd.Aniso(1024, 1, 5, 0.8, 10, 4, 20)
     xy = op.getNodes()
@@ -42,7 +44,7 @@ for rank in ranks:
 
     for _ in range(3):
         step()
-    op.set_timing(True)
+    op.set_timing(timing)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     steps = 20
@@ -53,7 +55,7 @@ for rank in ranks:
     ms = 1e3 * (time.perf_counter() - t0) / steps
     st = op.stats()
     print(json.dumps({"world": world, "rank": rank, "ms_per_apply": round(ms, 4), "host_ms_per_apply": round(host_ms, 4),
-                      "stage_ms": {k: round(v, 4) for k, v in op.stage_times().items()},
+                      "stage_ms": {k: round(v, 4) for k, v in op.stage_times().items()} if timing else None,
                       "t0_tasks_run": ex["t0_run"], "t0_tasks": ex["t0_tasks"], "halo_points": ex["halo_points"],
                       "m2l_clusters": st["hm_clusters"], "m2l_targets": st["m2l_targets"], "leaves": st["leaves"]}),
           flush=True)
