@@ -114,6 +114,7 @@ def lib():
             "aniso_comm_unique_id": [ctypes.c_char_p],
             "aniso_comm_init_rccl": [P, ctypes.c_char_p],
             "aniso_comm_init_callbacks": [P, ctypes.POINTER(Collectives)],
+            "aniso_comm_init_loopback": [P],
             "aniso_block_op_sharded_dev": [P, I, P, I64, P, I64, P],
             "aniso_memcpy": [P, P, ctypes.c_size_t],
         }
@@ -473,6 +474,11 @@ class Aniso:
     def comm_init_rccl(self, unique_id):
         """Attach an RCCL communicator (every rank together, after set_shard)."""
         _check(lib().aniso_comm_init_rccl(self.address, bytes(unique_id)))
+
+    def comm_init_loopback(self):
+        """Development: a loopback communicator (aniso_comm_init_loopback) to time one
+        rank's schedule of an N-GPU run on one GPU; results are not the operator's."""
+        _check(lib().aniso_comm_init_loopback(self.address))
 
     def comm_init_callbacks(self, coll):
         """Attach caller-supplied collectives (a Collectives structure; kept alive here)."""

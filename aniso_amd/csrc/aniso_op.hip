@@ -94,6 +94,10 @@ Operator::~Operator() {
         int prev = -1;  // restore the caller's device (the destructor runs from Python __del__)
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
+        if (comm) {  // the communicator before the streams its collectives ran on
+            (void)hipDeviceSynchronize();
+            comm.reset();
+        }
         for (auto& e : evPool) (void)hipEventDestroy(e);
         if (evFork) (void)hipEventDestroy(evFork);
         if (evJoin) (void)hipEventDestroy(evJoin);

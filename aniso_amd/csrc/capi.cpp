@@ -618,6 +618,14 @@ int aniso_comm_init_callbacks(aniso_handle h, const aniso_collectives* c) {
     });
 }
 
+int aniso_comm_init_loopback(aniso_handle h) {
+    ENTER(h);
+    return guarded([&] {
+        auto& op = get(h);
+        op.commInit(aniso::make_loopback_collectives(op.plan.nranks, op.plan.rank));
+    });
+}
+
 int aniso_block_op_sharded_dev(aniso_handle h, int which, double* x, int64_t ldx, double* y, int64_t ldy,
                                void* stream) {
     ENTER(h);

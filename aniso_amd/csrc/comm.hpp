@@ -36,6 +36,8 @@ class Collectives {
 
 std::unique_ptr<Collectives> make_rccl_collectives(const unsigned char* uniqueId, int nranks, int rank);
 std::unique_ptr<Collectives> make_callback_collectives(const aniso_collectives& c, int nranks, int rank);
+// development: a rank's schedule with the other ranks' data left out (timing on one GPU)
+std::unique_ptr<Collectives> make_loopback_collectives(int nranks, int rank);
 void rccl_unique_id(unsigned char* out);
 
 }  // namespace aniso

@@ -701,10 +701,17 @@ void Plan::buildClusters(const Tree& t) {
     // that go last
     const int upperBelow = tierRootLevel.empty() ? 0 : tierRootLevel[0] + (nranks > 1 ? 1 : 0);
     auto upper = [&](int w) { return t.level[m2lTgt[w]] < upperBelow; };
+    // their clusters wait for the tier chain, so their run time is the launch's tail:
+    // on a shard 4-target clusters, one target per wave (8 shards: 0.267-0.271 ms per
+    // block matvec against 0.279-0.289 with 16-target ones, r03t); on one GPU they are
+    // 6 % of the clusters and 16-target ones stay
+    int upperDepth = nranks > 1 ? 1 : 2;
+    if (const char* e = std::getenv("ANISO_HM_UPPER_DEPTH"))  // experiments only (0..2)
+        upperDepth = std::max(0, std::min(2, std::atoi(e)));
     std::vector<int64_t> key(nt);
     for (int w = 0; w < nt; ++w) {
         int a = m2lTgt[w];
-        const int dp = upper(w) ? std::min(depth, 2) : depth;
+        const int dp = upper(w) ? std::min(depth, upperDepth) : depth;
         for (int k = 0; k < dp && t.parent[a] != -1; ++k) a = t.parent[a];
         key[w] = ((int64_t)t.level[m2lTgt[w]] << 32) | (uint32_t)a;
     }

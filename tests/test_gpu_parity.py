@@ -1006,6 +1006,29 @@ def test_fused_top_of_tree_launch_matches_tier_launches(ks):
     assert _rel(outs[0], outs[1]) <= 1e-13 and _rel(outs[2], outs[1]) <= 1e-13
 
 
+def test_loopback_communicator_runs_a_rank_schedule():
+    """aniso_comm_init_loopback (development: one rank's schedule of an N-GPU run on
+    one GPU, tools/shard_time.py --native): the one-call sharded matvec runs on it and
+    leaves finite values in the owned slice (the other ranks' roots are left out, so
+    they are not the operator's)."""
+    torch = _torch()
+    import aniso_amd
+
+    a = aniso_amd.Aniso(64, 1, 5, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    a.set_shard(1, 4)
+    a.setCoeff(*rough_coeffs(xy, 6))
+    for m in range(9):
+        a.cache(m)
+    a.comm_init_loopback()
+    b, e = a.shard()
+    X = torch.tensor(np.random.default_rng(4).uniform(-1, 1, (5, a.N)), device="cuda")
+    Y = torch.full_like(X, float("nan"))
+    a.block_op_sharded_dev(2, X, Y)
+    a.sync()
+    assert bool(torch.isfinite(Y[:, b:e]).all())
+
+
 def test_fused_launch_timeline(monkeypatch):
     """ANISO_TOP_TRACE=1 (development): aniso_top_trace returns one record per block of
     the last fused top-of-tree launch -- the up tasks of tiers 1.. first, then every

@@ -15,6 +15,7 @@ from bench import demo_coeffs, gaussian  # noqa: E402
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 timing = "--no-timing" not in sys.argv  # --no-timing: no stage events (they add packets between the kernels)
+native = "--native" in sys.argv  # the library's one-call sharded matvec over a loopback communicator
 world = int(args[0]) if args else 8
 ranks = [int(a) for a in args[1:]] or [0]
 for rank in ranks:
@@ -31,12 +32,17 @@ for rank in ranks:
     x = torch.zeros(5, op.N, dtype=torch.float64, device="cuda")
     x[0] = torch.tensor(gaussian(xy), device="cuda")[perm]
     y = torch.zeros_like(x)
+    if native and world > 1:
+        op.comm_init_loopback()
     send = torch.zeros(max(C * R, 1), dtype=torch.float64, device="cuda")
     recv = torch.zeros(world * max(C * R, 1), dtype=torch.float64, device="cuda")
 
     def step():
         if world == 1:
             op.block_op_dev(2, x, y, tree=True)
+            return
+        if native:
+            op.block_op_sharded_dev(2, x, y)
             return
         op.block_op_begin_dev(2, x, y[:, b:e], send)
         recv[rank * C * R:(rank + 1) * C * R].copy_(send[: C * R])  # stands in for the all-gather
@@ -54,7 +60,7 @@ for rank in ranks:
     torch.cuda.synchronize()
     ms = 1e3 * (time.perf_counter() - t0) / steps
     st = op.stats()
-    print(json.dumps({"world": world, "rank": rank, "ms_per_apply": round(ms, 4), "host_ms_per_apply": round(host_ms, 4),
+    print(json.dumps({"world": world, "rank": rank, "native": native, "ms_per_apply": round(ms, 4), "host_ms_per_apply": round(host_ms, 4),
                       "stage_ms": {k: round(v, 4) for k, v in op.stage_times().items()} if timing else None,
                       "t0_tasks_run": ex["t0_run"], "t0_tasks": ex["t0_tasks"], "halo_points": ex["halo_points"],
                       "m2l_clusters": st["hm_clusters"], "m2l_targets": st["m2l_targets"], "leaves": st["leaves"]}),

@@ -13,8 +13,10 @@ import torch  # noqa: E402
 import aniso_amd  # noqa: E402
 from bench import demo_coeffs, gaussian  # noqa: E402
 
-world, rank = int(sys.argv[1]), int(sys.argv[2])
-out = sys.argv[3] if len(sys.argv) > 3 else None
+native = "--native" in sys.argv  # the library's one-call matvec over a loopback communicator
+argv = [a for a in sys.argv[1:] if not a.startswith("--")]
+world, rank = int(argv[0]), int(argv[1])
+out = argv[2] if len(argv) > 2 else None
 op = aniso_amd.Aniso(1024, 1, 5, 0.8, 10, 4, 20)
 xy = op.getNodes()
 perm = torch.tensor(op.tree_perm(), device="cuda", dtype=torch.int64)
@@ -30,11 +32,16 @@ x[0] = torch.tensor(gaussian(xy), device="cuda")[perm]
 y = torch.zeros_like(x)
 send = torch.zeros(max(C * R, 1), dtype=torch.float64, device="cuda")
 recv = torch.zeros(world * max(C * R, 1), dtype=torch.float64, device="cuda")
+if native and world > 1:
+    op.comm_init_loopback()
 
 
 def step():
     if world == 1:
         op.block_op_dev(2, x, y, tree=True)
+        return
+    if native:
+        op.block_op_sharded_dev(2, x, y)
         return
     op.block_op_begin_dev(2, x, y[:, b:e], send)
     recv[rank * C * R:(rank + 1) * C * R].copy_(send[: C * R])
