@@ -6,6 +6,7 @@
 
 #include <cmath>
 #include <stdexcept>
+#include <type_traits>
 #include <vector>
 
 #include "aniso_op.hpp"
@@ -151,7 +152,88 @@ __global__ void k_unpermute(int64_t n, const int* __restrict__ perm, const doubl
     if (k < n) orig[perm[k]] = tree[k];
 }
 
-constexpr int kMdotBlocks = 1024;
+// ---- the CGS2 sweeps with the basis held in registers (nv <= 48 vectors): one read of
+// V per sweep.  Each thread owns elements j of its block's chunk;
+// the per-block sums of the NV products reduce by xor shuffles inside a wave and then
+// over the 4 waves in a fixed order (deterministic).
+template <int NV>
+__device__ __forceinline__ void block_partials(const double (&acc)[NV], int nv, double* red, double* part) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+        if (k < nv) {
+            double v = acc[k];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+            if (lane == 0) red[wv * NV + k] = v;
+        }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nv; k += blockDim.x)
+        part[(size_t)k * gridDim.x + blockIdx.x] = ((red[k] + red[NV + k]) + red[2 * NV + k]) + red[3 * NV + k];
+}
+
+// pass 1: part[k][blk] = sum over the block's chunk of V[k][j] w[j]
+template <int NV>
+__global__ void __launch_bounds__(256) k_cgs_dot(int64_t n, int nv, const double* __restrict__ V, int64_t ldv,
+                                                 const double* __restrict__ w, double* __restrict__ part) {
+    __shared__ double red[4 * NV];
+    const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t j0 = (int64_t)blockIdx.x * chunk, j1 = min(n, j0 + chunk);
+    double acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+    for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
+        double v[NV];  // every load of the element in flight before the products
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = k < nv ? V[(size_t)k * ldv + j] : 0.0;
+        const double wj = w[j];
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+            if (k < nv) acc[k] = __builtin_fma(v[k], wj, acc[k]);
+    }
+    block_partials<NV>(acc, nv, red, part);
+}
+
+// pass 2 / 3: w[j] -= sum_k c[k] V[k][j] (k_maxpy's order), then either the products
+// of the updated w with the same V[k][j] (DOT: the reorthogonalisation's h = V^T w)
+// or its square (||w||^2 into part[blk])
+template <int NV, bool DOT>
+__global__ void __launch_bounds__(256) k_cgs_update(int64_t n, int nv, const double* __restrict__ V, int64_t ldv,
+                                                    const double* __restrict__ c, double* __restrict__ w,
+                                                    double* __restrict__ part) {
+    __shared__ double red[4 * NV];
+    __shared__ double cs[NV];
+    for (int k = threadIdx.x; k < nv; k += blockDim.x) cs[k] = -c[k];
+    __syncthreads();
+    const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t j0 = (int64_t)blockIdx.x * chunk, j1 = min(n, j0 + chunk);
+    constexpr int NA = DOT ? NV : 1;
+    double acc[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) acc[k] = 0.0;
+    for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
+        double v[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = k < nv ? V[(size_t)k * ldv + j] : 0.0;
+        double a = w[j];
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+            if (k < nv) a = __builtin_fma(cs[k], v[k], a);
+        w[j] = a;
+        if constexpr (DOT) {
+#pragma unroll
+            for (int k = 0; k < NV; ++k)
+                if (k < nv) acc[k] = __builtin_fma(v[k], a, acc[k]);
+        } else {
+            acc[0] = __builtin_fma(a, a, acc[0]);
+        }
+    }
+    block_partials<NA>(acc, DOT ? nv : 1, red, part);
+}
+
+constexpr int kCgsMaxRegs = 48;  // basis vectors the register-held sweeps take
+
+constexpr int kMdotBlocks = 2048;  // partial sums per reduction (per-block chunks of ~2.5K elements at 1M x 5)
 
 struct Krylov {
     int64_t n;
@@ -164,6 +246,43 @@ struct Krylov {
     }
     void maxpy(int nv, const double* V, int64_t ldv, const double* c, double sign, double* w) {
         k_maxpy<<<nblk(n), 256, (size_t)nv * sizeof(double), s>>>(n, nv, V, ldv, c, sign, w);
+    }
+    // the three sweeps of a CGS2 step over nv basis vectors: h = V^T w; w -= V h with
+    // h2 = V^T w from the same read of V; w -= V h2 with ||w||^2 (one read of V each
+    // for nv <= kCgsMaxRegs, else the two-pass kernels above)
+    template <typename F>
+    static void nv_dispatch(int nv, F&& f) {
+        if (nv <= 8) f(std::integral_constant<int, 8>{});
+        else if (nv <= 16) f(std::integral_constant<int, 16>{});
+        else if (nv <= 32) f(std::integral_constant<int, 32>{});
+        else f(std::integral_constant<int, kCgsMaxRegs>{});
+    }
+    void dot(int nv, const double* V, int64_t ldv, const double* w, double* out) {
+        if (nv > kCgsMaxRegs) return mdot(nv, V, ldv, w, out, false);
+        nv_dispatch(nv, [&](auto c) {
+            k_cgs_dot<decltype(c)::value><<<kMdotBlocks, 256, 0, s>>>(n, nv, V, ldv, w, part);
+        });
+        k_mdot_final<<<nv, 256, 0, s>>>(kMdotBlocks, part, 0, out);
+    }
+    void updateDot(int nv, const double* V, int64_t ldv, const double* c, double* w, double* out) {
+        if (nv > kCgsMaxRegs) {
+            maxpy(nv, V, ldv, c, -1.0, w);
+            return mdot(nv, V, ldv, w, out, false);
+        }
+        nv_dispatch(nv, [&](auto cc) {
+            k_cgs_update<decltype(cc)::value, true><<<kMdotBlocks, 256, 0, s>>>(n, nv, V, ldv, c, w, part);
+        });
+        k_mdot_final<<<nv, 256, 0, s>>>(kMdotBlocks, part, 0, out);
+    }
+    void updateNorm(int nv, const double* V, int64_t ldv, const double* c, double* w, double* nrm2) {
+        if (nv > kCgsMaxRegs) {
+            maxpy(nv, V, ldv, c, -1.0, w);
+            return mdot(1, w, ldv, w, nrm2, false);
+        }
+        nv_dispatch(nv, [&](auto cc) {
+            k_cgs_update<decltype(cc)::value, false><<<kMdotBlocks, 256, 0, s>>>(n, nv, V, ldv, c, w, part);
+        });
+        k_mdot_final<<<1, 256, 0, s>>>(kMdotBlocks, part, 0, nrm2);
     }
 };
 
@@ -334,8 +453,22 @@ int Operator::blockSolveDev(const double* rhs, double* x, int restart, double to
         launch_permute(N, perm, x + (size_t)k * N, xt + (size_t)k * N, s);
     }
     Krylov kr{L, s, bPart.as<double>()};
+    // the Hessenberg column's host copy (pinned: an asynchronous read the host waits
+    // for with an event, not a stream drain)
+    struct HostCol {
+        double* p = nullptr;
+        hipEvent_t ev = nullptr;
+        ~HostCol() {
+            if (p) (void)hipHostFree(p);
+            if (ev) (void)hipEventDestroy(ev);
+        }
+    } col;
+    HIP_CHECK(hipHostMalloc((void**)&col.p, (size_t)(m + 2) * sizeof(double), hipHostMallocDefault));
+    HIP_CHECK(hipEventCreateWithFlags(&col.ev, hipEventDisableTiming));
+    double* hcPinned = col.p;
+    hipEvent_t evH = col.ev;
     auto norm2 = [&](const double* v) {  // ||v||^2 into hd[m + 1], returned on the host
-        kr.mdot(1, v, L, v, hd + m + 1, false);
+        kr.dot(1, v, L, v, hd + m + 1);
         double h = 0;
         HIP_CHECK(hipMemcpyAsync(&h, hd + m + 1, sizeof(double), hipMemcpyDeviceToHost, s));
         HIP_CHECK(hipStreamSynchronize(s));
@@ -365,19 +498,26 @@ int Operator::blockSolveDev(const double* rhs, double* x, int restart, double to
             std::fill(g.begin(), g.end(), 0.0);
             g[0] = beta;
             int used = 0;
+            bool ahead = false;  // the matvec of V[i] is already enqueued
             for (int i = 0; i < m; ++i) {
                 double* vi = V + (size_t)i * L;
-                blockOpDev(2, vi, N, w, N, true, s);
-                // CGS2: h = V^T w, w -= V h, twice (the second pass adds its correction)
-                kr.mdot(i + 1, V, L, w, hd, false);
-                kr.maxpy(i + 1, V, L, hd, -1.0, w);
-                kr.mdot(i + 1, V, L, w, bY.as<double>(), false);
-                kr.maxpy(i + 1, V, L, bY.as<double>(), -1.0, w);
+                if (!ahead) blockOpDev(2, vi, N, w, N, true, s);
+                // CGS2: h = V^T w, w -= V h, twice (the second pass adds its correction),
+                // as three sweeps over V: h; w -= V h with h2 = V^T w; w -= V h2 with ||w||^2
+                kr.dot(i + 1, V, L, w, hd);
+                kr.updateDot(i + 1, V, L, hd, w, bY.as<double>());
+                kr.updateNorm(i + 1, V, L, bY.as<double>(), w, hd + m + 1);
                 k_axpby<<<nblk(i + 1), 256, 0, s>>>(i + 1, 1.0, bY.as<double>(), 1.0, hd);
-                kr.mdot(1, w, L, w, hd + m + 1, false);
                 k_scale_rsqrt<<<nblk(L), 256, 0, s>>>(L, w, hd + m + 1, V + (size_t)(i + 1) * L);
-                HIP_CHECK(hipMemcpyAsync(hc.data(), hd, (size_t)(m + 2) * sizeof(double), hipMemcpyDeviceToHost, s));
-                HIP_CHECK(hipStreamSynchronize(s));
+                HIP_CHECK(hipMemcpyAsync(hcPinned, hd, (size_t)(m + 2) * sizeof(double), hipMemcpyDeviceToHost, s));
+                HIP_CHECK(hipEventRecord(evH, s));
+                // the next step's matvec goes in before the host reads the column: the GPU
+                // runs it while the host applies the rotations (wasted once per cycle, at
+                // the step that converges)
+                ahead = i + 1 < m;
+                if (ahead) blockOpDev(2, V + (size_t)(i + 1) * L, N, w, N, true, s);
+                HIP_CHECK(hipEventSynchronize(evH));
+                std::copy(hcPinned, hcPinned + m + 2, hc.begin());
                 double* Hc = H.data() + (size_t)i * ld;
                 for (int k = 0; k <= i; ++k) Hc[k] = hc[k];
                 Hc[i + 1] = std::sqrt(std::max(hc[m + 1], 0.0));
