@@ -115,6 +115,8 @@ def lib():
             "aniso_comm_init_rccl": [P, ctypes.c_char_p],
             "aniso_comm_init_callbacks": [P, ctypes.POINTER(Collectives)],
             "aniso_comm_init_loopback": [P],
+            "aniso_krylov_dot": [P, I64, I, P, I64, P, P, P],
+            "aniso_krylov_update": [P, I64, I, P, I64, P, P, P, I, P],
             "aniso_block_op_sharded_dev": [P, I, P, I64, P, I64, P],
             "aniso_memcpy": [P, P, ctypes.c_size_t],
         }
@@ -163,6 +165,20 @@ def _dev_vec(t, n, name, at_least=False):
             and (t.numel() >= n if at_least else t.numel() == n)):
         raise AnisoError(1, f"{name} must be a contiguous float64 CUDA tensor of {'>= ' if at_least else ''}{n} entries")
     return ctypes.c_void_p(t.data_ptr())
+
+
+def _krylov_args(V, w, out, nout):
+    import torch
+
+    for name, t in (("V", V), ("w", w), ("out", out)):
+        if not (t.is_cuda and t.dtype == torch.float64):
+            raise ValueError(f"{name}: float64 CUDA tensor expected")
+    if V.dim() != 2 or V.stride(1) != 1 or V.shape[0] < 1:
+        raise ValueError("V: (nv, n) with unit inner stride")
+    if not (w.is_contiguous() and w.numel() == V.shape[1]):
+        raise ValueError("w: contiguous, n entries")
+    if not (out.is_contiguous() and out.numel() >= nout):
+        raise ValueError(f"out: contiguous, >= {nout} entries")
 
 
 def _dev_rows(t, rows, cols, name):
@@ -474,6 +490,35 @@ class Aniso:
     def comm_init_rccl(self, unique_id):
         """Attach an RCCL communicator (every rank together, after set_shard)."""
         _check(lib().aniso_comm_init_rccl(self.address, bytes(unique_id)))
+
+    def krylov_dot(self, V, w, out, stream=None):
+        """out[k] = V[k] . w for the nv rows of V (aniso_krylov_dot); float64 CUDA
+        tensors, V (nv, n) with unit inner stride, w (n,), out (>= nv,)."""
+        import torch
+
+        nv, n = V.shape
+        _krylov_args(V, w, out, nv)
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_krylov_dot(self.address, int(n), int(nv), ctypes.c_void_p(V.data_ptr()), int(V.stride(0)),
+                                      ctypes.c_void_p(w.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                      ctypes.c_void_p(s)))
+        return out
+
+    def krylov_update(self, V, c, w, out, dots=True, stream=None):
+        """w -= V^T c, then out[:nv] = V w and out[nv] = w . w (dots) or out[0] = w . w
+        (aniso_krylov_update)."""
+        import torch
+
+        nv, n = V.shape
+        _krylov_args(V, w, out, nv + 1 if dots else 1)
+        if not (c.is_cuda and c.dtype == torch.float64 and c.is_contiguous() and c.numel() >= nv):
+            raise ValueError("c: contiguous float64 CUDA tensor of >= nv entries")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        _check(lib().aniso_krylov_update(self.address, int(n), int(nv), ctypes.c_void_p(V.data_ptr()),
+                                         int(V.stride(0)), ctypes.c_void_p(c.data_ptr()),
+                                         ctypes.c_void_p(w.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                         int(bool(dots)), ctypes.c_void_p(s)))
+        return out
 
     def comm_init_loopback(self):
         """Development: a loopback communicator (aniso_comm_init_loopback) to time one

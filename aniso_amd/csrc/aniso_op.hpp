@@ -132,6 +132,10 @@ public:
     // X, Y point-major N x 16 doubles in tree order.  The mode's fp64 caches (directed
     // lists, A order) are built from its operators at the first call.  Unsharded only.
     void mrhs64Dev(int id, bool forward, const double* X, double* Y, hipStream_t s, int mask = kStageAll);
+    // the block solve's CGS2 sweeps as primitives (aniso_krylov_dot / _update)
+    void krylovDot(int64_t n, int nv, const double* V, int64_t ldv, const double* w, double* out, hipStream_t s);
+    void krylovUpdate(int64_t n, int nv, const double* V, int64_t ldv, const double* c, double* w, double* out,
+                      bool dots, hipStream_t s);
     int64_t f32Bytes() const { return f32Ready ? (int64_t)(d32Km2l.bytes + d32Knear.bytes) : 0; }
     hipStream_t stream() const { return own; }
     // raise (ANISO_ERR_RUNTIME) if a fused top-of-tree launch gave up waiting for its
@@ -212,6 +216,7 @@ private:
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
     DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
     DevBuf dTopTrace;           // ANISO_TOP_TRACE=1: the launch's per-block timeline
+    DevBuf dKryPart;            // partial sums of the Krylov primitives
     bool topTraceOn = false;
     int hmRing = 0;  // the cluster M2L's LDS ring depth (ANISO_HM_RING; 0: the one-block-in-flight form)
     int topTraceBlocks = 0;

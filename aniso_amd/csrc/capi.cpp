@@ -389,7 +389,7 @@ int aniso_block_solve_dev(aniso_handle h, const double* rhs, double* x, int rest
         CHECK_PTR(rhs);
         CHECK_PTR(x);
         auto& op = get(h);
-        hipStream_t s = stream ? (hipStream_t)stream : op.stream();
+        hipStream_t s = (hipStream_t)stream;
         const int it = op.blockSolveDev(rhs, x, restart, tol, maxit, hist, hist ? maxhist : 0, relres, s);
         if (iters) *iters = it;
     });
@@ -618,6 +618,31 @@ int aniso_comm_init_callbacks(aniso_handle h, const aniso_collectives* c) {
     });
 }
 
+int aniso_krylov_dot(aniso_handle h, int64_t n, int nv, const double* V, int64_t ldv, const double* w, double* out,
+                     void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(V);
+        CHECK_PTR(w);
+        CHECK_PTR(out);
+        auto& op = get(h);
+        op.krylovDot(n, nv, V, ldv, w, out, (hipStream_t)stream);
+    });
+}
+
+int aniso_krylov_update(aniso_handle h, int64_t n, int nv, const double* V, int64_t ldv, const double* c, double* w,
+                        double* out, int dots, void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(V);
+        CHECK_PTR(c);
+        CHECK_PTR(w);
+        CHECK_PTR(out);
+        auto& op = get(h);
+        op.krylovUpdate(n, nv, V, ldv, c, w, out, dots != 0, (hipStream_t)stream);
+    });
+}
+
 int aniso_comm_init_loopback(aniso_handle h) {
     ENTER(h);
     return guarded([&] {
@@ -633,7 +658,7 @@ int aniso_block_op_sharded_dev(aniso_handle h, int which, double* x, int64_t ldx
         CHECK_PTR(x);
         CHECK_PTR(y);
         auto& op = get(h);
-        op.blockOpShardedDev(which, x, ldx, y, ldy, stream ? (hipStream_t)stream : op.stream());
+        op.blockOpShardedDev(which, x, ldx, y, ldy, (hipStream_t)stream);
     });
 }
 

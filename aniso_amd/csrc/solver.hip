@@ -157,19 +157,34 @@ __global__ void k_unpermute(int64_t n, const int* __restrict__ perm, const doubl
 // the per-block sums of the NV products reduce by xor shuffles inside a wave and then
 // over the 4 waves in a fixed order (deterministic).
 template <int NV>
-__device__ __forceinline__ void block_partials(const double (&acc)[NV], int nv, double* red, double* part) {
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// per-block sums of acc[k] (k < nv) into part[k * gridDim.x + blockIdx.x], and with SQ
+// of acc[NA - 1] into row nv: wave sums by xor shuffles, then the 4 waves in a fixed order
+template <int NA, bool SQ>
+__device__ __forceinline__ void block_partials(const double (&acc)[NA], int nv, double* red, double* part) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int ND = SQ ? NA - 1 : NA;
 #pragma unroll
-    for (int k = 0; k < NV; ++k)
+    for (int k = 0; k < ND; ++k)
         if (k < nv) {
-            double v = acc[k];
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-            if (lane == 0) red[wv * NV + k] = v;
+            const double v = wave_sum<0>(acc[k]);
+            if (lane == 0) red[wv * NA + k] = v;
         }
+    if constexpr (SQ) {
+        const double v = wave_sum<0>(acc[NA - 1]);
+        if (lane == 0) red[wv * NA + NA - 1] = v;
+    }
     __syncthreads();
-    for (int k = threadIdx.x; k < nv; k += blockDim.x)
-        part[(size_t)k * gridDim.x + blockIdx.x] = ((red[k] + red[NV + k]) + red[2 * NV + k]) + red[3 * NV + k];
+    const int rows = SQ ? nv + 1 : nv;
+    for (int k = threadIdx.x; k < rows; k += blockDim.x) {
+        const int i = SQ && k == nv ? NA - 1 : k;
+        part[(size_t)k * gridDim.x + blockIdx.x] = ((red[i] + red[NA + i]) + red[2 * NA + i]) + red[3 * NA + i];
+    }
 }
 
 // pass 1: part[k][blk] = sum over the block's chunk of V[k][j] w[j]
@@ -191,23 +206,23 @@ __global__ void __launch_bounds__(256) k_cgs_dot(int64_t n, int nv, const double
         for (int k = 0; k < NV; ++k)
             if (k < nv) acc[k] = __builtin_fma(v[k], wj, acc[k]);
     }
-    block_partials<NV>(acc, nv, red, part);
+    block_partials<NV, false>(acc, nv, red, part);
 }
 
-// pass 2 / 3: w[j] -= sum_k c[k] V[k][j] (k_maxpy's order), then either the products
-// of the updated w with the same V[k][j] (DOT: the reorthogonalisation's h = V^T w)
-// or its square (||w||^2 into part[blk])
+// pass 2 / 3: w[j] -= sum_k c[k] V[k][j] (k_maxpy's order), then the products of the
+// updated w with the same V[k][j] (DOT: the reorthogonalisation's h = V^T w, rows
+// 0 .. nv-1) and its square (||w||^2: row nv with DOT, row 0 without)
 template <int NV, bool DOT>
 __global__ void __launch_bounds__(256) k_cgs_update(int64_t n, int nv, const double* __restrict__ V, int64_t ldv,
                                                     const double* __restrict__ c, double* __restrict__ w,
                                                     double* __restrict__ part) {
-    __shared__ double red[4 * NV];
+    constexpr int NA = DOT ? NV + 1 : 1;
+    __shared__ double red[4 * NA];
     __shared__ double cs[NV];
     for (int k = threadIdx.x; k < nv; k += blockDim.x) cs[k] = -c[k];
     __syncthreads();
     const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
     const int64_t j0 = (int64_t)blockIdx.x * chunk, j1 = min(n, j0 + chunk);
-    constexpr int NA = DOT ? NV : 1;
     double acc[NA];
 #pragma unroll
     for (int k = 0; k < NA; ++k) acc[k] = 0.0;
@@ -224,11 +239,11 @@ __global__ void __launch_bounds__(256) k_cgs_update(int64_t n, int nv, const dou
 #pragma unroll
             for (int k = 0; k < NV; ++k)
                 if (k < nv) acc[k] = __builtin_fma(v[k], a, acc[k]);
-        } else {
-            acc[0] = __builtin_fma(a, a, acc[0]);
         }
+        acc[NA - 1] = __builtin_fma(a, a, acc[NA - 1]);
     }
-    block_partials<NA>(acc, DOT ? nv : 1, red, part);
+    if constexpr (DOT) block_partials<NA, true>(acc, nv, red, part);
+    else block_partials<1, false>(acc, 1, red, part);
 }
 
 constexpr int kCgsMaxRegs = 48;  // basis vectors the register-held sweeps take
@@ -264,15 +279,17 @@ struct Krylov {
         });
         k_mdot_final<<<nv, 256, 0, s>>>(kMdotBlocks, part, 0, out);
     }
+    // w -= V c, then out[k] = V_k . w (k < nv) and out[nv] = w . w
     void updateDot(int nv, const double* V, int64_t ldv, const double* c, double* w, double* out) {
         if (nv > kCgsMaxRegs) {
             maxpy(nv, V, ldv, c, -1.0, w);
-            return mdot(nv, V, ldv, w, out, false);
+            mdot(nv, V, ldv, w, out, false);
+            return mdot(1, w, ldv, w, out + nv, false);
         }
         nv_dispatch(nv, [&](auto cc) {
             k_cgs_update<decltype(cc)::value, true><<<kMdotBlocks, 256, 0, s>>>(n, nv, V, ldv, c, w, part);
         });
-        k_mdot_final<<<nv, 256, 0, s>>>(kMdotBlocks, part, 0, out);
+        k_mdot_final<<<nv + 1, 256, 0, s>>>(kMdotBlocks, part, 0, out);
     }
     void updateNorm(int nv, const double* V, int64_t ldv, const double* c, double* w, double* nrm2) {
         if (nv > kCgsMaxRegs) {
@@ -424,6 +441,29 @@ done:
 // is CGS2 on the device.  rhs / x: device, original order, block b at b * N.
 // Returns the total step count (negative if not converged); hist gets the relative
 // residual estimate after every step.
+// The CGS2 sweeps as library primitives for a caller's own Krylov loop (the sharded
+// GMRES of aniso_amd.solve.gmres_dist reduces their outputs over the ranks between
+// the calls): out[k] = V_k . w; and w -= V c followed by out[k] = V_k . w, out[nv] =
+// w . w (dots) or out[0] = w . w.  Device pointers, on stream s.
+void Operator::krylovDot(int64_t n, int nv, const double* V, int64_t ldv, const double* w, double* out,
+                         hipStream_t s) {
+    if (n < 0 || nv < 1 || ldv < n) throw std::invalid_argument("krylov dot: bad sizes");
+    ensureDevice();
+    dKryPart.alloc(std::max(dKryPart.bytes, (size_t)kMdotBlocks * (nv + 2) * sizeof(double)));
+    Krylov kr{n, s, dKryPart.as<double>()};
+    kr.dot(nv, V, ldv, w, out);
+}
+
+void Operator::krylovUpdate(int64_t n, int nv, const double* V, int64_t ldv, const double* c, double* w,
+                            double* out, bool dots, hipStream_t s) {
+    if (n < 0 || nv < 1 || ldv < n) throw std::invalid_argument("krylov update: bad sizes");
+    ensureDevice();
+    dKryPart.alloc(std::max(dKryPart.bytes, (size_t)kMdotBlocks * (nv + 2) * sizeof(double)));
+    Krylov kr{n, s, dKryPart.as<double>()};
+    if (dots) kr.updateDot(nv, V, ldv, c, w, out);
+    else kr.updateNorm(nv, V, ldv, c, w, out);
+}
+
 int Operator::blockSolveDev(const double* rhs, double* x, int restart, double tol, int maxit, double* hist,
                             int maxhist, double* relresOut, hipStream_t s) {
     if (plan.nranks != 1) throw std::logic_error("block solve on a sharded handle");
@@ -443,7 +483,7 @@ int Operator::blockSolveDev(const double* rhs, double* x, int restart, double to
     bV.alloc((size_t)(m + 1) * L * sizeof(double));
     bPart.alloc((size_t)kMdotBlocks * (m + 2) * sizeof(double));
     bH.alloc((size_t)(m + 2) * sizeof(double));  // Hessenberg column (m + 1 entries), then ||w||^2
-    bY.alloc((size_t)(m + 1) * sizeof(double));
+    bY.alloc((size_t)(m + 2) * sizeof(double));  // h2 (m + 1 entries), then ||w||^2
     double *b = bB.as<double>(), *xt = bX.as<double>(), *w = bW.as<double>(), *r = bR.as<double>();
     double* V = bV.as<double>();
     double* hd = bH.as<double>();

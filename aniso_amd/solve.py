@@ -232,7 +232,7 @@ def gmres_mixed(op, B, tol=1e-12, m=40, inner_tol=1e-6, max_outer=30, max_cycles
     return X, max_outer, inner, rel
 
 
-def gmres_dist(apply, b, restart=400, tol=1e-11, maxit=400, x0=None, allreduce=None, hist=None):
+def gmres_dist(apply, b, restart=400, tol=1e-11, maxit=400, x0=None, allreduce=None, hist=None, kry=None):
     """Restarted GMRES with MATLAB's semantics (aniso.m:159-173: gmres(A, rhs, restart,
     tol, maxit); the Arnoldi/Givens structure of gmres.cpp:53-169) on vectors that may
     be row slices of a sharded problem.
@@ -248,7 +248,13 @@ def gmres_dist(apply, b, restart=400, tol=1e-11, maxit=400, x0=None, allreduce=N
     cycle, confirmed by the explicit residual at its end).
 
     Returns (x, total steps (negative if not converged), final relative residual).
-    hist (a list) receives the estimate after every step."""
+    hist (a list) receives the estimate after every step.
+
+    kry (an aniso_amd.Aniso handle, CUDA vectors): the orthogonalisation runs on the
+    library's sweeps (aniso_krylov_dot / _update: three reads of the basis per step
+    instead of four, fixed-order reductions), the new basis vector is scaled on the
+    device, and the next step's matvec is enqueued before the host reads the
+    Hessenberg column for its rotations."""
     import torch
 
     red = allreduce or (lambda t: t)
@@ -274,6 +280,8 @@ def gmres_dist(apply, b, restart=400, tol=1e-11, maxit=400, x0=None, allreduce=N
     total = 0
     m = restart
     V = torch.empty((m + 1, n), dtype=b.dtype, device=b.device)
+    if kry is not None:
+        return _gmres_dist_dev(apply, b, x, w, V, m, tol, maxit, red, normb, r, beta, hist, kry)
     for _ in range(maxit):
         if relres <= tol or beta == 0.0:
             break
@@ -319,5 +327,80 @@ def gmres_dist(apply, b, restart=400, tol=1e-11, maxit=400, x0=None, allreduce=N
         x += (V[:used].t() @ torch.tensor(y, dtype=b.dtype, device=b.device)).view_as(b)
         r = residual()
         beta = nrm(r)
+        relres = beta / normb
+    return x, (total if relres <= tol else -max(total, 1)), relres
+
+
+def _gmres_dist_dev(apply, b, x, w, V, m, tol, maxit, red, normb, r, beta, hist, kry):
+    """gmres_dist's loop on the library's Krylov sweeps (see gmres_dist: kry)."""
+    import torch
+
+    dev = b.device
+    hb = torch.zeros(m + 2, dtype=torch.float64, device=dev)   # V^T w
+    h2 = torch.zeros(m + 2, dtype=torch.float64, device=dev)   # V^T w', then ||w'||^2
+    sq = torch.zeros(1, dtype=torch.float64, device=dev)
+    col = torch.zeros(m + 2, dtype=torch.float64, device=dev)  # [h, ||w''||]
+    host = torch.zeros(m + 2, dtype=torch.float64).pin_memory()
+    wv = w.reshape(-1)
+    relres = beta / normb
+    total = 0
+    for _ in range(maxit):
+        if relres <= tol or beta == 0.0:
+            break
+        V[0] = r.reshape(-1) / beta
+        H = np.zeros((m + 1, m))
+        cs, sn, g = np.zeros(m), np.zeros(m), np.zeros(m + 1)
+        g[0] = beta
+        used = 0
+        ahead = False
+        for i in range(m):
+            if not ahead:
+                apply(V[i].view_as(b), w)
+            Vi = V[: i + 1]
+            kry.krylov_dot(Vi, wv, hb)
+            red(hb[: i + 1])
+            kry.krylov_update(Vi, hb, wv, h2, dots=True)  # h2[:i+1] = V^T w', h2[i+1] = ||w'||^2
+            red(h2[: i + 2])
+            kry.krylov_update(Vi, h2, wv, sq, dots=False)
+            hn2 = torch.clamp(h2[i + 1] - (h2[: i + 1] * h2[: i + 1]).sum(), min=0.0)
+            hn = torch.sqrt(hn2)
+            V[i + 1] = wv * torch.where(hn > 0, 1.0 / torch.where(hn > 0, hn, 1.0), 0.0)
+            col[: i + 1] = hb[: i + 1] + h2[: i + 1]
+            col[i + 1] = hn
+            host[: i + 2].copy_(col[: i + 2], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            ahead = i + 1 < m
+            if ahead:  # the next matvec runs while the host applies the rotations
+                apply(V[i + 1].view_as(b), w)
+            ev.synchronize()
+            hc = host[: i + 2].numpy()
+            H[: i + 1, i] = hc[: i + 1]
+            H[i + 1, i] = hc[i + 1]
+            for k in range(i):  # the previous rotations (gmres.cpp:136-139)
+                t = cs[k] * H[k, i] + sn[k] * H[k + 1, i]
+                H[k + 1, i] = -sn[k] * H[k, i] + cs[k] * H[k + 1, i]
+                H[k, i] = t
+            den = np.hypot(H[i, i], H[i + 1, i])
+            cs[i], sn[i] = (1.0, 0.0) if den == 0 else (H[i, i] / den, H[i + 1, i] / den)
+            H[i, i], H[i + 1, i] = den, 0.0
+            g[i + 1] = -sn[i] * g[i]
+            g[i] = cs[i] * g[i]
+            total += 1
+            used = i + 1
+            relres = abs(g[i + 1]) / normb
+            if hist is not None:
+                hist.append(relres)
+            if relres <= tol or hc[i + 1] == 0.0:
+                break
+        y = np.zeros(used)
+        for k in range(used - 1, -1, -1):
+            y[k] = (g[k] - H[k, k + 1:used] @ y[k + 1:]) / H[k, k] if H[k, k] != 0 else 0.0
+        x += (V[:used].t() @ torch.tensor(y, dtype=b.dtype, device=b.device)).view_as(b)
+        apply(x, w)
+        r = b - w
+        t = (r.reshape(-1) @ r.reshape(-1)).reshape(1)
+        red(t)
+        beta = float(t.sqrt())
         relres = beta / normb
     return x, (total if relres <= tol else -max(total, 1)), relres

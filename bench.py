@@ -469,12 +469,12 @@ def main():
             gb = rhs0[:, ob:oe].contiguous()
             gapply = adist.native_block_matvec(op, nb, "cuda") if native else adist.sharded_block_matvec(op, xchg)
             gred = xchg.allreduce
-        gmres_dist(gapply, gb, restart=2, tol=0.0, maxit=1, allreduce=gred)  # warm-up
+        gmres_dist(gapply, gb, restart=2, tol=0.0, maxit=1, allreduce=gred, kry=op)  # warm-up
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        _, _, grel = gmres_dist(gapply, gb, restart=args.gmres, tol=0.0, maxit=1, allreduce=gred)
+        _, _, grel = gmres_dist(gapply, gb, restart=args.gmres, tol=0.0, maxit=1, allreduce=gred, kry=op)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -486,8 +486,10 @@ def main():
         line["gmres"] = {"steps": args.gmres, "steps_per_s": round(args.gmres / gel, 3),
                          "ms_per_step": round(1e3 * gel / args.gmres, 4), "matvecs": args.gmres + 2,
                          "relres_after": grel,
-                         "method": "aniso_amd.solve.gmres_dist: restarted GMRES, CGS2 (2 all-reduces per step), "
-                                   "Krylov basis in HBM; tol 0 so exactly `steps` Arnoldi steps are timed"}
+                         "method": "aniso_amd.solve.gmres_dist: restarted GMRES, CGS2 (2 all-reduces per step) on "
+                                   "the library's sweeps (aniso_krylov_dot/_update), Krylov basis in HBM, the next "
+                                   "matvec enqueued ahead of the host's rotations; tol 0 so exactly `steps` Arnoldi "
+                                   "steps are timed"}
     if args.config4_sz > 0 and block:
         # BASELINE configs[3]: sz = 2048 (4,194,304 points), d = 1, mode 0 -- main.cpp's GMRES
         # matvec u - K_0(sigma_s .* u), the configuration BASELINE names for 8 GPUs --

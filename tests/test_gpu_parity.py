@@ -1006,6 +1006,63 @@ def test_fused_top_of_tree_launch_matches_tier_launches(ks):
     assert _rel(outs[0], outs[1]) <= 1e-13 and _rel(outs[2], outs[1]) <= 1e-13
 
 
+@pytest.mark.parametrize("nv", [1, 7, 16, 17, 40, 60])
+def test_krylov_primitives_match_torch(nv):
+    """aniso_krylov_dot / _update (the CGS2 sweeps of the block solve and of
+    gmres_dist: register-held bases up to 48 vectors, the two-pass kernels above)
+    against torch fp64 on random bases, n not a multiple of the block size."""
+    torch = _torch()
+    import aniso_amd
+
+    a = aniso_amd.Aniso(8, 1, 2, 0.8, 10, 4, 20)
+    g = torch.Generator(device="cuda").manual_seed(nv)
+    n = 300_007
+    V = torch.rand(nv, n, dtype=torch.float64, device="cuda", generator=g) - 0.5
+    w = torch.rand(n, dtype=torch.float64, device="cuda", generator=g) - 0.5
+    c = torch.rand(nv, dtype=torch.float64, device="cuda", generator=g) - 0.5
+    out = torch.zeros(nv + 1, dtype=torch.float64, device="cuda")
+    a.krylov_dot(V, w, out)
+    ref = V @ w
+    assert float((out[:nv] - ref).abs().max() / ref.abs().max()) <= 1e-12
+    w1, w2 = w.clone(), w.clone()
+    a.krylov_update(V, c, w1, out, dots=True)
+    wr = w - V.t() @ c
+    assert float((w1 - wr).abs().max() / wr.abs().max()) <= 1e-12
+    assert float((out[:nv] - V @ wr).abs().max() / (V @ wr).abs().max()) <= 1e-12
+    assert abs(float(out[nv]) - float(wr @ wr)) <= 1e-12 * float(wr @ wr)
+    sq = torch.zeros(1, dtype=torch.float64, device="cuda")
+    a.krylov_update(V, c, w2, sq, dots=False)
+    assert torch.equal(w1, w2)
+    assert abs(float(sq[0]) - float(wr @ wr)) <= 1e-12 * float(wr @ wr)
+
+
+def test_gmres_dist_on_library_sweeps_matches_torch_path():
+    """gmres_dist with kry (the library's sweeps, device scaling, the next matvec ahead
+    of the rotations) takes the same steps as its torch path on the block operator
+    and lands on the same solution."""
+    torch = _torch()
+    import aniso_amd
+    from aniso_amd.solve import gmres_dist
+
+    a = aniso_amd.Aniso(32, 1, 5, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    a.setCoeff(*main_coeffs(xy))
+    for m in range(9):
+        a.cache(m)
+    b = torch.tensor(np.random.default_rng(3).uniform(-1, 1, (5, a.N)), device="cuda")
+
+    def apply(x, y):
+        a.block_op_dev(2, x, y, tree=True)
+
+    for restart in (6, 40):
+        h0, h1 = [], []
+        x0, its0, r0 = gmres_dist(apply, b, restart=restart, tol=1e-11, maxit=20, hist=h0)
+        x1, its1, r1 = gmres_dist(apply, b, restart=restart, tol=1e-11, maxit=20, hist=h1, kry=a)
+        assert its0 == its1 and its1 > 0 and r1 <= 1e-11
+        assert np.allclose(h0, h1, rtol=1e-6, atol=1e-14)
+        assert float(torch.linalg.norm(x1 - x0) / torch.linalg.norm(x0)) <= 1e-10
+
+
 def test_loopback_communicator_runs_a_rank_schedule():
     """aniso_comm_init_loopback (development: one rank's schedule of an N-GPU run on
     one GPU, tools/shard_time.py --native): the one-call sharded matvec runs on it and
