@@ -695,6 +695,20 @@ __global__ void __launch_bounds__(256) k_near(int nl, const int4* __restrict__ l
 // dn = (node, parent code: LDS slot, -1 none/zero, -2 the task root; child slot, 0).
 // Phase 0 issues every independent global load of the task at once (locals of
 // all nodes and chain ancestors, leaf boxes, near partial offsets) into LDS.
+#ifdef ANISO_DOWN_TRACE  // development variant: per-task phase timestamps of the down pass
+__device__ long long g_downTrace[16384 * 6];
+__device__ __forceinline__ void down_mark(int f) {
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < 16384) {
+        g_downTrace[blockIdx.x * 6 + f] = (long long)__builtin_amdgcn_s_memrealtime();
+        if (f == 0) g_downTrace[blockIdx.x * 6 + 5] = (long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+    }
+}
+#define DOWN_MARK(f) down_mark(f)
+#else
+#define DOWN_MARK(f)
+#endif
+
 template <int K>
 __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     int maxTask, int maxLeaves, const int4* __restrict__ desc, const int* __restrict__ grpFix,
@@ -717,7 +731,9 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     int* NB = LS + maxLeaves;                              // maxLeaves: first of the leaf's near offsets in NO
     int* NC = NB + maxLeaves;                              // maxLeaves: their count
     int* NO = NC + maxLeaves;                              // maxNear: partial offsets addressed to this task
+    int2* CN = reinterpret_cast<int2*>(NO + maxNear + ((maxNear + 1) & 1));  // maxChain: (ancestor, child index), 8-B aligned
     const int task = blockIdx.x;
+    DOWN_MARK(0);
     // task record: (first node, nodes, first leaf entry, leaves), (owned points begin,
     // end, first chain entry, chain length), (first near offset, count, levels, 0)
     const int4 d0 = desc[3 * task], d1 = desc[3 * task + 1], d2 = desc[3 * task + 2];
@@ -727,14 +743,12 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     const int npts = pr.y - pr.x, ngrp = d2.z;
     const int* gs = grpFix + (size_t)task * (kTaskLevels + 1);
     const bool far = flags & kStageFar;
-    // ---- phase 0: independent loads
+    // ---- phase 0: the task's records, then (one more round) the locals they address --
+    // every load of a round independent, none behind another global load
     if (far) {
         for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) Rl[i] = (&P->R[0][0])[i];
         for (int k = threadIdx.x; k < nt; k += blockDim.x) DN[k] = dn[n0 + k];
-        for (int it = threadIdx.x; it < nt * RK; it += blockDim.x)
-            T[it] = local[(size_t)dn[n0 + it / RK].x * RK + it % RK];
-        for (int it = threadIdx.x; it < nc * RK; it += blockDim.x)
-            CH[it] = local[(size_t)chain[c0 + it / RK].x * RK + it % RK];
+        for (int k = threadIdx.x; k < nc; k += blockDim.x) CN[k] = chain[c0 + k];
     }
     for (int e = threadIdx.x; e < nl; e += blockDim.x) {
         LB[e] = leafBegin[l0 + e];
@@ -751,6 +765,12 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     if (threadIdx.x == 0) LB[nl] = pr.y;
     for (int j = threadIdx.x; j < d2.y; j += blockDim.x) NO[j] = nearOff[d2.x + j];
     __syncthreads();
+    if (far) {
+        for (int it = threadIdx.x; it < nt * RK; it += blockDim.x) T[it] = local[(size_t)DN[it / RK].x * RK + it % RK];
+        for (int it = threadIdx.x; it < nc * RK; it += blockDim.x) CH[it] = local[(size_t)CN[it / RK].x * RK + it % RK];
+        __syncthreads();
+    }
+    DOWN_MARK(1);
     // ---- phase 1: the root's parent total by the L2L chain from level 1
     // (bbfmm.h:1070-1071 along the ancestors), then the task's levels
     if (far) {
@@ -759,7 +779,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
                 const int r = threadIdx.x / K, i = threadIdx.x - (threadIdx.x / K) * K;
                 double v = (nc > 0 && threadIdx.x < RK) ? CH[threadIdx.x] : 0.0;
                 for (int jc = 1; jc < nc; ++jc) {
-                    const double* R = Rl + chain[c0 + jc].y * kRank * kRank;
+                    const double* R = Rl + CN[jc].y * kRank * kRank;
                     double a = threadIdx.x < RK ? CH[jc * RK + threadIdx.x] : 0.0;
 #pragma unroll
                     for (int c = 0; c < kRank; ++c) a += R[(r & 15) + c * kRank] * __shfl(v, c * K + i);
@@ -771,7 +791,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             for (int it = threadIdx.x; it < RK; it += blockDim.x) PT[it] = nc > 0 ? CH[it] : 0.0;
             __syncthreads();
             for (int jc = 1; jc < nc; ++jc) {
-                const double* R = Rl + chain[c0 + jc].y * kRank * kRank;
+                const double* R = Rl + CN[jc].y * kRank * kRank;
                 const int r = threadIdx.x / K, i = threadIdx.x - (threadIdx.x / K) * K;
                 double a = 0.0;
                 if (threadIdx.x < RK) {
@@ -785,6 +805,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             }
         }
         __syncthreads();
+        DOWN_MARK(2);
         for (int g = 0; g < ngrp; ++g) {
             const int s0 = gs[g], s1 = gs[g + 1];
             for (int it = threadIdx.x; it < (s1 - s0) * kRank; it += blockDim.x) {
@@ -808,6 +829,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             __syncthreads();
         }
     }
+    DOWN_MARK(3);
     // ---- phase 2: owned points: L2P + near gather
     for (int g = threadIdx.x; g < npts; g += blockDim.x) {
         const int kpos = pr.x + g;
@@ -859,7 +881,14 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
             for (int i = 0; i < K; ++i) out[(size_t)i * ldo + o] += scale * v[i];
         }
     }
+    DOWN_MARK(4);
 }
+
+#ifdef ANISO_DOWN_TRACE
+extern "C" __attribute__((visibility("default"))) int aniso_debug_down_trace(long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_downTrace), (size_t)n * 6 * sizeof(long long)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 // ----------------------------------------------------------------- corrections
 
@@ -944,7 +973,8 @@ size_t up_tier_lds(int maxTask, int K) {
 
 size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain, int K) {
     return (size_t)(4 * kRank * kRank + (maxTask + 1 + maxChain) * kRank * K + 4 * maxLeaves) * sizeof(double) +
-           (size_t)(4 * maxLeaves + 4 + maxNear) * sizeof(int) + (size_t)maxTask * sizeof(int4);
+           (size_t)(4 * maxLeaves + 4 + maxNear) * sizeof(int) + (size_t)maxTask * sizeof(int4) +
+           (size_t)maxChain * sizeof(int2);
 }
 
 void launch_up_tier(int K, int ntask, int taskBase, const int* taskList, int maxTask, const int4* desc,
