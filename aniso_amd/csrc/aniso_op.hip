@@ -83,7 +83,11 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_FUSE_SUB")) fuseSub = e[0] != '0';
     if (const char* e = std::getenv("ANISO_TOP_SPIN_LIMIT")) topSpinLimit = (unsigned)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("ANISO_TOP_TRACE")) topTraceOn = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ANISO_NEAR_IN_TOP")) nearInTop = std::atoi(e) != 0;
     hmRing = hm_ring_depth();
+    if (const char* e = std::getenv("ANISO_HM_WPE")) hmWpe = std::atoi(e);
+    if (const char* e = std::getenv("ANISO_NEAR_WPE")) nearWpe = std::atoi(e);
+    if (const char* e = std::getenv("ANISO_TOP_FUSED")) topFusedMode = std::atoi(e) != 0 ? 1 : 0;
     sigma_s.assign(geo.N, 0.0);
     sigma_t.assign(geo.N, 0.0);
     modes.resize(kernelSize);
@@ -733,18 +737,26 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     // the harmonic block apply runs its near field + corrections (they write `out`)
     // on a side stream beside the M2L (it writes the locals), forked as soon as the
     // weighted charges are complete: after the last up tier with a P2M leaf
-    const bool fork = harmonic && overlap;
-    const hipStream_t sn = fork ? side : s;
     const ModeArgs* tab = modeTable(K, nterm, ids, mixes);
     const CorrFold& cf = corrTable(K, nterm, ids, mixes);
+    const NearCorr nc{dNearCorrRow.as<uint16_t>(), dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
+                      cf.Wc.as<double>(), cf.Wm.as<double>(), P};
     const int ntier = (int)plan.upTierTask.size() - 1;  // 0: a lone leaf
+    // the upper tiers ride in the M2L launch (k_top_m2l_hc) when every leaf is in the
+    // bottom tier: the near field then forks after it
+    const bool topFused = harmonic && (mask & kStageFar) && topFusedOn();
+    // ANISO_NEAR_IN_TOP: the near field (+ corrections) as the last blocks of that
+    // launch (the one-block M2L form; a shard's phase 1 then leaves it to phase 2)
+    const bool ringOn = hmRing > 0 && hm_ring_xl(K, plan.hmMaxCl, hmRing) >= 0;
+    const bool nearFused = topFused && overlap && nearInTop && !ringOn && plan.nearCorrOk &&
+                           near_hs_fusable((int)plan.leaves.size(), plan.nearMaxLeaf, plan.nsMax,
+                                           dNearLoc.as<uint16_t>(), &nc, mask);
+    const bool fork = harmonic && overlap && !nearFused;
+    const hipStream_t sn = fork ? side : s;
     // the near field forks after the whole up pass on one GPU: forked after the
     // bottom tier it starved the latency-bound upper tiers the M2L waits on (up pass
     // 0.25 -> 0.14 ms, 644 -> 660 block matvec/s); a sharded apply starts it in
     // phase 1, beside the root exchange (8 shards: 0.317 vs 0.327 ms per rank)
-    // the upper tiers ride in the M2L launch (k_top_m2l_hc) when every leaf is in the
-    // bottom tier: the near field then forks after it
-    const bool topFused = harmonic && (mask & kStageFar) && topFusedOn();
     const int forkTier = phase == 0 && !topFused ? std::max(ntier - 1, 0) : plan.upLastLeafTier;
     // one up tier; a sharded apply's bottom tier runs this rank's tasks only (list)
     // and stores its tier-0 roots into send, its next tier reads the gathered ones
@@ -766,14 +778,12 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         if (harmonic) {
             // the corrections ride in the staged near kernel (d = 1, its table holds
             // every stencil neighbour; Plan::nearCorrRow)
-            const NearCorr nc{dNearCorrRow.as<uint16_t>(), dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
-                              cf.Wc.as<double>(), cf.Wm.as<double>(), P};
             corrFused = launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
                            dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(), dNearKOff.as<int64_t>(),
                            dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dSigDiag.as<double>(), hw,
                            dFT.as<double>(), operm, obase, ldo, mask, scale, out,
                            dNearLoc.as<uint16_t>(), dNsPtr.as<int64_t>(), dNsPts.as<int>(),
-                           plan.nsMax, plan.nearCorrOk ? &nc : nullptr, sn);
+                           plan.nsMax, plan.nearCorrOk ? &nc : nullptr, nearWpe, sn);
         } else if (plan.nearPartTotal > 0) {
             // symmetric U storage (K = 1 handles): one launch per term; the transposed
             // products go to partials summed over the terms
@@ -806,6 +816,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                      dHmBlk.as<int>(), dHmSlot.as<int>(), dAttM2L.as<double>(), dNcx.as<double>(), dNcy.as<double>(),
                      dNrx.as<double>(), dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(),
                      dNodeGeo.as<double>()};
+    hca.wpe = hmWpe;
     if (hmRing > 0) {
         const int xl = hm_ring_xl(K, plan.hmMaxCl, hmRing);
         hca.ring = xl < 0 ? 0 : hmRing;
@@ -833,7 +844,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         if (phase == 1) {
             const int ep = tm ? mark(s) : -1;
             span(1, e0, ep);
-            if (ntier < 1 || forkTier == 0) {
+            if ((ntier < 1 || forkTier == 0) && !nearFused) {
                 nearStage();
                 nearDone = true;
             }
@@ -863,7 +874,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     int ep = tm ? mark(s) : -1;
     span(1, e0, ep);
     if (phase == 2) e0 = pend.e0;
-    if (!nearDone) {
+    if (!nearDone && !nearFused) {
         nearStage();
         if (tm && sn == s) ep = mark(s);  // serial (ANISO_OVERLAP=0): the M2L span starts after the near field
     }
@@ -885,13 +896,18 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             ta.recv1 = phase == 2 ? rootsRecv : nullptr;
             ta.spinLimit = topSpinLimit;
             HIP_CHECK(hipHostGetDevicePointer((void**)&ta.err, topErr, 0));
+            const NearHsArgs na{(int)plan.leaves.size(), plan.nsMax, dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
+                                dNearLoc.as<uint16_t>(), dNsPtr.as<int64_t>(), dNsPts.as<int>(),
+                                dNearKOff.as<int64_t>(), dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(),
+                                dSigDiag.as<double>(), hw, dFT.as<double>(), operm, obase, ldo, mask, scale, out, nc};
             if (topTraceOn) {
-                topTraceBlocks = ta.nUp + ncl;
+                topTraceNear = nearFused ? (na.nl + 15) / 16 : 0;
+                topTraceBlocks = ta.nUp + ncl + topTraceNear;
                 if (dTopTrace.bytes < (size_t)topTraceBlocks * 4 * sizeof(int64_t))
                     dTopTrace.alloc((size_t)topTraceBlocks * 4 * sizeof(int64_t));
                 ta.trace = dTopTrace.as<int64_t>();
             }
-            launch_top_m2l_hc(K, ncl, plan.hmMaxCl, ua, ta, hca, s);
+            launch_top_m2l_hc(K, ncl, plan.hmMaxCl, ua, ta, hca, nearFused ? &na : nullptr, s);
         } else if (clustered) {
             m2lClusters(0, ncl, s);
         } else if (harmonic) {
@@ -1046,6 +1062,8 @@ std::vector<int64_t> Operator::topTrace() {
             int k = 1;
             while (k + 1 < ntier && b >= plan.upTierTask[k + 1] - u1) ++k;
             out.insert(out.end(), {(int64_t)-k, (int64_t)(k - 1), 0, 0});
+        } else if (b >= topTraceBlocks - topTraceNear) {  // a near-field group (16 leaves)
+            out.insert(out.end(), {(int64_t)-99, 0, 16, 0});
         } else {
             const int c = b - nUp, t0 = plan.hmClPtr[c], t1 = plan.hmClPtr[c + 1];
             out.insert(out.end(), {(int64_t)c, (int64_t)plan.hmClWait[c], (int64_t)(t1 - t0),

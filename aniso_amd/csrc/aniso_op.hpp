@@ -149,10 +149,12 @@ public:
     std::vector<int64_t> topTrace();
     bool harmonicReady() const { return useAtt && attReady; }
     bool clustersOn() const { return useClusters; }
-    // the block apply's upper up tiers ride in the clustered M2L launch (k_top_m2l_hc)
+    // the block apply's upper up tiers ride in the clustered M2L launch (k_top_m2l_hc);
+    // ANISO_TOP_FUSED=0 runs them as launches of their own before the clusters (a rank
+    // of 8: 0.262 against 0.251 ms, same-process A/B r03ls)
     bool topFusedOn() const {
         const int ntier = (int)plan.upTierTask.size() - 1;
-        return useClusters && top_fused_enabled() && ntier >= 2 && ntier <= kMaxTopTiers &&
+        return useClusters && topFusedMode != 0 && top_fused_enabled() && ntier >= 2 && ntier <= kMaxTopTiers &&
                plan.upLastLeafTier == 0 && plan.hmClWait.size() + 1 == plan.hmClPtr.size();
     }
     // bitwise-reproducible applies: the harmonic M2L as one wave per target (a fixed
@@ -219,7 +221,13 @@ private:
     DevBuf dKryPart;            // partial sums of the Krylov primitives
     bool topTraceOn = false;
     int hmRing = 0;  // the cluster M2L's LDS ring depth (ANISO_HM_RING; 0: the one-block-in-flight form)
-    int topTraceBlocks = 0;
+    int hmWpe = 0;   // ANISO_HM_WPE=3/4/8: the one-block form's occupancy (0: 4 where LDS allows)
+    int nearWpe = 4;  // ANISO_NEAR_WPE: the staged near field at 4 (<= 128 VGPRs) or 3 waves per SIMD
+    int topFusedMode = 1;  // ANISO_TOP_FUSED=0: the upper up tiers as launches of their own
+    // the near field's groups ride at the end of the fused top-of-tree + M2L launch
+    // instead of a side-stream launch (ANISO_NEAR_IN_TOP=1; on a shard in phase 2)
+    bool nearInTop = false;
+    int topTraceBlocks = 0, topTraceNear = 0;
     // the attached communicator and its halo exchange plan (commInit): per element of
     // the send / receive position lists its tree position and its place in the
     // peer-major buffers (base + b * stride for block b); doubles per peer

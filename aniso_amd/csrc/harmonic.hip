@@ -286,6 +286,20 @@ __device__ __forceinline__ void m2l_hc_store_target(double (&c)[4][K], double* a
     }
 }
 
+// x distance from a source point to the target's Chebyshev column j (j unrolled):
+// axs = source x - target centre, u0 / u1 = r cheb_0 / r cheb_1 (cheb_3 = -cheb_0,
+// cheb_2 = -cheb_1 for np = 4)
+__device__ __forceinline__ double cheb_dx(int j, double axs, double u0, double u1) {
+    return j == 0 ? axs - u0 : j == 1 ? axs - u1 : j == 2 ? axs + u1 : axs + u0;
+}
+
+// The same distances for the 4-wave form (LR): from wave-uniform values only,
+// dx_j = axs - r cheb_j (one FMA with two scalar operands; ~2-4 % more VALU, but no
+// VGPRs held for the target's columns).
+__device__ __forceinline__ double cheb_dx_lr(int j, double axs, double r, const Params* __restrict__ P) {
+    return __builtin_fma(-r, P->cheb[j], axs);
+}
+
 // The harmonic M2L in clusters: one 4-wave workgroup per
 // cluster (the active targets of one level under one ancestor kClusterDepth levels
 // up), the cluster's locals accumulated in LDS.  Each wave takes the cluster's
@@ -296,7 +310,9 @@ __device__ __forceinline__ void m2l_hc_store_target(double (&c)[4][K], double* a
 // (ds_add_f64).  The block stream drops by the in-cluster share (0.65 of the V
 // pairs at 64 targets per cluster, tools/vfrac.py); the summation order of the LDS
 // adds is not fixed (results repeat to rounding, not bitwise).
-template <int K, int NR>
+// LR: the 4-wave-per-SIMD form (<= 128 VGPRs, k_m2l_hc / k_top_m2l_hc with WPE = 4)
+// for launches whose LDS allows 4 workgroups per CU (small clusters: shards)
+template <int K, int NR, bool LR = false>
 __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, double* sm) {
     const int* __restrict__ clPtr = a.clPtr;
     const int* __restrict__ tgt = a.tgt;
@@ -336,9 +352,11 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // xa visible to every lane of the wave
         __builtin_amdgcn_wave_barrier();
-        double bx[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bx[j] = ncx[n] + nrx[n] * P->cheb[j];
+        // the target's Chebyshev x offsets: cheb_3 = -cheb_0, cheb_2 = -cheb_1 (np = 4), so
+        // dx_j = (ax - tcx) -+ u0 / u1 -- 4 VGPRs instead of 8 for the 4 coordinates
+        const double tcx = ncx[n], trx = nrx[n];
+        const double u0 = LR ? 0.0 : trx * P->cheb[0], u1 = LR ? 0.0 : trx * P->cheb[1];
+        auto dxj = [&](int j, double axs) { return LR ? cheb_dx_lr(j, axs, trx, P) : cheb_dx(j, axs, u0, u1); };
         const double by = ncy[n] + nry[n] * P->cheb[q];
         double c[4][K];
 #pragma unroll
@@ -377,14 +395,14 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                     }
     #pragma unroll
                     for (int g = 0; g < PG; ++g) {
-                        const double ax = ncx[B[g]] + nrx[B[g]] * chx;
+                        const double axs = (ncx[B[g]] - tcx) + nrx[B[g]] * chx;
                         const double dy = (ncy[B[g]] + nry[B[g]] * chy) - by;
                         const double dy2 = dy * dy;
                         double xw[K];
     #pragma unroll
                         for (int b = 0; b < K; ++b) xw[b] = hw.hw[b] * xm[g][b];
     #pragma unroll
-                        for (int j = 0; j < 4; ++j) hm_entry<K, false, NR>(e4[g][j], ax - bx[j], dy2, xw, c[j]);
+                        for (int j = 0; j < 4; ++j) hm_entry<K, false, NR>(e4[g][j], dxj(j, axs), dy2, xw, c[j]);
                     }
                 }
             }
@@ -393,18 +411,20 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                 const int cnt = (int)min<int64_t>(kWave, p1 - cb);
                 const int mySrc = lane < cnt ? src[cb + lane] : 0;
                 const int myBlk = lane < cnt ? blk[cb + lane] : 0;
-                const int mySlot = lane < cnt ? slot[cb + lane] : 0;
+                // LR: the partner's slot by a scalar load (needed only at the flush), one
+                // VGPR fewer across the stream
+                const int mySlot = !LR && lane < cnt ? slot[cb + lane] : 0;
                 for (int jj = 0; jj < cnt; ++jj) {
                     const int b = __builtin_amdgcn_readlane(myBlk, jj);
                     const int B = __builtin_amdgcn_readlane(mySrc, jj);
-                    const int sl = __builtin_amdgcn_readlane(mySlot, jj);
+                    const int sl = LR ? slot[cb + jj] : __builtin_amdgcn_readlane(mySlot, jj);
                     const dbl2* p = reinterpret_cast<const dbl2*>(E + (size_t)b * 256 + 16 * s + 4 * q);
                     const dbl2 k0 = p[0], k1 = p[1];
                     double xm[K];
                     const double* m = mult + ((size_t)B * kRank + s) * K;
     #pragma unroll
                     for (int bb = 0; bb < K; ++bb) xm[bb] = m[bb];
-                    const double ax = ncx[B] + nrx[B] * chx;
+                    const double axs = (ncx[B] - tcx) + nrx[B] * chx;
                     const double dy = (ncy[B] + nry[B] * chy) - by;
                     const double dy2 = dy * dy;
                     double xw[K], ob[K];
@@ -416,7 +436,7 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                     const double e4[4] = {k0.x, k0.y, k1.x, k1.y};
     #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        hm_entry2<K, NR>(e4[j], ax - bx[j], dy2, xw, xa + (4 * q + j) * K, c[j], ob);
+                        hm_entry2<K, NR>(e4[j], dxj(j, axs), dy2, xw, xa + (4 * q + j) * K, c[j], ob);
     #pragma unroll
                     for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // rows 4q'+j over the quad
                     if (q == 0) {
@@ -693,10 +713,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     m2l_hcr_cluster<K, NR, D, XL>((int)blockIdx.x, a, sm);
 }
 
+// WPE: waves per SIMD; 4 = the LR form (<= 128 VGPRs), 8 = the LR form with 8 waves
+// (512 threads) per cluster, 2 clusters per CU
 template <int K, int NR, int WPE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_m2l_hc(HcArgs a) {
+__global__ void __launch_bounds__(WPE == 8 ? 512 : 256) __attribute__((amdgpu_waves_per_eu(WPE == 8 ? 4 : WPE)))
+k_m2l_hc(HcArgs a) {
     extern __shared__ double sm[];
-    m2l_hc_cluster<K, NR>((int)blockIdx.x, a, sm);
+    m2l_hc_cluster<K, NR, (WPE >= 4)>((int)blockIdx.x, a, sm);
 }
 
 // ----------------------------------------------------------------- fused top of tree + M2L
@@ -762,15 +785,21 @@ __device__ __forceinline__ void top_mark(const TopArgs& t, int field) {
     }
 }
 
-template <int K, int NR, int D, bool XL>
+template <int K, int NR, int D, bool XL, bool LR = false>
 __device__ __forceinline__ void m2l_cluster_form(int cid, const HcArgs& a, double* sm) {
-    if constexpr (D == 0) m2l_hc_cluster<K, NR>(cid, a, sm);
+    if constexpr (D == 0) m2l_hc_cluster<K, NR, LR>(cid, a, sm);
     else m2l_hcr_cluster<K, NR, D, XL>(cid, a, sm);
 }
 
-template <int K, int NR, int WPE, int D, bool XL, bool TRACE = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
-k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a) {
+template <int K, int U, int NR, bool FUSE>
+__device__ __forceinline__ void near_hs_group(int g, const NearHsArgs& n, double* tab);
+
+// NEAR: the staged near field's groups (k_near_hs with fused corrections) are the last
+// blocks (ANISO_NEAR_IN_TOP).  The dispatcher hands out blocks in
+// order, so they take the slots the clusters free at the launch's tail.
+template <int K, int NR, int WPE, int D, bool XL, bool TRACE = false, bool NEAR = false>
+__global__ void __launch_bounds__(WPE == 8 ? 512 : 256) __attribute__((amdgpu_waves_per_eu(WPE == 8 ? 4 : WPE)))
+k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a, NearHsArgs n) {
     extern __shared__ double sm[];
     const int b = (int)blockIdx.x;
     top_mark<TRACE>(t, 0);
@@ -787,18 +816,26 @@ k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a) {
         return;
     }
     const int cid = b - t.nUp;
+    if constexpr (NEAR) {
+        if (cid >= t.nCl) {
+            top_mark<TRACE>(t, 1);
+            near_hs_group<K, 4, 2, true>(cid - t.nCl, n, sm);
+            top_mark<TRACE>(t, 2);
+            return;
+        }
+    }
     const int w = t.clWait[cid];
     if (w > 0) {  // its own copy: behind the wait's fence the source boxes load through the vector path
         top_wait(t, w, (unsigned)(t.blk0[w + 1] - t.blk0[w]));
         top_mark<TRACE>(t, 1);
-        m2l_cluster_form<K, NR, D, XL>(cid, a, sm);
+        m2l_cluster_form<K, NR, D, XL, (WPE >= 4)>(cid, a, sm);
         top_mark<TRACE>(t, 2);
         return;
     }
     // no store or fence on the way here, so the compiler keeps the wave-uniform
     // source-box reads (ncx[B] ...) on scalar loads as in k_m2l_hc
     top_mark<TRACE>(t, 1);
-    m2l_cluster_form<K, NR, D, XL>(cid, a, sm);
+    m2l_cluster_form<K, NR, D, XL, (WPE >= 4)>(cid, a, sm);
     top_mark<TRACE>(t, 2);
 }
 
@@ -947,20 +984,29 @@ template <int K>
 constexpr int kTabRow = (kStride<K> + 2) | 1;
 
 template <int K, int U, int NR, bool FUSE>
-__global__ void __launch_bounds__(256) k_near_hs(int nl, const int4* __restrict__ leafInfo,
-                                                 const int64_t* __restrict__ nearPtsPtr,
-                                                 const uint16_t* __restrict__ nearLoc, const int64_t* __restrict__ nsPtr,
-                                                 const int* __restrict__ nsPts, const int64_t* __restrict__ nearKOff,
-                                                 const double* __restrict__ E, const double* __restrict__ pxT,
-                                                 const double* __restrict__ pyT, const double* __restrict__ sigDiag,
-                                                 HarmWeights hw, const double* __restrict__ fT,
-                                                 const int* __restrict__ operm, int64_t obase, int64_t ldo, int flags,
-                                                 double scale, double* __restrict__ out, NearCorr nc) {
+__device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, double* tab) {
     constexpr int KS = kStride<K>;
     constexpr int RW = kTabRow<K>;  // table row: x, y, the charges (padded)
-    extern __shared__ double tab[];
+    const int nl = n.nl;
+    const int4* __restrict__ leafInfo = n.leafInfo;
+    const int64_t* __restrict__ nearPtsPtr = n.nearPtsPtr;
+    const uint16_t* __restrict__ nearLoc = n.nearLoc;
+    const int64_t* __restrict__ nsPtr = n.nsPtr;
+    const int* __restrict__ nsPts = n.nsPts;
+    const int64_t* __restrict__ nearKOff = n.nearKOff;
+    const double* __restrict__ E = n.E;
+    const double* __restrict__ pxT = n.pxT;
+    const double* __restrict__ pyT = n.pyT;
+    const double* __restrict__ sigDiag = n.sigDiag;
+    const HarmWeights& hw = n.hw;
+    const double* __restrict__ fT = n.fT;
+    const int* __restrict__ operm = n.operm;
+    const int64_t obase = n.obase, ldo = n.ldo;
+    const int flags = n.flags;
+    const double scale = n.scale;
+    double* __restrict__ out = n.out;
+    const NearCorr& nc = n.nc;
     const bool nearOn = (flags & kStageNear) != 0;
-    const int g = (int)blockIdx.x;
     if (nearOn) {
         const int64_t r0 = nsPtr[g];
         const int nr = (int)(nsPtr[g + 1] - r0);
@@ -1074,6 +1120,13 @@ __global__ void __launch_bounds__(256) k_near_hs(int nl, const int4* __restrict_
     }
 }
 
+// W4: capped at 128 VGPRs (4 waves per SIMD; ANISO_NEAR_WPE=4)
+template <int K, int U, int NR, bool FUSE, bool W4 = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W4 ? 4 : 1))) k_near_hs(NearHsArgs n) {
+    extern __shared__ double tab[];
+    near_hs_group<K, U, NR, FUSE>((int)blockIdx.x, n, tab);
+}
+
 
 // ----------------------------------------------------------------- launchers
 
@@ -1103,9 +1156,8 @@ void launch_m2l_hm(int K, int ntgt, const int* tgt, const int64_t* ptr, const in
 // XCD-contiguous cluster order all measured equal or slower, r01e-r01j), 3 waves per
 // SIMD; 1/r = v_rsq_f64 + ONE Newton step (~1e-13 relative per entry, 4 % faster
 // than two; the reduced-precision choice is tested at 1M points)
-size_t m2l_hc_lds(int K, int maxCl, int depth, bool xl) {
+size_t m2l_hc_lds(int K, int maxCl, int depth, bool xl, int nw) {
     size_t b = (size_t)maxCl * kRank * K * sizeof(double);
-    const int nw = 256 / kWave;
     if (depth == 0 || xl) b += (size_t)nw * kRank * K * sizeof(double);  // each wave's weighted target multipole
     if (depth == 0) return b;
     const size_t slot = 2048 + (size_t)kRank * K * 8 + 32;
@@ -1132,7 +1184,7 @@ int hm_ring_depth() {
 int hm_ring_xl(int K, int maxCl, int depth) {
     if (K > kRingMaxK) return -1;
     if (const char* e = std::getenv("ANISO_HM_RING_XL")) return std::atoi(e) != 0 ? 1 : 0;
-    return 3 * m2l_hc_lds(K, maxCl, depth, true) <= 160 * 1024 ? 1 : -1;
+    return 3 * m2l_hc_lds(K, maxCl, depth, true, 4) <= 160 * 1024 ? 1 : -1;
 }
 
 #define ANISO_HM_DISPATCH_RING(d, CALL)                                            \
@@ -1143,6 +1195,21 @@ int hm_ring_xl(int K, int maxCl, int depth) {
         case 4: { constexpr int DD = 4; CALL; } break;                             \
         default: throw std::invalid_argument("harmonic M2L: bad ring depth");      \
     }
+
+// The one-block cluster form's occupancy (K <= 5; K = 8 keeps 3), ANISO_HM_WPE:
+// 3 = 3 waves per SIMD (the default); 4 = 4 waves per SIMD (<= 128 VGPRs,
+// m2l_hc_cluster<LR>) in 4-wave workgroups, which needs 4 of them per CU in LDS
+// (small clusters: shards); 8 = the LR form in 8-wave workgroups, 2 per CU (a
+// 64-target cluster needs 43.5 KB of LDS).  The 4-wave forms measured slower (r03lr:
+// a rank of 8 0.300 against 0.269 ms fused, 0.268 against 0.256 with separate tier
+// launches; one GPU with 8-wave workgroups 1.300 against 1.324 ms, but 1.343 beside
+// the 4-wave near field).  shm4: the launch's LDS per workgroup with 4 waves.
+static int hm_form(int K, int wpe, size_t shm4) {
+    (void)shm4;
+    if (K > kRingMaxK || wpe == 3) return 3;
+    if (wpe == 4 || wpe == 8) return wpe;
+    return 3;
+}
 
 template <typename F>
 static void set_lds(F f, size_t shm) {
@@ -1163,12 +1230,18 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s) {
     if (maxCl > 64) throw std::invalid_argument("harmonic M2L cluster larger than 64 targets");
     const int depth = a.geo && K <= kRingMaxK ? a.ring : 0;
     const bool xl = a.ringXL;
-    const size_t shm = m2l_hc_lds(K, maxCl, depth, xl);
+    size_t shm = m2l_hc_lds(K, maxCl, depth, xl, 4);
+    const int form = depth == 0 ? hm_form(K, a.wpe, shm) : 3;
+    if (form == 8) shm = m2l_hc_lds(K, maxCl, depth, xl, 8);
     ANISO_HM_DISPATCH_K(K, ANISO_HM_DISPATCH_RING(depth, ({
         if constexpr (DD == 0 || KK > kRingMaxK) {
             auto f = k_m2l_hc<KK, 1, 3>;
+            if constexpr (KK <= kRingMaxK) {
+                if (form == 4) f = k_m2l_hc<KK, 1, 4>;
+                if (form == 8) f = k_m2l_hc<KK, 1, 8>;
+            }
             set_lds(f, shm);
-            f<<<ncl, 256, shm, s>>>(a);
+            f<<<ncl, form == 8 ? 512 : 256, shm, s>>>(a);
         } else {
             auto f = xl ? k_m2l_hcr<KK, 1, DD, true, 3> : k_m2l_hcr<KK, 1, DD, false, 2>;
             set_lds(f, shm);
@@ -1186,26 +1259,41 @@ bool top_fused_enabled() {
 #endif
 }
 
-void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs& t, const HcArgs& a, hipStream_t s) {
+void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs& t0, const HcArgs& a,
+                       const NearHsArgs* near, hipStream_t s) {
     if (maxCl > 64) throw std::invalid_argument("harmonic M2L cluster larger than 64 targets");
-    if (t.ntier < 2 || t.ntier > kMaxTopTiers || t.blk0[t.ntier] != t.nUp)
+    if (t0.ntier < 2 || t0.ntier > kMaxTopTiers || t0.blk0[t0.ntier] != t0.nUp)
         throw std::invalid_argument("fused top-of-tree launch: bad tier layout");
-    if (!t.err) throw std::invalid_argument("fused top-of-tree launch: no time-out flag");
+    if (!t0.err) throw std::invalid_argument("fused top-of-tree launch: no time-out flag");
     const int depth = a.geo && K <= kRingMaxK ? a.ring : 0;
+    if (near && (depth != 0 || near->nl <= 0))
+        throw std::invalid_argument("fused top-of-tree launch: the near field rides only with the one-block M2L");
     const bool xl = a.ringXL;
-    const size_t shm = std::max(m2l_hc_lds(K, maxCl, depth, xl), up_tier_lds(u.maxTask, K));
-    const unsigned nb = (unsigned)(t.nUp + ncl);
+    TopArgs t = t0;
+    t.nCl = ncl;
+    const NearHsArgs n = near ? *near : NearHsArgs{};
+    const unsigned nb = (unsigned)(t.nUp + ncl) + (near ? (unsigned)((near->nl + 15) / 16) : 0u);
     ANISO_HM_DISPATCH_K(K, ANISO_HM_DISPATCH_RING(depth, ({
+        size_t shm = std::max(m2l_hc_lds(KK, maxCl, depth, xl, 4), up_tier_lds(u.maxTask, KK));
+        if (near) shm = std::max(shm, (size_t)near->nsMax * kTabRow<KK> * sizeof(double));
+        const int form = DD == 0 && !near ? hm_form(KK, a.wpe, shm) : 3;
+        if (form == 8) shm = std::max(shm, m2l_hc_lds(KK, maxCl, depth, xl, 8));
         // the ring form with its target multipole in VGPRs needs ~216 of them at K = 5
         if constexpr (DD == 0 || KK > kRingMaxK) {
-            auto f = t.trace ? k_top_m2l_hc<KK, 1, 3, 0, false, true> : k_top_m2l_hc<KK, 1, 3, 0, false>;
+            auto f = near ? (t.trace ? k_top_m2l_hc<KK, 1, 3, 0, false, true, true>
+                                     : k_top_m2l_hc<KK, 1, 3, 0, false, false, true>)
+                          : (t.trace ? k_top_m2l_hc<KK, 1, 3, 0, false, true> : k_top_m2l_hc<KK, 1, 3, 0, false>);
+            if constexpr (KK <= kRingMaxK) {
+                if (form == 4) f = t.trace ? k_top_m2l_hc<KK, 1, 4, 0, false, true> : k_top_m2l_hc<KK, 1, 4, 0, false>;
+                if (form == 8) f = t.trace ? k_top_m2l_hc<KK, 1, 8, 0, false, true> : k_top_m2l_hc<KK, 1, 8, 0, false>;
+            }
             set_lds(f, shm);
-            f<<<nb, 256, shm, s>>>(u, t, a);
+            f<<<nb, form == 8 ? 512 : 256, shm, s>>>(u, t, a, n);
         } else {
             auto f = xl ? (t.trace ? k_top_m2l_hc<KK, 1, 3, DD, true, true> : k_top_m2l_hc<KK, 1, 3, DD, true>)
                         : (t.trace ? k_top_m2l_hc<KK, 1, 2, DD, false, true> : k_top_m2l_hc<KK, 1, 2, DD, false>);
             set_lds(f, shm);
-            f<<<nb, 256, shm, s>>>(u, t, a);
+            f<<<nb, 256, shm, s>>>(u, t, a, n);
         }
     })));
     HIP_LAUNCH_CHECK();
@@ -1214,28 +1302,32 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
 // near field: 16 lanes per leaf for leaves <= 16 points (4 leaves per wave), a wave
 // per leaf otherwise; 4 source columns in flight per lane (2 and 8, XCD-contiguous
 // leaves and leaf clusters measured slower, r01h); 1/r to full fp64 (two Newton steps)
+static bool near_hs_staged(int nl, int maxLeaf, int nsMax, const uint16_t* nearLoc) {
+    return nl > 0 && maxLeaf <= 16 && nsMax > 0 && nearLoc && (size_t)nsMax * kTabRow<8> * sizeof(double) <= 64 * 1024;
+}
+
+
+bool near_hs_fusable(int nl, int maxLeaf, int nsMax, const uint16_t* nearLoc, const NearCorr* corr, int flags) {
+    return near_hs_staged(nl, maxLeaf, nsMax, nearLoc) && corr && corr->rows && (flags & kStageNear);
+}
+
 bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
                     const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
                     const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
                     int64_t ldo, int flags, double scale, double* out, const uint16_t* nearLoc, const int64_t* nsPtr,
-                    const int* nsPts, int nsMax, const NearCorr* corr, hipStream_t s) {
+                    const int* nsPts, int nsMax, const NearCorr* corr, int wpe, hipStream_t s) {
     if (nl <= 0) return false;
-    const size_t tabBytes = (size_t)nsMax * kTabRow<8> * sizeof(double);
-    if (maxLeaf <= 16 && nsMax > 0 && nearLoc && tabBytes <= 64 * 1024) {  // sources staged in LDS (k_near_hs)
+    if (near_hs_staged(nl, maxLeaf, nsMax, nearLoc)) {  // sources staged in LDS (k_near_hs)
         const unsigned ng = (unsigned)((nl + 15) / 16);
         // the corrections ride along when the table is loaded (near field on)
-        const bool fuse = corr && corr->rows && (flags & kStageNear);
-        const NearCorr nc = fuse ? *corr : NearCorr{};
+        const bool fuse = near_hs_fusable(nl, maxLeaf, nsMax, nearLoc, corr, flags);
+        const NearHsArgs n{nl, nsMax, leafInfo, nearPtsPtr, nearLoc, nsPtr, nsPts, nearKOff, E, pxT, pyT, sigDiag, hw,
+                           fT, operm, obase, ldo, flags, scale, out, fuse ? *corr : NearCorr{}};
         ANISO_HM_DISPATCH_K(K, ({
             const size_t shm = (size_t)nsMax * kTabRow<KK> * sizeof(double);
-            if (fuse)
-                k_near_hs<KK, 4, 2, true><<<ng, 256, shm, s>>>(nl, leafInfo, nearPtsPtr, nearLoc, nsPtr, nsPts, nearKOff,
-                                                               E, pxT, pyT, sigDiag, hw, fT, operm, obase, ldo, flags,
-                                                               scale, out, nc);
-            else
-                k_near_hs<KK, 4, 2, false><<<ng, 256, shm, s>>>(nl, leafInfo, nearPtsPtr, nearLoc, nsPtr, nsPts,
-                                                                nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm, obase,
-                                                                ldo, flags, scale, out, nc);
+            auto f = fuse ? (wpe == 4 ? k_near_hs<KK, 4, 2, true, true> : k_near_hs<KK, 4, 2, true>)
+                          : (wpe == 4 ? k_near_hs<KK, 4, 2, false, true> : k_near_hs<KK, 4, 2, false>);
+            f<<<ng, 256, shm, s>>>(n);
         }));
         HIP_LAUNCH_CHECK();
         return fuse;

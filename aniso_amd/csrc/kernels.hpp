@@ -194,6 +194,7 @@ struct HcArgs {
     const double* geo = nullptr;  // per node {cx, cy, rx, ry} (the ring form, k_m2l_hcr)
     int ring = 0;                 // host: the ring form's depth (0: the one-block-in-flight form)
     bool ringXL = false;          // host: the ring form keeps the target multipole in LDS (3 waves / SIMD)
+    int wpe = 0;                  // host: one-block form's waves per SIMD, 3 or 4 (0: 4 where LDS allows it)
 };
 // The fused top-of-tree + clustered M2L launch (harmonic.hip k_top_m2l_hc, DESIGN.md
 // §3.10): blocks 0 .. nUp - 1 run the up tasks of tiers 1 .. ntier - 1 (tier k's
@@ -233,12 +234,8 @@ struct TopArgs {
     unsigned spinLimit;           // polls before a wait gives up (0: give up at once -- tests only)
     unsigned* err;                // host-visible sticky flag: set to 1 when a wait gave up
     int64_t* trace;               // development (ANISO_TOP_TRACE=1): per block {start, waited, end, hw id}
+    int nCl;                      // cluster blocks (set by the launcher); near-field groups follow them
 };
-bool top_fused_enabled();
-void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs& t, const HcArgs& a, hipStream_t s);
-void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s);
-int hm_ring_depth();  // ANISO_HM_RING (read at handle creation): the cluster M2L's LDS ring depth
-int hm_ring_xl(int K, int maxCl, int depth);  // its target multipole in LDS / VGPRs / ring off (1, 0, -1)
 // the fused corrections of the staged near field (d = 1; harmonic.hip k_near_hs)
 struct NearCorr {  // the fused corrections of k_near_hs (d = 1), or ignored when rows == nullptr
     const uint16_t* rows;
@@ -249,12 +246,47 @@ struct NearCorr {  // the fused corrections of k_near_hs (d = 1), or ignored whe
     const double* Wm;
     const Params* P;
 };
+// the staged near field's arguments (harmonic.hip k_near_hs, and the last blocks of
+// k_top_m2l_hc when the near field rides in that launch): 16 leaves per group
+struct NearHsArgs {
+    int nl;                  // target leaves
+    int nsMax;               // largest source table (rows)
+    const int4* leafInfo;
+    const int64_t* nearPtsPtr;
+    const uint16_t* nearLoc;
+    const int64_t* nsPtr;
+    const int* nsPts;
+    const int64_t* nearKOff;
+    const double* E;
+    const double* pxT;
+    const double* pyT;
+    const double* sigDiag;
+    HarmWeights hw;
+    const double* fT;
+    const int* operm;
+    int64_t obase;
+    int64_t ldo;
+    int flags;
+    double scale;
+    double* out;
+    NearCorr nc;
+};
+bool top_fused_enabled();
+// near: the staged near field with its corrections fused (near_hs_fusable) as the
+// launch's last blocks, or nullptr (it runs as a launch of its own)
+void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs& t, const HcArgs& a,
+                       const NearHsArgs* near, hipStream_t s);
+// whether launch_near_hm would run the staged near field with fused corrections
+bool near_hs_fusable(int nl, int maxLeaf, int nsMax, const uint16_t* nearLoc, const NearCorr* corr, int flags);
+void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s);
+int hm_ring_depth();  // ANISO_HM_RING (read at handle creation): the cluster M2L's LDS ring depth
+int hm_ring_xl(int K, int maxCl, int depth);  // its target multipole in LDS / VGPRs / ring off (1, 0, -1)
 // returns true when the corrections were fused (the caller skips launch_corr)
 bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int64_t* nearPtsPtr, const int* nearPts,
                     const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
                     const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
                     int64_t ldo, int flags, double scale, double* out, const uint16_t* nearLoc, const int64_t* nsPtr,
-                    const int* nsPts, int nsMax, const NearCorr* corr, hipStream_t s);
+                    const int* nsPts, int nsMax, const NearCorr* corr, int wpe, hipStream_t s);
 void launch_sub_slice(int64_t n, int nrhs, const double* x, int64_t ldx, const double* a, int64_t lda, double* y,
                       int64_t ldy, hipStream_t s);
 

@@ -603,14 +603,19 @@ def test_harmonic_symmetric_blocks_match_directed(sz, d, ks, monkeypatch):
                                                  (32, 1, 5, 20, "1", "0"), (32, 1, 5, 20, "1", "2x"),
                                                  (32, 1, 5, 20, "1", "4x"), (24, 1, 8, 20, "1", "3x"),
                                                  (19, 2, 3, 20, "1", "0"), (32, 1, 5, 20, "1", "3v"),
-                                                 (24, 1, 8, 20, "1", "3v"), (32, 1, 5, 20, "1", "3")])
+                                                 (24, 1, 8, 20, "1", "3v"), (32, 1, 5, 20, "1", "3"),
+                                                 (32, 1, 5, 20, "1", "0w4"), (32, 1, 5, 20, "1", "0w3"),
+                                                 (64, 1, 2, 20, "0", "0w4"), (19, 2, 3, 20, "1", "0w4"),
+                                                 (24, 1, 8, 20, "1", "0w4")])
 def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, ring, monkeypatch):
     """The clustered harmonic M2L (in-cluster V pairs read once by
     the smaller id, both products, locals summed in LDS) against one wave per target
     (aniso_set_deterministic); odd sz (non-uniform tree), directed storage, a
     maxLevel-limited tree; the LDS-ring form at depths 2-4 with the target multipole
     in LDS (x) or VGPRs (v), every block count it compiles for (2, 4, 5, 8), the
-    one-block-in-flight form (ANISO_HM_RING=0) and the default choice between them.
+    one-block-in-flight form (ANISO_HM_RING=0) and the default choice between them, that
+    form at 4 waves per SIMD (w4: m2l_hc_cluster<LR>, <= 128 VGPRs; K = 8 keeps 3) and
+    at 3 (w3).
     Also checks that in-cluster pairs exist, that the cluster plan reads fewer E
     blocks, and that the deterministic mode repeats bitwise."""
     torch = _torch()
@@ -618,8 +623,10 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, ring, monk
 
     monkeypatch.setenv("ANISO_SYMMETRIC", sym)
     monkeypatch.setenv("ANISO_HM_RING", ring[0])
-    if len(ring) > 1:
+    if len(ring) > 1 and ring[1] in "xv":
         monkeypatch.setenv("ANISO_HM_RING_XL", "1" if ring[1] == "x" else "0")
+    if "w" in ring:
+        monkeypatch.setenv("ANISO_HM_WPE", ring[ring.index("w") + 1])
     # 64-target clusters even at these sizes (the default depth keeps >= 512
     # clusters, which small trees only reach with 4-target clusters: no in-cluster pairs)
     monkeypatch.setenv("ANISO_HM_CLDEPTH", "3")
@@ -647,16 +654,22 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, ring, monk
     assert _rel(outs[0], outs[1]) <= 1e-13
 
 
-@pytest.mark.parametrize("ks,world,ring", [(5, 8, "3"), (2, 4, "3"), (3, 3, "3"), (5, 8, "0")])
+@pytest.mark.parametrize("ks,world,ring", [(5, 8, "3"), (2, 4, "3"), (3, 3, "3"), (5, 8, "0"), (5, 8, "0f"),
+                                           (5, 8, "0w4"), (2, 4, "0fw4"), (5, 8, "0fw4")])
 def test_small_clusters_on_shards_match_unsharded(ks, world, ring, monkeypatch):
     """The clustered M2L on the small clusters of an N-GPU shard (the adaptive depth
     gives 16-target clusters there) with 2, 4 (3 padded) and 5 blocks: every rank's
     two-phase apply equals the unsharded operator (the LDS-ring cluster form and the
-    one-block-in-flight form)."""
+    one-block-in-flight form; f: ANISO_TOP_FUSED=0, the upper tiers as launches of
+    their own; w4: the one-block form at 4 waves per SIMD)."""
     torch = _torch()
     import aniso_amd
 
-    monkeypatch.setenv("ANISO_HM_RING", ring)
+    monkeypatch.setenv("ANISO_HM_RING", ring[0])
+    if "f" in ring:
+        monkeypatch.setenv("ANISO_TOP_FUSED", "0")
+    if "w4" in ring:
+        monkeypatch.setenv("ANISO_HM_WPE", "4")
     sz = 256
     full = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
     xy = full.getNodes()
@@ -700,7 +713,9 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
     assert float(torch.linalg.norm(o1 - ref) / torch.linalg.norm(ref)) <= 1e-13
 
 
-@pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0", "ANISO_HM_RING=3"])
+@pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0", "ANISO_HM_RING=3",
+                                  "ANISO_HM_WPE=3", "ANISO_HM_WPE=4", "ANISO_HM_WPE=8", "ANISO_NEAR_IN_TOP=1",
+                                  "ANISO_NEAR_WPE=3", "ANISO_TOP_FUSED=0"])
 def test_block_matvec_knobs_agree(knob, monkeypatch):
     """Every remaining environment knob of the block apply:
     the serial near/M2L order, the separate x - mforward(x) subtraction and the

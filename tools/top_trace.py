@@ -59,7 +59,8 @@ if out:
     np.save(out, np.stack(runs))
 t0 = tr[:, 0].min()
 us = lambda v: (v - t0) / 100.0  # noqa: E731  (100 MHz ticks -> microseconds)
-up = tr[tr[:, 4] < 0]
+nr = tr[tr[:, 4] == -99]  # near-field groups riding at the end of the launch (ANISO_NEAR_IN_TOP=1)
+up = tr[(tr[:, 4] < 0) & (tr[:, 4] != -99)]
 cl = tr[tr[:, 4] >= 0]
 rep = {"world": world, "rank": rank, "launch_us": [round(float((r[:, 2].max() - r[:, 0].min()) / 100.0), 2) for r in runs],
        "blocks": int(tr.shape[0]), "up_blocks": int(up.shape[0]), "clusters": int(cl.shape[0])}
@@ -70,6 +71,11 @@ for k in sorted(set((-up[:, 4]).tolist())):
                      "last_waited": round(float(us(u[:, 1].max())), 2), "last_end": round(float(us(u[:, 2].max())), 2),
                      "mean_run_us": round(float((u[:, 2] - u[:, 1]).mean() / 100.0), 2)}
 rep["tiers"] = tiers
+if len(nr):
+    rep["near_groups"] = {"n": int(len(nr)), "start_us": {q: round(float(np.percentile(us(nr[:, 0]), p)), 2) for q, p in
+                                                      (("p0", 0), ("p50", 50), ("p100", 100))},
+                          "run_us_p50": round(float(np.percentile((nr[:, 2] - nr[:, 1]) / 100.0, 50)), 2),
+                          "end_us_max": round(float(us(nr[:, 2]).max()), 2)}
 dur = (cl[:, 2] - cl[:, 1]) / 100.0
 wait = (cl[:, 1] - cl[:, 0]) / 100.0
 reads = cl[:, 7]
@@ -92,6 +98,11 @@ rep["last"] = [{"cid": int(cl[i, 4]), "wait_tier": int(cl[i, 5]), "targets": int
 # concurrency: clusters resident at the p50 time
 mid = np.percentile(cl[:, 2], 50)
 rep["resident_at_p50_end"] = int(((cl[:, 0] <= mid) & (cl[:, 2] >= mid)).sum())
+# clusters (and near groups) resident every 50 us
+grid = np.arange(0.0, float(us(tr[:, 2]).max()) + 50.0, 50.0)
+rep["resident_clusters_50us"] = [int(((us(cl[:, 0]) <= t) & (us(cl[:, 2]) > t)).sum()) for t in grid]
+if len(nr):
+    rep["resident_near_50us"] = [int(((us(nr[:, 0]) <= t) & (us(nr[:, 2]) > t)).sum()) for t in grid]
 xcc = (tr[:, 3] >> 32) & 15
 rep["blocks_per_xcc"] = np.bincount(xcc, minlength=8).tolist()
 print(json.dumps(rep), flush=True)
