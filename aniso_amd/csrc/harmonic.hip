@@ -286,13 +286,6 @@ __device__ __forceinline__ void m2l_hc_store_target(double (&c)[4][K], double* a
     }
 }
 
-// x distance from a source point to the target's Chebyshev column j (j unrolled):
-// axs = source x - target centre, u0 / u1 = r cheb_0 / r cheb_1 (cheb_3 = -cheb_0,
-// cheb_2 = -cheb_1 for np = 4)
-__device__ __forceinline__ double cheb_dx(int j, double axs, double u0, double u1) {
-    return j == 0 ? axs - u0 : j == 1 ? axs - u1 : j == 2 ? axs + u1 : axs + u0;
-}
-
 // The same distances for the 4-wave form (LR): from wave-uniform values only,
 // dx_j = axs - r cheb_j (one FMA with two scalar operands; ~2-4 % more VALU, but no
 // VGPRs held for the target's columns).
@@ -352,11 +345,14 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // xa visible to every lane of the wave
         __builtin_amdgcn_wave_barrier();
-        // the target's Chebyshev x offsets: cheb_3 = -cheb_0, cheb_2 = -cheb_1 (np = 4), so
-        // dx_j = (ax - tcx) -+ u0 / u1 -- 4 VGPRs instead of 8 for the 4 coordinates
-        const double tcx = ncx[n], trx = nrx[n];
-        const double u0 = LR ? 0.0 : trx * P->cheb[0], u1 = LR ? 0.0 : trx * P->cheb[1];
-        auto dxj = [&](int j, double axs) { return LR ? cheb_dx_lr(j, axs, trx, P) : cheb_dx(j, axs, u0, u1); };
+        // the target's Chebyshev x coordinates: held in 8 VGPRs (the 3-wave form; the
+        // two-value form cheb_dx measured 3 % slower per block matvec, r03zc), or from
+        // wave-uniform values (LR, the 4-wave form, <= 128 VGPRs)
+        const double tcx = LR ? ncx[n] : 0.0, trx = nrx[n];
+        double bx[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bx[j] = LR ? 0.0 : ncx[n] + trx * P->cheb[j];
+        auto dxj = [&](int j, double axs) { return LR ? cheb_dx_lr(j, axs, trx, P) : axs - bx[j]; };
         const double by = ncy[n] + nry[n] * P->cheb[q];
         double c[4][K];
 #pragma unroll
@@ -395,7 +391,7 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                     }
     #pragma unroll
                     for (int g = 0; g < PG; ++g) {
-                        const double axs = (ncx[B[g]] - tcx) + nrx[B[g]] * chx;
+                        const double axs = LR ? (ncx[B[g]] - tcx) + nrx[B[g]] * chx : ncx[B[g]] + nrx[B[g]] * chx;
                         const double dy = (ncy[B[g]] + nry[B[g]] * chy) - by;
                         const double dy2 = dy * dy;
                         double xw[K];
@@ -424,7 +420,7 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                     const double* m = mult + ((size_t)B * kRank + s) * K;
     #pragma unroll
                     for (int bb = 0; bb < K; ++bb) xm[bb] = m[bb];
-                    const double axs = (ncx[B] - tcx) + nrx[B] * chx;
+                    const double axs = LR ? (ncx[B] - tcx) + nrx[B] * chx : ncx[B] + nrx[B] * chx;
                     const double dy = (ncy[B] + nry[B] * chy) - by;
                     const double dy2 = dy * dy;
                     double xw[K], ob[K];
