@@ -330,12 +330,18 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
     double* acc = sm;                                    // nt x 16 x K: the cluster's locals
     double* xa = sm + (size_t)nt * RK + (size_t)w * RK;  // this wave's target multipole, (-1)^b hw_b weighted
+    // targets go to the waves dynamically (an LDS counter, in slot order: the low slots
+    // own the most in-cluster dual pairs), not round-robin: a wave's load is the sum of
+    // its targets' reads, and with 4 targets per wave (shards) the static split left
+    // the cluster's slowest wave 5-8 % above the mean
+    __shared__ int nextTarget;
     for (int i = threadIdx.x; i < nt * RK; i += blockDim.x) acc[i] = 0.0;
+    if (threadIdx.x == 0) nextTarget = nw;
     __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const int s = lane >> 2, q = lane & 3;
     const double chx = P->cheb[s & 3], chy = P->cheb[s >> 2];
-    for (int ti = w; ti < nt; ti += nw) {
+    for (int ti = w; ti < nt;) {
         const int n = tgt[c0 + ti];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous target's xa reads are done
         __builtin_amdgcn_wave_barrier();
@@ -443,6 +449,9 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                 }
             }
         m2l_hc_store_target<K>(c, acc + (size_t)ti * kRank * K, lane, s, q);
+        int nx = 0;
+        if (lane == 0) nx = atomicAdd(&nextTarget, 1);
+        ti = __builtin_amdgcn_readlane(nx, 0);
     }
     __syncthreads();
     for (int e = threadIdx.x; e < nt * RK; e += blockDim.x) {
