@@ -296,7 +296,7 @@ __device__ __forceinline__ double cheb_dx_lr(int j, double axs, double r, const 
 // The harmonic M2L in clusters: one 4-wave workgroup per
 // cluster (the active targets of one level under one ancestor kClusterDepth levels
 // up), the cluster's locals accumulated in LDS.  Each wave takes the cluster's
-// targets round-robin and streams their pair lists as k_m2l_hm does; a pair whose
+// next target from an LDS counter and streams its pair list as k_m2l_hm does; a pair whose
 // partner is in the cluster (slot >= 0) is read once, by its smaller id, and also
 // yields the partner's product: per lane the 4 rows are summed in registers, the
 // quad's lanes by DPP, and the 16 x K result is added to the partner's LDS locals
