@@ -737,29 +737,6 @@ void Plan::buildClusters(const Tree& t) {
         o2.reserve(nt);
         for (const auto& g : seg) o2.insert(o2.end(), order.begin() + g[2], order.begin() + g[3]);
         order.swap(o2);
-#ifdef ANISO_HM_LPT
-        // inside a cluster, heaviest target first (its directed reads + 1.4 x the dual
-        // reads it owns): the waves take targets in slot order through an LDS counter
-        for (int k = 0; k < nt;) {
-            int e = k;
-            while (e < nt && key[order[e]] == key[order[k]]) ++e;
-            std::vector<std::pair<double, int>> lw;
-            for (int i = k; i < e; ++i) {
-                const int w = order[i], n = m2lTgt[w];
-                double l = 0.0;
-                for (int64_t a = attPtr[w]; a < attPtr[w + 1]; ++a) {
-                    const int b = attSrc[a];
-                    const bool same = widx[b] >= 0 && key[widx[b]] == key[w];
-                    if (same && b > n && attBlk[a] >= 0) l += 1.4;
-                    else if (!(same && b < n)) l += 1.0;
-                }
-                lw.push_back({-l, w});
-            }
-            std::stable_sort(lw.begin(), lw.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
-            for (int i = k; i < e; ++i) order[i] = lw[i - k].second;
-            k = e;
-        }
-#endif
     }
     std::vector<int> clOf(t.nn, -1), slotOf(t.nn, -1);
     int nc = 0;
