@@ -222,7 +222,7 @@ private:
     bool topTraceOn = false;
     int hmRing = 0;  // the cluster M2L's LDS ring depth (ANISO_HM_RING; 0: the one-block-in-flight form)
     int hmWpe = 0;   // ANISO_HM_WPE=3/4/8: the one-block form's occupancy (0: 4 where LDS allows)
-    int nearWpe = 4;  // ANISO_NEAR_WPE: the staged near field at 4 (<= 128 VGPRs) or 3 waves per SIMD
+    int nearWpe = 3;  // ANISO_NEAR_WPE: the staged near field at 3 (132 VGPRs, the default since r03zj) or 4 waves per SIMD (<= 128)
     int topFusedMode = 1;  // ANISO_TOP_FUSED=0: the upper up tiers as launches of their own
     // the near field's groups ride at the end of the fused top-of-tree + M2L launch
     // instead of a side-stream launch (ANISO_NEAR_IN_TOP=1; on a shard in phase 2)

@@ -715,7 +715,7 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
 
 @pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0", "ANISO_HM_RING=3",
                                   "ANISO_HM_WPE=3", "ANISO_HM_WPE=4", "ANISO_HM_WPE=8", "ANISO_NEAR_IN_TOP=1",
-                                  "ANISO_NEAR_WPE=3", "ANISO_TOP_FUSED=0"])
+                                  "ANISO_NEAR_WPE=4", "ANISO_TOP_FUSED=0"])
 def test_block_matvec_knobs_agree(knob, monkeypatch):
     """Every remaining environment knob of the block apply:
     the serial near/M2L order, the separate x - mforward(x) subtraction and the
