@@ -84,6 +84,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_TOP_SPIN_LIMIT")) topSpinLimit = (unsigned)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("ANISO_TOP_TRACE")) topTraceOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_IN_TOP")) nearInTop = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ANISO_NEAR_EARLY")) nearEarly = std::atoi(e) != 0;
     hmRing = hm_ring_depth();
     if (const char* e = std::getenv("ANISO_HM_WPE")) hmWpe = std::atoi(e);
     if (const char* e = std::getenv("ANISO_NEAR_WPE")) nearWpe = std::atoi(e);
@@ -302,6 +303,10 @@ void Operator::uploadPlan() {
         up(dHmSlot, plan.hmSlot);
         up(dHmNDir, plan.hmNDir);
         up(dHmClWait, plan.hmClWait);
+        up(dHmHaloPtr, plan.hmHaloPtr);
+        up(dHmFoldNode, plan.hmFoldNode);
+        up(dHmFoldPtr, plan.hmFoldPtr);
+        up(dHmFoldIdx, plan.hmFoldIdx);
         dTopCnt.alloc((kMaxTopTiers + 1) * sizeof(unsigned));
         attReady = false;
     }
@@ -500,12 +505,22 @@ void Operator::mappingHost(const double* charge, int id, double* out) {
 
 // k right-hand sides of one mode: up to 8 per batched apply (identity mix), or, for
 // more than 8 on an unsharded handle, 16 per apply of the fp64 MFMA operator
-// (f64op.hip; zero columns pad the last chunk)
+// (f64op.hip; zero columns pad the last chunk).  That operator keeps its own fp64
+// copy of the mode's operators on the directed lists (mrhs64Bytes: about 6 GB per
+// mode at 1M points, 24 GB at 4M), freed by setCoeff / cache(id): it is used only
+// when that copy fits in the free HBM, else the 8-column batches run.
 void Operator::mappingBatchedHost(const double* Q, int k, int id, double* Out) {
     if (k == 0) return;
     ensureDevice();
     const int64_t N = geo.N;
-    if (k > 8 && plan.nranks == 1) {
+    bool mfma = k > 8 && plan.nranks == 1;
+    if (mfma && !m64.count(id) && id >= 0 && id < kernelSize && modes[id].ready) {
+        size_t freeB = 0, totalB = 0;
+        HIP_CHECK(hipMemGetInfo(&freeB, &totalB));
+        const size_t need = mrhs64Bytes() + (size_t)64 * N * sizeof(double);  // + the four 16-column staging buffers
+        mfma = need + (size_t)(1ull << 30) <= freeB;  // keep a GiB of headroom
+    }
+    if (mfma) {
         if (id < 0 || id >= kernelSize) throw std::out_of_range("kernel id out of range");
         if (!modes[id].ready)
             throw std::runtime_error("mapping on kernel id " + std::to_string(id) + " before cache(" + std::to_string(id) + ")");
@@ -747,12 +762,21 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     const bool topFused = harmonic && (mask & kStageFar) && topFusedOn();
     // ANISO_NEAR_IN_TOP: the near field (+ corrections) as the last blocks of that
     // launch (the one-block M2L form; a shard's phase 1 then leaves it to phase 2)
-    const bool ringOn = hmRing > 0 && hm_ring_xl(K, plan.hmMaxCl, hmRing) >= 0;
+    const bool ringOn = hmRing > 0 && hm_ring_xl(K, plan.hmMaxLds, hmRing) >= 0;
     const bool nearFused = topFused && overlap && nearInTop && !ringOn && plan.nearCorrOk &&
                            near_hs_fusable((int)plan.leaves.size(), plan.nearMaxLeaf, plan.nsMax,
                                            dNearLoc.as<uint16_t>(), &nc, mask);
     const bool fork = harmonic && overlap && !nearFused;
     const hipStream_t sn = fork ? side : s;
+    // the staged near field with its fused corrections forms its charges from the
+    // input itself (NearHsArgs::xin), so it needs nothing from the up pass: it forks
+    // at the start of the apply, beside the latency-bound up tiers, and the up pass
+    // stores no fT / cT (ANISO_NEAR_EARLY=0: it forks after the up pass and reads them)
+    const bool nearIn = harmonic && nearEarly && !nearFused && plan.nearCorrOk && (mask & kStageNear) &&
+                        near_hs_fusable((int)plan.leaves.size(), plan.nearMaxLeaf, plan.nsMax,
+                                        dNearLoc.as<uint16_t>(), &nc, mask);
+    double* const fTw = nearIn ? nullptr : dFT.as<double>();
+    double* const cTw = nearIn ? nullptr : dCT.as<double>();
     // the near field forks after the whole up pass on one GPU: forked after the
     // bottom tier it starved the latency-bound upper tiers the M2L waits on (up pass
     // 0.25 -> 0.14 ms, 644 -> 660 block matvec/s); a sharded apply starts it in
@@ -764,13 +788,20 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         launch_up_tier(K, ntask, plan.upTierTask[k], list, plan.upMaxTask, dUpDesc.as<int4>(), dUpGrpFix.as<int>(),
                        dUpNode.as<int>(), dUpCode.as<int4>(), dUpGeom.as<double4>(), dUpLeaf.as<int2>(),
                        dPxT.as<double>(), dPyT.as<double>(), x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT,
-                       dWT.as<double>(), dFT.as<double>(), dCT.as<double>(), P, dMult.as<double>(),
+                       dWT.as<double>(), fTw, cTw, P, dMult.as<double>(),
                        recv ? dXRootSlot.as<int>() : nullptr, recv, send ? dXSendSlot.as<int>() : nullptr, send, s,
                        topFused && k == 0 ? dTopCnt.as<unsigned>() : nullptr);
-        if (fork && k == forkTier) HIP_CHECK(hipEventRecord(evFork, s));
+        if (fork && !nearIn && k == forkTier) HIP_CHECK(hipEventRecord(evFork, s));
     };
     auto tierTasks = [&](int k) { return plan.upTierTask[k + 1] - plan.upTierTask[k]; };
-    // near field + corrections (they need only fT / cT)
+    NearHsArgs nin{};  // nearIn: the input the near field forms its charges from
+    nin.xin = x;
+    nin.ldi = ldx;
+    nin.treeIn = treeIn ? 1 : 0;
+    nin.perm = dPerm.as<int>();
+    nin.sigT = sigT;
+    nin.wT = dWT.as<double>();
+    // near field + corrections (they need only fT / cT, or with nearIn the input)
     auto nearStage = [&] {
         if (fork) HIP_CHECK(hipStreamWaitEvent(side, evFork, 0));
         const int en = tm ? mark(sn) : -1;
@@ -783,7 +814,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                            dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dSigDiag.as<double>(), hw,
                            dFT.as<double>(), operm, obase, ldo, mask, scale, out,
                            dNearLoc.as<uint16_t>(), dNsPtr.as<int64_t>(), dNsPts.as<int>(),
-                           plan.nsMax, plan.nearCorrOk ? &nc : nullptr, nearWpe, sn);
+                           plan.nsMax, plan.nearCorrOk ? &nc : nullptr, nearWpe, sn, nearIn ? &nin : nullptr);
         } else if (plan.nearPartTotal > 0) {
             // symmetric U storage (K = 1 handles): one launch per term; the transposed
             // products go to partials summed over the terms
@@ -817,15 +848,23 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                      dNrx.as<double>(), dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(),
                      dNodeGeo.as<double>()};
     hca.wpe = hmWpe;
+    const bool halo = !plan.hmHaloNode.empty();
+    if (halo) {  // the halo form: partials of the cross-cluster partner products (Plan::hmHaloPtr)
+        const size_t hb = plan.hmHaloNode.size() * kRank * K * sizeof(double);
+        if (dHmPart.bytes < hb) dHmPart.alloc(hb);
+        hca.haloPtr = dHmHaloPtr.as<int>();
+        hca.hpart = dHmPart.as<double>();
+    }
     if (hmRing > 0) {
-        const int xl = hm_ring_xl(K, plan.hmMaxCl, hmRing);
+        const int xl = hm_ring_xl(K, plan.hmMaxLds, hmRing);
         hca.ring = xl < 0 ? 0 : hmRing;
         hca.ringXL = xl > 0;
     }
     auto m2lClusters = [&](int c0, int c1, hipStream_t st) {
         HcArgs a = hca;
         a.clPtr += c0;
-        launch_m2l_hc(K, c1 - c0, plan.hmMaxCl, a, st);
+        if (a.haloPtr) a.haloPtr += c0;
+        launch_m2l_hc(K, c1 - c0, plan.hmMaxLds, a, st);
     };
     int e0 = -1;
     bool nearDone = false;
@@ -833,6 +872,12 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         // up pass: tiers bottom-up; its P2M also forms the weighted charges fT (tree
         // order) the near field and the corrections read
         e0 = tm ? mark(s) : -1;
+        if (nearIn) {  // the near field first: beside the up pass (fork) or before it (serial)
+            if (fork) HIP_CHECK(hipEventRecord(evFork, s));
+            nearStage();
+            nearDone = true;
+            if (!fork && tm) e0 = mark(s);  // serial: the up span starts after the near field
+        }
         if (ntier < 1) {  // a lone leaf: no up pass
             launch_prepare(K, geo.N, x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(),
                            dFT.as<double>(), dCT.as<double>(), s);
@@ -844,7 +889,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         if (phase == 1) {
             const int ep = tm ? mark(s) : -1;
             span(1, e0, ep);
-            if ((ntier < 1 || forkTier == 0) && !nearFused) {
+            if ((ntier < 1 || forkTier == 0) && !nearFused && !nearDone) {
                 nearStage();
                 nearDone = true;
             }
@@ -883,7 +928,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             const UpArgs ua{plan.upMaxTask, dUpDesc.as<int4>(), dUpGrpFix.as<int>(), dUpNode.as<int>(),
                             dUpCode.as<int4>(), dUpGeom.as<double4>(), dUpLeaf.as<int2>(), dPxT.as<double>(),
                             dPyT.as<double>(), x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(),
-                            dFT.as<double>(), dCT.as<double>(), P, dMult.as<double>(),
+                            fTw, cTw, P, dMult.as<double>(),
                             phase == 2 ? dXRootSlot.as<int>() : nullptr};
             TopArgs ta{};
             const int u1 = plan.upTierTask[1];
@@ -907,7 +952,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                     dTopTrace.alloc((size_t)topTraceBlocks * 4 * sizeof(int64_t));
                 ta.trace = dTopTrace.as<int64_t>();
             }
-            launch_top_m2l_hc(K, ncl, plan.hmMaxCl, ua, ta, hca, nearFused ? &na : nullptr, s);
+            launch_top_m2l_hc(K, ncl, plan.hmMaxLds, ua, ta, hca, nearFused ? &na : nullptr, s);
         } else if (clustered) {
             m2lClusters(0, ncl, s);
         } else if (harmonic) {
@@ -920,6 +965,9 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                        dMult.as<double>(), plan.m2lMaxCanon, dM2LPart.as<double>(), dLocal.as<double>(), s);
         }
     }
+    if (halo && (topFused || clustered) && (mask & kStageFar))  // the halo partials into their nodes' locals
+        launch_hm_fold(K, (int)plan.hmFoldNode.size(), dHmFoldNode.as<int>(), dHmFoldPtr.as<int>(),
+                       dHmFoldIdx.as<int>(), dHmPart.as<double>(), dLocal.as<double>(), s);
     int e = tm ? mark(s) : -1;
     span(2, ep, e);
     ep = e;
@@ -1250,11 +1298,29 @@ void Operator::buildF32() {
 
 // the fp64 16-RHS caches of mode id (f64op.hip): the mode's blocks on the directed
 // lists, the M2L blocks rearranged in place into A order, the near blocks as tiles
+// Built into a local cache, entered into m64 only once every allocation and kernel
+// has succeeded: a failed build (out of HBM, a fault) leaves no half-built entry for
+// the next call to launch on (ANISO_FAULT_INJECT=mrhs64 makes it throw after its
+// allocations, for the test of that path).
+size_t Operator::mrhs64Bytes() {
+    buildMrhsPlan();
+    const F32Plan& f = f32;
+    size_t b = (size_t)std::max<int64_t>((int64_t)f.m2lSrc.size(), 1) * 256 * sizeof(double);
+    b += (size_t)std::max<int64_t>(f.nearTiles, 1) * 4 * sizeof(double);
+    b += (size_t)std::max<int64_t>(f.nearD, 1) * sizeof(double);  // the build's temporary
+    if (!d64Mult.p) b += 2 * (size_t)tree.nn * 256 * sizeof(double) + 2 * (size_t)geo.N * 16 * sizeof(double);
+    return b;
+}
+
 void Operator::buildMrhs64(int id) {
     buildMrhsPlan();
     const F32Plan& f = f32;
     const Params* P = dParams.as<Params>();
-    Mrhs64Cache& c = m64[id];
+    d64Mult.alloc((size_t)tree.nn * 256 * sizeof(double));
+    d64Local.alloc((size_t)tree.nn * 256 * sizeof(double));
+    d64FT.alloc((size_t)geo.N * 16 * sizeof(double));
+    d64CT.alloc((size_t)geo.N * 16 * sizeof(double));
+    Mrhs64Cache c;
     const int64_t np_ = (int64_t)f.m2lSrc.size();
     c.Km2l.alloc((size_t)std::max<int64_t>(np_, 1) * 256 * sizeof(double));
     launch_cache_m2l(np_, d32PairTgt.as<int>(), d32Src.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
@@ -1271,10 +1337,9 @@ void Operator::buildMrhs64(int id) {
                            d32Koff.as<int64_t>(), d32SrcCount.as<int>(), tmp.as<double>(), c.Knear.p, own);
         HIP_CHECK(hipStreamSynchronize(own));
     }
-    d64Mult.alloc((size_t)tree.nn * 256 * sizeof(double));
-    d64Local.alloc((size_t)tree.nn * 256 * sizeof(double));
-    d64FT.alloc((size_t)geo.N * 16 * sizeof(double));
-    d64CT.alloc((size_t)geo.N * 16 * sizeof(double));
+    if (const char* e = std::getenv("ANISO_FAULT_INJECT"))
+        if (std::string(e) == "mrhs64") throw std::runtime_error("fp64 16-RHS cache build failed (ANISO_FAULT_INJECT)");
+    m64.emplace(id, std::move(c));
 }
 
 void Operator::mrhs64Dev(int id, bool forward, const double* X, double* Y, hipStream_t s, int mask) {
@@ -1287,7 +1352,7 @@ void Operator::mrhs64Dev(int id, bool forward, const double* X, double* Y, hipSt
     ensureDevice();
     checkDeviceErrors();
     if (!m64.count(id)) buildMrhs64(id);
-    const Mrhs64Cache& c = m64[id];
+    const Mrhs64Cache& c = m64.at(id);
     const Params* P = dParams.as<Params>();
     const F32Plan& f = f32;
     const double scale = M_1_PI / 2.0;  // AnisoWrapper.cpp:129-130

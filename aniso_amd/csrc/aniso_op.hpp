@@ -216,6 +216,7 @@ private:
     bool useAtt = false, attReady = false;
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
+    DevBuf dHmHaloPtr, dHmFoldNode, dHmFoldPtr, dHmFoldIdx, dHmPart;  // the halo form (Plan::hmHaloPtr)
     DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
     DevBuf dTopTrace;           // ANISO_TOP_TRACE=1: the launch's per-block timeline
     DevBuf dKryPart;            // partial sums of the Krylov primitives
@@ -227,6 +228,9 @@ private:
     // the near field's groups ride at the end of the fused top-of-tree + M2L launch
     // instead of a side-stream launch (ANISO_NEAR_IN_TOP=1; on a shard in phase 2)
     bool nearInTop = false;
+    // the staged near field forms its charges from the input and forks at the start
+    // of the block apply, beside the up pass (ANISO_NEAR_EARLY=0: after it, from fT)
+    bool nearEarly = true;
     int topTraceBlocks = 0, topTraceNear = 0;
     // the attached communicator and its halo exchange plan (commInit): per element of
     // the send / receive position lists its tree position and its place in the
@@ -302,6 +306,7 @@ private:
     };
     std::map<int, Mrhs64Cache> m64;  // fp64 16-RHS caches per mode id
     void buildMrhs64(int id);
+    size_t mrhs64Bytes();  // HBM a buildMrhs64 would allocate
     DevBuf d64Rup, d64Rdn, d64Mult, d64Local, d64FT, d64CT;
     DevBuf d32PairTgt, d32SrcPtr, d32SrcNodes, d32KoffD, d32SrcCount;  // cache-build inputs of the 16-RHS plan
     struct F32Plan {

@@ -914,7 +914,7 @@ __global__ void __launch_bounds__(256) k_corr(int64_t b, int64_t e, const int* _
     if (k >= e) return;
     const int t = perm[k];
     double acc[K];
-    corr_point<D, K>(t, P, iperm, cT, Wc, Wm, flags,
+    corr_point<D, K>(t, P, iperm, [&](int64_t p, int r) { return cT[(size_t)p * KS + r]; }, Wc, Wm, flags,
                      [&](int, int sq2, int c, double (&f)[K]) {
                          load_charges<K>(fT + (size_t)iperm[(size_t)sq2 * (D * D) + c] * KS, f);
                      },

@@ -556,6 +556,10 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[16] = cl ? (int64_t)op.plan.hmSrc.size() : (int64_t)op.plan.attSrc.size();
         s[17] = op.f32Bytes();  // config 5's fp32 operator caches (0 before its first apply)
         s[18] = cl && op.topFusedOn() ? 1 : 0;
+        // the cluster plan itself (block handles; host-side, no GPU needed)
+        s[19] = (int64_t)op.plan.hmHaloNode.size();
+        s[20] = op.plan.hmMaxLds;
+        s[21] = (int64_t)op.plan.hmSrc.size();
     });
 }
 

@@ -6,20 +6,20 @@
 // Shared by k_corr (neighbour charges from fT in HBM) and the near field's fused
 // epilogue (k_near_hs: neighbour charges from its LDS source table); `charges(q9, c,
 // f)` returns the K weighted charges of point c of neighbour square q9 = 3 (dr+1) +
-// (dc+1), or false outside the grid.
+// (dc+1), or false outside the grid; `cval(k, r)` the unweighted charge r of tree
+// position k (cT, or the apply's input, k_near_hs).
 #pragma once
 
 #include "device_common.hpp"
 
 namespace aniso {
 
-template <int D, int K, class Charges>
+template <int D, int K, class Charges, class CVal>
 __device__ __forceinline__ void corr_point(int t, const Params* __restrict__ P, const int* __restrict__ iperm,
-                                           const double* __restrict__ cT, const double* __restrict__ Wc,
+                                           CVal cval, const double* __restrict__ Wc,
                                            const double* __restrict__ Wm, int flags, Charges charges,
                                            double (&acc)[K]) {
     constexpr int D2 = D * D;
-    constexpr int KS = kStride<K>;
     const int sz = P->sz;
     const int sq = t / D2, tq = t - sq * D2;
     const int i = sq / sz, j = sq - i * sz;
@@ -72,7 +72,7 @@ __device__ __forceinline__ void corr_point(int t, const Params* __restrict__ P, 
         for (int r = 0; r < K; ++r) {
             double hw[D2];
 #pragma unroll
-            for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cT[(size_t)itS[c] * KS + r];
+            for (int c = 0; c < D2; ++c) hw[c] = P->sqrtW[c] * cval((int64_t)itS[c], r);
             // Legendre coefficients cf_{n,k} = (interpolate * (sqrtW .* h))_{nk} / norm_nk,
             // contracted with the bases: pb[a][bb] = sum_{n >= a, k >= bb} cf_nk bx[n][a] by[k][bb]
             double pb[D][D];

@@ -286,6 +286,35 @@ __device__ __forceinline__ void m2l_hc_store_target(double (&c)[4][K], double* a
     }
 }
 
+// A cluster's LDS slots: its nt targets, then (the halo form) the nh halo nodes whose
+// partner products it accumulates for other clusters (Plan::hmHaloPtr).
+struct HcSlots {
+    int c0, nt, h0, nh;
+};
+
+__device__ __forceinline__ HcSlots hc_slots(int cid, const HcArgs& a) {
+    HcSlots s;
+    s.c0 = a.clPtr[cid];
+    s.nt = a.clPtr[cid + 1] - s.c0;
+    s.h0 = a.haloPtr ? a.haloPtr[cid] : 0;
+    s.nh = a.haloPtr ? a.haloPtr[cid + 1] - s.h0 : 0;
+    return s;
+}
+
+// the cluster's end: its targets' locals stored, its halo slots stored to their
+// partials (both scaled by om; the fold adds the partials, launch_hm_fold)
+template <int K>
+__device__ __forceinline__ void hc_flush(const HcSlots& c, const HcArgs& a, const double* acc) {
+    constexpr int RK = kRank * K;
+    for (int e = threadIdx.x; e < c.nt * RK; e += blockDim.x) {
+        const int k = e / RK, r = e - k * RK;
+        a.local[(size_t)a.tgt[c.c0 + k] * RK + r] = a.hw.om[r % K] * acc[e];
+    }
+    double* hp = a.hpart + (size_t)c.h0 * RK;
+    const double* ah = acc + (size_t)c.nt * RK;
+    for (int e = threadIdx.x; e < c.nh * RK; e += blockDim.x) hp[e] = a.hw.om[e % K] * ah[e];
+}
+
 // The same distances for the 4-wave form (LR): from wave-uniform values only,
 // dx_j = axs - r cheb_j (one FMA with two scalar operands; ~2-4 % more VALU, but no
 // VGPRs held for the target's columns).
@@ -322,20 +351,21 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
     const Params* __restrict__ P = a.P;
     const HarmWeights& hw = a.hw;
     const double* __restrict__ mult = a.mult;
-    double* __restrict__ local = a.local;
     constexpr int RK = kRank * K;
     constexpr int PG = 2;
-    const int c0 = clPtr[cid], nt = clPtr[cid + 1] - c0;
+    const HcSlots cs = hc_slots(cid, a);
+    const int c0 = cs.c0, nt = cs.nt, nsl = cs.nt + cs.nh;
+    (void)clPtr;
     const int nw = (int)(blockDim.x / kWave);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-    double* acc = sm;                                    // nt x 16 x K: the cluster's locals
-    double* xa = sm + (size_t)nt * RK + (size_t)w * RK;  // this wave's target multipole, (-1)^b hw_b weighted
+    double* acc = sm;                                     // (nt + nh) x 16 x K: the cluster's locals, its halo
+    double* xa = sm + (size_t)nsl * RK + (size_t)w * RK;  // this wave's target multipole, (-1)^b hw_b weighted
     // targets go to the waves dynamically (an LDS counter, in slot order: the low slots
     // own the most in-cluster dual pairs), not round-robin: a wave's load is the sum of
     // its targets' reads, and with 4 targets per wave (shards) the static split left
     // the cluster's slowest wave 5-8 % above the mean
     __shared__ int nextTarget;
-    for (int i = threadIdx.x; i < nt * RK; i += blockDim.x) acc[i] = 0.0;
+    for (int i = threadIdx.x; i < nsl * RK; i += blockDim.x) acc[i] = 0.0;
     if (threadIdx.x == 0) nextTarget = nw;
     __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
@@ -354,7 +384,7 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
         // the target's Chebyshev x coordinates: held in 8 VGPRs (the 3-wave form; the
         // two-value form cheb_dx measured 3 % slower per block matvec, r03zc), or from
         // wave-uniform values (LR, the 4-wave form, <= 128 VGPRs)
-        const double tcx = LR ? ncx[n] : 0.0, trx = nrx[n];
+        const double tcx = LR ? ncx[n] : 0.0, trx = nrx[n], tcx1 = ncx[n];
         double bx[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) bx[j] = LR ? 0.0 : ncx[n] + trx * P->cheb[j];
@@ -408,7 +438,11 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                     }
                 }
             }
-            // in-cluster canonical entries (stored as read): both products, one block in flight
+            // canonical entries (stored as read): both products, the partner's into its
+            // LDS slot (a cluster target, or a halo slot in the halo form); the next
+            // pair's block, source multipole and box are loaded before this pair's
+            // arithmetic (two blocks in flight per wave: in the halo form every pair is
+            // here)
             for (int64_t cb = pd; cb < p1; cb += kWave) {
                 const int cnt = (int)min<int64_t>(kWave, p1 - cb);
                 const int mySrc = lane < cnt ? src[cb + lane] : 0;
@@ -416,18 +450,35 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                 // LR: the partner's slot by a scalar load (needed only at the flush), one
                 // VGPR fewer across the stream
                 const int mySlot = !LR && lane < cnt ? slot[cb + lane] : 0;
-                for (int jj = 0; jj < cnt; ++jj) {
+                dbl2 k0, k1;
+                double xm[K], gcx, grx, gcy, gry;
+                auto fetch = [&](int jj, dbl2& a0, dbl2& a1, double (&x)[K], double& fcx, double& frx, double& fcy,
+                                 double& fry) {
                     const int b = __builtin_amdgcn_readlane(myBlk, jj);
                     const int B = __builtin_amdgcn_readlane(mySrc, jj);
-                    const int sl = LR ? slot[cb + jj] : __builtin_amdgcn_readlane(mySlot, jj);
                     const dbl2* p = reinterpret_cast<const dbl2*>(E + (size_t)b * 256 + 16 * s + 4 * q);
-                    const dbl2 k0 = p[0], k1 = p[1];
-                    double xm[K];
+                    a0 = p[0];
+                    a1 = p[1];
                     const double* m = mult + ((size_t)B * kRank + s) * K;
     #pragma unroll
-                    for (int bb = 0; bb < K; ++bb) xm[bb] = m[bb];
-                    const double axs = LR ? (ncx[B] - tcx) + nrx[B] * chx : ncx[B] + nrx[B] * chx;
-                    const double dy = (ncy[B] + nry[B] * chy) - by;
+                    for (int bb = 0; bb < K; ++bb) x[bb] = m[bb];
+                    fcx = ncx[B];
+                    frx = nrx[B];
+                    fcy = ncy[B];
+                    fry = nry[B];
+                };
+                fetch(0, k0, k1, xm, gcx, grx, gcy, gry);
+                for (int jj = 0; jj < cnt; ++jj) {
+                    // the next pair (the last one again at the end: an L1 hit, no branch
+                    // for the wait counts to merge over)
+                    dbl2 n0, n1;
+                    double xn[K], ncx1, nrx1, ncy1, nry1;
+                    fetch(min(jj + 1, cnt - 1), n0, n1, xn, ncx1, nrx1, ncy1, nry1);
+                    const int sl = LR ? slot[cb + jj] : __builtin_amdgcn_readlane(mySlot, jj);
+                    // the distances from wave-uniform values (as the LR form): 8 VGPRs
+                    // fewer than the held target columns bx, the same VALU count
+                    const double axs = (gcx - tcx1) + grx * chx;
+                    const double dy = (gcy + gry * chy) - by;
                     const double dy2 = dy * dy;
                     double xw[K], ob[K];
     #pragma unroll
@@ -438,7 +489,7 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                     const double e4[4] = {k0.x, k0.y, k1.x, k1.y};
     #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        hm_entry2<K, NR>(e4[j], dxj(j, axs), dy2, xw, xa + (4 * q + j) * K, c[j], ob);
+                        hm_entry2<K, NR>(e4[j], cheb_dx_lr(j, axs, trx, P), dy2, xw, xa + (4 * q + j) * K, c[j], ob);
     #pragma unroll
                     for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // rows 4q'+j over the quad
                     if (q == 0) {
@@ -446,6 +497,14 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
     #pragma unroll
                         for (int i = 0; i < K; ++i) atomicAdd(d + i, (i & 1) ? -ob[i] : ob[i]);
                     }
+                    k0 = n0;
+                    k1 = n1;
+    #pragma unroll
+                    for (int bb = 0; bb < K; ++bb) xm[bb] = xn[bb];
+                    gcx = ncx1;
+                    grx = nrx1;
+                    gcy = ncy1;
+                    gry = nry1;
                 }
             }
         m2l_hc_store_target<K>(c, acc + (size_t)ti * kRank * K, lane, s, q);
@@ -454,10 +513,7 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
         ti = __builtin_amdgcn_readlane(nx, 0);
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < nt * RK; e += blockDim.x) {
-        const int k = e / RK, r = e - k * RK;
-        local[(size_t)tgt[c0 + k] * RK + r] = hw.om[r % K] * acc[e];
-    }
+    hc_flush<K>(cs, a, acc);
 }
 
 // ---- the ring form of the cluster M2L ----
@@ -598,16 +654,17 @@ __device__ __forceinline__ void m2l_hcr_cluster(const int cid, const HcArgs& a, 
     const Params* __restrict__ P = a.P;
     const HarmWeights& hw = a.hw;
     const double* __restrict__ mult = a.mult;
-    double* __restrict__ local = a.local;
     constexpr int RK = kRank * K;
-    const int c0 = clPtr[cid], nt = clPtr[cid + 1] - c0;
+    const HcSlots cs = hc_slots(cid, a);
+    const int c0 = cs.c0, nt = cs.nt, nsl = cs.nt + cs.nh;
+    (void)clPtr;
     const int nw = (int)(blockDim.x / kWave);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-    double* acc = sm;                                                       // nt x 16 x K: the cluster's locals
-    double* xl = sm + (size_t)nt * RK + (XL ? (size_t)w * RK : 0);          // XL: this wave's target multipole
-    const unsigned ring = lds_offset(sm + (size_t)nt * RK + (XL ? (size_t)nw * RK : 0)) + (unsigned)(w * D * R::kSlot);
+    double* acc = sm;                                                       // (nt + nh) x 16 x K: locals, halo
+    double* xl = sm + (size_t)nsl * RK + (XL ? (size_t)w * RK : 0);         // XL: this wave's target multipole
+    const unsigned ring = lds_offset(sm + (size_t)nsl * RK + (XL ? (size_t)nw * RK : 0)) + (unsigned)(w * D * R::kSlot);
     const unsigned accOff = lds_offset(acc);
-    for (int i = threadIdx.x; i < nt * RK; i += blockDim.x) acc[i] = 0.0;
+    for (int i = threadIdx.x; i < nsl * RK; i += blockDim.x) acc[i] = 0.0;
     __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const int s = lane >> 2, q = lane & 3;
@@ -706,10 +763,7 @@ __device__ __forceinline__ void m2l_hcr_cluster(const int cid, const HcArgs& a, 
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int e = threadIdx.x; e < nt * RK; e += blockDim.x) {
-        const int k = e / RK, r = e - k * RK;
-        local[(size_t)tgt[c0 + k] * RK + r] = hw.om[r % K] * acc[e];
-    }
+    hc_flush<K>(cs, a, acc);
 }
 
 template <int K, int NR, int D, bool XL, int WPE>
@@ -718,13 +772,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     m2l_hcr_cluster<K, NR, D, XL>((int)blockIdx.x, a, sm);
 }
 
-// WPE: waves per SIMD; 4 = the LR form (<= 128 VGPRs), 8 = the LR form with 8 waves
-// (512 threads) per cluster, 2 clusters per CU
+// WPE, the cluster form's occupancy: 3 = 4-wave workgroups at 3 waves per SIMD (3 per
+// CU); 6 = 6-wave workgroups at 3 waves per SIMD (2 per CU: the halo form's 64-target
+// clusters need ~72 KB of LDS); 4 = the LR form (<= 128 VGPRs) in 4-wave workgroups;
+// 8 = the LR form with 8 waves (512 threads) per cluster, 2 clusters per CU
+template <int WPE>
+constexpr int kHcThreads = WPE == 8 ? 512 : WPE == 6 ? 384 : 256;
+template <int WPE>
+constexpr int kHcWaves = WPE == 8 ? 4 : WPE == 6 ? 3 : WPE;
+template <int WPE>
+constexpr bool kHcLR = WPE == 4 || WPE == 8;
+
 template <int K, int NR, int WPE>
-__global__ void __launch_bounds__(WPE == 8 ? 512 : 256) __attribute__((amdgpu_waves_per_eu(WPE == 8 ? 4 : WPE)))
+__global__ void __launch_bounds__(kHcThreads<WPE>) __attribute__((amdgpu_waves_per_eu(kHcWaves<WPE>)))
 k_m2l_hc(HcArgs a) {
     extern __shared__ double sm[];
-    m2l_hc_cluster<K, NR, (WPE >= 4)>((int)blockIdx.x, a, sm);
+    m2l_hc_cluster<K, NR, kHcLR<WPE>>((int)blockIdx.x, a, sm);
 }
 
 // ----------------------------------------------------------------- fused top of tree + M2L
@@ -803,7 +866,7 @@ __device__ __forceinline__ void near_hs_group(int g, const NearHsArgs& n, double
 // blocks (ANISO_NEAR_IN_TOP).  The dispatcher hands out blocks in
 // order, so they take the slots the clusters free at the launch's tail.
 template <int K, int NR, int WPE, int D, bool XL, bool TRACE = false, bool NEAR = false>
-__global__ void __launch_bounds__(WPE == 8 ? 512 : 256) __attribute__((amdgpu_waves_per_eu(WPE == 8 ? 4 : WPE)))
+__global__ void __launch_bounds__(kHcThreads<WPE>) __attribute__((amdgpu_waves_per_eu(kHcWaves<WPE>)))
 k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a, NearHsArgs n) {
     extern __shared__ double sm[];
     const int b = (int)blockIdx.x;
@@ -833,14 +896,14 @@ k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a, NearHsArgs n) {
     if (w > 0) {  // its own copy: behind the wait's fence the source boxes load through the vector path
         top_wait(t, w, (unsigned)(t.blk0[w + 1] - t.blk0[w]));
         top_mark<TRACE>(t, 1);
-        m2l_cluster_form<K, NR, D, XL, (WPE >= 4)>(cid, a, sm);
+        m2l_cluster_form<K, NR, D, XL, kHcLR<WPE>>(cid, a, sm);
         top_mark<TRACE>(t, 2);
         return;
     }
     // no store or fence on the way here, so the compiler keeps the wave-uniform
     // source-box reads (ncx[B] ...) on scalar loads as in k_m2l_hc
     top_mark<TRACE>(t, 1);
-    m2l_cluster_form<K, NR, D, XL, (WPE >= 4)>(cid, a, sm);
+    m2l_cluster_form<K, NR, D, XL, kHcLR<WPE>>(cid, a, sm);
     top_mark<TRACE>(t, 2);
 }
 
@@ -1012,6 +1075,17 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
     double* __restrict__ out = n.out;
     const NearCorr& nc = n.nc;
     const bool nearOn = (flags & kStageNear) != 0;
+    const bool fromIn = n.xin != nullptr;  // charges formed from the input (NearHsArgs)
+    // the K weighted charges f = x sigma_s w of tree position p
+    auto wcharges = [&](int64_t p, double (&f)[K]) {
+        if (fromIn) {
+            const double w = n.wT[p];
+#pragma unroll
+            for (int b = 0; b < K; ++b) f[b] = input_charge(n.xin, n.ldi, b, n.treeIn, n.perm, n.sigT, p) * w;
+        } else {
+            load_charges<K>(fT + (size_t)p * KS, f);
+        }
+    };
     if (nearOn) {
         const int64_t r0 = nsPtr[g];
         const int nr = (int)(nsPtr[g + 1] - r0);
@@ -1020,8 +1094,10 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
             double* row = tab + (size_t)i * RW;
             row[0] = pxT[p];
             row[1] = pyT[p];
+            double f[K];
+            wcharges(p, f);
 #pragma unroll
-            for (int v = 0; v < KS; ++v) row[2 + v] = fT[(size_t)p * KS + v];
+            for (int v = 0; v < K; ++v) row[2 + v] = f[v];
         }
     }
     __syncthreads();
@@ -1100,13 +1176,17 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
         if (t < nT) {
             const int64_t k = tb + t;
             double f[K];
-            load_charges<K>(fT + (size_t)k * KS, f);
+            wcharges(k, f);
             const double sd = nearOn ? sigDiag[k] : 0.0;
             const int64_t oi = out_index(operm, obase, k);
             double cr[K];  // FUSE: k_corr's contribution (d = 1), its neighbour charges from the table
             if constexpr (FUSE) {
                 const uint16_t* rw = nc.rows + ((size_t)li * 16 + t) * 9;
-                corr_point<1, K>(nc.perm[k], nc.P, nc.iperm, nc.cT, nc.Wc, nc.Wm, flags,
+                auto cval = [&](int64_t p, int r) {
+                    return fromIn ? input_charge(n.xin, n.ldi, r, n.treeIn, n.perm, n.sigT, p)
+                                  : nc.cT[(size_t)p * KS + r];
+                };
+                corr_point<1, K>(nc.perm[k], nc.P, nc.iperm, cval, nc.Wc, nc.Wm, flags,
                                  [&](int q9, int, int, double (&fc)[K]) {
                                      const double* row = tab + (size_t)rw[q9] * RW + 2;
 #pragma unroll
@@ -1201,20 +1281,24 @@ int hm_ring_xl(int K, int maxCl, int depth) {
         default: throw std::invalid_argument("harmonic M2L: bad ring depth");      \
     }
 
-// The one-block cluster form's occupancy (K <= 5; K = 8 keeps 3), ANISO_HM_WPE:
-// 3 = 3 waves per SIMD (the default); 4 = 4 waves per SIMD (<= 128 VGPRs,
-// m2l_hc_cluster<LR>) in 4-wave workgroups, which needs 4 of them per CU in LDS
-// (small clusters: shards); 8 = the LR form in 8-wave workgroups, 2 per CU (a
-// 64-target cluster needs 43.5 KB of LDS).  The 4-wave forms measured slower (r03lr:
-// a rank of 8 0.300 against 0.269 ms fused, 0.268 against 0.256 with separate tier
-// launches; one GPU with 8-wave workgroups 1.300 against 1.324 ms, but 1.343 beside
-// the 4-wave near field).  shm4: the launch's LDS per workgroup with 4 waves.
+// The one-block cluster form's occupancy, ANISO_HM_WPE:
+// 3 = 3 waves per SIMD in 4-wave workgroups; 6 = 3 waves per SIMD in 6-wave
+// workgroups (2 per CU); 4 = 4 waves per SIMD (<= 128 VGPRs, m2l_hc_cluster<LR>) in
+// 4-wave workgroups, which needs 4 of them per CU in LDS (small clusters: shards);
+// 8 = the LR form in 8-wave workgroups, 2 per CU.  The 4-wave-per-SIMD forms
+// measured slower (r03lr: a rank of 8 0.300 against 0.269 ms fused; one GPU with
+// 8-wave workgroups 1.300 against 1.324 ms, but 1.343 beside the 4-wave near field).
+// Default: 3 waves per SIMD, in 4-wave workgroups where 3 fit per CU in LDS
+// (shm4: the launch's LDS per workgroup with 4 waves), else in 6-wave ones (the halo
+// form's 64-target clusters: ~72 KB).
 static int hm_form(int K, int wpe, size_t shm4) {
-    (void)shm4;
-    if (K > kRingMaxK || wpe == 3) return 3;
-    if (wpe == 4 || wpe == 8) return wpe;
-    return 3;
+    if ((wpe == 4 || wpe == 8) && K <= kRingMaxK) return wpe;
+    if (wpe == 3 || wpe == 6) return wpe;
+    return 3 * shm4 <= 160 * 1024 ? 3 : 6;
 }
+
+static int hm_threads(int form) { return form == 8 ? 512 : form == 6 ? 384 : 256; }
+static int hm_waves(int form) { return hm_threads(form) / kWave; }
 
 template <typename F>
 static void set_lds(F f, size_t shm) {
@@ -1232,27 +1316,51 @@ static void set_lds(F f, size_t shm) {
 // than two; the reduced-precision choice is tested at 1M points)
 void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s) {
     if (ncl <= 0) return;
-    if (maxCl > 64) throw std::invalid_argument("harmonic M2L cluster larger than 64 targets");
     const int depth = a.geo && K <= kRingMaxK ? a.ring : 0;
     const bool xl = a.ringXL;
     size_t shm = m2l_hc_lds(K, maxCl, depth, xl, 4);
     const int form = depth == 0 ? hm_form(K, a.wpe, shm) : 3;
-    if (form == 8) shm = m2l_hc_lds(K, maxCl, depth, xl, 8);
+    if (form != 3) shm = m2l_hc_lds(K, maxCl, depth, xl, hm_waves(form));
+    if (shm > 160 * 1024) throw std::invalid_argument("harmonic M2L: a cluster and its halo exceed the LDS");
     ANISO_HM_DISPATCH_K(K, ANISO_HM_DISPATCH_RING(depth, ({
         if constexpr (DD == 0 || KK > kRingMaxK) {
-            auto f = k_m2l_hc<KK, 1, 3>;
+            auto f = form == 6 ? k_m2l_hc<KK, 1, 6> : k_m2l_hc<KK, 1, 3>;
             if constexpr (KK <= kRingMaxK) {
                 if (form == 4) f = k_m2l_hc<KK, 1, 4>;
                 if (form == 8) f = k_m2l_hc<KK, 1, 8>;
             }
             set_lds(f, shm);
-            f<<<ncl, form == 8 ? 512 : 256, shm, s>>>(a);
+            f<<<ncl, hm_threads(form), shm, s>>>(a);
         } else {
             auto f = xl ? k_m2l_hcr<KK, 1, DD, true, 3> : k_m2l_hcr<KK, 1, DD, false, 2>;
             set_lds(f, shm);
             f<<<ncl, 256, shm, s>>>(a);
         }
     })));
+    HIP_LAUNCH_CHECK();
+}
+
+// the halo form's fold (Plan::hmFoldPtr): one thread per (receiving node, entry),
+// its partials added in a fixed order
+template <int K>
+__global__ void __launch_bounds__(256) k_hm_fold(int nf, const int* __restrict__ node, const int* __restrict__ ptr,
+                                                 const int* __restrict__ idx, const double* __restrict__ hpart,
+                                                 double* __restrict__ local) {
+    constexpr int RK = kRank * K;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (int64_t)nf * RK) return;
+    const int f = (int)(g / RK), r = (int)(g - (int64_t)f * RK);
+    const int p0 = ptr[f], p1 = ptr[f + 1];
+    double v = 0.0;
+    for (int p = p0; p < p1; ++p) v += hpart[(size_t)idx[p] * RK + r];
+    local[(size_t)node[f] * RK + r] += v;
+}
+
+void launch_hm_fold(int K, int nf, const int* node, const int* ptr, const int* idx, const double* hpart,
+                    double* local, hipStream_t s) {
+    if (nf <= 0) return;
+    ANISO_HM_DISPATCH_K(K, (k_hm_fold<KK><<<blocks_for((int64_t)nf * kRank * KK, 256), 256, 0, s>>>(
+                               nf, node, ptr, idx, hpart, local)));
     HIP_LAUNCH_CHECK();
 }
 
@@ -1266,7 +1374,6 @@ bool top_fused_enabled() {
 
 void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs& t0, const HcArgs& a,
                        const NearHsArgs* near, hipStream_t s) {
-    if (maxCl > 64) throw std::invalid_argument("harmonic M2L cluster larger than 64 targets");
     if (t0.ntier < 2 || t0.ntier > kMaxTopTiers || t0.blk0[t0.ntier] != t0.nUp)
         throw std::invalid_argument("fused top-of-tree launch: bad tier layout");
     if (!t0.err) throw std::invalid_argument("fused top-of-tree launch: no time-out flag");
@@ -1282,18 +1389,20 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
         size_t shm = std::max(m2l_hc_lds(KK, maxCl, depth, xl, 4), up_tier_lds(u.maxTask, KK));
         if (near) shm = std::max(shm, (size_t)near->nsMax * kTabRow<KK> * sizeof(double));
         const int form = DD == 0 && !near ? hm_form(KK, a.wpe, shm) : 3;
-        if (form == 8) shm = std::max(shm, m2l_hc_lds(KK, maxCl, depth, xl, 8));
+        if (form != 3) shm = std::max(shm, m2l_hc_lds(KK, maxCl, depth, xl, hm_waves(form)));
+        if (shm > 160 * 1024) throw std::invalid_argument("fused top-of-tree launch: a cluster and its halo exceed the LDS");
         // the ring form with its target multipole in VGPRs needs ~216 of them at K = 5
         if constexpr (DD == 0 || KK > kRingMaxK) {
             auto f = near ? (t.trace ? k_top_m2l_hc<KK, 1, 3, 0, false, true, true>
                                      : k_top_m2l_hc<KK, 1, 3, 0, false, false, true>)
                           : (t.trace ? k_top_m2l_hc<KK, 1, 3, 0, false, true> : k_top_m2l_hc<KK, 1, 3, 0, false>);
+            if (form == 6) f = t.trace ? k_top_m2l_hc<KK, 1, 6, 0, false, true> : k_top_m2l_hc<KK, 1, 6, 0, false>;
             if constexpr (KK <= kRingMaxK) {
                 if (form == 4) f = t.trace ? k_top_m2l_hc<KK, 1, 4, 0, false, true> : k_top_m2l_hc<KK, 1, 4, 0, false>;
                 if (form == 8) f = t.trace ? k_top_m2l_hc<KK, 1, 8, 0, false, true> : k_top_m2l_hc<KK, 1, 8, 0, false>;
             }
             set_lds(f, shm);
-            f<<<nb, form == 8 ? 512 : 256, shm, s>>>(u, t, a, n);
+            f<<<nb, hm_threads(form), shm, s>>>(u, t, a, n);
         } else {
             auto f = xl ? (t.trace ? k_top_m2l_hc<KK, 1, 3, DD, true, true> : k_top_m2l_hc<KK, 1, 3, DD, true>)
                         : (t.trace ? k_top_m2l_hc<KK, 1, 2, DD, false, true> : k_top_m2l_hc<KK, 1, 2, DD, false>);
@@ -1320,14 +1429,23 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
                     const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
                     const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
                     int64_t ldo, int flags, double scale, double* out, const uint16_t* nearLoc, const int64_t* nsPtr,
-                    const int* nsPts, int nsMax, const NearCorr* corr, int wpe, hipStream_t s) {
+                    const int* nsPts, int nsMax, const NearCorr* corr, int wpe, hipStream_t s, const NearHsArgs* in) {
     if (nl <= 0) return false;
     if (near_hs_staged(nl, maxLeaf, nsMax, nearLoc)) {  // sources staged in LDS (k_near_hs)
         const unsigned ng = (unsigned)((nl + 15) / 16);
         // the corrections ride along when the table is loaded (near field on)
         const bool fuse = near_hs_fusable(nl, maxLeaf, nsMax, nearLoc, corr, flags);
-        const NearHsArgs n{nl, nsMax, leafInfo, nearPtsPtr, nearLoc, nsPtr, nsPts, nearKOff, E, pxT, pyT, sigDiag, hw,
-                           fT, operm, obase, ldo, flags, scale, out, fuse ? *corr : NearCorr{}};
+        NearHsArgs n{nl, nsMax, leafInfo, nearPtsPtr, nearLoc, nsPtr, nsPts, nearKOff, E, pxT, pyT, sigDiag, hw,
+                     fT, operm, obase, ldo, flags, scale, out, fuse ? *corr : NearCorr{}};
+        if (in && in->xin) {  // charges from the input (the near field beside the up pass)
+            if (!fuse) throw std::invalid_argument("near field from the input: only with its fused corrections");
+            n.xin = in->xin;
+            n.ldi = in->ldi;
+            n.treeIn = in->treeIn;
+            n.perm = in->perm;
+            n.sigT = in->sigT;
+            n.wT = in->wT;
+        }
         ANISO_HM_DISPATCH_K(K, ({
             const size_t shm = (size_t)nsMax * kTabRow<KK> * sizeof(double);
             auto f = fuse ? (wpe == 4 ? k_near_hs<KK, 4, 2, true, true> : k_near_hs<KK, 4, 2, true>)

@@ -126,8 +126,19 @@ struct Plan {
     int64_t hmDual = 0;
     // cross-cluster pairs read by the non-storing end: a directed copy of the stored
     // block (E of the reversed pair), appended after the stored blocks in the cache,
-    // so that k_m2l_hc reads every block in the stored orientation (16-B lane loads)
+    // so that k_m2l_hc reads every block in the stored orientation (16-B lane loads).
+    // Empty in the halo form (below, the default).
     std::vector<int> hmCopyOwner, hmCopyOther;
+    // the halo form: a cross-cluster V pair with both ends
+    // targets is read ONCE, by the cluster of its smaller id, which adds the partner's
+    // product to an LDS slot of its halo (slots nt .. nt + nh - 1 of cluster c, whose
+    // nodes are hmHaloNode[hmHaloPtr[c] ..]); at the cluster's end the halo slots go
+    // to a partial buffer, and a fold adds each node's partials to its locals (CSR:
+    // node hmFoldNode[f] receives halo slots hmFoldIdx[hmFoldPtr[f] .. hmFoldPtr[f+1])).
+    // input: ANISO_HM_HALO=0 keeps the directed copies (A/B runs)
+    bool hmHalo = true;
+    std::vector<int> hmHaloPtr, hmHaloNode, hmFoldPtr, hmFoldNode, hmFoldIdx;
+    int hmMaxLds = 0;  // largest cluster + halo (LDS slots of 16 x K doubles)
     // tiered up / down passes: tier k has root level
     // tierRootLevel[k] and bottom level tierBottomLevel[k] (k = 0 is the deepest).
     std::vector<int> tierRootLevel, tierBottomLevel;

@@ -669,6 +669,7 @@ void Plan::buildClusters(const Tree& t) {
     hmBlk.clear();
     hmSlot.clear();
     hmMaxCl = 0;
+    hmMaxLds = 0;
     hmDual = 0;
     hmCopyOwner.clear();
     hmCopyOther.clear();
@@ -690,7 +691,12 @@ void Plan::buildClusters(const Tree& t) {
         }
         return (int)seen.size();
     };
-    int depth = kClusterDepth;
+    if (const char* e = std::getenv("ANISO_HM_HALO")) hmHalo = e[0] != '0';
+    // the halo form reads every stored block once whatever the cluster size, so its
+    // clusters are 16 targets (depth 2: 44 LDS slots at most, 3 workgroups per CU)
+    // where the copy form needs 64 for its in-cluster share (1M points, one GPU:
+    // 1.225 against 1.273 ms per block matvec, M2L alone 0.73 against 0.84 ms, r04c)
+    int depth = hmHalo ? 2 : kClusterDepth;
     while (depth > 1 && clusterCount(depth) < kMinClusters) --depth;
     if (const char* e = std::getenv("ANISO_HM_CLDEPTH"))  // tuning/experiments only (1..kClusterDepth)
         depth = std::max(1, std::min(kClusterDepth, std::atoi(e)));
@@ -753,38 +759,69 @@ void Plan::buildClusters(const Tree& t) {
     hmClPtr.push_back(nt);
     for (size_t c = 0; c + 1 < hmClPtr.size(); ++c) hmMaxCl = std::max(hmMaxCl, hmClPtr[c + 1] - hmClPtr[c]);
     hmNDir.clear();
+    hmHaloPtr.assign(1, 0);
+    hmHaloNode.clear();
+    hmFoldPtr.assign(1, 0);
+    hmFoldNode.clear();
+    hmFoldIdx.clear();
     std::vector<int> dSrc, dBlk, dSlot;
-    for (int k = 0; k < nt; ++k) {
-        const int n = hmTgt[k], w = widx[n];
-        dSrc.clear();
-        dBlk.clear();
-        dSlot.clear();
-        for (int64_t e = attPtr[w]; e < attPtr[w + 1]; ++e) {
-            const int b = attSrc[e];
-            const bool same = clOf[b] >= 0 && clOf[b] == clOf[n] && t.level[b] == t.level[n];
-            if (same && b > n && attBlk[e] >= 0) {  // canonical end: one read, both products
-                dSrc.push_back(b);
-                dBlk.push_back(attBlk[e]);
-                dSlot.push_back(slotOf[b]);
-                continue;
+    std::vector<int> haloOf(t.nn, -1);
+    for (size_t c = 0; c + 1 < hmClPtr.size(); ++c) {
+        const int ncl = hmClPtr[c + 1] - hmClPtr[c], h0 = (int)hmHaloNode.size();
+        for (int k = hmClPtr[c]; k < hmClPtr[c + 1]; ++k) {
+            const int n = hmTgt[k], w = widx[n];
+            dSrc.clear();
+            dBlk.clear();
+            dSlot.clear();
+            for (int64_t e = attPtr[w]; e < attPtr[w + 1]; ++e) {
+                const int b = attSrc[e];
+                // a V pair with both ends targets (X pairs join different levels)
+                const bool vt = clOf[b] >= 0 && t.level[b] == t.level[n];
+                const bool same = vt && clOf[b] == clOf[n];
+                if (vt && b > n && attBlk[e] >= 0 && (same || hmHalo)) {  // canonical end: one read, both products
+                    dSrc.push_back(b);
+                    dBlk.push_back(attBlk[e]);
+                    if (same) {
+                        dSlot.push_back(slotOf[b]);
+                    } else {  // the partner's product goes to a halo slot of this cluster
+                        if (haloOf[b] < 0) {
+                            haloOf[b] = (int)hmHaloNode.size() - h0;
+                            hmHaloNode.push_back(b);
+                        }
+                        dSlot.push_back(ncl + haloOf[b]);
+                    }
+                    continue;
+                }
+                if (vt && b < n && (same || hmHalo)) continue;  // applied by b's wave (dual)
+                hmSrc.push_back(b);
+                if (attBlk[e] < 0) {  // a transposed read: read a directed copy of the block instead
+                    hmBlk.push_back((int)(attOwner.size() + hmCopyOwner.size()));
+                    hmCopyOwner.push_back(n);
+                    hmCopyOther.push_back(b);
+                } else {
+                    hmBlk.push_back(attBlk[e]);
+                }
+                hmSlot.push_back(-1);
             }
-            if (same && b < n) continue;  // applied by b's wave (dual)
-            hmSrc.push_back(b);
-            if (attBlk[e] < 0) {  // a transposed read: read a directed copy of the block instead
-                hmBlk.push_back((int)(attOwner.size() + hmCopyOwner.size()));
-                hmCopyOwner.push_back(n);
-                hmCopyOther.push_back(b);
-            } else {
-                hmBlk.push_back(attBlk[e]);
-            }
-            hmSlot.push_back(-1);
+            hmNDir.push_back((int)(hmSrc.size() - hmPtr.back()));
+            hmSrc.insert(hmSrc.end(), dSrc.begin(), dSrc.end());
+            hmBlk.insert(hmBlk.end(), dBlk.begin(), dBlk.end());
+            hmSlot.insert(hmSlot.end(), dSlot.begin(), dSlot.end());
+            hmDual += (int64_t)dSrc.size();
+            hmPtr.push_back((int64_t)hmSrc.size());
         }
-        hmNDir.push_back((int)(hmSrc.size() - hmPtr.back()));
-        hmSrc.insert(hmSrc.end(), dSrc.begin(), dSrc.end());
-        hmBlk.insert(hmBlk.end(), dBlk.begin(), dBlk.end());
-        hmSlot.insert(hmSlot.end(), dSlot.begin(), dSlot.end());
-        hmDual += (int64_t)dSrc.size();
-        hmPtr.push_back((int64_t)hmSrc.size());
+        for (size_t h = h0; h < hmHaloNode.size(); ++h) haloOf[hmHaloNode[h]] = -1;
+        hmHaloPtr.push_back((int)hmHaloNode.size());
+        hmMaxLds = std::max(hmMaxLds, ncl + (int)hmHaloNode.size() - h0);
+    }
+    // the fold: per receiving node, its halo slots in cluster order (a fixed order)
+    std::vector<std::vector<int>> recv(t.nn);
+    for (size_t h = 0; h < hmHaloNode.size(); ++h) recv[hmHaloNode[h]].push_back((int)h);
+    for (int n = 0; n < t.nn; ++n) {
+        if (recv[n].empty()) continue;
+        hmFoldNode.push_back(n);
+        hmFoldIdx.insert(hmFoldIdx.end(), recv[n].begin(), recv[n].end());
+        hmFoldPtr.push_back((int)hmFoldIdx.size());
     }
 }
 

@@ -194,7 +194,11 @@ struct HcArgs {
     const double* geo = nullptr;  // per node {cx, cy, rx, ry} (the ring form, k_m2l_hcr)
     int ring = 0;                 // host: the ring form's depth (0: the one-block-in-flight form)
     bool ringXL = false;          // host: the ring form keeps the target multipole in LDS (3 waves / SIMD)
-    int wpe = 0;                  // host: one-block form's waves per SIMD, 3 or 4 (0: 4 where LDS allows it)
+    int wpe = 0;                  // host: the cluster form's occupancy (harmonic.hip hm_form; 0: the default)
+    // the halo form (Plan::hmHaloPtr): cluster c's halo slots are partials
+    // haloPtr[c] .. haloPtr[c+1] - 1 of hpart (16 x K doubles each, stored scaled)
+    const int* haloPtr = nullptr;
+    double* hpart = nullptr;
 };
 // The fused top-of-tree + clustered M2L launch (harmonic.hip k_top_m2l_hc, DESIGN.md
 // §3.10): blocks 0 .. nUp - 1 run the up tasks of tiers 1 .. ntier - 1 (tier k's
@@ -270,6 +274,15 @@ struct NearHsArgs {
     double scale;
     double* out;
     NearCorr nc;
+    // charges from the apply's input (xin != nullptr): f = x sigma_s w and c = x
+    // sigma_s formed here (as up_task does), so the near field needs nothing from the
+    // up pass and can run beside it; else fT / cT (and nc.cT) as the up pass wrote them
+    const double* xin = nullptr;
+    int64_t ldi = 0;
+    int treeIn = 0;
+    const int* perm = nullptr;
+    const double* sigT = nullptr;
+    const double* wT = nullptr;
 };
 bool top_fused_enabled();
 // near: the staged near field with its corrections fused (near_hs_fusable) as the
@@ -279,6 +292,9 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
 // whether launch_near_hm would run the staged near field with fused corrections
 bool near_hs_fusable(int nl, int maxLeaf, int nsMax, const uint16_t* nearLoc, const NearCorr* corr, int flags);
 void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s);
+// the halo form's fold: local[node[f]] += sum of hpart[idx[ptr[f] .. ptr[f+1])] (16 x K each)
+void launch_hm_fold(int K, int nf, const int* node, const int* ptr, const int* idx, const double* hpart,
+                    double* local, hipStream_t s);
 int hm_ring_depth();  // ANISO_HM_RING (read at handle creation): the cluster M2L's LDS ring depth
 int hm_ring_xl(int K, int maxCl, int depth);  // its target multipole in LDS / VGPRs / ring off (1, 0, -1)
 // returns true when the corrections were fused (the caller skips launch_corr)
@@ -286,7 +302,8 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
                     const int64_t* nearKOff, const double* E, const double* pxT, const double* pyT,
                     const double* sigDiag, const HarmWeights& hw, const double* fT, const int* operm, int64_t obase,
                     int64_t ldo, int flags, double scale, double* out, const uint16_t* nearLoc, const int64_t* nsPtr,
-                    const int* nsPts, int nsMax, const NearCorr* corr, int wpe, hipStream_t s);
+                    const int* nsPts, int nsMax, const NearCorr* corr, int wpe, hipStream_t s,
+                    const NearHsArgs* in = nullptr);  // in->xin: the staged kernel's charges from the input
 void launch_sub_slice(int64_t n, int nrhs, const double* x, int64_t ldx, const double* a, int64_t lda, double* y,
                       int64_t ldy, hipStream_t s);
 

@@ -111,7 +111,7 @@ __device__ __forceinline__ void up_task(
                     cb[b] = input_charge(xin, ldi, b, treeIn, perm, sigT, kp);
                     fb[b] = on ? cb[b] * w : 0.0;
                 }
-                if (on) {  // for the near field and the corrections
+                if (on && fT) {  // for the near field and the corrections (fT null: they read the input)
                     store_charges<K>(fT + kp * kStride<K>, fb);
                     store_charges<K>(cT + kp * kStride<K>, cb);
                 }
@@ -142,8 +142,10 @@ __device__ __forceinline__ void up_task(
                     const int64_t kp = b0 + p;
                     const double c = input_charge(xin, ldi, b, treeIn, perm, sigT, kp);
                     const double f = c * wT[kp];
-                    fT[kp * kStride<K> + b] = f;  // for k_near and the corrections
-                    cT[kp * kStride<K> + b] = c;
+                    if (fT) {  // for k_near and the corrections
+                        fT[kp * kStride<K> + b] = f;
+                        cT[kp * kStride<K> + b] = c;
+                    }
                     double Sx[kNP], Sy[kNP];
                     cheb_weights(P, (pxT[kp] - cx) * irx, Sx);
                     cheb_weights(P, (pyT[kp] - cy) * iry, Sy);

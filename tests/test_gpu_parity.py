@@ -606,7 +606,9 @@ def test_harmonic_symmetric_blocks_match_directed(sz, d, ks, monkeypatch):
                                                  (24, 1, 8, 20, "1", "3v"), (32, 1, 5, 20, "1", "3"),
                                                  (32, 1, 5, 20, "1", "0w4"), (32, 1, 5, 20, "1", "0w3"),
                                                  (64, 1, 2, 20, "0", "0w4"), (19, 2, 3, 20, "1", "0w4"),
-                                                 (24, 1, 8, 20, "1", "0w4")])
+                                                 (24, 1, 8, 20, "1", "0w4"), (32, 1, 5, 20, "1", "0w6"),
+                                                 (32, 1, 5, 20, "1", "0h"), (19, 2, 3, 20, "1", "0h"),
+                                                 (32, 1, 5, 20, "1", "3xh"), (24, 1, 8, 20, "1", "0h")])
 def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, ring, monkeypatch):
     """The clustered harmonic M2L (in-cluster V pairs read once by
     the smaller id, both products, locals summed in LDS) against one wave per target
@@ -615,9 +617,12 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, ring, monk
     in LDS (x) or VGPRs (v), every block count it compiles for (2, 4, 5, 8), the
     one-block-in-flight form (ANISO_HM_RING=0) and the default choice between them, that
     form at 4 waves per SIMD (w4: m2l_hc_cluster<LR>, <= 128 VGPRs; K = 8 keeps 3) and
-    at 3 (w3).
+    at 3 (w3: 4-wave workgroups; w6: 6-wave ones).  By default cross-cluster pairs are
+    read once too (the halo form: partner products in LDS halo slots, folded into the
+    locals after the launch); h: ANISO_HM_HALO=0, the directed copies instead.
     Also checks that in-cluster pairs exist, that the cluster plan reads fewer E
-    blocks, and that the deterministic mode repeats bitwise."""
+    blocks (the halo form: exactly the stored blocks), and that the deterministic
+    mode repeats bitwise."""
     torch = _torch()
     import aniso_amd
 
@@ -627,6 +632,8 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, ring, monk
         monkeypatch.setenv("ANISO_HM_RING_XL", "1" if ring[1] == "x" else "0")
     if "w" in ring:
         monkeypatch.setenv("ANISO_HM_WPE", ring[ring.index("w") + 1])
+    halo = "h" not in ring
+    monkeypatch.setenv("ANISO_HM_HALO", "1" if halo else "0")
     # 64-target clusters even at these sizes (the default depth keeps >= 512
     # clusters, which small trees only reach with 4-target clusters: no in-cluster pairs)
     monkeypatch.setenv("ANISO_HM_CLDEPTH", "3")
@@ -651,6 +658,10 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, ring, monk
         outs.append(out.cpu().numpy())
     assert st[0]["harmonic"] == 1 and st[0]["hm_clusters"] > 0 and st[1]["hm_clusters"] == 0
     assert st[0]["hm_dual_pairs"] > 0 and st[0]["hm_block_reads"] < st[1]["hm_block_reads"]
+    if not halo:
+        assert st[0]["plan_halo_slots"] == 0
+    if halo and sym == "1":  # every stored block read exactly once
+        assert st[0]["hm_block_reads"] == st[0]["att_m2l_blocks"]
     assert _rel(outs[0], outs[1]) <= 1e-13
 
 
@@ -714,8 +725,9 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
 
 
 @pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0", "ANISO_HM_RING=3",
-                                  "ANISO_HM_WPE=3", "ANISO_HM_WPE=4", "ANISO_HM_WPE=8", "ANISO_NEAR_IN_TOP=1",
-                                  "ANISO_NEAR_WPE=4", "ANISO_TOP_FUSED=0"])
+                                  "ANISO_HM_WPE=3", "ANISO_HM_WPE=4", "ANISO_HM_WPE=6", "ANISO_HM_WPE=8",
+                                  "ANISO_NEAR_IN_TOP=1", "ANISO_NEAR_WPE=4", "ANISO_TOP_FUSED=0", "ANISO_HM_HALO=0",
+                                  "ANISO_NEAR_EARLY=0", "ANISO_NEAR_EARLY=0,ANISO_OVERLAP=0"])
 def test_block_matvec_knobs_agree(knob, monkeypatch):
     """Every remaining environment knob of the block apply:
     the serial near/M2L order, the separate x - mforward(x) subtraction and the
@@ -727,8 +739,9 @@ def test_block_matvec_knobs_agree(knob, monkeypatch):
     outs = []
     for env in (None, knob):
         if env:
-            k, v = env.split("=")
-            monkeypatch.setenv(k, v)
+            for kv in env.split(","):
+                k, v = kv.split("=")
+                monkeypatch.setenv(k, v)
         a = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
         xy = a.getNodes()
         a.setCoeff(*rough_coeffs(xy, 4))

@@ -32,6 +32,8 @@ for cfg in args.cfgs:
     for k, v in kv:
         os.environ[k] = v
     op = aniso_amd.Aniso(args.sz, 1, args.ks, 0.8, 10, 4, 20)
+    if world > 1:  # the shard's plan is built here: under the same knobs
+        op.set_shard(rank, world)
     for k, v in saved.items():
         if v is None:
             os.environ.pop(k, None)
@@ -39,8 +41,6 @@ for cfg in args.cfgs:
             os.environ[k] = v
     xy = op.getNodes()
     perm = torch.tensor(op.tree_perm(), device="cuda", dtype=torch.int64)
-    if world > 1:
-        op.set_shard(rank, world)
     op.setCoeff(*(demo_coeffs(xy) if args.ks > 1 else main_coeffs(xy)))
     for m in range(2 * args.ks - 1):
         op.cache(m)
@@ -90,8 +90,11 @@ for rep in range(args.reps):
             r["st"] = {k: round(v, 4) for k, v in r["op"].stage_times().items()}
             r["op"].set_timing(False)
         r["op"].sync()
+ref = runs[0]["y"][:, runs[0]["b"]:runs[0]["e"]]
 for r in runs:
     s = r["op"].stats()
+    d = r["y"][:, r["b"]:r["e"]]
+    rel = float(torch.linalg.norm(d - ref) / torch.linalg.norm(ref))  # same input: outputs agree to rounding
     print(json.dumps({"cfg": r["cfg"], "world": world, "rank": rank, "ms": r["ms"], "best_ms": min(r["ms"]),
                       "stage_ms": r["st"], "clusters": s["hm_clusters"],
-                      "block_reads": s["hm_block_reads"]}), flush=True)
+                      "block_reads": s["hm_block_reads"], "rel_vs_first": rel}), flush=True)
