@@ -130,9 +130,12 @@ def lib():
     return _lib
 
 
-def exported_symbols():
-    """Names of the entry points declared in include/aniso_mi355x.h."""
-    hdr = open(os.path.join(_HERE, "..", "include", "aniso_mi355x.h")).read()
+def exported_symbols(public_only=False):
+    """Names of the entry points declared in include/aniso_mi355x.h (the drop-in
+    boundary) and, unless public_only, include/aniso_mi355x_dev.h (development and
+    test entries)."""
+    heads = ["aniso_mi355x.h"] + ([] if public_only else ["aniso_mi355x_dev.h"])
+    hdr = "".join(open(os.path.join(_HERE, "..", "include", h)).read() for h in heads)
     import re
 
     return sorted(set(re.findall(r"^(?:int|const char \*)\s*\**\s*(aniso_\w+)\s*\(", hdr, re.M)))

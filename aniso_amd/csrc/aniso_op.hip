@@ -121,7 +121,10 @@ void Operator::getNodes(double* xy) const {
 }
 
 void Operator::setShard(int rank, int nranks) {
-    comm.reset();  // a communicator belongs to one shard layout
+    if (comm) {  // a communicator belongs to one shard layout; drain its collectives first
+        if (device >= 0) HIP_CHECK(hipDeviceSynchronize());
+        comm.reset();
+    }
     plan.build(tree, np, rank, nranks);
     plan.buildExchange(tree, geo.sz, geo.d2);
     plan.buildTopWait(tree);
@@ -1449,6 +1452,7 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
                                std::to_string(c->nranks) + ") differ from the handle's shard (" +
                                std::to_string(plan.rank) + " of " + std::to_string(plan.nranks) + ")");
     ensureDevice();
+    if (comm && device >= 0) HIP_CHECK(hipDeviceSynchronize());  // collectives in flight on the old one
     comm.reset();
     const int P = c->nranks, me = c->rank;
     const int64_t nr = (int64_t)plan.xHalo.size() / 2;

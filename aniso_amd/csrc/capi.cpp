@@ -8,6 +8,7 @@
 #include <string>
 
 #include "../../include/aniso_mi355x.h"
+#include "../../include/aniso_mi355x_dev.h"
 #include "aniso_op.hpp"
 #include "kernels.hpp"
 
@@ -582,6 +583,7 @@ int aniso_top_trace(aniso_handle h, int64_t* rec, int64_t cap, int64_t* n) {
     ENTER(h);
     return guarded([&] {
         CHECK_PTR(n);
+        if (rec && cap < 0) throw std::invalid_argument("aniso_top_trace: cap must be >= 0");
         const auto t = get(h).topTrace();
         *n = (int64_t)t.size() / 8;
         if (rec) std::copy(t.begin(), t.begin() + std::min<int64_t>(cap, *n) * 8, rec);

@@ -18,6 +18,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_exports_every_header_symbol():
     names = aniso_amd.exported_symbols()
     assert len(names) >= 25
+    # the drop-in boundary stays free of the development entries (aniso_mi355x_dev.h)
+    public = aniso_amd.exported_symbols(public_only=True)
+    for dev in ("aniso_top_trace", "aniso_comm_init_loopback", "aniso_line_integrals", "aniso_stage_times",
+                "aniso_set_timing", "aniso_mapping_stages_dev", "aniso_tree_list"):
+        assert dev in names and dev not in public, dev
+    for core in ("aniso_create", "aniso_destroy", "aniso_num_nodes", "aniso_get_nodes", "aniso_set_coeff",
+                 "aniso_cache", "aniso_mapping", "aniso_mapping_batched", "aniso_block_op", "aniso_block_solve"):
+        assert core in public, core
     L = aniso_amd.lib()
     for n in names:
         assert hasattr(L, n), n
