@@ -307,9 +307,7 @@ void Operator::uploadPlan() {
         up(dHmNDir, plan.hmNDir);
         up(dHmClWait, plan.hmClWait);
         up(dHmHaloPtr, plan.hmHaloPtr);
-        up(dHmFoldNode, plan.hmFoldNode);
-        up(dHmFoldPtr, plan.hmFoldPtr);
-        up(dHmFoldIdx, plan.hmFoldIdx);
+        up(dHmHaloPos, plan.hmHaloPos);
         dTopCnt.alloc((kMaxTopTiers + 1) * sizeof(unsigned));
         attReady = false;
     }
@@ -326,6 +324,7 @@ void Operator::uploadPlan() {
     up(dDnLeafGeom, plan.dnLeafGeom);
     up(dDnChainPtr, plan.dnChainPtr);
     up(dDnChain, plan.dnChain);
+    up(dDnChainFold, plan.dnChainFold);
     up(dDnNearPtr, plan.dnNearPtr);
     up(dDnNearOff, plan.dnNearOff);
     dNearPart.alloc((size_t)std::max<int64_t>(plan.nearPartTotal, 1) * workK * sizeof(double));
@@ -856,6 +855,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         const size_t hb = plan.hmHaloNode.size() * kRank * K * sizeof(double);
         if (dHmPart.bytes < hb) dHmPart.alloc(hb);
         hca.haloPtr = dHmHaloPtr.as<int>();
+        hca.haloPos = dHmHaloPos.as<int>();
         hca.hpart = dHmPart.as<double>();
     }
     if (hmRing > 0) {
@@ -968,9 +968,6 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                        dMult.as<double>(), plan.m2lMaxCanon, dM2LPart.as<double>(), dLocal.as<double>(), s);
         }
     }
-    if (halo && (topFused || clustered) && (mask & kStageFar))  // the halo partials into their nodes' locals
-        launch_hm_fold(K, (int)plan.hmFoldNode.size(), dHmFoldNode.as<int>(), dHmFoldPtr.as<int>(),
-                       dHmFoldIdx.as<int>(), dHmPart.as<double>(), dLocal.as<double>(), s);
     int e = tm ? mark(s) : -1;
     span(2, ep, e);
     ep = e;
@@ -990,7 +987,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                          dDnLeafPts.as<int>(), dDnLeafNear.as<int2>(), dDnLeafGeom.as<double4>(), dPxT.as<double>(),
                          dPyT.as<double>(), operm, obase, ldo, dDnNearOff.as<int>(), plan.dnMaxNear,
                          dNearPart.as<double>(), dDnChain.as<int2>(), plan.dnMaxChain, mask, scale, out, subX, subLd,
-                         s);
+                         s, halo && clustered ? dHmPart.as<double>() : nullptr, dDnChainFold.as<int>());
     if (tm) {
         const int e2 = mark(s);
         span(5, ep, e2);
@@ -1080,6 +1077,15 @@ void Operator::blockOpHost(int which, const double* u, const double* sigmaS, dou
     blockOpDev(which, dHostIn.as<double>(), N, dHostOut.as<double>(), N, false, own, gval, sigT);
     HIP_CHECK(hipMemcpyAsync(out, dHostOut.p, bytes, hipMemcpyDeviceToHost, own));
     HIP_CHECK(hipStreamSynchronize(own));
+    if (recoverTopTimeout(own)) {  // the fused launch timed out: the same apply on the tier launches
+        struct Restore {
+            bool& f;
+            ~Restore() { f = false; }
+        } restore{forceUnfused};
+        blockOpDev(which, dHostIn.as<double>(), N, dHostOut.as<double>(), N, false, own, gval, sigT);
+        HIP_CHECK(hipMemcpyAsync(out, dHostOut.p, bytes, hipMemcpyDeviceToHost, own));
+        HIP_CHECK(hipStreamSynchronize(own));
+    }
     checkDeviceErrors();
 }
 
@@ -1560,6 +1566,15 @@ void Operator::checkDeviceErrors() {
     throw std::runtime_error(
         "hand-off time-out in the fused top-of-tree M2L launch (k_top_m2l_hc): a cluster gave up waiting for the "
         "upper up tiers, so the output of an apply enqueued earlier on this handle is invalid");
+}
+
+bool Operator::recoverTopTimeout(hipStream_t s) {
+    if (!topErr || *(volatile unsigned*)topErr == 0) return false;
+    HIP_CHECK(hipStreamSynchronize(s));  // every launch that could still raise it has finished
+    *(volatile unsigned*)topErr = 0;
+    forceUnfused = true;
+    ++topRecoveries;
+    return true;
 }
 
 void Operator::sync() {

@@ -141,6 +141,13 @@ public:
     // raise (ANISO_ERR_RUNTIME) if a fused top-of-tree launch gave up waiting for its
     // producers since the last check: its locals, and so the apply's output, are invalid
     void checkDeviceErrors();
+    // recovery from a fused-launch time-out where the library owns the timeline (the
+    // host-pointer block operator, the block solve): if the flag is set, drain `s`,
+    // clear it, switch the fused launch off for the rest of the call (forceUnfused)
+    // and count it; the caller then re-runs the apply on the tier launches
+    bool recoverTopTimeout(hipStream_t s);
+    int64_t topRecoveries = 0;  // applies re-run after a time-out (aniso_stats)
+    bool forceUnfused = false;
     // wait for every apply enqueued by this handle (both streams), then check
     void sync();
     // development timeline of the last fused top-of-tree launch (ANISO_TOP_TRACE=1,
@@ -154,7 +161,8 @@ public:
     // of 8: 0.262 against 0.251 ms, same-process A/B r03ls)
     bool topFusedOn() const {
         const int ntier = (int)plan.upTierTask.size() - 1;
-        return useClusters && topFusedMode != 0 && top_fused_enabled() && ntier >= 2 && ntier <= kMaxTopTiers &&
+        return useClusters && topFusedMode != 0 && !forceUnfused && top_fused_enabled() && ntier >= 2 &&
+               ntier <= kMaxTopTiers &&
                plan.upLastLeafTier == 0 && plan.hmClWait.size() + 1 == plan.hmClPtr.size();
     }
     // bitwise-reproducible applies: the harmonic M2L as one wave per target (a fixed
@@ -216,7 +224,7 @@ private:
     bool useAtt = false, attReady = false;
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
-    DevBuf dHmHaloPtr, dHmFoldNode, dHmFoldPtr, dHmFoldIdx, dHmPart;  // the halo form (Plan::hmHaloPtr)
+    DevBuf dHmHaloPtr, dHmHaloPos, dHmPart, dDnChainFold;  // the halo form (Plan::hmHaloPtr)
     DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
     DevBuf dTopTrace;           // ANISO_TOP_TRACE=1: the launch's per-block timeline
     DevBuf dKryPart;            // partial sums of the Krylov primitives

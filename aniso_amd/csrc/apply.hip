@@ -717,7 +717,8 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     const double4* __restrict__ leafGeom, const double* __restrict__ pxT, const double* __restrict__ pyT,
     const int* __restrict__ operm, int64_t obase, int64_t ldo, const int* __restrict__ nearOff, int maxNear,
     const double* __restrict__ nearPart, const int2* __restrict__ chain, int maxChain, int flags, double scale,
-    double* __restrict__ out, const double* __restrict__ xsub, int64_t ldx) {
+    double* __restrict__ out, const double* __restrict__ xsub, int64_t ldx, const double* __restrict__ hpart,
+    const int* __restrict__ chainFold) {
     constexpr int RK = kRank * K;
     extern __shared__ double sm[];
     int4* DN = reinterpret_cast<int4*>(sm);                // maxTask node records
@@ -732,6 +733,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     int* NC = NB + maxLeaves;                              // maxLeaves: their count
     int* NO = NC + maxLeaves;                              // maxNear: partial offsets addressed to this task
     int2* CN = reinterpret_cast<int2*>(NO + maxNear + ((maxNear + 1) & 1));  // maxChain: (ancestor, child index), 8-B aligned
+    int* CF = reinterpret_cast<int*>(CN + maxChain);       // maxChain: the ancestors' halo partials (packed)
     const int task = blockIdx.x;
     DOWN_MARK(0);
     // task record: (first node, nodes, first leaf entry, leaves), (owned points begin,
@@ -748,7 +750,10 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     if (far) {
         for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) Rl[i] = (&P->R[0][0])[i];
         for (int k = threadIdx.x; k < nt; k += blockDim.x) DN[k] = dn[n0 + k];
-        for (int k = threadIdx.x; k < nc; k += blockDim.x) CN[k] = chain[c0 + k];
+        for (int k = threadIdx.x; k < nc; k += blockDim.x) {
+            CN[k] = chain[c0 + k];
+            CF[k] = hpart && chainFold ? chainFold[c0 + k] : 0;  // no chain records: no chain partials
+        }
     }
     for (int e = threadIdx.x; e < nl; e += blockDim.x) {
         LB[e] = leafBegin[l0 + e];
@@ -766,8 +771,21 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
     for (int j = threadIdx.x; j < d2.y; j += blockDim.x) NO[j] = nearOff[d2.x + j];
     __syncthreads();
     if (far) {
-        for (int it = threadIdx.x; it < nt * RK; it += blockDim.x) T[it] = local[(size_t)DN[it / RK].x * RK + it % RK];
-        for (int it = threadIdx.x; it < nc * RK; it += blockDim.x) CH[it] = local[(size_t)CN[it / RK].x * RK + it % RK];
+        // a node's local = its cluster's store + the halo partials other clusters left
+        // for it (the halo form of the cluster M2L: packed (first << 3) | count, one
+        // receiver-contiguous range), all loads of one round
+        auto total = [&](int n, int fold, int e) {
+            double v = local[(size_t)n * RK + e];
+            const int cnt = fold & 7;
+            const double* hp = hpart + (size_t)(fold >> 3) * RK + e;
+            for (int j = 0; j < cnt; ++j) v += hp[(size_t)j * RK];
+            return v;
+        };
+        for (int it = threadIdx.x; it < nt * RK; it += blockDim.x) {
+            const int4 d = DN[it / RK];
+            T[it] = total(d.x, hpart ? d.w : 0, it % RK);
+        }
+        for (int it = threadIdx.x; it < nc * RK; it += blockDim.x) CH[it] = total(CN[it / RK].x, CF[it / RK], it % RK);
         __syncthreads();
     }
     DOWN_MARK(1);
@@ -974,7 +992,7 @@ size_t up_tier_lds(int maxTask, int K) {
 size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain, int K) {
     return (size_t)(4 * kRank * kRank + (maxTask + 1 + maxChain) * kRank * K + 4 * maxLeaves) * sizeof(double) +
            (size_t)(4 * maxLeaves + 4 + maxNear) * sizeof(int) + (size_t)maxTask * sizeof(int4) +
-           (size_t)maxChain * sizeof(int2);
+           (size_t)maxChain * (sizeof(int2) + sizeof(int));
 }
 
 void launch_up_tier(int K, int ntask, int taskBase, const int* taskList, int maxTask, const int4* desc,
@@ -1074,13 +1092,13 @@ void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* 
                       const int2* leafNear, const double4* leafGeom, const double* pxT, const double* pyT,
                       const int* operm, int64_t obase, int64_t ldo, const int* nearOff, int maxNear,
                       const double* nearPart, const int2* chain, int maxChain, int flags, double scale, double* out,
-                      const double* xsub, int64_t ldx, hipStream_t s) {
+                      const double* xsub, int64_t ldx, hipStream_t s, const double* hpart, const int* chainFold) {
     if (ntask <= 0) return;
     const size_t shm = down_tier_lds(maxTask, maxLeaves, maxNear, maxChain, K);
     ANISO_DISPATCH_K(K, (k_down_tier<KK><<<ntask, kTierThreads, shm, s>>>(
                             maxTask, maxLeaves, desc, grpFix, dn, local, P, leafSlot, leafBegin, leafNear, leafGeom,
                             pxT, pyT, operm, obase, ldo, nearOff, maxNear, nearPart, chain, maxChain, flags, scale,
-                            out, xsub, ldx)));
+                            out, xsub, ldx, hpart, chainFold)));
     HIP_LAUNCH_CHECK();
 }
 

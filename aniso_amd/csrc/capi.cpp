@@ -561,6 +561,7 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[19] = (int64_t)op.plan.hmHaloNode.size();
         s[20] = op.plan.hmMaxLds;
         s[21] = (int64_t)op.plan.hmSrc.size();
+        s[22] = op.topRecoveries;
     });
 }
 

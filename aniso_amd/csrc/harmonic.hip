@@ -302,7 +302,7 @@ __device__ __forceinline__ HcSlots hc_slots(int cid, const HcArgs& a) {
 }
 
 // the cluster's end: its targets' locals stored, its halo slots stored to their
-// partials (both scaled by om; the fold adds the partials, launch_hm_fold)
+// partials (both scaled by om; the down pass adds the partials, k_down_tier)
 template <int K>
 __device__ __forceinline__ void hc_flush(const HcSlots& c, const HcArgs& a, const double* acc) {
     constexpr int RK = kRank * K;
@@ -310,9 +310,11 @@ __device__ __forceinline__ void hc_flush(const HcSlots& c, const HcArgs& a, cons
         const int k = e / RK, r = e - k * RK;
         a.local[(size_t)a.tgt[c.c0 + k] * RK + r] = a.hw.om[r % K] * acc[e];
     }
-    double* hp = a.hpart + (size_t)c.h0 * RK;
     const double* ah = acc + (size_t)c.nt * RK;
-    for (int e = threadIdx.x; e < c.nh * RK; e += blockDim.x) hp[e] = a.hw.om[e % K] * ah[e];
+    for (int e = threadIdx.x; e < c.nh * RK; e += blockDim.x) {
+        const int k = e / RK, r = e - k * RK;
+        a.hpart[(size_t)a.haloPos[c.h0 + k] * RK + r] = a.hw.om[r % K] * ah[e];
+    }
 }
 
 // The same distances for the 4-wave form (LR): from wave-uniform values only,
@@ -467,26 +469,23 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                     fcy = ncy[B];
                     fry = nry[B];
                 };
-                fetch(0, k0, k1, xm, gcx, grx, gcy, gry);
-                for (int jj = 0; jj < cnt; ++jj) {
-                    // the next pair (the last one again at the end: an L1 hit, no branch
-                    // for the wait counts to merge over)
-                    dbl2 n0, n1;
-                    double xn[K], ncx1, nrx1, ncy1, nry1;
-                    fetch(min(jj + 1, cnt - 1), n0, n1, xn, ncx1, nrx1, ncy1, nry1);
+                // pair jj from one register set while the next pair loads into the
+                // other (unrolled by two: no register copies between the sets)
+                auto pair = [&](int jj, const dbl2& a0, const dbl2& a1, const double (&xv)[K], double fcx,
+                                double frx, double fcy, double fry) {
                     const int sl = LR ? slot[cb + jj] : __builtin_amdgcn_readlane(mySlot, jj);
                     // the distances from wave-uniform values (as the LR form): 8 VGPRs
                     // fewer than the held target columns bx, the same VALU count
-                    const double axs = (gcx - tcx1) + grx * chx;
-                    const double dy = (gcy + gry * chy) - by;
+                    const double axs = (fcx - tcx1) + frx * chx;
+                    const double dy = (fcy + fry * chy) - by;
                     const double dy2 = dy * dy;
                     double xw[K], ob[K];
     #pragma unroll
                     for (int bb = 0; bb < K; ++bb) {
-                        xw[bb] = hw.hw[bb] * xm[bb];
+                        xw[bb] = hw.hw[bb] * xv[bb];
                         ob[bb] = 0.0;
                     }
-                    const double e4[4] = {k0.x, k0.y, k1.x, k1.y};
+                    const double e4[4] = {a0.x, a0.y, a1.x, a1.y};
     #pragma unroll
                     for (int j = 0; j < 4; ++j)
                         hm_entry2<K, NR>(e4[j], cheb_dx_lr(j, axs, trx, P), dy2, xw, xa + (4 * q + j) * K, c[j], ob);
@@ -497,14 +496,18 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
     #pragma unroll
                         for (int i = 0; i < K; ++i) atomicAdd(d + i, (i & 1) ? -ob[i] : ob[i]);
                     }
-                    k0 = n0;
-                    k1 = n1;
-    #pragma unroll
-                    for (int bb = 0; bb < K; ++bb) xm[bb] = xn[bb];
-                    gcx = ncx1;
-                    grx = nrx1;
-                    gcy = ncy1;
-                    gry = nry1;
+                };
+                dbl2 m0, m1;
+                double xn[K], hcx, hrx, hcy, hry;
+                fetch(0, k0, k1, xm, gcx, grx, gcy, gry);
+                for (int jj = 0; jj < cnt; jj += 2) {
+                    // the next pair (the last one again at the end: an L1 hit, no branch
+                    // for the wait counts to merge over)
+                    fetch(min(jj + 1, cnt - 1), m0, m1, xn, hcx, hrx, hcy, hry);
+                    pair(jj, k0, k1, xm, gcx, grx, gcy, gry);
+                    if (jj + 1 >= cnt) break;
+                    fetch(min(jj + 2, cnt - 1), k0, k1, xm, gcx, grx, gcy, gry);
+                    pair(jj + 1, m0, m1, xn, hcx, hrx, hcy, hry);
                 }
             }
         m2l_hc_store_target<K>(c, acc + (size_t)ti * kRank * K, lane, s, q);
@@ -1337,30 +1340,6 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s) {
             f<<<ncl, 256, shm, s>>>(a);
         }
     })));
-    HIP_LAUNCH_CHECK();
-}
-
-// the halo form's fold (Plan::hmFoldPtr): one thread per (receiving node, entry),
-// its partials added in a fixed order
-template <int K>
-__global__ void __launch_bounds__(256) k_hm_fold(int nf, const int* __restrict__ node, const int* __restrict__ ptr,
-                                                 const int* __restrict__ idx, const double* __restrict__ hpart,
-                                                 double* __restrict__ local) {
-    constexpr int RK = kRank * K;
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= (int64_t)nf * RK) return;
-    const int f = (int)(g / RK), r = (int)(g - (int64_t)f * RK);
-    const int p0 = ptr[f], p1 = ptr[f + 1];
-    double v = 0.0;
-    for (int p = p0; p < p1; ++p) v += hpart[(size_t)idx[p] * RK + r];
-    local[(size_t)node[f] * RK + r] += v;
-}
-
-void launch_hm_fold(int K, int nf, const int* node, const int* ptr, const int* idx, const double* hpart,
-                    double* local, hipStream_t s) {
-    if (nf <= 0) return;
-    ANISO_HM_DISPATCH_K(K, (k_hm_fold<KK><<<blocks_for((int64_t)nf * kRank * KK, 256), 256, 0, s>>>(
-                               nf, node, ptr, idx, hpart, local)));
     HIP_LAUNCH_CHECK();
 }
 

@@ -138,6 +138,11 @@ struct Plan {
     // input: ANISO_HM_HALO=0 keeps the directed copies (A/B runs)
     bool hmHalo = true;
     std::vector<int> hmHaloPtr, hmHaloNode, hmFoldPtr, hmFoldNode, hmFoldIdx;
+    // the partials are stored receiver-contiguously: halo slot h at position
+    // hmHaloPos[h] (its place in hmFoldIdx), so node n's partials are one range,
+    // packed per node as (first << 3) | count in hmFoldOf[n] (0: none); the down pass
+    // adds them where it loads the locals (dnNode[.][3], dnChainFold)
+    std::vector<int> hmHaloPos, hmFoldOf;
     int hmMaxLds = 0;  // largest cluster + halo (LDS slots of 16 x K doubles)
     // tiered up / down passes: tier k has root level
     // tierRootLevel[k] and bottom level tierBottomLevel[k] (k = 0 is the deepest).
@@ -168,6 +173,7 @@ struct Plan {
     int dnMaxNear = 1;
     std::vector<int> dnChainPtr;                 // per task: its root's ancestors below the tree root,
     std::vector<std::array<int, 2>> dnChain;     // top-down (node, child slot): the parent total's L2L chain
+    std::vector<int> dnChainFold;                // per chain entry: its node's halo partials (hmFoldOf)
     int dnMaxChain = 1;
     // per task three int4 records (nodes, leaves / owned points, chain / near
     // offsets, levels) + kTaskLevels+1 level starts; per leaf entry its box

@@ -586,6 +586,7 @@ void Plan::buildDownTasks(const Tree& t) {
     // zero), so the tasks of all tiers go in ONE launch and leafless tasks are dropped.
     dnChainPtr.assign(1, 0);
     dnChain.clear();
+    dnChainFold.clear();
     dnMaxChain = 1;
     std::vector<int> anc;
     for (int k = (int)tierRootLevel.size() - 1; k >= 0; --k) {  // top-down
@@ -603,12 +604,15 @@ void Plan::buildDownTasks(const Tree& t) {
                     slotOf[n] = (int)dnNode.size() - base;
                     const int p = t.parent[n];  // the root's total is zero
                     const int pc = (p < 0 || t.parent[p] < 0) ? -1 : n == r ? -2 : slotOf[p];
-                    dnNode.push_back({n, pc, t.slot[n], 0});
+                    dnNode.push_back({n, pc, t.slot[n], hmFoldOf.empty() ? 0 : hmFoldOf[n]});
                 }
             }
             anc.clear();  // ancestors of r below the root, top-down
             for (int a = t.parent[r]; a >= 0 && t.parent[a] >= 0; a = t.parent[a]) anc.push_back(a);
-            for (auto it = anc.rbegin(); it != anc.rend(); ++it) dnChain.push_back({*it, t.slot[*it]});
+            for (auto it = anc.rbegin(); it != anc.rend(); ++it) {
+                dnChain.push_back({*it, t.slot[*it]});
+                dnChainFold.push_back(hmFoldOf.empty() ? 0 : hmFoldOf[*it]);
+            }
             dnChainPtr.push_back((int)dnChain.size());
             dnMaxChain = std::max(dnMaxChain, (int)anc.size());
             const int nearBase = (int)dnNearOff.size();
@@ -814,11 +818,17 @@ void Plan::buildClusters(const Tree& t) {
         hmHaloPtr.push_back((int)hmHaloNode.size());
         hmMaxLds = std::max(hmMaxLds, ncl + (int)hmHaloNode.size() - h0);
     }
-    // the fold: per receiving node, its halo slots in cluster order (a fixed order)
+    // the fold: per receiving node, its halo slots in cluster order (a fixed order),
+    // stored receiver-contiguously (hmHaloPos)
     std::vector<std::vector<int>> recv(t.nn);
     for (size_t h = 0; h < hmHaloNode.size(); ++h) recv[hmHaloNode[h]].push_back((int)h);
+    hmHaloPos.assign(hmHaloNode.size(), -1);
+    hmFoldOf.assign(t.nn, 0);
     for (int n = 0; n < t.nn; ++n) {
         if (recv[n].empty()) continue;
+        if (recv[n].size() > 7 || hmFoldIdx.size() >= (1u << 27)) throw std::logic_error("halo fold record overflow");
+        hmFoldOf[n] = (int)((hmFoldIdx.size() << 3) | recv[n].size());
+        for (size_t j = 0; j < recv[n].size(); ++j) hmHaloPos[recv[n][j]] = (int)(hmFoldIdx.size() + j);
         hmFoldNode.push_back(n);
         hmFoldIdx.insert(hmFoldIdx.end(), recv[n].begin(), recv[n].end());
         hmFoldPtr.push_back((int)hmFoldIdx.size());

@@ -163,7 +163,7 @@ void launch_down_tier(int K, int ntask, int maxTask, int maxLeaves, const int4* 
                       const int* operm, int64_t obase, int64_t ldo, const int* nearOff, int maxNear,
                       const double* nearPart, const int2* chain, int maxChain, int flags, double scale, double* out,
                       const double* xsub, int64_t ldx,
-                      hipStream_t s);
+                      hipStream_t s, const double* hpart = nullptr, const int* chainFold = nullptr);
 // corrections of all terms in one launch, added to out: Wc / Wm the terms'
 // stencil and singular tables folded with their mixes (Operator::corrTable)
 void launch_corr(int K, int d, int64_t b, int64_t e, const int* perm, const int* iperm, const double* cT,
@@ -195,9 +195,11 @@ struct HcArgs {
     int ring = 0;                 // host: the ring form's depth (0: the one-block-in-flight form)
     bool ringXL = false;          // host: the ring form keeps the target multipole in LDS (3 waves / SIMD)
     int wpe = 0;                  // host: the cluster form's occupancy (harmonic.hip hm_form; 0: the default)
-    // the halo form (Plan::hmHaloPtr): cluster c's halo slots are partials
-    // haloPtr[c] .. haloPtr[c+1] - 1 of hpart (16 x K doubles each, stored scaled)
+    // the halo form (Plan::hmHaloPtr): cluster c's halo slots h = haloPtr[c] ..
+    // haloPtr[c+1] - 1 go to partial haloPos[h] of hpart (16 x K doubles each, stored
+    // scaled, receiver-contiguous: the down pass adds them to the locals)
     const int* haloPtr = nullptr;
+    const int* haloPos = nullptr;
     double* hpart = nullptr;
 };
 // The fused top-of-tree + clustered M2L launch (harmonic.hip k_top_m2l_hc, DESIGN.md
@@ -292,9 +294,7 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
 // whether launch_near_hm would run the staged near field with fused corrections
 bool near_hs_fusable(int nl, int maxLeaf, int nsMax, const uint16_t* nearLoc, const NearCorr* corr, int flags);
 void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s);
-// the halo form's fold: local[node[f]] += sum of hpart[idx[ptr[f] .. ptr[f+1])] (16 x K each)
-void launch_hm_fold(int K, int nf, const int* node, const int* ptr, const int* idx, const double* hpart,
-                    double* local, hipStream_t s);
+
 int hm_ring_depth();  // ANISO_HM_RING (read at handle creation): the cluster M2L's LDS ring depth
 int hm_ring_xl(int K, int maxCl, int depth);  // its target multipole in LDS / VGPRs / ring off (1, 0, -1)
 // returns true when the corrections were fused (the caller skips launch_corr)

@@ -514,10 +514,23 @@ int Operator::blockSolveDev(const double* rhs, double* x, int restart, double to
         HIP_CHECK(hipStreamSynchronize(s));
         return h;
     };
+    // a fused-launch time-out (recoverTopTimeout) re-runs the apply it spoiled on the
+    // tier launches, and the rest of the solve keeps them
+    struct Restore {
+        bool& f;
+        bool v;
+        ~Restore() { f = v; }
+    } restore{forceUnfused, forceUnfused};
     auto residual = [&] {  // r = b - A x
         blockOpDev(2, xt, N, w, N, true, s);
         k_sub<<<nblk(L), 256, 0, s>>>(L, b, w, r);
-        return std::sqrt(norm2(r));
+        double h = norm2(r);
+        if (recoverTopTimeout(s)) {
+            blockOpDev(2, xt, N, w, N, true, s);
+            k_sub<<<nblk(L), 256, 0, s>>>(L, b, w, r);
+            h = norm2(r);
+        }
+        return std::sqrt(h);
     };
     const double normb = std::sqrt(norm2(b));
     int nh = 0, total = 0;
@@ -541,22 +554,32 @@ int Operator::blockSolveDev(const double* rhs, double* x, int restart, double to
             bool ahead = false;  // the matvec of V[i] is already enqueued
             for (int i = 0; i < m; ++i) {
                 double* vi = V + (size_t)i * L;
-                if (!ahead) blockOpDev(2, vi, N, w, N, true, s);
                 // CGS2: h = V^T w, w -= V h, twice (the second pass adds its correction),
-                // as three sweeps over V: h; w -= V h with h2 = V^T w; w -= V h2 with ||w||^2
-                kr.dot(i + 1, V, L, w, hd);
-                kr.updateDot(i + 1, V, L, hd, w, bY.as<double>());
-                kr.updateNorm(i + 1, V, L, bY.as<double>(), w, hd + m + 1);
-                k_axpby<<<nblk(i + 1), 256, 0, s>>>(i + 1, 1.0, bY.as<double>(), 1.0, hd);
-                k_scale_rsqrt<<<nblk(L), 256, 0, s>>>(L, w, hd + m + 1, V + (size_t)(i + 1) * L);
-                HIP_CHECK(hipMemcpyAsync(hcPinned, hd, (size_t)(m + 2) * sizeof(double), hipMemcpyDeviceToHost, s));
-                HIP_CHECK(hipEventRecord(evH, s));
+                // as three sweeps over V: h; w -= V h with h2 = V^T w; w -= V h2 with
+                // ||w||^2; then the next basis vector and the column's host copy
+                auto orth = [&] {
+                    kr.dot(i + 1, V, L, w, hd);
+                    kr.updateDot(i + 1, V, L, hd, w, bY.as<double>());
+                    kr.updateNorm(i + 1, V, L, bY.as<double>(), w, hd + m + 1);
+                    k_axpby<<<nblk(i + 1), 256, 0, s>>>(i + 1, 1.0, bY.as<double>(), 1.0, hd);
+                    k_scale_rsqrt<<<nblk(L), 256, 0, s>>>(L, w, hd + m + 1, V + (size_t)(i + 1) * L);
+                    HIP_CHECK(hipMemcpyAsync(hcPinned, hd, (size_t)(m + 2) * sizeof(double), hipMemcpyDeviceToHost, s));
+                    HIP_CHECK(hipEventRecord(evH, s));
+                };
+                if (!ahead) blockOpDev(2, vi, N, w, N, true, s);
+                orth();
                 // the next step's matvec goes in before the host reads the column: the GPU
                 // runs it while the host applies the rotations (wasted once per cycle, at
                 // the step that converges)
                 ahead = i + 1 < m;
                 if (ahead) blockOpDev(2, V + (size_t)(i + 1) * L, N, w, N, true, s);
                 HIP_CHECK(hipEventSynchronize(evH));
+                if (recoverTopTimeout(s)) {  // this step's matvec (or the next one's) timed out: redo both
+                    blockOpDev(2, vi, N, w, N, true, s);
+                    orth();
+                    if (ahead) blockOpDev(2, V + (size_t)(i + 1) * L, N, w, N, true, s);
+                    HIP_CHECK(hipEventSynchronize(evH));
+                }
                 std::copy(hcPinned, hcPinned + m + 2, hc.begin());
                 double* Hc = H.data() + (size_t)i * ld;
                 for (int k = 0; k <= i; ++k) Hc[k] = hc[k];

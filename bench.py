@@ -33,7 +33,12 @@ Also reported on the same JSON line:
   rel_err_vs_cpu  GPU vs CPU oracle on those inputs, plus the 45-term block
                 composition at sz=256;
   mode0_matvec_per_s, deterministic_matvec_per_s  secondary legs on the same
-                operator, measured before the headline leg.
+                operator, measured before the headline leg;
+  config2, config4, config5  BASELINE's other configs:
+                129,600 points at d = 3 (matvec/s, roofline, rel_err vs the oracle),
+                4M points sharded over the run's GPUs (matvec/s, per-rank roofline), the
+                16-RHS fp32 mixed-precision solve (seconds, iterations, rel_err vs fp64
+                GMRES); config2 and config5 on one GPU only.
 """
 import argparse
 import json
@@ -115,6 +120,116 @@ def block_ref(o, U, ss, g):
     return U - out
 
 
+def fwd_roofline(st, times, nb=1):
+    """HBM roofline of the per-mode (single-RHS handle) apply's two streams, timed by the
+    apply's HIP stage events: the M2L (k_m2l: 2 KB per stored merged block, the multipole
+    read and local written per target, the transposed product per canonical pair) and the
+    near field (8 B per stored near entry)."""
+    m2l_b = 2048.0 * st["stored_m2l"] + 2.0 * 128.0 * nb * st["m2l_targets"] + 128.0 * nb * st["m2l_canon"]
+    near_b = 8.0 * st["stored_near"]
+    out = {}
+    for k, b, ms in (("m2l", m2l_b, times["m2l"]), ("near", near_b, times["near"])):
+        gbs = b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        out[k] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(gbs / HBM_PEAK_GBS, 4), "kernel_ms": round(ms, 5), "algorithmic_bytes": int(b)}
+    return out
+
+
+def config2_leg(args, with_cpu):
+    """BASELINE configs[1]: sz = 120 (N = 129,600), d = 3, ns = 8,
+    maxLevel = 5, mode 0, main.cpp's coefficients; main.cpp's GMRES matvec
+    u - K_0(sigma_s .* u) (main.cpp:125-136), chained in tree order on one GPU, with the
+    roofline of its M2L and near-field streams; rel_err: one mapping(q, 0) against the
+    CPU oracle at the same full size (its cache build is ~20 s of the CPU leg)."""
+    import torch
+
+    import aniso_amd
+
+    op = aniso_amd.Aniso(120, 3, 1, args.g, 8, 4, 5)
+    xy = op.getNodes()
+    ss, st = main_coeffs(xy)
+    op.setCoeff(ss, st)
+    op.cache(0)
+    perm = torch.tensor(op.tree_perm(), device="cuda", dtype=torch.int64)
+    x = torch.tensor(gaussian(xy), device="cuda")[perm]
+    y = torch.zeros_like(x)
+    for _ in range(3):
+        op.forward_tree_dev(x, y)
+        x, y = y, x
+    op.set_timing(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        op.forward_tree_dev(x, y)
+        x, y = y, x
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    times = op.stage_times()
+    op.set_timing(False)
+    stats = op.stats()
+    leg = {"workload": "configs[1]: sz=120 (N=129600), d=3, ns=8, np=4, maxLevel=5 (bbfmm depth 5), mode 0: main.cpp "
+                       "GMRES matvec u - K_0(sigma_s .* u), main.cpp coefficients, chained, tree order",
+           "N": op.N, "matvec_per_s": round(args.steps / el, 3), "ms_per_step": round(1e3 * el / args.steps, 4),
+           "steps": args.steps, "stage_ms": {k: round(v, 5) for k, v in times.items()},
+           "roofline": fwd_roofline(stats, times), "rel_err_vs_cpu": None}
+    if with_cpu:
+        from oracle.oracle_py import Oracle
+
+        o = Oracle(120, 3, 1, args.g, 8, 4, 5)
+        o.setCoeff(ss, st)
+        o.cache(0)
+        q = gaussian(xy) * ss + np.random.default_rng(7).uniform(-0.1, 0.1, op.N)
+        ref = o.mapping(q, 0)
+        o.close()
+        got = op.mapping(q, 0)
+        leg["rel_err_vs_cpu"] = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
+    op.close()
+    return leg
+
+
+def config5_leg(args):
+    """BASELINE configs[4]: the configs[2] geometry (N = 1M),
+    mode 0, 16 right-hand sides b_k = K_0 q_k (q_k Gaussian bumps centred by
+    mt19937_64(seed = k)): aniso_amd.solve.gmres_mixed -- the Krylov basis and inner
+    operator in fp32 (16-RHS MFMA operator), fp64 iterative refinement on the fp64 MFMA
+    operator to ||r|| / ||b|| <= 1e-12 -- timed after a warm-up solve; rel_err against 16
+    fp64 device GMRES(80) solves (main.cpp:121-141, aniso_gmres) of the same systems."""
+    import torch
+
+    import aniso_amd
+    from aniso_amd.solve import config5_charges, gmres_mixed, rhs_block
+
+    a = aniso_amd.Aniso(args.sz, args.d, 1, args.g, args.ns, 4, args.max_level)
+    xy = a.getNodes()
+    a.setCoeff(*main_coeffs(xy))
+    a.cache(0)
+    Q = np.stack([config5_charges(xy, s) for s in range(16)])
+    B = rhs_block(a, torch.tensor(Q, device="cuda"))
+    gmres_mixed(a, B, tol=1e-12)  # warm-up: builds the fp32 and fp64 16-RHS caches
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    X, outer, inner, rel = gmres_mixed(a, B, tol=1e-12, m=40, inner_tol=1e-6)
+    torch.cuda.synchronize()
+    t_mixed = time.perf_counter() - t0
+    Xh = X.cpu().numpy()
+    # the fp64 reference: aniso_gmres solves A x = K_0 q (it forms rhs = K_0 q itself,
+    # main.cpp:123), the same systems as B = K_0 Q above
+    errs, its = [], []
+    t0 = time.perf_counter()
+    for k in range(16):
+        it, x, _, _ = a.gmres(Q[k], m=80, maxit=400, tol=1e-12)
+        its.append(it)
+        errs.append(float(np.linalg.norm(Xh[k] - x) / np.linalg.norm(x)))
+    t_ref = time.perf_counter() - t0
+    leg = {"workload": "configs[4]: configs[2] geometry (N=1048576, d=1, ns=10), mode 0, 16 RHS, fp32 mixed precision: "
+                       "fp32 Krylov basis + fp32 16-RHS MFMA inner operator, fp64 refinement on the fp64 MFMA operator",
+           "seconds": round(t_mixed, 4), "outer_refinements": outer, "inner_iterations": inner,
+           "final_rel_residual_max": float(rel.max()), "rel_err_vs_fp64_gmres_max": max(errs),
+           "fp64_gmres_16_solves_s": round(t_ref, 4), "fp64_gmres_iterations": its}
+    a.close()
+    return leg
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -155,7 +270,7 @@ def cpu_baseline(args, coeffs, op, block_check):
     ss, st = coeffs(xy)
     o.setCoeff(ss, st)
     u = gaussian(xy) * ss + np.random.default_rng(3).uniform(-0.1, 0.1, o.N)
-    per_mode, port_mode, t_cache, errs = {}, {}, 0.0, {}
+    per_mode, port_mode, t_cache, errs, spread = {}, {}, 0.0, {}, {}
     for m in modes:
         t0 = time.time()
         o.cache(m)
@@ -170,6 +285,7 @@ def cpu_baseline(args, coeffs, op, block_check):
                 o.mapping(u, m)
                 ts.append(time.perf_counter() - t1)
             dst[m] = float(np.median(ts))
+            spread[(m, alloc)] = (min(ts), max(ts))
         o.set_reference_alloc(False)
         o.uncache(m)
         got = op.mapping(u, m)
@@ -181,6 +297,10 @@ def cpu_baseline(args, coeffs, op, block_check):
     t_port = float(np.mean(list(port_mode.values())))
     per_matvec = ks * (2 * ks - 1) if block else 1  # aniso.m's loop: ks x (2ks-1) mapping calls per mforward
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    try:
+        visible = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        visible = os.cpu_count() or 1
     return {
         "value": 1.0 / (per_matvec * t_apply),
         "unit": "matvec/s",
@@ -194,7 +314,14 @@ def cpu_baseline(args, coeffs, op, block_check):
                    + ", ".join(f"mode {m} {t * 1e3:.0f} ms" for m, t in per_mode.items())
                    + f"; one matvec = {per_matvec} mode-applies (the reference's loop); cache build {t_cache:.1f} s "
                    f"not timed; OMP threads={cores}"),
+        # OpenMP threads: OMP_NUM_THREADS as the GPU box sets it for one GPU's job (16: the
+        # box's CPU share per GPU; the reference's own runs used one thread per core)
+        "thread_policy": (f"OMP_NUM_THREADS={cores} (the job's CPU share on the GPU box); "
+                          f"{visible} CPUs visible to the process, os.cpu_count()={os.cpu_count()}"),
         "mode_apply_s": {str(m): round(t, 4) for m, t in per_mode.items()},
+        "mode_apply_spread_s": {f"{m}{'' if a else '_port'}": [round(lo, 4), round(hi, 4)]
+                                for (m, a), (lo, hi) in spread.items()},
+        "reps_per_mode": args.cpu_reps,
         "port_value": 1.0 / (per_matvec * t_port),
         "port_mode_apply_s": {str(m): round(t, 4) for m, t in port_mode.items()},
     }, errs
@@ -212,7 +339,7 @@ def main():
     ap.add_argument("--ks", type=int, default=5)
     ap.add_argument("--g", type=float, default=0.8)
     ap.add_argument("--max-level", type=int, default=20)
-    ap.add_argument("--cpu-reps", type=int, default=2,
+    ap.add_argument("--cpu-reps", type=int, default=3,
                     help="timed oracle applies per mode and timing mode (after one warm-up)")
     ap.add_argument("--cpu-check-sz", type=int, default=256, help="sz of the 45-term block composition check")
     ap.add_argument("--no-cpu", action="store_true")
@@ -229,6 +356,10 @@ def main():
     ap.add_argument("--no-solve", action="store_true", help="skip the one-GPU aniso.m solve (aniso_block_solve)")
     ap.add_argument("--config4-sz", type=int, default=2048,
                     help="secondary leg: BASELINE configs[3] (4M points, mode 0, sharded over the run's GPUs); 0 skips")
+    ap.add_argument("--config2", type=int, default=1,
+                    help="secondary leg (one GPU): BASELINE configs[1], 129,600 points, d=3, maxLevel 5; 0 skips")
+    ap.add_argument("--config5", type=int, default=1,
+                    help="secondary leg (one GPU): BASELINE configs[4], 16-RHS fp32 mixed-precision solve; 0 skips")
     args = ap.parse_args()
 
     import torch
@@ -365,9 +496,9 @@ def main():
     # target node (16 x nb doubles each).  Per-mode stream (k_m2l): the stored merged
     # operators of every mode term, the same per-target bytes per term, one
     # transposed partial (16 x nb doubles) per canonical pair and term.
-    # Clustered (k_m2l_hc, §3.10): an in-cluster pair's stored block is read once for
-    # both ends; a pair crossing clusters is still read by each end (block_reads).
-    # The algorithmic bytes count every stored block once.
+    # Clustered (k_m2l_hc, §3.10): every stored block is read once for both ends (the
+    # halo form; block_reads = the stored blocks).  The algorithmic bytes count every
+    # stored block once.
     harmonic = block and my_stats["harmonic"] == 1
     if harmonic and my_stats["hm_clusters"] > 0:
         m2l_bytes = 2048.0 * my_stats["att_m2l_blocks"] + 2.0 * 128.0 * nb * my_stats["m2l_targets"]
@@ -525,6 +656,7 @@ def main():
         for _ in range(2):
             step4(x4, y4)
             x4, y4 = y4, x4
+        op4.set_timing(True)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -536,6 +668,8 @@ def main():
         if world > 1:
             dist.barrier()
         el4 = time.perf_counter() - t4
+        times4 = op4.stage_times()
+        op4.set_timing(False)
         if world > 1:
             t = torch.tensor([el4], device="cuda", dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -544,7 +678,10 @@ def main():
                                        "u - K_0(sigma_s .* u), sharded by FMM subtree over the run's GPUs",
                            "N": op4.N, "matvec_per_s": round(args.steps / el4, 3),
                            "ms_per_step": round(1e3 * el4 / args.steps, 4), "steps": args.steps,
-                           "scaling": "strong", "n_gpus": world}
+                           "scaling": "strong", "n_gpus": world,
+                           "stage_ms": {k: round(v_, 5) for k, v_ in times4.items()},
+                           # this rank's M2L and near-field streams (its shard's stored blocks)
+                           "roofline": fwd_roofline(op4.stats(), times4)}
         del op4
     if args.verify:
         # one matvec of a fixed block vector through this (possibly sharded) path vs
@@ -606,6 +743,12 @@ def main():
         line["block_solve"] = {"call": "gmres(A, rhs, 400, 1e-11, 400), A(u) = u - mforward(u) (aniso.m:159-173)",
                                "iterations": its, "relres": srel, "seconds": round(sel, 4),
                                "ms_per_iteration": round(1e3 * sel / max(abs(its), 1), 4)}
+    # BASELINE's one-GPU configs[1] and configs[4] (after the block solve: their handles'
+    # allocations would otherwise be recycled into the solve's 16.8 GB Krylov basis)
+    if world == 1 and block and args.config2:
+        line["config2"] = config2_leg(args, with_cpu=not args.no_cpu)
+    if world == 1 and block and args.config5:
+        line["config5"] = config5_leg(args)
     if rank == 0 and world == 1 and not args.no_cpu:
         def block_check(sz):
             """x - mforward(x) (aniso.m:155) at sz: HIP harmonic block apply vs the

@@ -1142,12 +1142,16 @@ def test_fused_launch_timeline(monkeypatch):
     assert int(cl[:, 7].sum()) == st["hm_block_reads"]
 
 
-def test_fused_top_of_tree_time_out_is_an_error(monkeypatch):
+def test_fused_top_of_tree_time_out_recovers(monkeypatch):
     """A hand-off wait of k_top_m2l_hc that gives up (forced here: ANISO_TOP_SPIN_LIMIT=0
-    makes every waiting block give up at its first poll) must surface as
-    ANISO_ERR_RUNTIME -- from aniso_sync, and from a host-pointer call, which
-    synchronises itself -- never as a silently wrong matvec; the flag is reported once.
-    A default handle reports nothing."""
+    makes every waiting block give up at its first poll) is never a silently wrong
+    matvec.  Where the library owns the timeline it recovers inside the handle: the
+    host-pointer block operator re-runs the apply on the separate tier launches and
+    returns the right matvec (<= 1e-13 against a default handle; aniso_stats counts one
+    recovery per call), and aniso.m's block solve re-runs every spoiled step and
+    converges to the default handle's solution.  A device-pointer apply, already
+    consumed by later work when the flag is read, still surfaces as ANISO_ERR_RUNTIME
+    from aniso_sync, once."""
     torch = _torch()
     import aniso_amd
 
@@ -1160,20 +1164,32 @@ def test_fused_top_of_tree_time_out_is_an_error(monkeypatch):
     for m in range(2 * ks - 1):
         a.cache(m)
     assert a.stats()["top_fused"] == 1
-    U = torch.tensor(np.random.default_rng(1).uniform(-1, 1, (ks, a.N)), device="cuda")
+    b = aniso_amd.Aniso(256, 1, ks, 0.8, 10, 4, 20)
+    b.setCoeff(*main_coeffs(xy))
+    for m in range(2 * ks - 1):
+        b.cache(m)
+    Uh = np.random.default_rng(1).uniform(-1, 1, (ks, a.N))
+    ref = b.block_op(2, Uh)
+    got = a.block_op(2, Uh)
+    assert a.stats()["top_recoveries"] == 1 and a.stats()["top_fused"] == 1
+    assert _rel(got, ref) <= 1e-13
+    # the device-pointer path cannot be re-run after the fact: an error, reported once
+    U = torch.tensor(Uh, device="cuda")
     out = torch.zeros_like(U)
     a.block_op_dev(2, U, out)
     with pytest.raises(aniso_amd.AnisoError) as ei:
         a.sync()
     assert ei.value.code == 2 and "time-out" in str(ei.value)
     a.sync()  # reported once
-    with pytest.raises(aniso_amd.AnisoError) as ei:
-        a.block_op(2, U.cpu().numpy())
-    assert ei.value.code == 2
-    b = aniso_amd.Aniso(256, 1, ks, 0.8, 10, 4, 20)
-    b.setCoeff(*main_coeffs(xy))
-    for m in range(2 * ks - 1):
-        b.cache(m)
+    # aniso.m's solve (aniso.m:159-173) recovers step by step
+    rhs = np.zeros((ks, a.N))
+    rhs[0] = np.exp(-25 * ((xy[:, 0] - 0.5) ** 2 + (xy[:, 1] - 0.5) ** 2))
+    r0 = a.stats()["top_recoveries"]
+    ita, xa, _, rela = a.block_solve(rhs.reshape(-1), restart=20, tol=1e-10, maxit=10)
+    itb, xb, _, relb = b.block_solve(rhs.reshape(-1), restart=20, tol=1e-10, maxit=10)
+    assert ita > 0 and itb > 0 and rela <= 1e-10
+    assert a.stats()["top_recoveries"] > r0 and b.stats()["top_recoveries"] == 0
+    assert _rel(xa, xb) <= 1e-9
     b.block_op_dev(2, U, out)
     b.sync()
 
