@@ -617,12 +617,13 @@ class Aniso:
         return ptr, idx
 
     def stats(self):
-        s = np.zeros(23, dtype=np.int64)
+        s = np.zeros(25, dtype=np.int64)
         _check(lib().aniso_stats(self.address, s.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
         keys = ["near_entries", "m2l_entries", "m2l_pairs", "leaves", "m2l_targets", "tree_nodes", "max_leaf", "N",
                 "stored_near", "stored_m2l", "m2l_canon", "near_partial", "harmonic", "att_m2l_blocks",
                 "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "top_fused",
-                "plan_halo_slots", "plan_max_lds_slots", "plan_block_reads", "top_recoveries"]
+                "plan_halo_slots", "plan_max_lds_slots", "plan_block_reads", "top_recoveries",
+                "near_hs_stored", "near_hs_partials"]
         return dict(zip(keys, (int(v) for v in s)))
 
     def sync(self):

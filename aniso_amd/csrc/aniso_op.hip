@@ -72,6 +72,11 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     plan.nearSymmetric = ks == 1;
     if (const char* e = std::getenv("ANISO_NEAR_SYMMETRIC")) plan.nearSymmetric = e[0] == '1';
     plan.maxCanon = ks == 1 ? kMaxCanon : kMaxCanonBlock;
+    // ANISO_NEAR_HS_SYM=1: the harmonic block apply stores the U pairs between owned
+    // leaves once (Plan::nearSymHs; K <= 5: the canonical loop's registers leave K = 8
+    // at one wave per SIMD).  Off by default: measured slower
+    plan.nearSymHs = false;
+    if (const char* e = std::getenv("ANISO_NEAR_HS_SYM")) plan.nearSymHs = ks > 1 && ks <= 5 && e[0] == '1';
     plan.build(tree, np, 0, 1);
     plan.buildExchange(tree, geo.sz, geo.d2);
     plan.buildTopWait(tree);
@@ -266,7 +271,7 @@ void Operator::ensureWork(int K) {
     HIP_CHECK(hipMemset(dMult.p, 0, dMult.bytes));
     HIP_CHECK(hipMemset(dLocal.p, 0, dLocal.bytes));
     dM2LPart.alloc((size_t)std::max(plan.m2lCanon, 1) * kRank * K * sizeof(double));
-    dNearPart.alloc((size_t)std::max<int64_t>(plan.nearPartTotal, 1) * K * sizeof(double));
+    dNearPart.alloc((size_t)std::max<int64_t>({plan.nearPartTotal, plan.hsPartTotal, 1}) * K * sizeof(double));
 }
 
 static std::vector<int4> to_int4(const std::vector<std::array<int, 4>>& v) {
@@ -327,7 +332,21 @@ void Operator::uploadPlan() {
     up(dDnChainFold, plan.dnChainFold);
     up(dDnNearPtr, plan.dnNearPtr);
     up(dDnNearOff, plan.dnNearOff);
-    dNearPart.alloc((size_t)std::max<int64_t>(plan.nearPartTotal, 1) * workK * sizeof(double));
+    dNearPart.alloc((size_t)std::max<int64_t>({plan.nearPartTotal, plan.hsPartTotal, 1}) * workK * sizeof(double));
+    if (plan.nearSymHsOn) {
+        up(dHsPtsPtr, plan.hsPtsPtr);
+        up(dHsLoc, plan.hsLoc);
+        up(dHsKOff, plan.hsKOff);
+        std::vector<int2> hs(plan.hsSym.size());
+        for (size_t i = 0; i < hs.size(); ++i) hs[i] = make_int2(plan.hsSym[i][0], plan.hsSym[i][1]);
+        up(dHsSym, hs);
+        up(dHsSrcPtr, plan.hsSrcPtr);
+        up(dHsSrc, plan.hsSrc);
+        up(dHsDst, plan.hsDst);
+        up(dNearSelfRow, plan.nearSelfRow);
+        up(dNearGrpInPtr, plan.nearGrpInPtr);
+        up(dNearGrpIn, plan.nearGrpIn);
+    }
     up(dLeafInfo, to_int4(plan.leafInfo));
     up(dNearPtsPtr, plan.nearPtsPtr);
     up(dNearPts, plan.nearPts);
@@ -440,16 +459,20 @@ void Operator::buildAttCache() {
     const Params* P = dParams.as<Params>();
     const int64_t npairs = (int64_t)(plan.attOwner.size() + plan.hmCopyOwner.size());  // stored blocks + copies
     dAttM2L.alloc((size_t)npairs * 256 * sizeof(double));
-    dAttNear.alloc((size_t)plan.nearKTotal * sizeof(double));
+    // the near blocks in the layout the harmonic near field reads: directed, or with
+    // symmetric U storage its own lists (Plan::buildNearHs)
+    const bool hs = plan.nearSymHsOn;
+    const std::vector<int64_t>& nptr = hs ? plan.hsSrcPtr : plan.nearPtr;
+    dAttNear.alloc((size_t)(hs ? plan.hsKTotal : plan.nearKTotal) * sizeof(double));
     dSigDiag.alloc((size_t)geo.N * sizeof(double));
     int maxSrc = 1;
-    for (size_t li = 0; li < plan.leaves.size(); ++li)
-        maxSrc = std::max<int>(maxSrc, (int)(plan.nearPtr[li + 1] - plan.nearPtr[li]));
+    for (size_t li = 0; li < plan.leaves.size(); ++li) maxSrc = std::max<int>(maxSrc, (int)(nptr[li + 1] - nptr[li]));
     launch_cache_att_m2l(npairs, dAttOwner.as<int>(), dAttOther.as<int>(), dNcx.as<double>(), dNcy.as<double>(),
                          dNrx.as<double>(), dNry.as<double>(), dStCoef.as<double>(), P, dAttM2L.as<double>(), own);
-    launch_cache_near((int)plan.leaves.size(), dLeaves.as<int>(), dNearPtr.as<int64_t>(), dNearSrc.as<int>(),
-                      dNearKOff.as<int64_t>(), dBegin.as<int64_t>(), dCount.as<int64_t>(), dPxT.as<double>(),
-                      dPyT.as<double>(), dStCoef.as<double>(), P, kAttMode, maxSrc, dAttNear.as<double>(), own);
+    launch_cache_near((int)plan.leaves.size(), dLeaves.as<int>(), (hs ? dHsSrcPtr : dNearPtr).as<int64_t>(),
+                      (hs ? dHsSrc : dNearSrc).as<int>(), (hs ? dHsKOff : dNearKOff).as<int64_t>(),
+                      dBegin.as<int64_t>(), dCount.as<int64_t>(), dPxT.as<double>(), dPyT.as<double>(),
+                      dStCoef.as<double>(), P, kAttMode, maxSrc, dAttNear.as<double>(), own);
     launch_sigma_diag(geo.N, dPxT.as<double>(), dPyT.as<double>(), dStCoef.as<double>(), P, dSigDiag.as<double>(),
                       own);
     HIP_CHECK(hipStreamSynchronize(own));
@@ -765,7 +788,10 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     // ANISO_NEAR_IN_TOP: the near field (+ corrections) as the last blocks of that
     // launch (the one-block M2L form; a shard's phase 1 then leaves it to phase 2)
     const bool ringOn = hmRing > 0 && hm_ring_xl(K, plan.hmMaxLds, hmRing) >= 0;
-    const bool nearFused = topFused && overlap && nearInTop && !ringOn && plan.nearCorrOk &&
+    // symmetric U storage (Plan::nearSymHsOn): the harmonic near field reads its own
+    // column lists and leaves the partner products of other groups to the down pass
+    const bool hsSym = harmonic && plan.nearSymHsOn;
+    const bool nearFused = topFused && overlap && nearInTop && !ringOn && !hsSym && plan.nearCorrOk &&
                            near_hs_fusable((int)plan.leaves.size(), plan.nearMaxLeaf, plan.nsMax,
                                            dNearLoc.as<uint16_t>(), &nc, mask);
     const bool fork = harmonic && overlap && !nearFused;
@@ -787,7 +813,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     // one up tier; a sharded apply's bottom tier runs this rank's tasks only (list)
     // and stores its tier-0 roots into send, its next tier reads the gathered ones
     auto upTier = [&](int k, const int* list, int ntask, const double* recv, double* send) {
-        launch_up_tier(K, ntask, plan.upTierTask[k], list, plan.upMaxTask, dUpDesc.as<int4>(), dUpGrpFix.as<int>(),
+        launch_up_tier(K, ntask, plan.upTierTask[k], list, plan.upTierMaxTask[k], dUpDesc.as<int4>(), dUpGrpFix.as<int>(),
                        dUpNode.as<int>(), dUpCode.as<int4>(), dUpGeom.as<double4>(), dUpLeaf.as<int2>(),
                        dPxT.as<double>(), dPyT.as<double>(), x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT,
                        dWT.as<double>(), fTw, cTw, P, dMult.as<double>(),
@@ -797,12 +823,26 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     };
     auto tierTasks = [&](int k) { return plan.upTierTask[k + 1] - plan.upTierTask[k]; };
     NearHsArgs nin{};  // nearIn: the input the near field forms its charges from
-    nin.xin = x;
-    nin.ldi = ldx;
-    nin.treeIn = treeIn ? 1 : 0;
-    nin.perm = dPerm.as<int>();
-    nin.sigT = sigT;
-    nin.wT = dWT.as<double>();
+    if (nearIn) {
+        nin.xin = x;
+        nin.ldi = ldx;
+        nin.treeIn = treeIn ? 1 : 0;
+        nin.perm = dPerm.as<int>();
+        nin.sigT = sigT;
+        nin.wT = dWT.as<double>();
+    }
+    if (hsSym) {
+        nin.nearSym = dHsSym.as<int2>();
+        nin.colDst = dHsDst.as<int>();
+        nin.selfRow = dNearSelfRow.as<uint16_t>();
+        nin.nearPart = dNearPart.as<double>();
+        nin.grpInPtr = dNearGrpInPtr.as<int>();
+        nin.grpIn = dNearGrpIn.as<int>();
+        nin.grpSlots = plan.nearGrpSlots;
+    }
+    const int64_t* const hmPtsPtr = (hsSym ? dHsPtsPtr : dNearPtsPtr).as<int64_t>();
+    const int64_t* const hmKOff = (hsSym ? dHsKOff : dNearKOff).as<int64_t>();
+    const uint16_t* const hmLoc = (hsSym ? dHsLoc : dNearLoc).as<uint16_t>();
     // near field + corrections (they need only fT / cT, or with nearIn the input)
     auto nearStage = [&] {
         if (fork) HIP_CHECK(hipStreamWaitEvent(side, evFork, 0));
@@ -811,12 +851,11 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         if (harmonic) {
             // the corrections ride in the staged near kernel (d = 1, its table holds
             // every stencil neighbour; Plan::nearCorrRow)
-            corrFused = launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(),
-                           dNearPtsPtr.as<int64_t>(), dNearPts.as<int>(), dNearKOff.as<int64_t>(),
-                           dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(), dSigDiag.as<double>(), hw,
-                           dFT.as<double>(), operm, obase, ldo, mask, scale, out,
-                           dNearLoc.as<uint16_t>(), dNsPtr.as<int64_t>(), dNsPts.as<int>(),
-                           plan.nsMax, plan.nearCorrOk ? &nc : nullptr, nearWpe, sn, nearIn ? &nin : nullptr);
+            corrFused = launch_near_hm(K, (int)plan.leaves.size(), plan.nearMaxLeaf, dLeafInfo.as<int4>(), hmPtsPtr,
+                           dNearPts.as<int>(), hmKOff, dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(),
+                           dSigDiag.as<double>(), hw, dFT.as<double>(), operm, obase, ldo, mask, scale, out, hmLoc,
+                           dNsPtr.as<int64_t>(), dNsPts.as<int>(), plan.nsMax, plan.nearCorrOk ? &nc : nullptr,
+                           nearWpe, sn, &nin);
         } else if (plan.nearPartTotal > 0) {
             // symmetric U storage (K = 1 handles): one launch per term; the transposed
             // products go to partials summed over the terms
@@ -928,7 +967,9 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     }
     if (mask & kStageFar) {
         if (topFused) {
-            const UpArgs ua{plan.upMaxTask, dUpDesc.as<int4>(), dUpGrpFix.as<int>(), dUpNode.as<int>(),
+            // the launch's LDS holds the largest task of tiers >= 1 only (tier 0 runs apart)
+            // (sizing it for the 85-node tier-0 tasks too cost 0.3-0.5 %, r04j)
+            const UpArgs ua{plan.upMaxTaskFrom(1), dUpDesc.as<int4>(), dUpGrpFix.as<int>(), dUpNode.as<int>(),
                             dUpCode.as<int4>(), dUpGeom.as<double4>(), dUpLeaf.as<int2>(), dPxT.as<double>(),
                             dPyT.as<double>(), x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT, dWT.as<double>(),
                             fTw, cTw, P, dMult.as<double>(),
@@ -944,10 +985,11 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             ta.recv1 = phase == 2 ? rootsRecv : nullptr;
             ta.spinLimit = topSpinLimit;
             HIP_CHECK(hipHostGetDevicePointer((void**)&ta.err, topErr, 0));
-            const NearHsArgs na{(int)plan.leaves.size(), plan.nsMax, dLeafInfo.as<int4>(), dNearPtsPtr.as<int64_t>(),
-                                dNearLoc.as<uint16_t>(), dNsPtr.as<int64_t>(), dNsPts.as<int>(),
-                                dNearKOff.as<int64_t>(), dAttNear.as<double>(), dPxT.as<double>(), dPyT.as<double>(),
-                                dSigDiag.as<double>(), hw, dFT.as<double>(), operm, obase, ldo, mask, scale, out, nc};
+            const NearHsArgs na{(int)plan.leaves.size(), plan.nsMax, dLeafInfo.as<int4>(), hmPtsPtr, hmLoc,
+                          dNsPtr.as<int64_t>(), dNsPts.as<int>(), hmKOff, dAttNear.as<double>(), dPxT.as<double>(),
+                          dPyT.as<double>(), dSigDiag.as<double>(), hw, dFT.as<double>(), operm, obase, ldo, mask,
+                          scale, out, nc};
+
             if (topTraceOn) {
                 topTraceNear = nearFused ? (na.nl + 15) / 16 : 0;
                 topTraceBlocks = ta.nUp + ncl + topTraceNear;
@@ -986,7 +1028,9 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                          dDnGrpFix.as<int>(), dDnNode.as<int4>(), dLocal.as<double>(), P, dDnLeafSlot.as<int>(),
                          dDnLeafPts.as<int>(), dDnLeafNear.as<int2>(), dDnLeafGeom.as<double4>(), dPxT.as<double>(),
                          dPyT.as<double>(), operm, obase, ldo, dDnNearOff.as<int>(), plan.dnMaxNear,
-                         dNearPart.as<double>(), dDnChain.as<int2>(), plan.dnMaxChain, mask, scale, out, subX, subLd,
+                         // the near partials: a single-RHS symmetric plan, or the harmonic one's
+                         (harmonic ? hsSym : plan.nearPartTotal > 0) ? dNearPart.as<double>() : nullptr,
+                         dDnChain.as<int2>(), plan.dnMaxChain, mask, scale, out, subX, subLd,
                          s, halo && clustered ? dHmPart.as<double>() : nullptr, dDnChainFold.as<int>());
     if (tm) {
         const int e2 = mark(s);

@@ -292,6 +292,10 @@ private:
     DevBuf dDnTaskPtr, dDnGrpPtr, dDnGrp, dDnNode, dDnLeafPtr, dDnLeafSlot, dDnLeafIdx, dDnLeafPts, dDnPtsRange, dDnDesc, dDnGrpFix, dDnLeafGeom;  // down
     DevBuf dLeafInfo, dNearPtsPtr, dNearPts;
     DevBuf dNsPtr, dNsPts, dNearLoc;  // near field sources staged per workgroup (k_near_hs)
+    // the harmonic near field's symmetric U storage (Plan::nearSymHsOn): its column
+    // lists, canonical partner blocks and the leaves' first table rows
+    DevBuf dHsPtsPtr, dHsLoc, dHsKOff, dHsSym, dHsSrcPtr, dHsSrc, dHsDst, dNearSelfRow;
+    DevBuf dNearGrpInPtr, dNearGrpIn;
     DevBuf dNearCorrRow;              // d = 1: the stencil's table rows (corrections fused into k_near_hs)
     DevBuf dXT0Tasks, dXRootRecv, dXRootSlot, dXSendSlot;  // sharded up pass (plan.buildExchange)
     DevBuf dM2LNDir, dM2LCanonBase, dM2LInPtr, dM2LOutSlot, dM2LPart;  // symmetric M2L

@@ -861,7 +861,7 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
         double v[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) v[i] = 0.0;
-        if (flags & kStageNear) {
+        if ((flags & kStageNear) && nearPart) {  // nullptr: this apply's near field left no partials
             const int* no = NO + NB[lo];
             for (int j = 0; j < NC[lo]; ++j) {
                 const double* pp = nearPart + ((size_t)no[j] + t) * K;

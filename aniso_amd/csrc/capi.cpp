@@ -562,6 +562,9 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         s[20] = op.plan.hmMaxLds;
         s[21] = (int64_t)op.plan.hmSrc.size();
         s[22] = op.topRecoveries;
+        // the harmonic near field's symmetric U storage (0: directed, Plan::nearSymHsOn)
+        s[23] = op.plan.nearSymHsOn ? op.plan.hsStored : 0;
+        s[24] = op.plan.nearSymHsOn ? op.plan.hsPartTotal : 0;
     });
 }
 

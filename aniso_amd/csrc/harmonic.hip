@@ -862,7 +862,7 @@ __device__ __forceinline__ void m2l_cluster_form(int cid, const HcArgs& a, doubl
     else m2l_hcr_cluster<K, NR, D, XL>(cid, a, sm);
 }
 
-template <int K, int U, int NR, bool FUSE>
+template <int K, int U, int NR, bool FUSE, bool SYM = false>
 __device__ __forceinline__ void near_hs_group(int g, const NearHsArgs& n, double* tab);
 
 // NEAR: the staged near field's groups (k_near_hs with fused corrections) are the last
@@ -1054,7 +1054,7 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
 template <int K>
 constexpr int kTabRow = (kStride<K> + 2) | 1;
 
-template <int K, int U, int NR, bool FUSE>
+template <int K, int U, int NR, bool FUSE, bool SYM>
 __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, double* tab) {
     constexpr int KS = kStride<K>;
     constexpr int RW = kTabRow<K>;  // table row: x, y, the charges (padded)
@@ -1089,6 +1089,11 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
             load_charges<K>(fT + (size_t)p * KS, f);
         }
     };
+    // SYM: symmetric U storage (NearHsArgs::colDst; its own instance: the canonical
+    // loop's registers would cost the directed kernel a wave per SIMD); the partner
+    // products within the group go to LDS slots after the table, 16 rows x K each
+    const bool sym = SYM && nearOn;
+    double* dslot = tab + (size_t)n.nsMax * RW;
     if (nearOn) {
         const int64_t r0 = nsPtr[g];
         const int nr = (int)(nsPtr[g + 1] - r0);
@@ -1103,6 +1108,10 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
             for (int v = 0; v < K; ++v) row[2 + v] = f[v];
         }
     }
+#ifdef ANISO_NEAR_SYM_ATOMIC
+    if (sym)
+        for (int i = threadIdx.x; i < 256 * K; i += blockDim.x) dslot[i] = 0.0;
+#endif
     __syncthreads();
     const int gl = threadIdx.x & 15;
     const int li = g * 16 + (int)(threadIdx.x >> 4);
@@ -1114,7 +1123,9 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
         pb = nearPtsPtr[li];
         koff = nearKOff[li];
     }
-    const int nT = info.z, S = nearOn ? info.w : 0;
+    const int nT = info.z;
+    // the directed columns (symmetric storage: the canonical blocks follow them)
+    const int S = !nearOn ? 0 : sym && active ? n.nearSym[li].x : info.w;
     const int64_t tb = info.y;
     const int nq = (nT + 3) >> 2;
     const int cstr = 2 * nq;
@@ -1162,6 +1173,73 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
             }
         }
     }
+    if constexpr (SYM) if (sym && active) {
+        // canonical partner blocks (the U pairs this leaf stores, bbfmm.h:1081-1099): one
+        // read of E(t, s) serves both ends -- this leaf's rows as above, and the
+        // partner's point s, whose product sums the leaf's rows (in-lane, then over the
+        // row quads by DPP: every lane of an active leaf takes part, padded rows read 0)
+        // and goes to the pair's LDS slot or to the partner's partial slot (colDst).
+        // The reversed direction has cos = -c: (-1)^b on the leaf's charges, (-1)^i on
+        // the product (as hm_entry2 in the cluster M2L).  UC columns in flight per lane.
+        constexpr int UC = 2;
+        double xa[4][K];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = 4 * rq + j;
+            const double* row = tab + (size_t)(n.selfRow[li] + min(t, max(nT - 1, 0))) * RW + 2;
+#pragma unroll
+            for (int b = 0; b < K; ++b) xa[j][b] = t < nT ? ((b & 1) ? -hw.hw[b] : hw.hw[b]) * row[b] : 0.0;
+        }
+        const dbl2* kc = reinterpret_cast<const dbl2*>(E + koff) + 2 * rq;
+        const int S1 = n.nearSym[li].y;
+        const int* __restrict__ dst = n.colDst + pb;
+        for (int c0 = S + cph; c0 < S1; c0 += UC * 4) {
+            dbl2 kk[UC][2];
+            int ix[UC], dd[UC];
+#pragma unroll
+            for (int u = 0; u < UC; ++u) {
+                const int sc = min(c0 + u * 4, S1 - 1);
+                const bool ok = c0 + u * 4 < S1 && rq < nq;
+                const dbl2* p = kc + (size_t)sc * cstr;
+                kk[u][0] = ok ? __builtin_nontemporal_load(p) : dbl2{0.0, 0.0};
+                kk[u][1] = ok ? __builtin_nontemporal_load(p + 1) : dbl2{0.0, 0.0};
+                ix[u] = nearLoc[pb + sc];
+                dd[u] = dst[sc];
+            }
+#pragma unroll
+            for (int u = 0; u < UC; ++u) {
+                if (c0 + u * 4 >= S1) break;  // uniform over the quad (one column phase)
+                const double* row = tab + (size_t)ix[u] * RW;
+                const double sx = row[0], sy = row[1];
+                double xw[K], ob[K];
+#pragma unroll
+                for (int b = 0; b < K; ++b) {
+                    xw[b] = hw.hw[b] * row[2 + b];
+                    ob[b] = 0.0;
+                }
+                const double e4[4] = {kk[u][0].x, kk[u][0].y, kk[u][1].x, kk[u][1].y};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const double dy = sy - ty[j];
+                    hm_entry2<K, NR>(e4[j], sx - tx[j], dy * dy, xw, xa[j], a[j], ob);
+                }
+#pragma unroll
+                for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // the leaf's rows: over the row quads
+                // lane rq of the quad stores products i = rq (and rq + 4)
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    if ((i & 3) != rq) continue;
+                    const double v = (i & 1) ? -ob[i] : ob[i];
+#ifdef ANISO_NEAR_SYM_ATOMIC
+                    if (dd[u] < 0) atomicAdd(dslot + (size_t)(~dd[u]) * K + i, v);
+#else
+                    if (dd[u] < 0) dslot[(size_t)(~dd[u]) * K + i] = v;
+#endif
+                    else n.nearPart[(size_t)dd[u] * K + i] = hw.om[i] * v;
+                }
+            }
+        }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)  // sum over the column phases
 #pragma unroll
@@ -1171,11 +1249,29 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
             v += dpp_f64<0x128>(v);  // row_ror:8
             a[j][i] = v;
         }
+    if (sym) __syncthreads();  // every partner product of the group is in LDS
     if (rowOk) {  // lane (rq, cph) finishes row 4 rq + cph: one pass with every lane active
         const int t = 4 * rq + cph;
         double av[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) av[i] = cph == 0 ? a[0][i] : cph == 1 ? a[1][i] : cph == 2 ? a[2][i] : a[3][i];
+#ifdef ANISO_NEAR_SYM_ATOMIC
+        if (sym && t < nT) {
+            const double* d = dslot + ((size_t)(li & 15) * 16 + t) * K;
+#pragma unroll
+            for (int i = 0; i < K; ++i) av[i] += d[i];
+        }
+        if (false) {
+#else
+        if (sym && t < nT) {  // the products this group's smaller-id partners left for the row, in slot order
+#endif
+            const int q1 = n.grpInPtr[li + 1];
+            for (int q = n.grpInPtr[li]; q < q1; ++q) {
+                const double* d = dslot + ((size_t)n.grpIn[q] * 16 + t) * K;
+#pragma unroll
+                for (int i = 0; i < K; ++i) av[i] += d[i];
+            }
+        }
         if (t < nT) {
             const int64_t k = tb + t;
             double f[K];
@@ -1208,11 +1304,21 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
     }
 }
 
+// the staged near field's LDS: the source table, and with symmetric U storage the
+// group's partner product slots (16 rows x K each)
+template <int K>
+static size_t near_hs_lds(const NearHsArgs& n) {
+    return (size_t)n.nsMax * kTabRow<K> * sizeof(double) + (n.colDst ? (size_t)n.grpSlots * 16 * K * sizeof(double) : 0);
+}
+
 // W4: capped at 128 VGPRs (4 waves per SIMD; ANISO_NEAR_WPE=4)
-template <int K, int U, int NR, bool FUSE, bool W4 = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W4 ? 4 : 1))) k_near_hs(NearHsArgs n) {
+#ifndef ANISO_NEAR_SYM_WPE
+#define ANISO_NEAR_SYM_WPE 1
+#endif
+template <int K, int U, int NR, bool FUSE, bool W4 = false, bool SYM = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W4 ? 4 : SYM ? ANISO_NEAR_SYM_WPE : 1))) k_near_hs(NearHsArgs n) {
     extern __shared__ double tab[];
-    near_hs_group<K, U, NR, FUSE>((int)blockIdx.x, n, tab);
+    near_hs_group<K, U, NR, FUSE, SYM>((int)blockIdx.x, n, tab);
 }
 
 
@@ -1359,6 +1465,8 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
     const int depth = a.geo && K <= kRingMaxK ? a.ring : 0;
     if (near && (depth != 0 || near->nl <= 0))
         throw std::invalid_argument("fused top-of-tree launch: the near field rides only with the one-block M2L");
+    if (near && near->colDst)
+        throw std::invalid_argument("fused top-of-tree launch: the near field rides only with directed U storage");
     const bool xl = a.ringXL;
     TopArgs t = t0;
     t.nCl = ncl;
@@ -1366,7 +1474,7 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
     const unsigned nb = (unsigned)(t.nUp + ncl) + (near ? (unsigned)((near->nl + 15) / 16) : 0u);
     ANISO_HM_DISPATCH_K(K, ANISO_HM_DISPATCH_RING(depth, ({
         size_t shm = std::max(m2l_hc_lds(KK, maxCl, depth, xl, 4), up_tier_lds(u.maxTask, KK));
-        if (near) shm = std::max(shm, (size_t)near->nsMax * kTabRow<KK> * sizeof(double));
+        if (near) shm = std::max(shm, near_hs_lds<KK>(*near));
         const int form = DD == 0 && !near ? hm_form(KK, a.wpe, shm) : 3;
         if (form != 3) shm = std::max(shm, m2l_hc_lds(KK, maxCl, depth, xl, hm_waves(form)));
         if (shm > 160 * 1024) throw std::invalid_argument("fused top-of-tree launch: a cluster and its halo exceed the LDS");
@@ -1425,10 +1533,22 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
             n.sigT = in->sigT;
             n.wT = in->wT;
         }
+        if (in && in->colDst) {  // symmetric U storage (the column lists passed are its own)
+            if (!in->nearSym || !in->selfRow || !in->nearPart || !in->grpInPtr)  // grpIn: may be empty
+                throw std::invalid_argument("symmetric staged near field: missing lists");
+            n.nearSym = in->nearSym;
+            n.colDst = in->colDst;
+            n.selfRow = in->selfRow;
+            n.nearPart = in->nearPart;
+            n.grpInPtr = in->grpInPtr;
+            n.grpIn = in->grpIn;
+            n.grpSlots = in->grpSlots;
+        }
         ANISO_HM_DISPATCH_K(K, ({
-            const size_t shm = (size_t)nsMax * kTabRow<KK> * sizeof(double);
-            auto f = fuse ? (wpe == 4 ? k_near_hs<KK, 4, 2, true, true> : k_near_hs<KK, 4, 2, true>)
-                          : (wpe == 4 ? k_near_hs<KK, 4, 2, false, true> : k_near_hs<KK, 4, 2, false>);
+            const size_t shm = near_hs_lds<KK>(n);
+            auto f = n.colDst ? (fuse ? k_near_hs<KK, 4, 2, true, false, true> : k_near_hs<KK, 4, 2, false, false, true>)
+                     : fuse ? (wpe == 4 ? k_near_hs<KK, 4, 2, true, true> : k_near_hs<KK, 4, 2, true>)
+                            : (wpe == 4 ? k_near_hs<KK, 4, 2, false, true> : k_near_hs<KK, 4, 2, false>);
             f<<<ng, 256, shm, s>>>(n);
         }));
         HIP_LAUNCH_CHECK();
@@ -1438,6 +1558,7 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
     ANISO_HM_DISPATCH_K(K, (k_near_hm<KK, G, 4, 2><<<blocks_for((int64_t)nl * G, 256), 256, 0, s>>>(           \
                                nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm, \
                                obase, ldo, flags, scale, out)))
+    if (in && in->colDst) throw std::invalid_argument("symmetric near storage needs the staged near field");
     if (maxLeaf <= 16) {
         ANISO_NEAR_HM(16);
     } else {

@@ -5,6 +5,7 @@
 // (aniso_cache) and uploaded to HBM; the per-apply work is all on the GPU.
 #pragma once
 
+#include <algorithm>
 #include <array>
 #include <cstdint>
 #include <string>
@@ -100,6 +101,36 @@ struct Plan {
     // (0xFFFF outside the grid), so k_near_hs applies the corrections from its table
     std::vector<uint16_t> nearCorrRow;
     bool nearCorrOk = false;
+    // input: the staged near field of block handles with symmetric U storage (DESIGN.md
+    // §3.11): a U pair of two owned leaves <= 16 points is stored once, by its smaller
+    // id, whose lanes apply it both ways from one read.  The partner's product goes to
+    // LDS when the partner is in the same 16-leaf group, else to a partial slot the
+    // down pass adds (nearInPtr / nearInOff).  Per leaf: hsSym = (directed columns,
+    // all columns: the canonical ones, partner by partner, follow the directed ones),
+    // per column hsDst = where its partner product goes (>= 0 the partial slot of that
+    // point, < 0 ~(its LDS row: group slot x 16 + point); 0 for directed columns), and
+    // nearSelfRow = the table row of the leaf's first point.  Built only when every
+    // owned leaf fits the staged kernel (nearSymHsOn), else the harmonic near field
+    // reads the directed lists.
+    bool nearSymHs = false;
+    bool nearSymHsOn = false;
+    std::vector<int> hsDst;
+    std::vector<uint16_t> nearSelfRow;
+    // its column lists (beside the directed nearPtsPtr / nearLoc / nearKOff, which the
+    // per-mode kernels keep): table rows per column, E offsets, (directed, all)
+    // columns per leaf, source nodes per leaf (the att cache build), partial slots
+    std::vector<int64_t> hsPtsPtr, hsKOff, hsSrcPtr;
+    std::vector<uint16_t> hsLoc;
+    std::vector<std::array<int, 2>> hsSym;
+    std::vector<int> hsSrc;
+    int64_t hsKTotal = 0, hsPartTotal = 0, hsStored = 0;
+    // the partner products within a 16-leaf group go to LDS slots (16 rows x K each,
+    // one per in-group canonical block, <= kNearGrpSlots per group; the rest to
+    // partials): per leaf the slots it receives (CSR, ascending), summed in that
+    // fixed order -- no atomics, so the apply stays deterministic
+    static constexpr int kNearGrpSlots = 48;
+    std::vector<int> nearGrpInPtr, nearGrpIn;
+    int nearGrpSlots = 0;
     int64_t nearKTotal = 0;
     std::vector<int> m2lTgt;                   // active target nodes with M2L work
     std::vector<int64_t> m2lPtr;               // CSR over m2lTgt -> source nodes
@@ -153,6 +184,14 @@ struct Plan {
     std::vector<int> upTierTask, upTaskPtr, upGrpPtr, upGrp, upNode;
     std::vector<std::array<int, 4>> upCode;
     int upMaxTask = 1;
+    // per tier: its largest task (a launch sizes its LDS for its own tiers only: the
+    // fused top-of-tree launch runs tiers >= 1, 21-node tasks instead of tier 0's 85)
+    std::vector<int> upTierMaxTask;
+    int upMaxTaskFrom(int k0) const {
+        int m = 1;
+        for (size_t k = (size_t)k0; k < upTierMaxTask.size(); ++k) m = std::max(m, upTierMaxTask[k]);
+        return m;
+    }
     int upLastLeafTier = 0;  // last up tier with a P2M leaf: fT / cT are complete after it
     // the same, as records the kernel loads in one round: per task (first node,
     // nodes, first point, levels) + kTaskLevels+1 level starts; per node the box
@@ -207,6 +246,7 @@ struct Plan {
     void buildUpTasks(const Tree& t);
     void buildClusters(const Tree& t);
     void buildDownTasks(const Tree& t);
+    void buildNearHs(const Tree& t, const std::vector<int>& leafIdx);
 };
 
 std::vector<int64_t> shard_cuts(const Tree& t, int nranks);

@@ -249,10 +249,11 @@ std::vector<int64_t> shard_cuts(const Tree& t, int nranks) {
 void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     (void)np;
     if (nranks_ < 1 || rank_ < 0 || rank_ >= nranks_) throw std::invalid_argument("bad shard rank/nranks");
-    const bool symNear = nearSymmetric;
+    const bool symNear = nearSymmetric, symHs = nearSymHs;
     const int capCanon = maxCanon;
     *this = Plan();
     nearSymmetric = symNear;
+    nearSymHs = symHs;
     maxCanon = std::max(0, std::min(kMaxCanon, capCanon));
     rank = rank_;
     nranks = nranks_;
@@ -461,12 +462,124 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
             }
             for (int64_t j = nearPtsPtr[g0]; j < nearPtsPtr[g1]; ++j)
                 nearLoc[j] = (uint16_t)(std::lower_bound(u.begin(), u.end(), nearPts[j]) - u.begin());
+
             nsPts.insert(nsPts.end(), u.begin(), u.end());
             nsPtr.push_back((int64_t)nsPts.size());
             nsMax = std::max<int>(nsMax, (int)u.size());
         }
     }
+    buildNearHs(t, leafIdx);
     buildDownTasks(t);
+}
+
+// The staged near field of the harmonic block apply with symmetric U storage (see
+// Plan::nearSymHs; bbfmm.h:1081-1099): its own column lists beside the directed ones
+// (which the per-mode kernels keep), over the same source tables.  Per leaf the columns
+// are [directed: itself, W, U members not both owned here | canonical: owned U members
+// with a larger id], the canonical ones in one block per partner leaf.
+void Plan::buildNearHs(const Tree& t, const std::vector<int>& leafIdx) {
+    hsPtsPtr.assign(1, 0);
+    hsLoc.clear();
+    hsKOff.clear();
+    hsSym.clear();
+    hsSrcPtr.assign(1, 0);
+    hsSrc.clear();
+    hsDst.clear();
+    nearSelfRow.clear();
+    hsKTotal = 0;
+    hsPartTotal = 0;
+    hsStored = 0;
+    nearGrpInPtr.assign(1, 0);
+    nearGrpIn.clear();
+    nearGrpSlots = 0;
+    nearSymHsOn = nearSymHs && !nearSymmetric && nearMaxLeaf <= 16 && !leaves.empty() &&
+                  nsPtr.size() == (leaves.size() + 15) / 16 + 1 &&
+                  (size_t)nsMax * 11 * 8 <= 64 * 1024;  // near_hs_staged's test (K <= 8)
+    if (!nearSymHsOn) return;
+    std::vector<std::vector<int>> inRef(leaves.size()), grpIn(16);
+    std::vector<int> u, dir, can;
+    for (size_t g0 = 0; g0 < leaves.size(); g0 += 16) {
+        const size_t g1 = std::min(leaves.size(), g0 + 16);
+        int q = 0;  // the group's LDS slots: one per in-group canonical block, in (leaf, partner) order
+        for (auto& v : grpIn) v.clear();
+        u.assign(nsPts.begin() + nsPtr[g0 / 16], nsPts.begin() + nsPtr[g0 / 16 + 1]);  // sorted unique
+        auto row = [&](int64_t pos) {
+            auto it = std::lower_bound(u.begin(), u.end(), (int)pos);
+            if (it == u.end() || *it != (int)pos) throw std::logic_error("staged near field: source not in its table");
+            return (uint16_t)(it - u.begin());
+        };
+        for (size_t li = g0; li < g1; ++li) {
+            const int i = leaves[li];
+            dir.clear();
+            can.clear();
+            for (int64_t k = t.uPtr[i]; k < t.uPtr[i + 1]; ++k) {
+                const int b = t.uIdx[k];
+                if (t.isEmpty[b]) continue;
+                if (b != i && leafIdx[b] >= 0) {  // both leaves owned: stored once, by the smaller id
+                    if (i < b) can.push_back(b);
+                    continue;
+                }
+                dir.push_back(b);
+            }
+            for (int64_t k = t.wPtr[i]; k < t.wPtr[i + 1]; ++k)
+                if (!t.isEmpty[t.wIdx[k]]) dir.push_back(t.wIdx[k]);
+            hsKOff.push_back(hsKTotal);
+            int S = 0;
+            for (int b : dir) {
+                hsSrc.push_back(b);
+                for (int64_t u0 = 0; u0 < t.count[b]; ++u0) {
+                    hsLoc.push_back(row(t.begin[b] + u0));
+                    hsDst.push_back(0);  // directed: no partner product
+                }
+                S += (int)t.count[b];
+            }
+            const int Sdir = S;
+            for (int b : can) {
+                const int lb = leafIdx[b];
+                if (lb / 16 == (int)li / 16 && q < kNearGrpSlots) {
+                    grpIn[lb % 16].push_back(q);  // the partner is in this group: an LDS slot
+#ifdef ANISO_NEAR_SYM_ATOMIC  // A/B builds only: the partner's own LDS rows, added atomically
+                    for (int64_t u0 = 0; u0 < t.count[b]; ++u0) hsDst.push_back(~(int)((lb % 16) * 16 + u0));
+#else
+                    for (int64_t u0 = 0; u0 < t.count[b]; ++u0) hsDst.push_back(~(int)(q * 16 + u0));
+#endif
+                    ++q;
+                } else {
+                    inRef[lb].push_back((int)hsPartTotal);  // else its partial slots, sender-contiguous
+                    for (int64_t u0 = 0; u0 < t.count[b]; ++u0) hsDst.push_back((int)(hsPartTotal + u0));
+                    hsPartTotal += t.count[b];
+                }
+                hsSrc.push_back(b);
+                for (int64_t u0 = 0; u0 < t.count[b]; ++u0) hsLoc.push_back(row(t.begin[b] + u0));
+                S += (int)t.count[b];
+            }
+            hsSym.push_back({Sdir, S});
+            hsKTotal += (int64_t)S * ((t.count[i] + 3) & ~(int64_t)3);
+            hsStored += (int64_t)S * t.count[i];
+            hsPtsPtr.push_back((int64_t)hsLoc.size());
+            hsSrcPtr.push_back((int64_t)hsSrc.size());
+            nearSelfRow.push_back(row(t.begin[i]));  // the leaf's own points: one run of table rows
+        }
+        // per leaf its incoming slots, ascending (= by sender): summed in that order
+        for (size_t li = g0; li < g1; ++li) {
+            const auto& v = grpIn[li - g0];
+            nearGrpIn.insert(nearGrpIn.end(), v.begin(), v.end());
+            nearGrpInPtr.push_back((int)nearGrpIn.size());
+        }
+        nearGrpSlots = std::max(nearGrpSlots, q);
+#ifdef ANISO_NEAR_SYM_ATOMIC
+        nearGrpSlots = 16;
+#endif
+    }
+    if (hsPartTotal > ((int64_t)1 << 31) - 1) throw std::invalid_argument("near partials overflow");
+    // the down pass gathers the partials through the same per-leaf lists as the
+    // single-RHS symmetric near field (a block handle has none of those)
+    nearInPtr.assign(1, 0);
+    nearInOff.clear();
+    for (auto& v : inRef) {
+        nearInOff.insert(nearInOff.end(), v.begin(), v.end());
+        nearInPtr.push_back((int)nearInOff.size());
+    }
 }
 
 
@@ -504,6 +617,7 @@ void Plan::buildUpTasks(const Tree& t) {
     upGeom.clear();
     upLeaf.clear();
     upMaxTask = 1;
+    upTierMaxTask.assign(tierRootLevel.size(), 1);
     for (size_t k = 0; k < tierRootLevel.size(); ++k) {  // bottom-up
         for (int r = 0; r < t.nn; ++r) {
             if (t.level[r] != tierRootLevel[k] || t.isEmpty[r]) continue;
@@ -546,6 +660,7 @@ void Plan::buildUpTasks(const Tree& t) {
             upTaskPtr.push_back((int)upNode.size());
             upTaskRoot.push_back(r);
             upMaxTask = std::max(upMaxTask, (int)upNode.size() - base);
+            upTierMaxTask[k] = std::max(upTierMaxTask[k], (int)upNode.size() - base);
         }
         upTierTask.push_back((int)upTaskPtr.size() - 1);
     }

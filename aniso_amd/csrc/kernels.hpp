@@ -285,6 +285,18 @@ struct NearHsArgs {
     const int* perm = nullptr;
     const double* sigT = nullptr;
     const double* wT = nullptr;
+    // symmetric U storage (Plan::nearSymHsOn; colDst == nullptr: every column
+    // directed): per leaf (directed columns, all columns), per column where its
+    // partner product goes, the leaf's first table row; partials of other groups
+    const int2* nearSym = nullptr;
+    const int* colDst = nullptr;
+    const uint16_t* selfRow = nullptr;
+    double* nearPart = nullptr;
+    // the in-group partner products' LDS slots (Plan::nearGrpIn): per leaf the slots
+    // it receives, and the most slots of a group (the launch's LDS)
+    const int* grpInPtr = nullptr;
+    const int* grpIn = nullptr;
+    int grpSlots = 0;
 };
 bool top_fused_enabled();
 // near: the staged near field with its corrections fused (near_hs_fusable) as the

@@ -37,7 +37,7 @@ int aniso_tree_size(aniso_handle h, int *nnodes, int *max_level);
 int aniso_tree_nodes(aniso_handle h, int *ints, double *geom);
 /* which: 0=U 1=V 2=W 3=X.  ptr has nnodes+1 entries; idx (may be NULL) ptr[nnodes] */
 int aniso_tree_list(aniso_handle h, int which, int64_t *ptr, int *idx);
-/* stats[0..22]: near entries, M2L entries, M2L pairs, leaves (owned), targets with
+/* stats[0..24]: near entries, M2L entries, M2L pairs, leaves (owned), targets with
  * M2L work, tree nodes, max leaf size, N, then the symmetric storage actually
  * streamed per apply: stored near entries, stored M2L blocks, canonical M2L
  * pairs (partial slots), near partial entries; then 1 if the block operator runs
@@ -51,8 +51,10 @@ int aniso_tree_list(aniso_handle h, int which, int64_t *ptr, int *idx);
  * products, one read per stored block), the largest cluster + halo (LDS slots) and
  * the E blocks the clusters read per apply; then the applies re-run on the tier
  * launches after a hand-off time-out of the fused launch (the host-pointer block
- * operator and the block solve recover; device-pointer entries report it).
- * stats must hold 23 entries. */
+ * operator and the block solve recover; device-pointer entries report it); then
+ * the harmonic near field's symmetric U storage: its stored E entries and partner
+ * partial entries (both 0 when it reads every near block directed).
+ * stats must hold 25 entries. */
 int aniso_stats(aniso_handle h, int64_t *stats);
 /* per-stage device times (ms), averaged over every apply since aniso_set_timing(h, 1)
  * (HIP events recorded in-stream, 8 floats): exchange (between the two phases of a

@@ -727,7 +727,9 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
 @pytest.mark.parametrize("knob", ["ANISO_OVERLAP=0", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0", "ANISO_HM_RING=3",
                                   "ANISO_HM_WPE=3", "ANISO_HM_WPE=4", "ANISO_HM_WPE=6", "ANISO_HM_WPE=8",
                                   "ANISO_NEAR_IN_TOP=1", "ANISO_NEAR_WPE=4", "ANISO_TOP_FUSED=0", "ANISO_HM_HALO=0",
-                                  "ANISO_NEAR_EARLY=0", "ANISO_NEAR_EARLY=0,ANISO_OVERLAP=0"])
+                                  "ANISO_NEAR_EARLY=0", "ANISO_NEAR_EARLY=0,ANISO_OVERLAP=0", "ANISO_NEAR_HS_SYM=1",
+                                  "ANISO_NEAR_HS_SYM=1,ANISO_NEAR_EARLY=0", "ANISO_NEAR_HS_SYM=1,ANISO_OVERLAP=0",
+                                  "ANISO_NEAR_HS_SYM=1,ANISO_TOP_FUSED=0"])
 def test_block_matvec_knobs_agree(knob, monkeypatch):
     """Every remaining environment knob of the block apply:
     the serial near/M2L order, the separate x - mforward(x) subtraction and the
@@ -803,17 +805,23 @@ def _two_phase_shards(sz, d, ks, ml, coef, world, X, ref, g=0.8, ns=10):
     return float(torch.linalg.norm(got - ref) / torch.linalg.norm(ref)), nans, halo / X.shape[1]
 
 
-@pytest.mark.parametrize("sz,d,ks,ml,coeffs,world", [
-    (64, 1, 5, 20, "main", 2), (64, 1, 5, 20, "rough", 8), (48, 2, 3, 20, "rough", 3), (30, 3, 1, 20, "main", 4),
-    (40, 1, 2, 3, "rough", 3), (16, 1, 5, 20, "main", 3), (11, 3, 1, 20, "rough", 2), (1, 3, 1, 20, "main", 2)])
-def test_two_phase_sharded_apply_reads_only_own_and_halo(sz, d, ks, ml, coeffs, world):
+@pytest.mark.parametrize("sz,d,ks,ml,coeffs,world,sym", [
+    (64, 1, 5, 20, "main", 2, 0), (64, 1, 5, 20, "rough", 8, 0), (48, 2, 3, 20, "rough", 3, 0),
+    (30, 3, 1, 20, "main", 4, 0), (40, 1, 2, 3, "rough", 3, 0), (16, 1, 5, 20, "main", 3, 0),
+    (11, 3, 1, 20, "rough", 2, 0), (1, 3, 1, 20, "main", 2, 0), (64, 1, 5, 20, "rough", 3, 1),
+    (48, 2, 3, 20, "rough", 2, 1)])
+def test_two_phase_sharded_apply_reads_only_own_and_halo(sz, d, ks, ml, coeffs, world, sym, monkeypatch):
     """The multi-GPU apply (own + halo up pass, tier-0 root all-gather, owned slice
     out) on NaN-poisoned inputs equals the unsharded tree-order operator: the
     exchange plan covers everything each rank's kernels read (uniform, odd-sized,
     maxLevel-limited and single-leaf trees; 1, 2, 3 (padded to 4) and 5 right-hand
-    sides; even and odd world sizes)."""
+    sides; even and odd world sizes; sym: the near field's symmetric U storage,
+    whose pairs with a ghost leaf stay directed)."""
     torch = _torch()
     import aniso_amd
+
+    if sym:
+        monkeypatch.setenv("ANISO_NEAR_HS_SYM", "1")
 
     full = aniso_amd.Aniso(sz, d, ks, 0.8, 10, 4, ml)
     xy = full.getNodes()

@@ -143,3 +143,37 @@ def test_block_mixes_follow_aniso_m(nb, g):
                 w = (g ** b - g ** nb) / (1 - g ** nb) if chi else 1.0
                 ref[abs(i - j), iid, b] += w
         assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("env", ["1", "", "0"])
+def test_block_near_symmetric_u_storage_plan(monkeypatch, env):
+    """ANISO_NEAR_HS_SYM=1: block handles store a U pair of two owned leaves once
+    (Plan::buildNearHs, the symmetric storage of bbfmm.h:1081-1099 applied to the
+    harmonic near field): the stored E entries are the directed ones minus one
+    direction of every such pair.  Off by default."""
+    if env:
+        monkeypatch.setenv("ANISO_NEAR_HS_SYM", env)
+    a = aniso_amd.Aniso(64, 1, 5, 0.8, 8, 4, 20)
+    s = a.stats()
+    if env != "1":
+        assert s["near_hs_stored"] == 0 and s["near_hs_partials"] == 0
+        return
+    ints, _ = a.tree_nodes()
+    ptr, idx = a.tree_list(0)
+    leaf = (ints[:, 7] == 1) & (ints[:, 8] == 0)
+    cnt = ints[:, 9].astype(np.int64)
+    skipped = 0
+    for i in np.nonzero(leaf)[0]:
+        for b in idx[ptr[i]:ptr[i + 1]]:
+            if b > i and leaf[b]:
+                skipped += cnt[i] * cnt[b]
+    assert skipped > 0
+    assert s["near_hs_stored"] == s["stored_near"] - skipped
+    assert 0 < s["near_hs_partials"] < skipped
+    # a shard keeps the pairs with a ghost leaf directed: every rank stores at least
+    # its share, and the shards together store the directed entries of the cut pairs
+    tot = 0
+    for r in range(2):
+        a.set_shard(r, 2)
+        tot += a.stats()["near_hs_stored"]
+    assert s["near_hs_stored"] < tot < s["stored_near"]

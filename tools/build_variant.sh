@@ -11,5 +11,5 @@ mkdir -p $D $ROOT/build/include
 cp $ROOT/include/*.h $ROOT/build/include/
 rm -rf $D/csrc && cp -r $ROOT/aniso_amd/csrc $D/csrc
 rm -f $D/csrc/*.o
-make -s -C $D/csrc -j8 HIPFLAGS="--offload-arch=gfx950 -munsafe-fp-atomics $DEFS" 2>&1 | grep -v "warning\|note:\|^ *[0-9]* |\|^ *|\|generated" || true
+make -s -C $D/csrc -j8 HIPFLAGS="--offload-arch=gfx950 -munsafe-fp-atomics $DEFS" CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -Wno-unused-result $DEFS" 2>&1 | grep -v "warning\|note:\|^ *[0-9]* |\|^ *|\|generated" || true
 ls -la $D/libaniso_mi355x.so
