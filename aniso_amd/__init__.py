@@ -104,6 +104,8 @@ def lib():
             "aniso_forward_f32_stages_dev": [P, P, I, P, P],
             "aniso_set_deterministic": [P, I],
             "aniso_shard_exchange": [P, I, lp],
+            "aniso_shard_exchange_one": [P, lp],
+            "aniso_shard_one_halo": [P, lp],
             "aniso_shard_halo": [P, lp],
             "aniso_shard_roots": [P, ip, ip, ip],
             "aniso_forward_tree_begin_dev": [P, P, P, P, P],
@@ -572,6 +574,20 @@ class Aniso:
                 "t0_tasks", "nranks"]
         return dict(zip(keys, (int(v) for v in info)))
 
+    def shard_exchange_one(self):
+        """The one-collective exchange of this shard (aniso_shard_exchange_one), host only."""
+        info = np.zeros(5, dtype=np.int64)
+        _check(lib().aniso_shard_exchange_one(self.address, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        keys = ["ok", "own_t0_tasks", "need_nodes", "halo_ranges", "halo_points"]
+        return dict(zip(keys, (int(v) for v in info)))
+
+    def shard_one_halo(self):
+        """(n, 2) ranges of the input the one-collective exchange fills outside the own range."""
+        n = self.shard_exchange_one()["halo_ranges"]
+        r = np.zeros(2 * n + 1, dtype=np.int64)
+        _check(lib().aniso_shard_one_halo(self.address, r.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        return r[:2 * n].reshape(n, 2)
+
     def shard_halo(self):
         """(n, 2) array of [b, e) tree-position ranges outside the own range the input must hold."""
         n = self.shard_exchange()["halo_ranges"]
@@ -617,13 +633,13 @@ class Aniso:
         return ptr, idx
 
     def stats(self):
-        s = np.zeros(25, dtype=np.int64)
+        s = np.zeros(26, dtype=np.int64)
         _check(lib().aniso_stats(self.address, s.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
         keys = ["near_entries", "m2l_entries", "m2l_pairs", "leaves", "m2l_targets", "tree_nodes", "max_leaf", "N",
                 "stored_near", "stored_m2l", "m2l_canon", "near_partial", "harmonic", "att_m2l_blocks",
                 "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "top_fused",
                 "plan_halo_slots", "plan_max_lds_slots", "plan_block_reads", "top_recoveries",
-                "near_hs_stored", "near_hs_partials"]
+                "near_hs_stored", "near_hs_partials", "one_exchange_applies"]
         return dict(zip(keys, (int(v) for v in s)))
 
     def sync(self):

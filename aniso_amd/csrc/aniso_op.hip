@@ -90,6 +90,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_TOP_TRACE")) topTraceOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_IN_TOP")) nearInTop = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_EARLY")) nearEarly = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ANISO_ONE_EXCHANGE")) oneXOn = std::atoi(e) != 0;
     hmRing = hm_ring_depth();
     if (const char* e = std::getenv("ANISO_HM_WPE")) hmWpe = std::atoi(e);
     if (const char* e = std::getenv("ANISO_NEAR_WPE")) nearWpe = std::atoi(e);
@@ -129,6 +130,7 @@ void Operator::setShard(int rank, int nranks) {
     if (comm) {  // a communicator belongs to one shard layout; drain its collectives first
         if (device >= 0) HIP_CHECK(hipDeviceSynchronize());
         comm.reset();
+        oxReady = false;
     }
     plan.build(tree, np, rank, nranks);
     plan.buildExchange(tree, geo.sz, geo.d2);
@@ -152,7 +154,8 @@ void Operator::ensureDevice() {
     }
     HIP_CHECK(hipGetDevice(&device));
     HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
-    // side stream at normal priority (a high-priority one measured slower, r01f)
+    // side stream at normal priority (a high-priority one measured slower, r01f; the
+    // lowest priority 11-25 % slower, r04l)
     HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&evFork, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
@@ -351,6 +354,7 @@ void Operator::uploadPlan() {
     up(dNearPtsPtr, plan.nearPtsPtr);
     up(dNearPts, plan.nearPts);
     up(dXT0Tasks, plan.xT0Tasks);
+    up(dXOwnT0Tasks, plan.xOwnT0Tasks);
     up(dXRootRecv, plan.xRootRecv);
     up(dNsPtr, plan.nsPtr);
     up(dNsPts, plan.nsPts);
@@ -803,6 +807,11 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     const bool nearIn = harmonic && nearEarly && !nearFused && plan.nearCorrOk && (mask & kStageNear) &&
                         near_hs_fusable((int)plan.leaves.size(), plan.nearMaxLeaf, plan.nsMax,
                                         dNearLoc.as<uint16_t>(), &nc, mask);
+    // the one-collective exchange (blockOpShardedDev): phase 1 runs the own tier-0
+    // tasks only and leaves the near field to phase 2, after the exchange
+    const bool oneX = oneXActive && phase != 0;
+    if (oneX && !(harmonic && nearIn))
+        throw std::logic_error("one-collective exchange: the apply is not the harmonic one with its near field from the input");
     double* const fTw = nearIn ? nullptr : dFT.as<double>();
     double* const cTw = nearIn ? nullptr : dCT.as<double>();
     // the near field forks after the whole up pass on one GPU: forked after the
@@ -914,7 +923,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         // up pass: tiers bottom-up; its P2M also forms the weighted charges fT (tree
         // order) the near field and the corrections read
         e0 = tm ? mark(s) : -1;
-        if (nearIn) {  // the near field first: beside the up pass (fork) or before it (serial)
+        if (nearIn && !oneX) {  // the near field first: beside the up pass (fork) or before it (serial)
             if (fork) HIP_CHECK(hipEventRecord(evFork, s));
             nearStage();
             nearDone = true;
@@ -925,13 +934,15 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                            dFT.as<double>(), dCT.as<double>(), s);
             if (fork) HIP_CHECK(hipEventRecord(evFork, s));
         }
-        if (phase == 1 && ntier >= 1)
-            upTier(0, dXT0Tasks.as<int>(), (int)plan.xT0Tasks.size(), nullptr, rootsSend);
+        if (phase == 1 && ntier >= 1) {
+            if (oneX) upTier(0, dXOwnT0Tasks.as<int>(), (int)plan.xOwnT0Tasks.size(), nullptr, rootsSend);
+            else upTier(0, dXT0Tasks.as<int>(), (int)plan.xT0Tasks.size(), nullptr, rootsSend);
+        }
         for (int k = 0; k < (topFused ? 1 : ntier) && phase == 0; ++k) upTier(k, nullptr, tierTasks(k), nullptr, nullptr);
         if (phase == 1) {
             const int ep = tm ? mark(s) : -1;
             span(1, e0, ep);
-            if ((ntier < 1 || forkTier == 0) && !nearFused && !nearDone) {
+            if ((ntier < 1 || forkTier == 0) && !nearFused && !nearDone && !oneX) {
                 nearStage();
                 nearDone = true;
             }
@@ -948,6 +959,11 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         pend.active = false;
         const int ex = tm ? mark(s) : -1;
         span(0, pend.ePack, ex);  // the caller's root exchange
+        if (oneX && !nearDone) {  // the near field after the one exchange (it filled the input's halo)
+            if (fork) HIP_CHECK(hipEventRecord(evFork, s));
+            nearStage();
+            nearDone = true;
+        }
         if (topFused) {  // the upper tiers run inside the M2L launch below
         } else if (ntier >= 2) {  // the first upper tier reads the gathered roots (and stores them for the M2L)
             upTier(1, nullptr, tierTasks(1), rootsRecv, nullptr);
@@ -1505,34 +1521,69 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
     if (comm && device >= 0) HIP_CHECK(hipDeviceSynchronize());  // collectives in flight on the old one
     comm.reset();
     const int P = c->nranks, me = c->rank;
-    const int64_t nr = (int64_t)plan.xHalo.size() / 2;
     DevBuf a, b;
-    a.alloc(sizeof(double));
-    b.alloc((size_t)P * sizeof(double));
-    double v = (double)nr;
-    HIP_CHECK(hipMemcpy(a.p, &v, sizeof(double), hipMemcpyHostToDevice));
-    c->allgather(a.as<double>(), b.as<double>(), 1, own);
-    HIP_CHECK(hipStreamSynchronize(own));
-    std::vector<double> counts(P);
-    HIP_CHECK(hipMemcpy(counts.data(), b.p, (size_t)P * sizeof(double), hipMemcpyDeviceToHost));
-    int64_t mx = 1;
-    for (double x : counts) mx = std::max<int64_t>(mx, (int64_t)x);
-    std::vector<double> mine((size_t)2 * mx, -1.0);
-    for (int64_t i = 0; i < 2 * nr; ++i) mine[i] = (double)plan.xHalo[i];
-    a.alloc((size_t)2 * mx * sizeof(double));
-    b.alloc((size_t)P * 2 * mx * sizeof(double));
-    HIP_CHECK(hipMemcpy(a.p, mine.data(), (size_t)2 * mx * sizeof(double), hipMemcpyHostToDevice));
-    c->allgather(a.as<double>(), b.as<double>(), (size_t)2 * mx, own);
-    HIP_CHECK(hipStreamSynchronize(own));
-    std::vector<double> all((size_t)P * 2 * mx);
-    HIP_CHECK(hipMemcpy(all.data(), b.p, all.size() * sizeof(double), hipMemcpyDeviceToHost));
+    // every rank's lists (one all-gather of the counts, one of the padded lists); a
+    // loopback communicator (development: one rank's schedule on one GPU) has no
+    // peers, so their lists come from their plans built here
+    struct PeerLists {
+        std::vector<double> halo, oneHalo, needNodes, ok;
+    };
+    std::vector<PeerLists> peerLists;
+    if (c->loopback()) {
+        peerLists.resize(P);
+        for (int r = 0; r < P; ++r) {
+            Plan q;  // the same plan inputs (Plan::build keeps these), rank r's shard
+            if (r != me) {
+                q.nearSymmetric = plan.nearSymmetric;
+                q.nearSymHs = plan.nearSymHs;
+                q.maxCanon = plan.maxCanon;
+                q.build(tree, np, r, P);
+                q.buildExchange(tree, geo.sz, geo.d2);
+            }
+            const Plan& src = r == me ? plan : q;
+            peerLists[r].halo.assign(src.xHalo.begin(), src.xHalo.end());
+            peerLists[r].oneHalo.assign(src.xOneHalo.begin(), src.xOneHalo.end());
+            peerLists[r].needNodes.assign(src.xNeedNodes.begin(), src.xNeedNodes.end());
+            peerLists[r].ok.assign(1, src.xOneOk ? 1.0 : 0.0);
+        }
+    }
+    auto gatherList = [&](std::vector<double> PeerLists::*field, const std::vector<double>& mineV,
+                          std::vector<std::vector<double>>& allV) {
+        allV.assign(P, {});
+        if (!peerLists.empty()) {
+            for (int r = 0; r < P; ++r) allV[r] = peerLists[r].*field;
+            return;
+        }
+        double n = (double)mineV.size();
+        a.alloc(sizeof(double));
+        b.alloc((size_t)P * sizeof(double));
+        HIP_CHECK(hipMemcpy(a.p, &n, sizeof(double), hipMemcpyHostToDevice));
+        c->allgather(a.as<double>(), b.as<double>(), 1, own);
+        HIP_CHECK(hipStreamSynchronize(own));
+        std::vector<double> cnt(P);
+        HIP_CHECK(hipMemcpy(cnt.data(), b.p, (size_t)P * sizeof(double), hipMemcpyDeviceToHost));
+        size_t m = 1;
+        for (double x : cnt) m = std::max(m, (size_t)x);
+        std::vector<double> pad(m, -1.0);
+        std::copy(mineV.begin(), mineV.end(), pad.begin());
+        a.alloc(m * sizeof(double));
+        b.alloc((size_t)P * m * sizeof(double));
+        HIP_CHECK(hipMemcpy(a.p, pad.data(), m * sizeof(double), hipMemcpyHostToDevice));
+        c->allgather(a.as<double>(), b.as<double>(), m, own);
+        HIP_CHECK(hipStreamSynchronize(own));
+        std::vector<double> flat((size_t)P * m);
+        HIP_CHECK(hipMemcpy(flat.data(), b.p, flat.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (int r = 0; r < P; ++r)
+            allV[r].assign(flat.begin() + (size_t)r * m, flat.begin() + (size_t)r * m + (size_t)cnt[r]);
+    };
+    std::vector<std::vector<double>> haloAll;
+    gatherList(&PeerLists::halo, std::vector<double>(plan.xHalo.begin(), plan.xHalo.end()), haloAll);
     const auto cuts = shard_cuts(tree, P);
     if (cuts[me] != plan.ownBegin || cuts[me + 1] != plan.ownEnd) throw std::logic_error("shard cuts disagree with the plan");
     const int nb = ks;
     auto ranges = [&](int r) {  // rank r's halo ranges
         std::vector<std::pair<int64_t, int64_t>> v;
-        for (int64_t i = 0; i < (int64_t)counts[r]; ++i)
-            v.push_back({(int64_t)all[((size_t)r * mx + i) * 2], (int64_t)all[((size_t)r * mx + i) * 2 + 1]});
+        for (size_t i = 0; i + 1 < haloAll[r].size(); i += 2) v.push_back({(int64_t)haloAll[r][i], (int64_t)haloAll[r][i + 1]});
         return v;
     };
     auto intersect = [](const std::vector<std::pair<int64_t, int64_t>>& rs, int64_t lo, int64_t hi,
@@ -1580,7 +1631,108 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
     dXRootsSend.alloc((size_t)std::max<int64_t>(rec, 1) * sizeof(double));
     dXRootsRecv.alloc((size_t)std::max<int64_t>(rec * P, 1) * sizeof(double));
     HIP_CHECK(hipMemset(dXRootsSend.p, 0, dXRootsSend.bytes));
+    // ---- the one-collective layout: every rank's needed multipoles (node lists, one
+    // all-gather of the counts and one of the lists) and its input ranges (as above)
+    oxReady = false;
+    std::vector<std::vector<double>> oksAll;
+    gatherList(&PeerLists::ok, std::vector<double>(1, plan.xOneOk ? 1.0 : 0.0), oksAll);
+    bool allOk = true;
+    for (const auto& o : oksAll) allOk = allOk && !o.empty() && o[0] > 0.5;
+    if (allOk) {  // every rank decides alike: all take part in the same collectives
+        std::vector<std::vector<double>> oneAll, nodesAll;
+        gatherList(&PeerLists::oneHalo, std::vector<double>(plan.xOneHalo.begin(), plan.xOneHalo.end()), oneAll);
+        gatherList(&PeerLists::needNodes, std::vector<double>(plan.xNeedNodes.begin(), plan.xNeedNodes.end()), nodesAll);
+        const int RK = kRank * rootRhs(nb);
+        auto ownerOf = [&](int n) {
+            return (int)(std::upper_bound(cuts.begin() + 1, cuts.end() - 1, tree.begin[n]) - (cuts.begin() + 1));
+        };
+        auto pts = [&](int r, int64_t lo, int64_t hi, std::vector<int64_t>& out) {  // rank r's ranges inside [lo, hi)
+            for (size_t i = 0; i + 1 < oneAll[r].size(); i += 2)
+                for (int64_t k = std::max((int64_t)oneAll[r][i], lo); k < std::min((int64_t)oneAll[r][i + 1], hi); ++k)
+                    out.push_back(k);
+        };
+        auto nodes = [&](int r, int owner, std::vector<int>& out) {  // rank r's needed nodes owned by `owner`
+            for (double v : nodesAll[r])
+                if (ownerOf((int)v) == owner) out.push_back((int)v);
+        };
+        std::vector<int64_t> sp_, sb_, ss_, rp_, rb_, rs_, snb, rnb;
+        std::vector<int> sn_, rn_;
+        oxScount.assign(P, 0);
+        oxSoff.assign(P, 0);
+        oxRcount.assign(P, 0);
+        oxRoff.assign(P, 0);
+        int64_t so = 0, ro = 0;
+        for (int p = 0; p < P; ++p) {
+            oxSoff[p] = so;
+            oxRoff[p] = ro;
+            if (p == me) continue;
+            std::vector<int64_t> sp, rp;
+            std::vector<int> sn, rn;
+            pts(p, plan.ownBegin, plan.ownEnd, sp);  // p's positions inside my range
+            pts(me, cuts[p], cuts[p + 1], rp);       // mine inside p's range
+            nodes(p, me, sn);                        // p's nodes in my subtrees
+            nodes(me, p, rn);                        // mine in p's
+            for (size_t i = 0; i < sp.size(); ++i) {
+                sp_.push_back(sp[i]);
+                sb_.push_back(so + (int64_t)i);
+                ss_.push_back((int64_t)sp.size());
+            }
+            for (size_t i = 0; i < rp.size(); ++i) {
+                rp_.push_back(rp[i]);
+                rb_.push_back(ro + (int64_t)i);
+                rs_.push_back((int64_t)rp.size());
+            }
+            const int64_t sn0 = so + (int64_t)sp.size() * nb, rn0 = ro + (int64_t)rp.size() * nb;
+            for (size_t j = 0; j < sn.size(); ++j) {
+                sn_.push_back(sn[j]);
+                snb.push_back(sn0 + (int64_t)j * RK);
+            }
+            for (size_t j = 0; j < rn.size(); ++j) {
+                rn_.push_back(rn[j]);
+                rnb.push_back(rn0 + (int64_t)j * RK);
+            }
+            oxScount[p] = (int64_t)sp.size() * nb + (int64_t)sn.size() * RK;
+            oxRcount[p] = (int64_t)rp.size() * nb + (int64_t)rn.size() * RK;
+            so += oxScount[p];
+            ro += oxRcount[p];
+        }
+        oxNsendPts = (int64_t)sp_.size();
+        oxNrecvPts = (int64_t)rp_.size();
+        oxNsendNodes = (int64_t)sn_.size();
+        oxNrecvNodes = (int64_t)rn_.size();
+        if (oxNrecvNodes != (int64_t)plan.xNeedNodes.size())
+            throw std::logic_error("one-collective exchange: a needed multipole has no owner");
+        up(dOxSendPos, sp_);
+        up(dOxSendBase, sb_);
+        up(dOxSendStride, ss_);
+        up(dOxRecvPos, rp_);
+        up(dOxRecvBase, rb_);
+        up(dOxRecvStride, rs_);
+        up(dOxSendNode, sn_);
+        up(dOxSendNodeBase, snb);
+        up(dOxRecvNode, rn_);
+        up(dOxRecvNodeBase, rnb);
+        dOxSendBuf.alloc((size_t)std::max<int64_t>(so, 1) * sizeof(double));
+        dOxRecvBuf.alloc((size_t)std::max<int64_t>(ro, 1) * sizeof(double));
+        oxReady = true;
+    }
     comm = std::move(c);
+}
+
+// Can this sharded matvec take the one-collective exchange?  Its phase 1 must leave
+// nothing to the halo: the harmonic block apply with the near field formed from the
+// input (run in phase 2, after the exchange) and no padded right-hand sides.
+bool Operator::oneExchangeUsable(int which) {
+    if (!oxReady || !oneXOn || !plan.xOneOk || !rhs_supported(ks) || !nearEarly || !plan.nearCorrOk) return false;
+    const int nm = 2 * ks - 1;
+    const auto mix = blockMixes(ks, g, which != 0);
+    std::vector<int> ids(nm);
+    for (int m = 0; m < nm; ++m) ids[m] = m;
+    HarmWeights hw;
+    if (!harmonicWeights(ks, nm, ids.data(), mix.data(), hw)) return false;
+    const NearCorr probe{dNearCorrRow.as<uint16_t>(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    return near_hs_fusable((int)plan.leaves.size(), plan.nearMaxLeaf, plan.nsMax, dNearLoc.as<uint16_t>(), &probe,
+                           kStageAll);
 }
 
 void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, int64_t ldy, hipStream_t s) {
@@ -1588,6 +1740,36 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
     if (ldx < geo.N || ldy < geo.N) throw std::invalid_argument("sharded block operator: leading dimension below N");
     ensureDevice();
     const int nb = ks;
+    double* yo = y + plan.ownBegin;
+    const int64_t rec = (int64_t)plan.xRootChunk * kRank * rootRhs(nb);
+    if (oneExchangeUsable(which)) {
+        // phase 1 (own tier-0 subtrees), then ONE grouped exchange: the roots to every
+        // rank, and from each owner the input positions and multipoles this rank reads;
+        // then phase 2 (near field, upper tiers + M2L, down pass)
+        oneXActive = true;
+        try {
+            blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 1, dXRootsSend.as<double>(), nullptr);
+            const int RK = kRank * rootRhs(nb);
+            launch_halo_pack(oxNsendPts, nb, dOxSendPos.as<int64_t>(), dOxSendBase.as<int64_t>(),
+                             dOxSendStride.as<int64_t>(), x, ldx, dOxSendBuf.as<double>(), s);
+            launch_rows_pack(oxNsendNodes, RK, dOxSendNode.as<int>(), dOxSendNodeBase.as<int64_t>(),
+                             dMult.as<double>(), dOxSendBuf.as<double>(), s);
+            comm->gatherExchange(dXRootsSend.as<double>(), dXRootsRecv.as<double>(), (size_t)std::max<int64_t>(rec, 0),
+                                 dOxSendBuf.as<double>(), oxScount.data(), oxSoff.data(), dOxRecvBuf.as<double>(),
+                                 oxRcount.data(), oxRoff.data(), s);
+            launch_halo_unpack(oxNrecvPts, nb, dOxRecvPos.as<int64_t>(), dOxRecvBase.as<int64_t>(),
+                               dOxRecvStride.as<int64_t>(), dOxRecvBuf.as<double>(), x, ldx, s);
+            launch_rows_unpack(oxNrecvNodes, RK, dOxRecvNode.as<int>(), dOxRecvNodeBase.as<int64_t>(),
+                               dOxRecvBuf.as<double>(), dMult.as<double>(), s);
+            blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 2, nullptr, dXRootsRecv.as<double>());
+        } catch (...) {
+            oneXActive = false;
+            throw;
+        }
+        oneXActive = false;
+        ++oneXApplies;
+        return;
+    }
     // the input's halo from its owners
     launch_halo_pack(hxNsend, nb, dHxSendPos.as<int64_t>(), dHxSendBase.as<int64_t>(), dHxSendStride.as<int64_t>(),
                      x, ldx, dHxSendBuf.as<double>(), s);
@@ -1596,9 +1778,7 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
     launch_halo_unpack(hxNrecv, nb, dHxRecvPos.as<int64_t>(), dHxRecvBase.as<int64_t>(), dHxRecvStride.as<int64_t>(),
                        dHxRecvBuf.as<double>(), x, ldx, s);
     // phase 1, the tier-0 root all-gather, phase 2 (the owned slice of y)
-    double* yo = y + plan.ownBegin;
     blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 1, dXRootsSend.as<double>(), nullptr);
-    const int64_t rec = (int64_t)plan.xRootChunk * kRank * rootRhs(nb);
     if (rec > 0) comm->allgather(dXRootsSend.as<double>(), dXRootsRecv.as<double>(), (size_t)rec, s);
     blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 2, nullptr, dXRootsRecv.as<double>());
 }

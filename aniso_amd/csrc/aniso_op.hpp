@@ -147,6 +147,7 @@ public:
     // and count it; the caller then re-runs the apply on the tier launches
     bool recoverTopTimeout(hipStream_t s);
     int64_t topRecoveries = 0;  // applies re-run after a time-out (aniso_stats)
+    int64_t oneXApplies = 0;    // sharded matvecs through the one-collective exchange (aniso_stats)
     bool forceUnfused = false;
     // wait for every apply enqueued by this handle (both streams), then check
     void sync();
@@ -248,6 +249,16 @@ private:
     DevBuf dXRootsSend, dXRootsRecv;
     std::vector<int64_t> hxScount, hxSoff, hxRcount, hxRoff;
     int64_t hxNsend = 0, hxNrecv = 0;
+    // the one-collective exchange (Plan::xOneOk; ANISO_ONE_EXCHANGE=0 keeps the halo
+    // all-to-all before phase 1): per peer one buffer part = its input positions
+    // (block-major, as the halo exchange) then its multipole rows (16 x K each);
+    // oneXActive marks the two phases of such a matvec for applyBlock
+    DevBuf dOxSendPos, dOxSendBase, dOxSendStride, dOxRecvPos, dOxRecvBase, dOxRecvStride;
+    DevBuf dOxSendNode, dOxSendNodeBase, dOxRecvNode, dOxRecvNodeBase, dOxSendBuf, dOxRecvBuf, dXOwnT0Tasks;
+    std::vector<int64_t> oxScount, oxSoff, oxRcount, oxRoff;
+    int64_t oxNsendPts = 0, oxNrecvPts = 0, oxNsendNodes = 0, oxNrecvNodes = 0;
+    bool oxReady = false, oneXActive = false, oneXOn = true;
+    bool oneExchangeUsable(int which);
     // sticky time-out flag of the fused launch's in-kernel hand-offs, in host-visible
     // memory (the kernel stores 1 there when a wait gives up; checked at every API
     // entry and by sync(), never read on the device)

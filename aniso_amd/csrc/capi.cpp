@@ -433,6 +433,28 @@ int aniso_shard_exchange(aniso_handle h, int nrhs, int64_t* info) {
     });
 }
 
+int aniso_shard_exchange_one(aniso_handle h, int64_t* info) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(info);
+        const auto& p = get(h).plan;
+        info[0] = p.xOneOk ? 1 : 0;
+        info[1] = (int64_t)p.xOwnT0Tasks.size();
+        info[2] = (int64_t)p.xNeedNodes.size();
+        info[3] = (int64_t)p.xOneHalo.size() / 2;
+        info[4] = p.xOneHaloPoints;
+    });
+}
+
+int aniso_shard_one_halo(aniso_handle h, int64_t* ranges) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(ranges);
+        const auto& p = get(h).plan;
+        std::copy(p.xOneHalo.begin(), p.xOneHalo.end(), ranges);
+    });
+}
+
 int aniso_shard_halo(aniso_handle h, int64_t* ranges) {
     ENTER(h);
     return guarded([&] {
@@ -565,6 +587,7 @@ int aniso_stats(aniso_handle h, int64_t* s) {
         // the harmonic near field's symmetric U storage (0: directed, Plan::nearSymHsOn)
         s[23] = op.plan.nearSymHsOn ? op.plan.hsStored : 0;
         s[24] = op.plan.nearSymHsOn ? op.plan.hsPartTotal : 0;
+        s[25] = op.oneXApplies;  // sharded matvecs through the one-collective exchange
     });
 }
 

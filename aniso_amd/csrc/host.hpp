@@ -235,6 +235,18 @@ struct Plan {
     int xRootChunk = 0;               // roots per rank in the all-gather (the largest contribution)
     std::vector<int64_t> xHalo;       // [b, e) pairs of tree positions needed outside [ownBegin, ownEnd)
     int64_t xHaloPoints = 0;
+    // The one-collective exchange: a rank runs only the
+    // tier-0 tasks of its own subtrees (xOwnT0Tasks); after them one grouped
+    // send/receive carries the tier-0 roots to every rank together with, from each
+    // owner, the multipoles below the root level that this rank's M2L reads
+    // (xNeedNodes) and the input at the positions its near field, corrections and
+    // upper-tier P2M read outside its range (xOneHalo, [b, e) pairs).  xOneOk: the
+    // tree allows it (every own tier-0 subtree inside the own range).
+    std::vector<int> xOwnT0Tasks;
+    std::vector<int> xNeedNodes;      // ascending node ids, owned by other ranks
+    std::vector<int64_t> xOneHalo;
+    int64_t xOneHaloPoints = 0;
+    bool xOneOk = false;
 
     void build(const Tree& t, int np, int rank, int nranks);
     // the exchange plan above; sz / d2: the square grid of the correction stencil

@@ -1015,6 +1015,11 @@ void Plan::buildExchange(const Tree& t, int sz, int d2) {
         if (!ok) nearCorrRow.clear();
     }
     xT0Tasks.clear();
+    xOwnT0Tasks.clear();
+    xNeedNodes.clear();
+    xOneHalo.clear();
+    xOneHaloPoints = 0;
+    xOneOk = false;
     xRootSend.clear();
     xRootRecv.clear();
     xRootSlot.clear();
@@ -1111,6 +1116,42 @@ void Plan::buildExchange(const Tree& t, int sz, int d2) {
     for (size_t j = 0; j < xRootSend.size(); ++j) xSendSlot[xRootSend[j]] = (int)j;
     for (int r : xRootSend)
         if (!runs[taskOf[r] - t0]) throw std::logic_error("exchange plan: a sent root's task does not run here");
+    // ---- the one-collective form: own tier-0 tasks only, the rest comes from the owners
+    auto ownerOf = [&](int64_t pos) {
+        return (int)(std::upper_bound(cuts.begin() + 1, cuts.end() - 1, pos) - (cuts.begin() + 1));
+    };
+    bool ok = true;
+    for (int r : xRootSend) {
+        xOwnT0Tasks.push_back(taskOf[r]);
+        ok = ok && t.begin[r] >= ownBegin && t.begin[r] + t.count[r] <= ownEnd;
+    }
+    std::sort(xOwnT0Tasks.begin(), xOwnT0Tasks.end());
+    std::vector<char> needNode(t.nn, 0);
+    auto markNeed = [&](int n) {  // a multipole below L0 in another rank's subtree
+        if (t.level[n] > L0 && ownerOf(t.begin[n]) != rank) needNode[n] = 1;
+    };
+    for (int n : m2lTgt) {
+        for (int64_t k = t.vPtr[n]; k < t.vPtr[n + 1]; ++k)
+            if (!t.isEmpty[t.vIdx[k]]) markNeed(t.vIdx[k]);
+        for (int64_t k = t.xPtr[n]; k < t.xPtr[n + 1]; ++k)
+            if (!t.isEmpty[t.xIdx[k]]) markNeed(t.xIdx[k]);
+    }
+    for (int n = 0; n < t.nn; ++n)
+        if (needNode[n]) xNeedNodes.push_back(n);
+    for (int64_t p = 0; p < N;) {  // the input this rank reads outside its range: near, stencil, upper-tier P2M
+        auto want = [&](int64_t q) { return (need[q] || !covered[q]) && !(q >= ownBegin && q < ownEnd); };
+        if (!want(p)) {
+            ++p;
+            continue;
+        }
+        int64_t e = p;
+        while (e < N && want(e)) ++e;
+        xOneHalo.push_back(p);
+        xOneHalo.push_back(e);
+        xOneHaloPoints += e - p;
+        p = e;
+    }
+    xOneOk = ok && nranks > 1;
 }
 
 }  // namespace aniso

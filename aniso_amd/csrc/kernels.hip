@@ -334,4 +334,36 @@ void launch_halo_unpack(int64_t n, int nb, const int64_t* pos, const int64_t* ba
     HIP_LAUNCH_CHECK();
 }
 
+// multipole rows of the one-collective exchange: row j (node[j], len doubles) <-> the
+// buffer at base[j]
+__global__ void k_rows_pack(int64_t n, int len, const int* __restrict__ node, const int64_t* __restrict__ base,
+                            const double* __restrict__ src, double* __restrict__ buf) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * len) return;
+    const int64_t j = e / len, c = e - j * len;
+    buf[base[j] + c] = src[(size_t)node[j] * len + c];
+}
+
+__global__ void k_rows_unpack(int64_t n, int len, const int* __restrict__ node, const int64_t* __restrict__ base,
+                              const double* __restrict__ buf, double* __restrict__ dst) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * len) return;
+    const int64_t j = e / len, c = e - j * len;
+    dst[(size_t)node[j] * len + c] = buf[base[j] + c];
+}
+
+void launch_rows_pack(int64_t n, int len, const int* node, const int64_t* base, const double* src, double* buf,
+                      hipStream_t s) {
+    if (n <= 0) return;
+    k_rows_pack<<<blocks_for(n * len, 256), 256, 0, s>>>(n, len, node, base, src, buf);
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_rows_unpack(int64_t n, int len, const int* node, const int64_t* base, const double* buf, double* dst,
+                        hipStream_t s) {
+    if (n <= 0) return;
+    k_rows_unpack<<<blocks_for(n * len, 256), 256, 0, s>>>(n, len, node, base, buf, dst);
+    HIP_LAUNCH_CHECK();
+}
+
 }  // namespace aniso

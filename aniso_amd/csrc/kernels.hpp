@@ -341,6 +341,11 @@ void launch_halo_pack(int64_t n, int nb, const int64_t* pos, const int64_t* base
                       const double* x, int64_t ldx, double* buf, hipStream_t s);
 void launch_halo_unpack(int64_t n, int nb, const int64_t* pos, const int64_t* base, const int64_t* stride,
                         const double* buf, double* x, int64_t ldx, hipStream_t s);
+// the one-collective exchange's multipole rows (node[j]'s len doubles <-> buf + base[j])
+void launch_rows_pack(int64_t n, int len, const int* node, const int64_t* base, const double* src, double* buf,
+                      hipStream_t s);
+void launch_rows_unpack(int64_t n, int len, const int* node, const int64_t* base, const double* buf, double* dst,
+                        hipStream_t s);
 
 // host-callable device helpers used by tests through the C ABI
 void launch_line_integrals(int n, const double* seg, const double* stcoef, const Params* P, double* out,

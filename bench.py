@@ -584,11 +584,21 @@ def main():
         "cache_build_s": round(t_cache, 3),
         "roofline": roofline,
     }
+    one_x = world > 1 and native and op.stats()["one_exchange_applies"] > 0
     if world > 1:
         line["exchange"] = {"root_allgather_bytes_per_rank": 8 * xchg.C * xchg.R,
                             "halo_bytes_received": xchg.halo_bytes(), "backend": args.backend,
                             "comm": ("library (aniso_block_op_sharded_dev: halo all-to-all, phase 1, root all-gather, "
                                      "phase 2 in one call)" if native else "aniso_amd.dist.ShardExchange")}
+        if one_x:  # own tier-0 subtrees, then ONE grouped exchange
+            o1 = op.shard_exchange_one()
+            line["exchange"].update({
+                "comm": "library (aniso_block_op_sharded_dev: own tier-0 subtrees, then one grouped send/receive "
+                        "of the roots, the multipoles below the root level and the input each rank reads, then "
+                        "phase 2)",
+                "collectives_per_matvec": 1,
+                "halo_bytes_received": 8 * nb * o1["halo_points"] + 8 * xchg.R * o1["need_nodes"],
+                "multipoles_received": o1["need_nodes"], "input_points_received": o1["halo_points"]})
     line.update(sec)  # mode-0 operator and deterministic block matvec (measured before the headline leg)
     if args.gmres > 0 and block:
         # GMRES over this run's (possibly sharded) block matvec: aniso_amd.solve.gmres_dist,
@@ -714,7 +724,8 @@ def main():
         sq = torch.tensor([float(torch.sum((got[:, b_:e_] - ref[:, b_:e_]) ** 2)),
                            float(torch.sum(ref[:, b_:e_] ** 2))], dtype=torch.float64)
         if world > 1:
-            hal = [torch.arange(lo, hi, device="cuda") for lo, hi in xchg.halos[rank]]
+            ranges = op.shard_one_halo() if one_x else xchg.halos[rank]
+            hal = [torch.arange(int(lo), int(hi), device="cuda") for lo, hi in ranges]
             if hal:
                 hi_ = torch.cat(hal)
                 if native:

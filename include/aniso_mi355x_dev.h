@@ -31,13 +31,20 @@ int aniso_comm_init_loopback(aniso_handle h);
 /* the same restricted to the stages in mask (ANISO_STAGE_*; the identity x is always there) */
 int aniso_forward_f32_stages_dev(aniso_handle h, const float *x, int mask, float *y, void *stream);
 /* ---- introspection (tests / benchmarks) ---- */
+/* the one-collective exchange of aniso_block_op_sharded_dev:
+ * info[0..4] = 1 if the shard layout allows it, the rank's own tier-0 tasks, the
+ * multipoles below the tier-0 root level it receives, the input ranges and points
+ * outside its range it receives (near field, corrections, upper-tier P2M) */
+int aniso_shard_exchange_one(aniso_handle h, int64_t *info);
+/* its input ranges: 2 x info[3] tree positions [b, e) */
+int aniso_shard_one_halo(aniso_handle h, int64_t *ranges);
 int aniso_tree_size(aniso_handle h, int *nnodes, int *max_level);
 /* per node ints[11*i ..]: parent, child0..3, level, slot, isLeaf, isEmpty, nSource, begin;
  * geom[4*i ..]: cx, cy, rx, ry */
 int aniso_tree_nodes(aniso_handle h, int *ints, double *geom);
 /* which: 0=U 1=V 2=W 3=X.  ptr has nnodes+1 entries; idx (may be NULL) ptr[nnodes] */
 int aniso_tree_list(aniso_handle h, int which, int64_t *ptr, int *idx);
-/* stats[0..24]: near entries, M2L entries, M2L pairs, leaves (owned), targets with
+/* stats[0..25]: near entries, M2L entries, M2L pairs, leaves (owned), targets with
  * M2L work, tree nodes, max leaf size, N, then the symmetric storage actually
  * streamed per apply: stored near entries, stored M2L blocks, canonical M2L
  * pairs (partial slots), near partial entries; then 1 if the block operator runs
@@ -53,8 +60,9 @@ int aniso_tree_list(aniso_handle h, int which, int64_t *ptr, int *idx);
  * launches after a hand-off time-out of the fused launch (the host-pointer block
  * operator and the block solve recover; device-pointer entries report it); then
  * the harmonic near field's symmetric U storage: its stored E entries and partner
- * partial entries (both 0 when it reads every near block directed).
- * stats must hold 25 entries. */
+ * partial entries (both 0 when it reads every near block directed); then the
+ * sharded matvecs run through the one-collective exchange (section 5).
+ * stats must hold 26 entries. */
 int aniso_stats(aniso_handle h, int64_t *stats);
 /* per-stage device times (ms), averaged over every apply since aniso_set_timing(h, 1)
  * (HIP events recorded in-stream, 8 floats): exchange (between the two phases of a

@@ -1510,3 +1510,134 @@ def test_native_exchange_one_rank_rccl_and_callbacks():
         sh.block_op_sharded_dev(2, X.clone(), y)
         sh.sync()
         assert float(torch.linalg.norm(y - ref) / torch.linalg.norm(ref)) <= 1e-13, kind
+
+
+class _ThreadCollectives:
+    """aniso_collectives between handles of one process, one thread per rank (the
+    ranks share the box's one GPU; ctypes drops the GIL inside the library's calls):
+    host-staged through shared slots and a barrier."""
+
+    def __init__(self, world, rank, shared):
+        import aniso_amd
+
+        self.world, self.rank, self.sh, self.lib = world, rank, shared, aniso_amd
+        self.struct = aniso_amd.Collectives(None, aniso_amd.COLL_ALLGATHER(self._ag),
+                                            aniso_amd.COLL_ALLTOALLV(self._a2a), aniso_amd.COLL_ALLREDUCE(self._ar))
+
+    def _host(self, ptr, n):
+        buf = np.empty(int(n), dtype=np.float64)
+        if n:
+            self.lib.memcpy(buf.ctypes.data, ptr, 8 * int(n))
+        return buf
+
+    def _put(self, ptr, arr):
+        arr = np.ascontiguousarray(arr, dtype=np.float64)
+        if arr.size:
+            self.lib.memcpy(ptr, arr.ctypes.data, 8 * arr.size)
+
+    def _guard(self, fn):
+        try:
+            fn()
+            return 0
+        except Exception as ex:  # noqa: BLE001 -- the library turns the status into its error
+            self.sh["errors"].append(repr(ex))
+            self.sh["bar"].abort()
+            return 1
+
+    def _ag(self, ctx, send, recv, count, stream):
+        def run():
+            self.sh["slot"][self.rank] = self._host(send, count)
+            self.sh["bar"].wait()
+            self._put(recv, np.concatenate([self.sh["slot"][r] for r in range(self.world)]))
+            self.sh["bar"].wait()
+        return self._guard(run)
+
+    def _a2a(self, ctx, send, sc, so, recv, rc, ro, stream):
+        def run():
+            self.sh["slot"][self.rank] = [self._host(send + 8 * int(so[p]), int(sc[p])) for p in range(self.world)]
+            self.sh["bar"].wait()
+            for p in range(self.world):
+                if p != self.rank and int(rc[p]):
+                    part = self.sh["slot"][p][self.rank]
+                    assert part.size == int(rc[p])
+                    self._put(recv + 8 * int(ro[p]), part)
+            self.sh["bar"].wait()
+        return self._guard(run)
+
+    def _ar(self, ctx, buf, count, stream):
+        def run():
+            self.sh["slot"][self.rank] = self._host(buf, count)
+            self.sh["bar"].wait()
+            self._put(buf, np.sum([self.sh["slot"][r] for r in range(self.world)], axis=0))
+            self.sh["bar"].wait()
+        return self._guard(run)
+
+
+@pytest.mark.parametrize("sz,world,one", [(64, 2, "1"), (64, 2, "0"), (64, 4, "1"), (64, 8, "1"), (64, 3, "1"),
+                                          (96, 3, "1")])
+def test_native_exchange_ranks_as_threads(sz, world, one, monkeypatch):
+    """The library's one-call sharded block matvec (aniso_block_op_sharded_dev) with
+    `world` ranks as threads of one process on the box's GPU, each rank's input valid
+    only at its own range (NaN elsewhere), the collectives host-staged between the
+    threads: the one-collective exchange (own tier-0 subtrees, then the roots, the
+    multipoles below the root level and the input the rank reads from each owner in
+    one grouped exchange) and, with ANISO_ONE_EXCHANGE=0 or where the cuts split a
+    tier-0 subtree, the two-collective one; the owned slices equal the unsharded
+    matvec."""
+    torch = _torch()
+    import threading
+
+    import aniso_amd
+
+    monkeypatch.setenv("ANISO_ONE_EXCHANGE", one)
+    ks = 5
+    full = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
+    xy = full.getNodes()
+    coef = rough_coeffs(xy, 2)
+    full.setCoeff(*coef)
+    for m in range(2 * ks - 1):
+        full.cache(m)
+    X = torch.tensor(np.random.default_rng(world).uniform(-1, 1, (ks, full.N)), device="cuda")
+    ref = torch.zeros_like(X)
+    full.block_op_dev(2, X, ref, tree=True)
+    torch.cuda.synchronize()
+    hs = []
+    for r in range(world):
+        h = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
+        h.set_shard(r, world)
+        h.setCoeff(*coef)
+        for m in range(2 * ks - 1):
+            h.cache(m)
+        hs.append(h)
+    oks = [h.shard_exchange_one()["ok"] for h in hs]
+    shared = dict(bar=threading.Barrier(world, timeout=60), slot=[None] * world, errors=[])
+    colls = [_ThreadCollectives(world, r, shared) for r in range(world)]
+    outs = [None] * world
+
+    def run(r):
+        try:
+            h = hs[r]
+            h.comm_init_callbacks(colls[r].struct)
+            b, e = h.shard()
+            x = torch.full_like(X, float("nan"))
+            x[:, b:e] = X[:, b:e]
+            y = torch.zeros_like(X)
+            for _ in range(2):  # a second matvec reuses the exchange plan
+                h.block_op_sharded_dev(2, x, y)
+            h.sync()
+            outs[r] = y[:, b:e].clone()
+        except Exception as ex:  # noqa: BLE001
+            shared["errors"].append(repr(ex))
+            shared["bar"].abort()
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(120)
+    assert not shared["errors"], shared["errors"]
+    Y = torch.cat(outs, dim=1)
+    assert not torch.isnan(Y).any()
+    assert float(torch.linalg.norm(Y - ref) / torch.linalg.norm(ref)) <= 1e-13
+    used = [h.stats()["one_exchange_applies"] for h in hs]
+    assert used == [2 * int(one == "1" and all(oks))] * world

@@ -177,3 +177,28 @@ def test_block_near_symmetric_u_storage_plan(monkeypatch, env):
         a.set_shard(r, 2)
         tot += a.stats()["near_hs_stored"]
     assert s["near_hs_stored"] < tot < s["stored_near"]
+
+
+@pytest.mark.parametrize("sz,ks,nranks", [(64, 5, 2), (64, 5, 3), (64, 5, 8), (48, 2, 4)])
+def test_one_collective_exchange_plan(sz, ks, nranks):
+    """The one-collective exchange (Plan::buildExchange, DESIGN.md §5): each rank runs
+    exactly the tier-0 tasks of its own subtrees (a partition of all of them), needs
+    multipoles below the root level from other ranks, and reads fewer input points
+    outside its range than the two-collective halo (its halo subtrees' points)."""
+    a = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
+    own_total, oks = 0, []
+    for r in range(nranks):
+        a.set_shard(r, nranks)
+        one, two = a.shard_exchange_one(), a.shard_exchange(ks)
+        assert one["own_t0_tasks"] == two["roots_sent"] <= two["t0_run"]
+        own_total += one["own_t0_tasks"]
+        oks.append(one["ok"])
+        if one["ok"]:
+            assert one["need_nodes"] > 0
+            assert 0 < one["halo_points"] < two["halo_points"]
+    assert own_total == a.shard_exchange(ks)["t0_tasks"]
+    # at 3 ranks of 4,096 points the cuts split level-2 subtrees (the tier-0 roots):
+    # those ranks keep the two-collective exchange (commInit requires every rank's ok)
+    assert all(oks) == (nranks != 3)
+    a.set_shard(0, 1)
+    assert a.shard_exchange_one()["ok"] == 0  # one rank: nothing to exchange
