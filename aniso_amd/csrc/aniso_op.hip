@@ -91,6 +91,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_NEAR_IN_TOP")) nearInTop = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_EARLY")) nearEarly = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_ONE_EXCHANGE")) oneXOn = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ANISO_HM_MIN_LDS")) hmMinLds = std::max(0, std::min(160 * 1024, std::atoi(e)));
     hmRing = hm_ring_depth();
     if (const char* e = std::getenv("ANISO_HM_WPE")) hmWpe = std::atoi(e);
     if (const char* e = std::getenv("ANISO_NEAR_WPE")) nearWpe = std::atoi(e);
@@ -898,6 +899,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                      dNrx.as<double>(), dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(),
                      dNodeGeo.as<double>()};
     hca.wpe = hmWpe;
+    hca.minLds = hmMinLds;
     const bool halo = !plan.hmHaloNode.empty();
     if (halo) {  // the halo form: partials of the cross-cluster partner products (Plan::hmHaloPtr)
         const size_t hb = plan.hmHaloNode.size() * kRank * K * sizeof(double);

@@ -231,6 +231,7 @@ private:
     DevBuf dKryPart;            // partial sums of the Krylov primitives
     bool topTraceOn = false;
     int hmRing = 0;  // the cluster M2L's LDS ring depth (ANISO_HM_RING; 0: the one-block-in-flight form)
+    int hmMinLds = 0;  // ANISO_HM_MIN_LDS: the cluster launch's LDS floor in bytes (HcArgs::minLds)
     int hmWpe = 0;   // ANISO_HM_WPE=3/4/8: the one-block form's occupancy (0: 4 where LDS allows)
     int nearWpe = 3;  // ANISO_NEAR_WPE: the staged near field at 3 (132 VGPRs, the default since r03zj) or 4 waves per SIMD (<= 128)
     int topFusedMode = 1;  // ANISO_TOP_FUSED=0: the upper up tiers as launches of their own

@@ -1430,6 +1430,7 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s) {
     size_t shm = m2l_hc_lds(K, maxCl, depth, xl, 4);
     const int form = depth == 0 ? hm_form(K, a.wpe, shm) : 3;
     if (form != 3) shm = m2l_hc_lds(K, maxCl, depth, xl, hm_waves(form));
+    shm = std::max(shm, (size_t)a.minLds);
     if (shm > 160 * 1024) throw std::invalid_argument("harmonic M2L: a cluster and its halo exceed the LDS");
     ANISO_HM_DISPATCH_K(K, ANISO_HM_DISPATCH_RING(depth, ({
         if constexpr (DD == 0 || KK > kRingMaxK) {
@@ -1477,6 +1478,7 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
         if (near) shm = std::max(shm, near_hs_lds<KK>(*near));
         const int form = DD == 0 && !near ? hm_form(KK, a.wpe, shm) : 3;
         if (form != 3) shm = std::max(shm, m2l_hc_lds(KK, maxCl, depth, xl, hm_waves(form)));
+        shm = std::max(shm, (size_t)a.minLds);
         if (shm > 160 * 1024) throw std::invalid_argument("fused top-of-tree launch: a cluster and its halo exceed the LDS");
         // the ring form with its target multipole in VGPRs needs ~216 of them at K = 5
         if constexpr (DD == 0 || KK > kRingMaxK) {

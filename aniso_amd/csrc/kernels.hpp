@@ -201,6 +201,9 @@ struct HcArgs {
     const int* haloPtr = nullptr;
     const int* haloPos = nullptr;
     double* hpart = nullptr;
+    // host: the cluster launch's LDS at least this (bytes): fewer cluster workgroups per
+    // CU, so a near-field workgroup fits beside them (ANISO_HM_MIN_LDS, A/B runs)
+    int minLds = 0;
 };
 // The fused top-of-tree + clustered M2L launch (harmonic.hip k_top_m2l_hc, DESIGN.md
 // §3.10): blocks 0 .. nUp - 1 run the up tasks of tiers 1 .. ntier - 1 (tier k's
