@@ -1663,11 +1663,22 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
         oxSoff.assign(P, 0);
         oxRcount.assign(P, 0);
         oxRoff.assign(P, 0);
+        // per peer part: the tier-0 root records (rec doubles, every peer gets this
+        // rank's), the input positions (block-major), the multipole rows -- one send
+        // and one receive per peer
+        std::vector<int64_t> rtS, rtR, rtD;
         int64_t so = 0, ro = 0;
         for (int p = 0; p < P; ++p) {
             oxSoff[p] = so;
             oxRoff[p] = ro;
             if (p == me) continue;
+            if (rec > 0) {
+                rtS.push_back(so);
+                rtR.push_back(ro);
+                rtD.push_back((int64_t)p * rec);
+                so += rec;
+                ro += rec;
+            }
             std::vector<int64_t> sp, rp;
             std::vector<int> sn, rn;
             pts(p, plan.ownBegin, plan.ownEnd, sp);  // p's positions inside my range
@@ -1693,11 +1704,15 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
                 rn_.push_back(rn[j]);
                 rnb.push_back(rn0 + (int64_t)j * RK);
             }
-            oxScount[p] = (int64_t)sp.size() * nb + (int64_t)sn.size() * RK;
-            oxRcount[p] = (int64_t)rp.size() * nb + (int64_t)rn.size() * RK;
-            so += oxScount[p];
-            ro += oxRcount[p];
+            so += (int64_t)sp.size() * nb + (int64_t)sn.size() * RK;
+            ro += (int64_t)rp.size() * nb + (int64_t)rn.size() * RK;
+            oxScount[p] = so - oxSoff[p];
+            oxRcount[p] = ro - oxRoff[p];
         }
+        oxRootParts = (int64_t)rtS.size();
+        up(dOxRootSend, rtS);
+        up(dOxRootRecv, rtR);
+        up(dOxRootDst, rtD);
         oxNsendPts = (int64_t)sp_.size();
         oxNrecvPts = (int64_t)rp_.size();
         oxNsendNodes = (int64_t)sn_.size();
@@ -1752,13 +1767,19 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
         try {
             blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 1, dXRootsSend.as<double>(), nullptr);
             const int RK = kRank * rootRhs(nb);
+            launch_parts_copy(oxRootParts, rec, nullptr, dOxRootSend.as<int64_t>(), dXRootsSend.as<double>(),
+                              dOxSendBuf.as<double>(), s);  // this rank's roots into every peer's part
             launch_halo_pack(oxNsendPts, nb, dOxSendPos.as<int64_t>(), dOxSendBase.as<int64_t>(),
                              dOxSendStride.as<int64_t>(), x, ldx, dOxSendBuf.as<double>(), s);
             launch_rows_pack(oxNsendNodes, RK, dOxSendNode.as<int>(), dOxSendNodeBase.as<int64_t>(),
                              dMult.as<double>(), dOxSendBuf.as<double>(), s);
-            comm->gatherExchange(dXRootsSend.as<double>(), dXRootsRecv.as<double>(), (size_t)std::max<int64_t>(rec, 0),
-                                 dOxSendBuf.as<double>(), oxScount.data(), oxSoff.data(), dOxRecvBuf.as<double>(),
-                                 oxRcount.data(), oxRoff.data(), s);
+            comm->alltoallv(dOxSendBuf.as<double>(), oxScount.data(), oxSoff.data(), dOxRecvBuf.as<double>(),
+                            oxRcount.data(), oxRoff.data(), s);
+            if (rec > 0)
+                HIP_CHECK(hipMemcpyAsync(dXRootsRecv.as<double>() + (size_t)plan.rank * rec, dXRootsSend.as<double>(),
+                                         (size_t)rec * sizeof(double), hipMemcpyDeviceToDevice, s));
+            launch_parts_copy(oxRootParts, rec, dOxRootRecv.as<int64_t>(), dOxRootDst.as<int64_t>(),
+                              dOxRecvBuf.as<double>(), dXRootsRecv.as<double>(), s);  // the peers' roots in slot order
             launch_halo_unpack(oxNrecvPts, nb, dOxRecvPos.as<int64_t>(), dOxRecvBase.as<int64_t>(),
                                dOxRecvStride.as<int64_t>(), dOxRecvBuf.as<double>(), x, ldx, s);
             launch_rows_unpack(oxNrecvNodes, RK, dOxRecvNode.as<int>(), dOxRecvNodeBase.as<int64_t>(),

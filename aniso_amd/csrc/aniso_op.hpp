@@ -251,11 +251,14 @@ private:
     std::vector<int64_t> hxScount, hxSoff, hxRcount, hxRoff;
     int64_t hxNsend = 0, hxNrecv = 0;
     // the one-collective exchange (Plan::xOneOk; ANISO_ONE_EXCHANGE=0 keeps the halo
-    // all-to-all before phase 1): per peer one buffer part = its input positions
-    // (block-major, as the halo exchange) then its multipole rows (16 x K each);
+    // all-to-all before phase 1): per peer one buffer part = the tier-0 root records,
+    // its input positions (block-major, as the halo exchange), its multipole rows
+    // (16 x K each);
     // oneXActive marks the two phases of such a matvec for applyBlock
     DevBuf dOxSendPos, dOxSendBase, dOxSendStride, dOxRecvPos, dOxRecvBase, dOxRecvStride;
     DevBuf dOxSendNode, dOxSendNodeBase, dOxRecvNode, dOxRecvNodeBase, dOxSendBuf, dOxRecvBuf, dXOwnT0Tasks;
+    DevBuf dOxRootSend, dOxRootRecv, dOxRootDst;  // the root records' place in each peer part
+    int64_t oxRootParts = 0;
     std::vector<int64_t> oxScount, oxSoff, oxRcount, oxRoff;
     int64_t oxNsendPts = 0, oxNrecvPts = 0, oxNsendNodes = 0, oxNrecvNodes = 0;
     bool oxReady = false, oneXActive = false, oneXOn = true;

@@ -99,30 +99,6 @@ class RcclCollectives : public Collectives {
         Rccl& R = Rccl::get();
         R.check(R.allReduce(buf, buf, count, ncclFloat64, ncclSum, comm_, s), "ncclAllReduce");
     }
-    // the roots to every peer and each peer's own part, point to point over xGMI in
-    // one group (one launch latency instead of an all-gather after an all-to-all)
-    void gatherExchange(const double* gsend, double* grecv, size_t gcount, const double* send, const int64_t* sc,
-                        const int64_t* so, double* recv, const int64_t* rc, const int64_t* ro,
-                        hipStream_t s) override {
-        Rccl& R = Rccl::get();
-        if (gcount > 0) {
-            const hipError_t e = hipMemcpyAsync(grecv + (size_t)rank * gcount, gsend, gcount * sizeof(double),
-                                                hipMemcpyDeviceToDevice, s);
-            if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
-        }
-        R.check(R.groupStart(), "ncclGroupStart");
-        for (int p = 0; p < nranks; ++p) {
-            if (p == rank) continue;
-            if (gcount > 0) {
-                R.check(R.send(gsend, gcount, ncclFloat64, p, comm_, s), "ncclSend");
-                R.check(R.recv(grecv + (size_t)p * gcount, gcount, ncclFloat64, p, comm_, s), "ncclRecv");
-            }
-            if (sc[p] > 0) R.check(R.send(send + so[p], (size_t)sc[p], ncclFloat64, p, comm_, s), "ncclSend");
-            if (rc[p] > 0) R.check(R.recv(recv + ro[p], (size_t)rc[p], ncclFloat64, p, comm_, s), "ncclRecv");
-        }
-        R.check(R.groupEnd(), "ncclGroupEnd");
-    }
-
   private:
     ncclComm_t comm_ = nullptr;
 };

@@ -31,14 +31,6 @@ class Collectives {
                            const int64_t* rcount, const int64_t* roff, hipStream_t s) = 0;
     // buf (count doubles, device) = its sum over the ranks
     virtual void allreduce(double* buf, size_t count, hipStream_t s) = 0;
-    // the one-collective exchange: an all-gather (gsend -> grecv) and a per-peer
-    // all-to-all together; RCCL issues both as one group of sends and receives
-    virtual void gatherExchange(const double* gsend, double* grecv, size_t gcount, const double* send,
-                                const int64_t* scount, const int64_t* soff, double* recv, const int64_t* rcount,
-                                const int64_t* roff, hipStream_t s) {
-        if (gcount > 0) allgather(gsend, grecv, gcount, s);
-        alltoallv(send, scount, soff, recv, rcount, roff, s);
-    }
     // development: no peers (make_loopback_collectives); commInit then builds the
     // peers' exchange lists from their plans instead of gathering them
     virtual bool loopback() const { return false; }

@@ -352,6 +352,23 @@ __global__ void k_rows_unpack(int64_t n, int len, const int* __restrict__ node, 
     dst[(size_t)node[j] * len + c] = buf[base[j] + c];
 }
 
+// n parts of len doubles: dst[dstOff[j] + c] = src[(srcOff ? srcOff[j] : 0) + c]
+__global__ void k_parts_copy(int64_t n, int64_t len, const int64_t* __restrict__ srcOff,
+                             const int64_t* __restrict__ dstOff, const double* __restrict__ src,
+                             double* __restrict__ dst) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * len) return;
+    const int64_t j = e / len, c = e - j * len;
+    dst[dstOff[j] + c] = src[(srcOff ? srcOff[j] : 0) + c];
+}
+
+void launch_parts_copy(int64_t n, int64_t len, const int64_t* srcOff, const int64_t* dstOff, const double* src,
+                       double* dst, hipStream_t s) {
+    if (n <= 0 || len <= 0) return;
+    k_parts_copy<<<blocks_for(n * len, 256), 256, 0, s>>>(n, len, srcOff, dstOff, src, dst);
+    HIP_LAUNCH_CHECK();
+}
+
 void launch_rows_pack(int64_t n, int len, const int* node, const int64_t* base, const double* src, double* buf,
                       hipStream_t s) {
     if (n <= 0) return;

@@ -344,6 +344,9 @@ void launch_halo_pack(int64_t n, int nb, const int64_t* pos, const int64_t* base
                       const double* x, int64_t ldx, double* buf, hipStream_t s);
 void launch_halo_unpack(int64_t n, int nb, const int64_t* pos, const int64_t* base, const int64_t* stride,
                         const double* buf, double* x, int64_t ldx, hipStream_t s);
+// n parts of len doubles: dst + dstOff[j] <- src + srcOff[j] (srcOff nullptr: src)
+void launch_parts_copy(int64_t n, int64_t len, const int64_t* srcOff, const int64_t* dstOff, const double* src,
+                       double* dst, hipStream_t s);
 // the one-collective exchange's multipole rows (node[j]'s len doubles <-> buf + base[j])
 void launch_rows_pack(int64_t n, int len, const int* node, const int64_t* base, const double* src, double* buf,
                       hipStream_t s);
