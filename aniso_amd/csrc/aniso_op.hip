@@ -1740,7 +1740,8 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
 // nothing to the halo: the harmonic block apply with the near field formed from the
 // input (run in phase 2, after the exchange) and no padded right-hand sides.
 bool Operator::oneExchangeUsable(int which) {
-    if (!oxReady || !oneXOn || !plan.xOneOk || !rhs_supported(ks) || !nearEarly || !plan.nearCorrOk) return false;
+    if (!oxReady || !oneXOn || !plan.xOneOk || !rhs_supported(ks) || !nearEarly || nearInTop || !plan.nearCorrOk)
+        return false;
     const int nm = 2 * ks - 1;
     const auto mix = blockMixes(ks, g, which != 0);
     std::vector<int> ids(nm);
