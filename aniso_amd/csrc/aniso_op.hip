@@ -91,7 +91,6 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_NEAR_IN_TOP")) nearInTop = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_EARLY")) nearEarly = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_ONE_EXCHANGE")) oneXOn = std::atoi(e) != 0;
-    if (const char* e = std::getenv("ANISO_HM_MIN_LDS")) hmMinLds = std::max(0, std::min(160 * 1024, std::atoi(e)));
     hmRing = hm_ring_depth();
     if (const char* e = std::getenv("ANISO_HM_WPE")) hmWpe = std::atoi(e);
     if (const char* e = std::getenv("ANISO_NEAR_WPE")) nearWpe = std::atoi(e);
@@ -356,6 +355,8 @@ void Operator::uploadPlan() {
     up(dNearPts, plan.nearPts);
     up(dXT0Tasks, plan.xT0Tasks);
     up(dXOwnT0Tasks, plan.xOwnT0Tasks);
+    up(dNearGrpEarly, plan.nearGrpEarly);
+    up(dNearGrpLate, plan.nearGrpLate);
     up(dXRootRecv, plan.xRootRecv);
     up(dNsPtr, plan.nsPtr);
     up(dNsPts, plan.nsPts);
@@ -899,7 +900,6 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                      dNrx.as<double>(), dNry.as<double>(), P, hw, dMult.as<double>(), dLocal.as<double>(),
                      dNodeGeo.as<double>()};
     hca.wpe = hmWpe;
-    hca.minLds = hmMinLds;
     const bool halo = !plan.hmHaloNode.empty();
     if (halo) {  // the halo form: partials of the cross-cluster partner products (Plan::hmHaloPtr)
         const size_t hb = plan.hmHaloNode.size() * kRank * K * sizeof(double);
@@ -925,6 +925,15 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         // up pass: tiers bottom-up; its P2M also forms the weighted charges fT (tree
         // order) the near field and the corrections read
         e0 = tm ? mark(s) : -1;
+        if (nearIn && oneX && !plan.nearGrpEarly.empty()) {
+            // one-collective form: the groups that read only the own range start now,
+            // beside the own tier-0 tasks; the rest waits for the exchange (phase 2)
+            nin.grpList = dNearGrpEarly.as<int>();
+            nin.ngrp = (int)plan.nearGrpEarly.size();
+            if (fork) HIP_CHECK(hipEventRecord(evFork, s));
+            nearStage();
+            if (!fork && tm) e0 = mark(s);
+        }
         if (nearIn && !oneX) {  // the near field first: beside the up pass (fork) or before it (serial)
             if (fork) HIP_CHECK(hipEventRecord(evFork, s));
             nearStage();
@@ -961,9 +970,13 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         pend.active = false;
         const int ex = tm ? mark(s) : -1;
         span(0, pend.ePack, ex);  // the caller's root exchange
-        if (oneX && !nearDone) {  // the near field after the one exchange (it filled the input's halo)
+        if (oneX && !nearDone) {  // the rest of the near field after the one exchange (it filled the input's halo)
+            nin.grpList = dNearGrpLate.as<int>();
+            nin.ngrp = (int)plan.nearGrpLate.size();
             if (fork) HIP_CHECK(hipEventRecord(evFork, s));
             nearStage();
+            nin.grpList = nullptr;
+            nin.ngrp = 0;
             nearDone = true;
         }
         if (topFused) {  // the upper tiers run inside the M2L launch below
@@ -1768,23 +1781,46 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
         try {
             blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 1, dXRootsSend.as<double>(), nullptr);
             const int RK = kRank * rootRhs(nb);
-            launch_parts_copy(oxRootParts, rec, nullptr, dOxRootSend.as<int64_t>(), dXRootsSend.as<double>(),
-                              dOxSendBuf.as<double>(), s);  // this rank's roots into every peer's part
-            launch_halo_pack(oxNsendPts, nb, dOxSendPos.as<int64_t>(), dOxSendBase.as<int64_t>(),
-                             dOxSendStride.as<int64_t>(), x, ldx, dOxSendBuf.as<double>(), s);
-            launch_rows_pack(oxNsendNodes, RK, dOxSendNode.as<int>(), dOxSendNodeBase.as<int64_t>(),
-                             dMult.as<double>(), dOxSendBuf.as<double>(), s);
+            // one pack launch (this rank's roots into every peer's part, the input
+            // positions and the multipole rows each peer reads), one all-to-all-v, one
+            // unpack launch (the peers' roots into the slot layout, the own roots, the
+            // input's halo, the multipoles)
+            OxArgs pk;
+            pk.nRoot = oxRootParts;
+            pk.rec = rec;
+            pk.rootOff = dOxRootSend.as<int64_t>();
+            pk.roots = dXRootsSend.as<double>();
+            pk.nPts = oxNsendPts;
+            pk.nb = nb;
+            pk.pos = dOxSendPos.as<int64_t>();
+            pk.base = dOxSendBase.as<int64_t>();
+            pk.stride = dOxSendStride.as<int64_t>();
+            pk.x = x;
+            pk.ldx = ldx;
+            pk.nNode = oxNsendNodes;
+            pk.len = RK;
+            pk.node = dOxSendNode.as<int>();
+            pk.nodeBase = dOxSendNodeBase.as<int64_t>();
+            pk.mult = dMult.as<double>();
+            pk.buf = dOxSendBuf.as<double>();
+            launch_ox(pk, true, s);
             comm->alltoallv(dOxSendBuf.as<double>(), oxScount.data(), oxSoff.data(), dOxRecvBuf.as<double>(),
                             oxRcount.data(), oxRoff.data(), s);
-            if (rec > 0)
-                HIP_CHECK(hipMemcpyAsync(dXRootsRecv.as<double>() + (size_t)plan.rank * rec, dXRootsSend.as<double>(),
-                                         (size_t)rec * sizeof(double), hipMemcpyDeviceToDevice, s));
-            launch_parts_copy(oxRootParts, rec, dOxRootRecv.as<int64_t>(), dOxRootDst.as<int64_t>(),
-                              dOxRecvBuf.as<double>(), dXRootsRecv.as<double>(), s);  // the peers' roots in slot order
-            launch_halo_unpack(oxNrecvPts, nb, dOxRecvPos.as<int64_t>(), dOxRecvBase.as<int64_t>(),
-                               dOxRecvStride.as<int64_t>(), dOxRecvBuf.as<double>(), x, ldx, s);
-            launch_rows_unpack(oxNrecvNodes, RK, dOxRecvNode.as<int>(), dOxRecvNodeBase.as<int64_t>(),
-                               dOxRecvBuf.as<double>(), dMult.as<double>(), s);
+            OxArgs uk = pk;
+            uk.rootOff = dOxRootRecv.as<int64_t>();
+            uk.rootDst = dOxRootDst.as<int64_t>();
+            uk.roots = dXRootsRecv.as<double>();
+            uk.ownRoots = rec > 0 ? dXRootsSend.as<double>() : nullptr;
+            uk.ownDst = (int64_t)plan.rank * rec;
+            uk.nPts = oxNrecvPts;
+            uk.pos = dOxRecvPos.as<int64_t>();
+            uk.base = dOxRecvBase.as<int64_t>();
+            uk.stride = dOxRecvStride.as<int64_t>();
+            uk.nNode = oxNrecvNodes;
+            uk.node = dOxRecvNode.as<int>();
+            uk.nodeBase = dOxRecvNodeBase.as<int64_t>();
+            uk.buf = dOxRecvBuf.as<double>();
+            launch_ox(uk, false, s);
             blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 2, nullptr, dXRootsRecv.as<double>());
         } catch (...) {
             oneXActive = false;

@@ -231,7 +231,6 @@ private:
     DevBuf dKryPart;            // partial sums of the Krylov primitives
     bool topTraceOn = false;
     int hmRing = 0;  // the cluster M2L's LDS ring depth (ANISO_HM_RING; 0: the one-block-in-flight form)
-    int hmMinLds = 0;  // ANISO_HM_MIN_LDS: the cluster launch's LDS floor in bytes (HcArgs::minLds)
     int hmWpe = 0;   // ANISO_HM_WPE=3/4/8: the one-block form's occupancy (0: 4 where LDS allows)
     int nearWpe = 3;  // ANISO_NEAR_WPE: the staged near field at 3 (132 VGPRs, the default since r03zj) or 4 waves per SIMD (<= 128)
     int topFusedMode = 1;  // ANISO_TOP_FUSED=0: the upper up tiers as launches of their own
@@ -258,6 +257,7 @@ private:
     DevBuf dOxSendPos, dOxSendBase, dOxSendStride, dOxRecvPos, dOxRecvBase, dOxRecvStride;
     DevBuf dOxSendNode, dOxSendNodeBase, dOxRecvNode, dOxRecvNodeBase, dOxSendBuf, dOxRecvBuf, dXOwnT0Tasks;
     DevBuf dOxRootSend, dOxRootRecv, dOxRootDst;  // the root records' place in each peer part
+    DevBuf dNearGrpEarly, dNearGrpLate;           // Plan::nearGrpEarly / nearGrpLate
     int64_t oxRootParts = 0;
     std::vector<int64_t> oxScount, oxSoff, oxRcount, oxRoff;
     int64_t oxNsendPts = 0, oxNrecvPts = 0, oxNsendNodes = 0, oxNrecvNodes = 0;

@@ -1318,7 +1318,7 @@ static size_t near_hs_lds(const NearHsArgs& n) {
 template <int K, int U, int NR, bool FUSE, bool W4 = false, bool SYM = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W4 ? 4 : SYM ? ANISO_NEAR_SYM_WPE : 1))) k_near_hs(NearHsArgs n) {
     extern __shared__ double tab[];
-    near_hs_group<K, U, NR, FUSE, SYM>((int)blockIdx.x, n, tab);
+    near_hs_group<K, U, NR, FUSE, SYM>(n.grpList ? n.grpList[blockIdx.x] : (int)blockIdx.x, n, tab);
 }
 
 
@@ -1430,7 +1430,6 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s) {
     size_t shm = m2l_hc_lds(K, maxCl, depth, xl, 4);
     const int form = depth == 0 ? hm_form(K, a.wpe, shm) : 3;
     if (form != 3) shm = m2l_hc_lds(K, maxCl, depth, xl, hm_waves(form));
-    shm = std::max(shm, (size_t)a.minLds);
     if (shm > 160 * 1024) throw std::invalid_argument("harmonic M2L: a cluster and its halo exceed the LDS");
     ANISO_HM_DISPATCH_K(K, ANISO_HM_DISPATCH_RING(depth, ({
         if constexpr (DD == 0 || KK > kRingMaxK) {
@@ -1478,7 +1477,6 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
         if (near) shm = std::max(shm, near_hs_lds<KK>(*near));
         const int form = DD == 0 && !near ? hm_form(KK, a.wpe, shm) : 3;
         if (form != 3) shm = std::max(shm, m2l_hc_lds(KK, maxCl, depth, xl, hm_waves(form)));
-        shm = std::max(shm, (size_t)a.minLds);
         if (shm > 160 * 1024) throw std::invalid_argument("fused top-of-tree launch: a cluster and its halo exceed the LDS");
         // the ring form with its target multipole in VGPRs needs ~216 of them at K = 5
         if constexpr (DD == 0 || KK > kRingMaxK) {
@@ -1521,7 +1519,7 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
                     const int* nsPts, int nsMax, const NearCorr* corr, int wpe, hipStream_t s, const NearHsArgs* in) {
     if (nl <= 0) return false;
     if (near_hs_staged(nl, maxLeaf, nsMax, nearLoc)) {  // sources staged in LDS (k_near_hs)
-        const unsigned ng = (unsigned)((nl + 15) / 16);
+        unsigned ng = (unsigned)((nl + 15) / 16);
         // the corrections ride along when the table is loaded (near field on)
         const bool fuse = near_hs_fusable(nl, maxLeaf, nsMax, nearLoc, corr, flags);
         NearHsArgs n{nl, nsMax, leafInfo, nearPtsPtr, nearLoc, nsPtr, nsPts, nearKOff, E, pxT, pyT, sigDiag, hw,
@@ -1534,6 +1532,12 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
             n.perm = in->perm;
             n.sigT = in->sigT;
             n.wT = in->wT;
+        }
+        if (in && in->grpList) {  // a subset of the groups
+            n.grpList = in->grpList;
+            n.ngrp = in->ngrp;
+            ng = (unsigned)in->ngrp;
+            if (ng == 0) return fuse;
         }
         if (in && in->colDst) {  // symmetric U storage (the column lists passed are its own)
             if (!in->nearSym || !in->selfRow || !in->nearPart || !in->grpInPtr)  // grpIn: may be empty
@@ -1561,6 +1565,7 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
                                nl, leafInfo, nearPtsPtr, nearPts, nearKOff, E, pxT, pyT, sigDiag, hw, fT, operm, \
                                obase, ldo, flags, scale, out)))
     if (in && in->colDst) throw std::invalid_argument("symmetric near storage needs the staged near field");
+    if (in && in->grpList) throw std::invalid_argument("a near-field group subset needs the staged near field");
     if (maxLeaf <= 16) {
         ANISO_NEAR_HM(16);
     } else {

@@ -243,6 +243,9 @@ struct Plan {
     // upper-tier P2M read outside its range (xOneHalo, [b, e) pairs).  xOneOk: the
     // tree allows it (every own tier-0 subtree inside the own range).
     std::vector<int> xOwnT0Tasks;
+    // the staged near field's 16-leaf groups whose source table lies in the own range
+    // (they run beside phase 1) and the others (after the exchange)
+    std::vector<int> nearGrpEarly, nearGrpLate;
     std::vector<int> xNeedNodes;      // ascending node ids, owned by other ranks
     std::vector<int64_t> xOneHalo;
     int64_t xOneHaloPoints = 0;

@@ -1016,6 +1016,8 @@ void Plan::buildExchange(const Tree& t, int sz, int d2) {
     }
     xT0Tasks.clear();
     xOwnT0Tasks.clear();
+    nearGrpEarly.clear();
+    nearGrpLate.clear();
     xNeedNodes.clear();
     xOneHalo.clear();
     xOneHaloPoints = 0;
@@ -1152,6 +1154,13 @@ void Plan::buildExchange(const Tree& t, int sz, int d2) {
         p = e;
     }
     xOneOk = ok && nranks > 1;
+    nearGrpEarly.clear();
+    nearGrpLate.clear();
+    for (size_t g = 0; g + 1 < nsPtr.size(); ++g) {
+        bool own = true;
+        for (int64_t r = nsPtr[g]; r < nsPtr[g + 1] && own; ++r) own = nsPts[r] >= ownBegin && nsPts[r] < ownEnd;
+        (own ? nearGrpEarly : nearGrpLate).push_back((int)g);
+    }
 }
 
 }  // namespace aniso

@@ -334,52 +334,36 @@ void launch_halo_unpack(int64_t n, int nb, const int64_t* pos, const int64_t* ba
     HIP_LAUNCH_CHECK();
 }
 
-// multipole rows of the one-collective exchange: row j (node[j], len doubles) <-> the
-// buffer at base[j]
-__global__ void k_rows_pack(int64_t n, int len, const int* __restrict__ node, const int64_t* __restrict__ base,
-                            const double* __restrict__ src, double* __restrict__ buf) {
+// the one-collective exchange's pack / unpack (kernels.hpp OxArgs): one thread per
+// double of the roots, then of the input positions, then of the multipole rows
+template <bool PACK>
+__global__ void k_ox(OxArgs a) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n * len) return;
-    const int64_t j = e / len, c = e - j * len;
-    buf[base[j] + c] = src[(size_t)node[j] * len + c];
+    const int64_t nr = a.nRoot * a.rec, np = a.nPts * a.nb, nn = a.nNode * a.len;
+    if (e < nr) {
+        const int64_t j = e / a.rec, c = e - j * a.rec;
+        if (PACK) a.buf[a.rootOff[j] + c] = a.roots[c];
+        else a.roots[a.rootDst[j] + c] = a.buf[a.rootOff[j] + c];
+    } else if (e < nr + np) {
+        const int64_t t = e - nr, b = t / a.nPts, i = t - b * a.nPts;  // consecutive lanes: consecutive positions
+        const int64_t q = a.base[i] + b * a.stride[i];
+        if (PACK) a.buf[q] = a.x[(size_t)b * a.ldx + a.pos[i]];
+        else a.x[(size_t)b * a.ldx + a.pos[i]] = a.buf[q];
+    } else if (e < nr + np + nn) {
+        const int64_t t = e - nr - np, j = t / a.len, c = t - j * a.len;
+        if (PACK) a.buf[a.nodeBase[j] + c] = a.mult[(size_t)a.node[j] * a.len + c];
+        else a.mult[(size_t)a.node[j] * a.len + c] = a.buf[a.nodeBase[j] + c];
+    } else if (!PACK && a.ownRoots && e < nr + np + nn + a.rec) {
+        const int64_t c = e - nr - np - nn;
+        a.roots[a.ownDst + c] = a.ownRoots[c];
+    }
 }
 
-__global__ void k_rows_unpack(int64_t n, int len, const int* __restrict__ node, const int64_t* __restrict__ base,
-                              const double* __restrict__ buf, double* __restrict__ dst) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n * len) return;
-    const int64_t j = e / len, c = e - j * len;
-    dst[(size_t)node[j] * len + c] = buf[base[j] + c];
-}
-
-// n parts of len doubles: dst[dstOff[j] + c] = src[(srcOff ? srcOff[j] : 0) + c]
-__global__ void k_parts_copy(int64_t n, int64_t len, const int64_t* __restrict__ srcOff,
-                             const int64_t* __restrict__ dstOff, const double* __restrict__ src,
-                             double* __restrict__ dst) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n * len) return;
-    const int64_t j = e / len, c = e - j * len;
-    dst[dstOff[j] + c] = src[(srcOff ? srcOff[j] : 0) + c];
-}
-
-void launch_parts_copy(int64_t n, int64_t len, const int64_t* srcOff, const int64_t* dstOff, const double* src,
-                       double* dst, hipStream_t s) {
-    if (n <= 0 || len <= 0) return;
-    k_parts_copy<<<blocks_for(n * len, 256), 256, 0, s>>>(n, len, srcOff, dstOff, src, dst);
-    HIP_LAUNCH_CHECK();
-}
-
-void launch_rows_pack(int64_t n, int len, const int* node, const int64_t* base, const double* src, double* buf,
-                      hipStream_t s) {
+void launch_ox(const OxArgs& a, bool pack, hipStream_t s) {
+    const int64_t n = a.nRoot * a.rec + a.nPts * a.nb + a.nNode * a.len + (!pack && a.ownRoots ? a.rec : 0);
     if (n <= 0) return;
-    k_rows_pack<<<blocks_for(n * len, 256), 256, 0, s>>>(n, len, node, base, src, buf);
-    HIP_LAUNCH_CHECK();
-}
-
-void launch_rows_unpack(int64_t n, int len, const int* node, const int64_t* base, const double* buf, double* dst,
-                        hipStream_t s) {
-    if (n <= 0) return;
-    k_rows_unpack<<<blocks_for(n * len, 256), 256, 0, s>>>(n, len, node, base, buf, dst);
+    if (pack) k_ox<true><<<blocks_for(n, 256), 256, 0, s>>>(a);
+    else k_ox<false><<<blocks_for(n, 256), 256, 0, s>>>(a);
     HIP_LAUNCH_CHECK();
 }
 

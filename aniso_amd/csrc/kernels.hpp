@@ -201,9 +201,6 @@ struct HcArgs {
     const int* haloPtr = nullptr;
     const int* haloPos = nullptr;
     double* hpart = nullptr;
-    // host: the cluster launch's LDS at least this (bytes): fewer cluster workgroups per
-    // CU, so a near-field workgroup fits beside them (ANISO_HM_MIN_LDS, A/B runs)
-    int minLds = 0;
 };
 // The fused top-of-tree + clustered M2L launch (harmonic.hip k_top_m2l_hc, DESIGN.md
 // §3.10): blocks 0 .. nUp - 1 run the up tasks of tiers 1 .. ntier - 1 (tier k's
@@ -300,6 +297,11 @@ struct NearHsArgs {
     const int* grpInPtr = nullptr;
     const int* grpIn = nullptr;
     int grpSlots = 0;
+    // the 16-leaf groups to run (ngrp of them; nullptr: all, in order): a sharded
+    // apply's one-collective form runs the groups that read only the own range before
+    // the exchange and the rest after it (Plan::nearGrpEarly / nearGrpLate)
+    const int* grpList = nullptr;
+    int ngrp = 0;
 };
 bool top_fused_enabled();
 // near: the staged near field with its corrections fused (near_hs_fusable) as the
@@ -344,14 +346,33 @@ void launch_halo_pack(int64_t n, int nb, const int64_t* pos, const int64_t* base
                       const double* x, int64_t ldx, double* buf, hipStream_t s);
 void launch_halo_unpack(int64_t n, int nb, const int64_t* pos, const int64_t* base, const int64_t* stride,
                         const double* buf, double* x, int64_t ldx, hipStream_t s);
-// n parts of len doubles: dst + dstOff[j] <- src + srcOff[j] (srcOff nullptr: src)
-void launch_parts_copy(int64_t n, int64_t len, const int64_t* srcOff, const int64_t* dstOff, const double* src,
-                       double* dst, hipStream_t s);
-// the one-collective exchange's multipole rows (node[j]'s len doubles <-> buf + base[j])
-void launch_rows_pack(int64_t n, int len, const int* node, const int64_t* base, const double* src, double* buf,
-                      hipStream_t s);
-void launch_rows_unpack(int64_t n, int len, const int* node, const int64_t* base, const double* buf, double* dst,
-                        hipStream_t s);
+// the one-collective exchange's pack (send) or unpack (receive) in one launch: root
+// records (nRoot parts of rec doubles at rootOff in buf; unpack: to rootDst in roots,
+// and this rank's own record from ownRoots), input positions (pos / base / stride as
+// the halo exchange, nb blocks of x), multipole rows (node / nodeBase, len doubles)
+struct OxArgs {
+    int64_t nRoot = 0, rec = 0;
+    const int64_t* rootOff = nullptr;
+    const int64_t* rootDst = nullptr;
+    double* roots = nullptr;           // pack: this rank's records (read); unpack: the slot layout (written)
+    const double* ownRoots = nullptr;  // unpack: this rank's records, copied to its own slot
+    int64_t ownDst = 0;
+    int64_t nPts = 0;
+    int nb = 0;
+    const int64_t* pos = nullptr;
+    const int64_t* base = nullptr;
+    const int64_t* stride = nullptr;
+    double* x = nullptr;
+    int64_t ldx = 0;
+    int64_t nNode = 0;
+    int len = 0;
+    const int* node = nullptr;
+    const int64_t* nodeBase = nullptr;
+    double* mult = nullptr;
+    double* buf = nullptr;
+};
+void launch_ox(const OxArgs& a, bool pack, hipStream_t s);
+
 
 // host-callable device helpers used by tests through the C ABI
 void launch_line_integrals(int n, const double* seg, const double* stcoef, const Params* P, double* out,
