@@ -1048,11 +1048,12 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
 // coalesced, and every column then reads its source from LDS by its 16-bit row
 // (nearLoc).  Only the E stream stays in HBM.  Same lane layout as k_near_hm<G=16>.
 
-// Table row stride: x, y, the charges, rounded up to an odd number of doubles, so the
+// Table row stride: x, y, the K charges, rounded up to an odd number of doubles, so the
 // up to 16 different rows one wave reads at a time fall on different LDS banks (an
-// even stride of 8 doubles put every 4th row on the same banks).
+// even stride of 8 doubles put every 4th row on the same banks).  K = 5: 7 doubles
+// (not 9), so a 16-leaf group's table takes 32 KB instead of 41 KB at 1M points.
 template <int K>
-constexpr int kTabRow = (kStride<K> + 2) | 1;
+constexpr int kTabRow = (K + 2) | 1;
 
 template <int K, int U, int NR, bool FUSE, bool SYM>
 __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, double* tab) {
