@@ -1146,9 +1146,8 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
         for (int i = 0; i < K; ++i) a[j][i] = 0.0;
     if (rowOk) {
         const dbl2* kc = reinterpret_cast<const dbl2*>(E + koff) + 2 * rq;
-        for (int c0 = cph; c0 < S; c0 += U * 4) {
-            dbl2 kk[U][2];
-            int ix[U];
+        // U columns per lane and step: their E quads (16 B x 2) and table rows
+        auto fetch = [&](int c0, dbl2 (&kk)[U][2], int (&ix)[U]) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int sc = c0 + u * 4;
@@ -1158,6 +1157,8 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
                 kk[u][1] = ok ? __builtin_nontemporal_load(p + 1) : dbl2{0.0, 0.0};
                 ix[u] = nearLoc[pb + min(sc, S - 1)];
             }
+        };
+        auto step = [&](const dbl2 (&kk)[U][2], const int (&ix)[U]) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const double* row = tab + (size_t)ix[u] * RW;
@@ -1172,6 +1173,12 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
                     hm_entry<K, true, NR>(e4[j], sx - tx[j], dy * dy, xw, a[j]);
                 }
             }
+        };
+        for (int c0 = cph; c0 < S; c0 += U * 4) {
+            dbl2 kk[U][2];
+            int ix[U];
+            fetch(c0, kk, ix);
+            step(kk, ix);
         }
     }
     if constexpr (SYM) if (sym && active) {
