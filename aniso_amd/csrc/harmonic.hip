@@ -83,12 +83,15 @@ __device__ __forceinline__ void cheb_T(double c, double (&T)[K]) {
 }
 
 // One entry: E at (dx, dy) from the source, harmonic-weighted source charges xw;
-// o[i] += T_i(c) (E / r) V.  guard0: r = 0 possible (near field), the entry adds 0.
+// o[i] += T_i(c) (E / r) V.  guard0: r = 0 possible (near field): r^2 is raised to
+// 1e-300 there, so 1/r stays finite and the entry adds exactly 0 through E = 0 (the
+// mode-shared cache stores 0 at r = 0, kernels.hip pair_kernel): one v_max_f64
+// instead of a compare and two selects per entry, the same bits elsewhere.
 template <int K, bool guard0, int NR = 2>
 __device__ __forceinline__ void hm_entry(double e, double dx, double dy2, const double (&xw)[K], double (&o)[K]) {
-    const double r2 = __builtin_fma(dx, dx, dy2);
-    double ri = rsqrt_nr<NR>(r2);
-    if constexpr (guard0) ri = r2 > 0.0 ? ri : 0.0;
+    double r2 = __builtin_fma(dx, dx, dy2);
+    if constexpr (guard0) r2 = __builtin_fmax(r2, 1e-300);
+    const double ri = rsqrt_nr<NR>(r2);
     const double c = dx * ri;
     double T[K];
     cheb_T<K>(c, T);
