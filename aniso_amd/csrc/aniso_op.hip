@@ -91,6 +91,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_NEAR_IN_TOP")) nearInTop = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_EARLY")) nearEarly = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_ONE_EXCHANGE")) oneXOn = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ANISO_NEAR_ORDER")) nearOrderUp = std::strcmp(e, "first") != 0;
     hmRing = hm_ring_depth();
     if (const char* e = std::getenv("ANISO_HM_WPE")) hmWpe = std::atoi(e);
     if (const char* e = std::getenv("ANISO_NEAR_WPE")) nearWpe = std::atoi(e);
@@ -934,10 +935,17 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             nearStage();
             if (!fork && tm) e0 = mark(s);
         }
+        // the fork point is the start of the apply, but the near field's launch is issued
+        // after the bottom up tier's, so the dispatcher tends to hand the up tasks their
+        // workgroup slots first (0.6-1.2 % per block matvec on one GPU, 1.6 % on a rank
+        // of 8, r04z; ANISO_NEAR_ORDER=first issues it first)
+        const bool nearAfterUp = nearIn && !oneX && fork && nearOrderUp && phase == 0 && ntier >= 1;
         if (nearIn && !oneX) {  // the near field first: beside the up pass (fork) or before it (serial)
             if (fork) HIP_CHECK(hipEventRecord(evFork, s));
-            nearStage();
-            nearDone = true;
+            if (!nearAfterUp) {
+                nearStage();
+                nearDone = true;
+            }
             if (!fork && tm) e0 = mark(s);  // serial: the up span starts after the near field
         }
         if (ntier < 1) {  // a lone leaf: no up pass
@@ -949,7 +957,13 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             if (oneX) upTier(0, dXOwnT0Tasks.as<int>(), (int)plan.xOwnT0Tasks.size(), nullptr, rootsSend);
             else upTier(0, dXT0Tasks.as<int>(), (int)plan.xT0Tasks.size(), nullptr, rootsSend);
         }
-        for (int k = 0; k < (topFused ? 1 : ntier) && phase == 0; ++k) upTier(k, nullptr, tierTasks(k), nullptr, nullptr);
+        for (int k = 0; k < (topFused ? 1 : ntier) && phase == 0; ++k) {
+            upTier(k, nullptr, tierTasks(k), nullptr, nullptr);
+            if (k == 0 && nearAfterUp) {
+                nearStage();
+                nearDone = true;
+            }
+        }
         if (phase == 1) {
             const int ep = tm ? mark(s) : -1;
             span(1, e0, ep);

@@ -240,6 +240,7 @@ private:
     // the staged near field forms its charges from the input and forks at the start
     // of the block apply, beside the up pass (ANISO_NEAR_EARLY=0: after it, from fT)
     bool nearEarly = true;
+    bool nearOrderUp = true;  // the near launch issued after the bottom up tier's (ANISO_NEAR_ORDER=first: before)
     int topTraceBlocks = 0, topTraceNear = 0;
     // the attached communicator and its halo exchange plan (commInit): per element of
     // the send / receive position lists its tree position and its place in the

@@ -729,7 +729,7 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
                                   "ANISO_NEAR_IN_TOP=1", "ANISO_NEAR_WPE=4", "ANISO_TOP_FUSED=0", "ANISO_HM_HALO=0",
                                   "ANISO_NEAR_EARLY=0", "ANISO_NEAR_EARLY=0,ANISO_OVERLAP=0", "ANISO_NEAR_HS_SYM=1",
                                   "ANISO_NEAR_HS_SYM=1,ANISO_NEAR_EARLY=0", "ANISO_NEAR_HS_SYM=1,ANISO_OVERLAP=0",
-                                  "ANISO_NEAR_HS_SYM=1,ANISO_TOP_FUSED=0"])
+                                  "ANISO_NEAR_HS_SYM=1,ANISO_TOP_FUSED=0", "ANISO_NEAR_ORDER=first"])
 def test_block_matvec_knobs_agree(knob, monkeypatch):
     """Every remaining environment knob of the block apply:
     the serial near/M2L order, the separate x - mforward(x) subtraction and the
