@@ -986,7 +986,7 @@ void launch_sub_slice(int64_t n, int nrhs, const double* x, int64_t ldx, const d
 
 size_t up_tier_lds(int maxTask, int K) {
     return (size_t)(4 * kRank * kRank + maxTask * (kRank * K + 4)) * sizeof(double) +
-           (size_t)3 * maxTask * sizeof(int) + (size_t)maxTask * sizeof(int4);
+           (size_t)7 * maxTask * sizeof(int) + (size_t)maxTask * sizeof(int4);  // LB, LC, ND, RS (4 per node)
 }
 
 size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain, int K) {

@@ -276,7 +276,7 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
             const int bspan = 3;  // levels of the bottom tier (3: 4x the tasks at 1/4 the LDS; down 0.124 -> 0.090 ms, r01g)
             tierRootLevel.push_back(std::max(1, D - (bspan - 1)));
             tierBottomLevel.push_back(D);
-            const int span = 2;  // levels per upper tier (1, 3 and 4 measured equal or slower, r01g)
+            const int span = 2;  // levels per upper tier (1, 3 and 4 measured equal or slower, r01g; 3 and 4 on a rank of 8 +9 % / +35 %, r04ac)
             while (tierRootLevel.back() > 1) {
                 tierBottomLevel.push_back(tierRootLevel.back() - 1);
                 tierRootLevel.push_back(std::max(1, tierRootLevel.back() - span));

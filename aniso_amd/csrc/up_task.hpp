@@ -53,6 +53,7 @@ __device__ __forceinline__ void up_task(
     int* LB = reinterpret_cast<int*>(G + (size_t)maxTask * 4);  // maxTask: leaf point offset, count, node
     int* LC = LB + maxTask;
     int* ND = LC + maxTask;
+    int* RS = ND + maxTask;  // recv: per (node, child) the gathered record slot of a tier-0 root child (-1: none)
     const int4 d = desc[task];  // first node, nodes, first point, levels
     const int n0 = d.x, nt = d.y, ngrp = d.w;
     const int64_t b0 = d.z;
@@ -76,14 +77,27 @@ __device__ __forceinline__ void up_task(
         ND[k] = node[n0 + k];
     }
     __syncthreads();
-    if (recv) {  // the gathered tier-0 roots under this task: stored for the M2L (all lanes, coalesced)
-        for (int it = threadIdx.x; it < nt * 4 * kRank * K; it += blockDim.x) {
-            const int k = it / (4 * kRank * K), q = (it / (kRank * K)) & 3, e = it % (kRank * K);
-            const int4 c = CD[k];
+    if (recv) {
+        // the gathered tier-0 roots under this task: their record slots in one round of
+        // independent loads, then the records stored for the M2L (all lanes, coalesced;
+        // the slot lookup inside the copy loop made every iteration two dependent
+        // round trips: 42 us per 5-node task on a rank of 8, r04ab)
+        for (int i = threadIdx.x; i < nt * 4; i += blockDim.x) {
+            const int4 c = CD[i >> 2];
+            const int q = i & 3;
             const int cq = q == 0 ? c.x : q == 1 ? c.y : q == 2 ? c.z : c.w;
-            if (c.x == kLeafCode || cq >= -1) continue;
-            const int rs = rootSlot[-cq - 2];
-            if (rs >= 0) mult[(size_t)(-cq - 2) * kRank * K + e] = recv[(size_t)rs * kRank * K + e];
+            RS[i] = (c.x == kLeafCode || cq >= -1) ? -1 : rootSlot[-cq - 2];
+        }
+        __syncthreads();
+        constexpr int RK = kRank * K;
+        for (int it = threadIdx.x; it < nt * 4 * RK; it += blockDim.x) {
+            const int i = it / RK, e = it - i * RK;
+            const int rs = RS[i];
+            if (rs < 0) continue;
+            const int4 c = CD[i >> 2];
+            const int q = i & 3;
+            const int cq = q == 0 ? c.x : q == 1 ? c.y : q == 2 ? c.z : c.w;
+            mult[(size_t)(-cq - 2) * RK + e] = recv[(size_t)rs * RK + e];
         }
     }
     // P2M of the task's leaves (bbfmm.h:737-748): 16 lanes per leaf, one point per
@@ -182,7 +196,7 @@ __device__ __forceinline__ void up_task(
                 const double* R = Rl + q * kRank * kRank + r;  // transposed: R[rr * 16 + r]
                 const double* cm = M + (size_t)(cq >= 0 ? cq : 0) * kRank * K;  // child in this task (LDS)
                 if (cq < 0) {  // root of the tier below: HBM (or the gathered records)
-                    const int rs = recv ? rootSlot[-cq - 2] : -1;
+                    const int rs = recv ? RS[4 * k + q] : -1;
                     cm = rs >= 0 ? recv + (size_t)rs * kRank * K : mult + (size_t)(-cq - 2) * kRank * K;
                 }
 #pragma unroll
