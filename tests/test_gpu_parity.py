@@ -1573,9 +1573,10 @@ class _ThreadCollectives:
         return self._guard(run)
 
 
-@pytest.mark.parametrize("sz,world,one", [(64, 2, "1"), (64, 2, "0"), (64, 4, "1"), (64, 8, "1"), (64, 3, "1"),
-                                          (96, 3, "1")])
-def test_native_exchange_ranks_as_threads(sz, world, one, monkeypatch):
+@pytest.mark.parametrize("sz,world,one,d,ml", [(64, 2, "1", 1, 20), (64, 2, "0", 1, 20), (64, 4, "1", 1, 20),
+                                               (64, 8, "1", 1, 20), (64, 3, "1", 1, 20), (96, 3, "1", 1, 20),
+                                               (40, 2, "1", 1, 3), (32, 2, "1", 2, 20)])
+def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     """The library's one-call sharded block matvec (aniso_block_op_sharded_dev) with
     `world` ranks as threads of one process on the box's GPU, each rank's input valid
     only at its own range (NaN elsewhere), the collectives host-staged between the
@@ -1583,7 +1584,8 @@ def test_native_exchange_ranks_as_threads(sz, world, one, monkeypatch):
     multipoles below the root level and the input the rank reads from each owner in
     one grouped exchange) and, with ANISO_ONE_EXCHANGE=0 or where the cuts split a
     tier-0 subtree, the two-collective one; the owned slices equal the unsharded
-    matvec."""
+    matvec.  The maxLevel-limited tree (leaves above 16 points: no staged near field)
+    and d = 2 (no fused corrections) take the two-collective form by themselves."""
     torch = _torch()
     import threading
 
@@ -1591,7 +1593,7 @@ def test_native_exchange_ranks_as_threads(sz, world, one, monkeypatch):
 
     monkeypatch.setenv("ANISO_ONE_EXCHANGE", one)
     ks = 5
-    full = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
+    full = aniso_amd.Aniso(sz, d, ks, 0.8, 10, 4, ml)
     xy = full.getNodes()
     coef = rough_coeffs(xy, 2)
     full.setCoeff(*coef)
@@ -1603,13 +1605,14 @@ def test_native_exchange_ranks_as_threads(sz, world, one, monkeypatch):
     torch.cuda.synchronize()
     hs = []
     for r in range(world):
-        h = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
+        h = aniso_amd.Aniso(sz, d, ks, 0.8, 10, 4, ml)
         h.set_shard(r, world)
         h.setCoeff(*coef)
         for m in range(2 * ks - 1):
             h.cache(m)
         hs.append(h)
     oks = [h.shard_exchange_one()["ok"] for h in hs]
+    staged = d == 1 and ml == 20  # the harmonic near field from the input, fused corrections
     shared = dict(bar=threading.Barrier(world, timeout=60), slot=[None] * world, errors=[])
     colls = [_ThreadCollectives(world, r, shared) for r in range(world)]
     outs = [None] * world
@@ -1640,4 +1643,4 @@ def test_native_exchange_ranks_as_threads(sz, world, one, monkeypatch):
     assert not torch.isnan(Y).any()
     assert float(torch.linalg.norm(Y - ref) / torch.linalg.norm(ref)) <= 1e-13
     used = [h.stats()["one_exchange_applies"] for h in hs]
-    assert used == [2 * int(one == "1" and all(oks))] * world
+    assert used == [2 * int(one == "1" and all(oks) and staged)] * world
