@@ -1513,7 +1513,10 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
 
 // near field: 16 lanes per leaf for leaves <= 16 points (4 leaves per wave), a wave
 // per leaf otherwise; 4 source columns in flight per lane (2 and 8, XCD-contiguous
-// leaves and leaf clusters measured slower, r01h); 1/r to full fp64 (two Newton steps)
+// leaves and leaf clusters measured slower, r01h); 1/r to full fp64 (two Newton steps).
+// The staged kernel k_near_hs takes 2 columns per step: 121 VGPRs, so 4 waves per
+// SIMD fit beside its 32 KB source table (standalone 3-6 % faster than 4 columns at 3
+// waves, r04ak)
 static bool near_hs_staged(int nl, int maxLeaf, int nsMax, const uint16_t* nearLoc) {
     return nl > 0 && maxLeaf <= 16 && nsMax > 0 && nearLoc && (size_t)nsMax * kTabRow<8> * sizeof(double) <= 64 * 1024;
 }
@@ -1564,8 +1567,8 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
         ANISO_HM_DISPATCH_K(K, ({
             const size_t shm = near_hs_lds<KK>(n);
             auto f = n.colDst ? (fuse ? k_near_hs<KK, 4, 2, true, false, true> : k_near_hs<KK, 4, 2, false, false, true>)
-                     : fuse ? (wpe == 4 ? k_near_hs<KK, 4, 2, true, true> : k_near_hs<KK, 4, 2, true>)
-                            : (wpe == 4 ? k_near_hs<KK, 4, 2, false, true> : k_near_hs<KK, 4, 2, false>);
+                     : fuse ? (wpe == 4 ? k_near_hs<KK, 2, 2, true, true> : k_near_hs<KK, 2, 2, true>)
+                            : (wpe == 4 ? k_near_hs<KK, 2, 2, false, true> : k_near_hs<KK, 2, 2, false>);
             f<<<ng, 256, shm, s>>>(n);
         }));
         HIP_LAUNCH_CHECK();
