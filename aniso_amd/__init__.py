@@ -656,7 +656,8 @@ class Aniso:
         _check(lib().aniso_set_deterministic(self.address, int(bool(on))))
 
     def set_timing(self, on):
-        _check(lib().aniso_set_timing(self.address, int(bool(on))))
+        """0/False off, 1/True every stage, 2 the M2L and near-field spans only."""
+        _check(lib().aniso_set_timing(self.address, int(on)))
 
     def stage_times(self):
         t = (ctypes.c_float * 8)()

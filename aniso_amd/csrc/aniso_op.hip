@@ -772,9 +772,10 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         down_tier_lds(plan.dnMaxTask, plan.dnMaxLeaves, plan.dnMaxNear, plan.dnMaxChain, K) > 160 * 1024)
         throw std::logic_error("up/down pass task exceeds one workgroup's LDS at " + std::to_string(K) + " right-hand sides");
     const Params* P = dParams.as<Params>();
-    const bool tm = timeStages;
+    const bool tr = timeStages != 0;  // the roofline spans: M2L (stage 2), near field (4)
+    const bool tm = timeStages == 1;  // every stage
     auto span = [&](int stage, int a, int b) {
-        if (tm) spans.push_back({stage, a, b});
+        if (a >= 0 && b >= 0) spans.push_back({stage, a, b});
     };
     const int* operm = treeOut ? nullptr : dPerm.as<int>();
     const int64_t obase = treeOut ? plan.ownBegin : 0;
@@ -858,7 +859,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     // near field + corrections (they need only fT / cT, or with nearIn the input)
     auto nearStage = [&] {
         if (fork) HIP_CHECK(hipStreamWaitEvent(side, evFork, 0));
-        const int en = tm ? mark(sn) : -1;
+        const int en = tr ? mark(sn) : -1;
         bool corrFused = false;
         if (harmonic) {
             // the corrections ride in the staged near kernel (d = 1, its table holds
@@ -885,7 +886,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                         dNearPts.as<int>(), dNearKOff.as<int64_t>(), tab, nterm, dFT.as<double>(), operm, obase, ldo,
                         mask, scale, 0, out, s);
         }
-        const int e1 = tm ? mark(sn) : -1;
+        const int e1 = tr ? mark(sn) : -1;
         span(4, en, e1);
         if (!corrFused)
             launch_corr(K, geo.d, plan.ownBegin, plan.ownEnd, dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
@@ -1003,12 +1004,12 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         }
         e0 = ex;  // the up span of phase 2: upper tiers
     }
-    int ep = tm ? mark(s) : -1;
+    int ep = tr ? mark(s) : -1;
     span(1, e0, ep);
     if (phase == 2) e0 = pend.e0;
     if (!nearDone && !nearFused) {
         nearStage();
-        if (tm && sn == s) ep = mark(s);  // serial (ANISO_OVERLAP=0): the M2L span starts after the near field
+        if (tr && sn == s) ep = mark(s);  // serial (ANISO_OVERLAP=0): the M2L span starts after the near field
     }
     if (mask & kStageFar) {
         if (topFused) {
@@ -1055,7 +1056,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                        dMult.as<double>(), plan.m2lMaxCanon, dM2LPart.as<double>(), dLocal.as<double>(), s);
         }
     }
-    int e = tm ? mark(s) : -1;
+    int e = tr ? mark(s) : -1;
     span(2, ep, e);
     ep = e;
     if (!harmonic && (mask & kStageFar) && plan.m2lCanon > 0) {
@@ -1077,8 +1078,8 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                          (harmonic ? hsSym : plan.nearPartTotal > 0) ? dNearPart.as<double>() : nullptr,
                          dDnChain.as<int2>(), plan.dnMaxChain, mask, scale, out, subX, subLd,
                          s, halo && clustered ? dHmPart.as<double>() : nullptr, dDnChainFold.as<int>());
-    if (tm) {
-        const int e2 = mark(s);
+    if (tr) {
+        const int e2 = tm ? mark(s) : -1;
         span(5, ep, e2);
         span(7, e0, e2);
         ++applies;
@@ -1178,9 +1179,10 @@ void Operator::blockOpHost(int which, const double* u, const double* sigmaS, dou
     checkDeviceErrors();
 }
 
-void Operator::setTiming(bool on) {
-    timeStages = on;
-    if (on) {
+void Operator::setTiming(int level) {
+    if (level < 0 || level > 2) throw std::invalid_argument("timing level must be 0, 1 or 2");
+    timeStages = level;
+    if (level) {
         evUsed = 0;
         spans.clear();
         applies = 0;

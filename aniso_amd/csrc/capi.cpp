@@ -593,7 +593,7 @@ int aniso_stats(aniso_handle h, int64_t* s) {
 
 int aniso_set_timing(aniso_handle h, int on) {
     ENTER(h);
-    return guarded([&] { get(h).setTiming(on != 0); });
+    return guarded([&] { get(h).setTiming(on); });  // 0 off, 1 every stage, 2 M2L + near only
 }
 
 int aniso_stage_times(aniso_handle h, float* t) {

@@ -68,7 +68,9 @@ int aniso_stats(aniso_handle h, int64_t *stats);
  * (HIP events recorded in-stream, 8 floats): exchange (between the two phases of a
  * sharded apply: the caller's root all-gather; 0 otherwise), up (weighted charges +
  * P2M/M2M tiers), m2l, gather (transposed M2L products), near, down (L2L/L2P tiers + transposed
- * near products), corr, total.  A block apply sums each stage over its mode terms. */
+ * near products), corr, total.  A block apply sums each stage over its mode terms.
+ * aniso_set_timing(h, 2) records the m2l and near spans only (the others read 0):
+ * fewer in-stream events inside a timed region.  Other levels: ANISO_ERR_INVALID. */
 int aniso_set_timing(aniso_handle h, int on);
 int aniso_stage_times(aniso_handle h, float *t8);
 /* development: the per-block timeline of the last fused top-of-tree launch, recorded

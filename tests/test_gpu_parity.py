@@ -1042,6 +1042,38 @@ def test_fused_top_of_tree_launch_matches_tier_launches(ks):
     assert _rel(outs[0], outs[1]) <= 1e-13 and _rel(outs[2], outs[1]) <= 1e-13
 
 
+def test_stage_timer_levels():
+    """aniso_set_timing: level 1 times every stage, level 2 (bench.py's timed region)
+    only the M2L and near-field spans; the output is the same at every level, and a
+    level outside 0..2 is ANISO_ERR_INVALID."""
+    torch = _torch()
+    import aniso_amd
+
+    a = aniso_amd.Aniso(128, 1, 5, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    a.setCoeff(*rough_coeffs(xy, 6))
+    for m in range(9):
+        a.cache(m)
+    U = torch.tensor(np.random.default_rng(4).uniform(-1, 1, (5, a.N)), device="cuda")
+    outs, times = [], []
+    for level in (0, 1, 2):
+        a.set_timing(level)
+        out = torch.zeros_like(U)
+        for _ in range(2):
+            a.block_op_dev(2, U, out)
+        a.sync()
+        times.append(a.stage_times())
+        a.set_timing(0)
+        outs.append(out.cpu().numpy())
+    assert _rel(outs[1], outs[0]) <= 1e-13 and _rel(outs[2], outs[0]) <= 1e-13
+    full, roof = times[1], times[2]
+    assert all(full[k] > 0 for k in ("up", "m2l", "near", "down", "total"))
+    assert roof["m2l"] > 0 and roof["near"] > 0
+    assert all(roof[k] == 0 for k in ("exchange", "up", "gather", "down", "corr", "total"))
+    with pytest.raises(aniso_amd.AnisoError):
+        a.set_timing(3)
+
+
 @pytest.mark.parametrize("nv", [1, 7, 16, 17, 40, 60])
 def test_krylov_primitives_match_torch(nv):
     """aniso_krylov_dot / _update (the CGS2 sweeps of the block solve and of
