@@ -349,8 +349,8 @@ def cpu_baseline(args, coeffs, op, block_check):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)  # 50 x 1.2 ms: the steady state, seconds of run time
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="block", choices=["block", "mode0"])
     ap.add_argument("--sz", type=int, default=1024)
     ap.add_argument("--d", type=int, default=1)
