@@ -82,6 +82,7 @@ def lib():
             "aniso_tree_nodes": [P, ip, dp],
             "aniso_tree_list": [P, I, lp, ip],
             "aniso_stats": [P, lp],
+            "aniso_stats_n": [P, lp, I, ip],
             "aniso_set_timing": [P, I],
             "aniso_stage_times": [P, fp],
             "aniso_line_integrals": [P, dp, I, dp],
@@ -120,6 +121,16 @@ def lib():
             "aniso_krylov_dot": [P, I64, I, P, I64, P, P, P],
             "aniso_krylov_update": [P, I64, I, P, I64, P, P, P, I, P],
             "aniso_block_op_sharded_dev": [P, I, P, I64, P, I64, P],
+            "aniso_arnoldi_state_size": [I, lp],
+            "aniso_arnoldi_begin": [P, I64, I, P, I64, P, P, D, P, P],
+            "aniso_arnoldi_step": [P, I64, I, I, P, I64, P, P, P, P],
+            "aniso_arnoldi_project": [P, I64, I, P, I64, P, P, P],
+            "aniso_arnoldi_coef": [P, I, I, P, P, P],
+            "aniso_arnoldi_update": [P, I64, I, I, P, I64, P, P, P, P],
+            "aniso_arnoldi_column": [P, I, I, P, P, P, P],
+            "aniso_arnoldi_solution": [P, I64, I, I, P, I64, P, P, P],
+            "aniso_mapped_alloc": [ctypes.c_size_t, ctypes.POINTER(P), ctypes.POINTER(P)],
+            "aniso_mapped_free": [P],
             "aniso_memcpy": [P, P, ctypes.c_size_t],
         }
         for name, args in sig.items():
@@ -195,6 +206,28 @@ def _dev_rows(t, rows, cols, name):
             and t.stride(1) == 1 and t.shape[0] == rows and t.shape[1] >= cols and (rows == 1 or t.stride(0) >= cols)):
         raise AnisoError(1, f"{name} must be a ({rows}, >= {cols}) float64 CUDA tensor with unit column stride")
     return ctypes.c_void_p(t.data_ptr())
+
+
+class MappedStatus:
+    """A few doubles of pinned host memory mapped into the device (aniso_mapped_alloc):
+    kernels store a status word through .dev, the host reads .host after an event."""
+
+    def __init__(self, n=4):
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        _check(lib().aniso_mapped_alloc(8 * n, ctypes.byref(h), ctypes.byref(d)))
+        self._h, self.dev, self.n = h, d, n
+        self.host = np.ctypeslib.as_array(ctypes.cast(h, ctypes.POINTER(ctypes.c_double)), shape=(n,))
+
+    def close(self):
+        if self._h:
+            lib().aniso_mapped_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Aniso:
@@ -525,6 +558,78 @@ class Aniso:
                                          int(bool(dots)), ctypes.c_void_p(s)))
         return out
 
+    # ---- DCGS2 Arnoldi primitives (aniso_arnoldi_*).  V: (rows, n) float64
+    # CUDA tensor with unit inner stride (the Krylov vectors); w, x: n entries; state: from
+    # arnoldi_state(m); status: a MappedStatus (or None); red / out: float64 CUDA tensors.
+    def arnoldi_state(self, m):
+        import torch
+
+        n = ctypes.c_int64()
+        _check(lib().aniso_arnoldi_state_size(int(m), ctypes.byref(n)))
+        return torch.zeros(n.value, dtype=torch.float64, device="cuda")
+
+    @staticmethod
+    def _arn_v(V, rows):
+        import torch
+
+        if not (isinstance(V, torch.Tensor) and V.is_cuda and V.dtype == torch.float64 and V.dim() == 2
+                and V.stride(1) == 1 and V.shape[0] >= rows):
+            raise ValueError(f"V: float64 CUDA (>= {rows}, n) with unit inner stride")
+        return ctypes.c_void_p(V.data_ptr()), int(V.shape[1]), int(V.stride(0))
+
+    @staticmethod
+    def _arn_t(t, n, name):
+        import torch
+
+        if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()
+                and t.numel() >= n):
+            raise ValueError(f"{name}: contiguous float64 CUDA tensor of >= {n} entries")
+        return ctypes.c_void_p(t.data_ptr())
+
+    @staticmethod
+    def _arn_s(stream):
+        import torch
+
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream if stream is None else stream)
+
+    def arnoldi_begin(self, V, m, state, normb, rr=None, status=None, stream=None):
+        pv, n, ld = self._arn_v(V, 1)
+        _check(lib().aniso_arnoldi_begin(self.address, n, int(m), pv, ld, self._arn_t(state, 1, "state"),
+                                         None if rr is None else self._arn_t(rr, 1, "rr"), float(normb),
+                                         None if status is None else status.dev, self._arn_s(stream)))
+
+    def arnoldi_step(self, V, m, j, w, state, status=None, stream=None):
+        pv, n, ld = self._arn_v(V, j + 2)
+        _check(lib().aniso_arnoldi_step(self.address, n, int(m), int(j), pv, ld, self._arn_t(w, n, "w"),
+                                        self._arn_t(state, 1, "state"), None if status is None else status.dev,
+                                        self._arn_s(stream)))
+
+    def arnoldi_project(self, V, j, w, out, stream=None):
+        pv, n, ld = self._arn_v(V, j + 1)
+        _check(lib().aniso_arnoldi_project(self.address, n, int(j), pv, ld, self._arn_t(w, n, "w"),
+                                           self._arn_t(out, j + 1, "out"), self._arn_s(stream)))
+
+    def arnoldi_coef(self, m, j, state, red, stream=None):
+        _check(lib().aniso_arnoldi_coef(self.address, int(m), int(j), self._arn_t(state, 1, "state"),
+                                        self._arn_t(red, j + 1, "red"), self._arn_s(stream)))
+
+    def arnoldi_update(self, V, m, j, w, state, out, stream=None):
+        pv, n, ld = self._arn_v(V, j + 2)
+        _check(lib().aniso_arnoldi_update(self.address, n, int(m), int(j), pv, ld, self._arn_t(w, n, "w"),
+                                          self._arn_t(state, 1, "state"), self._arn_t(out, j + 2, "out"),
+                                          self._arn_s(stream)))
+
+    def arnoldi_column(self, m, j, state, red, status=None, stream=None):
+        _check(lib().aniso_arnoldi_column(self.address, int(m), int(j), self._arn_t(state, 1, "state"),
+                                          self._arn_t(red, j + 2, "red"), None if status is None else status.dev,
+                                          self._arn_s(stream)))
+
+    def arnoldi_solution(self, V, m, used, state, x, stream=None):
+        pv, n, ld = self._arn_v(V, max(int(used), 1))
+        _check(lib().aniso_arnoldi_solution(self.address, n, int(m), int(used), pv, ld,
+                                            self._arn_t(state, 1, "state"), self._arn_t(x, n, "x"),
+                                            self._arn_s(stream)))
+
     def comm_init_loopback(self):
         """Development: a loopback communicator (aniso_comm_init_loopback) to time one
         rank's schedule of an N-GPU run on one GPU; results are not the operator's."""
@@ -633,13 +738,15 @@ class Aniso:
         return ptr, idx
 
     def stats(self):
-        s = np.zeros(26, dtype=np.int64)
-        _check(lib().aniso_stats(self.address, s.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        s = np.zeros(32, dtype=np.int64)
+        n = ctypes.c_int()
+        _check(lib().aniso_stats_n(self.address, s.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(s),
+                                   ctypes.byref(n)))
         keys = ["near_entries", "m2l_entries", "m2l_pairs", "leaves", "m2l_targets", "tree_nodes", "max_leaf", "N",
                 "stored_near", "stored_m2l", "m2l_canon", "near_partial", "harmonic", "att_m2l_blocks",
                 "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "top_fused",
                 "plan_halo_slots", "plan_max_lds_slots", "plan_block_reads", "top_recoveries",
-                "near_hs_stored", "near_hs_partials", "one_exchange_applies"]
+                "near_hs_stored", "near_hs_partials", "one_exchange_applies", "mrhs_m2l_pairs"]
         return dict(zip(keys, (int(v) for v in s)))
 
     def sync(self):

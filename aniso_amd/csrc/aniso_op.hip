@@ -547,9 +547,10 @@ void Operator::mappingBatchedHost(const double* Q, int k, int id, double* Out) {
     const int64_t N = geo.N;
     bool mfma = k > 8 && plan.nranks == 1;
     if (mfma && !m64.count(id) && id >= 0 && id < kernelSize && modes[id].ready) {
+        // the plan first (mrhs64Bytes builds and uploads it), then the free HBM it leaves
+        const size_t need = mrhs64Bytes() + (size_t)64 * N * sizeof(double);  // + the four 16-column staging buffers
         size_t freeB = 0, totalB = 0;
         HIP_CHECK(hipMemGetInfo(&freeB, &totalB));
-        const size_t need = mrhs64Bytes() + (size_t)64 * N * sizeof(double);  // + the four 16-column staging buffers
         mfma = need + (size_t)(1ull << 30) <= freeB;  // keep a GiB of headroom
     }
     if (mfma) {
@@ -1575,7 +1576,7 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
             peerLists[r].halo.assign(src.xHalo.begin(), src.xHalo.end());
             peerLists[r].oneHalo.assign(src.xOneHalo.begin(), src.xOneHalo.end());
             peerLists[r].needNodes.assign(src.xNeedNodes.begin(), src.xNeedNodes.end());
-            peerLists[r].ok.assign(1, src.xOneOk ? 1.0 : 0.0);
+            peerLists[r].ok.assign(1, (r == me ? oneExchangeLocal() : src.xOneOk) ? 1.0 : 0.0);
         }
     }
     auto gatherList = [&](std::vector<double> PeerLists::*field, const std::vector<double>& mineV,
@@ -1666,7 +1667,11 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
     // all-gather of the counts and one of the lists) and its input ranges (as above)
     oxReady = false;
     std::vector<std::vector<double>> oksAll;
-    gatherList(&PeerLists::ok, std::vector<double>(1, plan.xOneOk ? 1.0 : 0.0), oksAll);
+    // every rank's shard- and process-dependent part of the decision (its plan, its
+    // staged near field, its knobs): the one-collective form only where all of them
+    // hold, so that oxReady, and with it the collectives each matvec issues, is the
+    // same on every rank (oneExchangeUsable adds only rank-independent checks)
+    gatherList(&PeerLists::ok, std::vector<double>(1, oneExchangeLocal() ? 1.0 : 0.0), oksAll);
     bool allOk = true;
     for (const auto& o : oksAll) allOk = allOk && !o.empty() && o[0] > 0.5;
     if (allOk) {  // every rank decides alike: all take part in the same collectives
@@ -1767,19 +1772,31 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
 
 // Can this sharded matvec take the one-collective exchange?  Its phase 1 must leave
 // nothing to the halo: the harmonic block apply with the near field formed from the
-// input (run in phase 2, after the exchange) and no padded right-hand sides.
-bool Operator::oneExchangeUsable(int which) {
-    if (!oxReady || !oneXOn || !plan.xOneOk || !rhs_supported(ks) || !nearEarly || nearInTop || !plan.nearCorrOk)
+// input (run in phase 2, after the exchange) and no padded right-hand sides -- exactly
+// applyBlock's `harmonic && nearIn` for this call.  The decision must be the same on
+// every rank (the ranks issue matching collectives), so it is split: the part that
+// depends on a rank's shard or process (oneExchangeLocal) is all-gathered at commInit
+// into oxReady; what is left here depends only on the problem (ks, g, which) and on
+// the mode caches, which every rank builds alike before a block matvec.
+bool Operator::oneExchangeLocal() const {
+    if (!plan.xOneOk || !oneXOn || !useAtt || !rhs_supported(ks) || !nearEarly || nearInTop || !plan.nearCorrOk ||
+        plan.nearPartTotal > 0)
         return false;
+    const NearCorr probe{dNearCorrRow.as<uint16_t>(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    return near_hs_fusable((int)plan.leaves.size(), plan.nearMaxLeaf, plan.nsMax, dNearLoc.as<uint16_t>(), &probe,
+                           kStageAll);
+}
+
+bool Operator::oneExchangeUsable(int which) {
+    if (!oxReady) return false;
+    if (!attReady)  // mode caches differ between ranks would split the decision: refuse before any collective
+        throw std::logic_error("sharded block operator before cache(): every rank caches its modes first");
     const int nm = 2 * ks - 1;
     const auto mix = blockMixes(ks, g, which != 0);
     std::vector<int> ids(nm);
     for (int m = 0; m < nm; ++m) ids[m] = m;
     HarmWeights hw;
-    if (!harmonicWeights(ks, nm, ids.data(), mix.data(), hw)) return false;
-    const NearCorr probe{dNearCorrRow.as<uint16_t>(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    return near_hs_fusable((int)plan.leaves.size(), plan.nearMaxLeaf, plan.nsMax, dNearLoc.as<uint16_t>(), &probe,
-                           kStageAll);
+    return harmonicWeights(ks, nm, ids.data(), mix.data(), hw);
 }
 
 void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, int64_t ldy, hipStream_t s) {
@@ -1860,7 +1877,7 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
 }
 
 void Operator::checkDeviceErrors() {
-    if (!topErr) return;
+    if (!topErr || ownTimeline) return;
     if (*(volatile unsigned*)topErr == 0) return;
     *(volatile unsigned*)topErr = 0;
     throw std::runtime_error(

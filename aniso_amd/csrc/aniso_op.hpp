@@ -20,6 +20,8 @@
 
 namespace aniso {
 
+int64_t arn_state_doubles(int m);  // the Arnoldi state block of restart length m (arnoldi.hpp)
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -136,6 +138,24 @@ public:
     void krylovDot(int64_t n, int nv, const double* V, int64_t ldv, const double* w, double* out, hipStream_t s);
     void krylovUpdate(int64_t n, int nv, const double* V, int64_t ldv, const double* c, double* w, double* out,
                       bool dots, hipStream_t s);
+    // DCGS2 Arnoldi primitives on a caller's state block (arnoldi.hpp; aniso_arnoldi_*):
+    // begin a cycle (V[0] = the residual; rr: its all-reduced |r|^2, or null: this rank's),
+    // one step on one rank, or its parts around a caller's all-reduces (project / update
+    // write this rank's row sums; coef / column take the reduced ones), and the cycle's
+    // update x += P T R^-1 g
+    void arnoldiBegin(int64_t n, int m, const double* V, int64_t ldv, double* st, const double* rr, double normb,
+                      double* status, hipStream_t s);
+    void arnoldiStep(int64_t n, int m, int j, double* V, int64_t ldv, const double* w, double* st, double* status,
+                     hipStream_t s);
+    void arnoldiProject(int64_t n, int j, const double* V, int64_t ldv, const double* w, double* out, hipStream_t s);
+    void arnoldiCoef(int m, int j, double* st, const double* red, hipStream_t s);
+    void arnoldiUpdate(int64_t n, int m, int j, double* V, int64_t ldv, const double* w, const double* st, double* out,
+                       hipStream_t s);
+    void arnoldiColumn(int m, int j, double* st, const double* red, double* status, hipStream_t s);
+    void arnoldiSolution(int64_t n, int m, int used, const double* V, int64_t ldv, double* st, double* x,
+                         hipStream_t s);
+    // directed M2L pairs of the 16-right-hand-side operators (0 before their plan is built)
+    int64_t mrhsM2LPairs() const { return mrhsPlanReady ? (int64_t)f32.m2lSrc.size() : 0; }
     int64_t f32Bytes() const { return f32Ready ? (int64_t)(d32Km2l.bytes + d32Knear.bytes) : 0; }
     hipStream_t stream() const { return own; }
     // raise (ANISO_ERR_RUNTIME) if a fused top-of-tree launch gave up waiting for its
@@ -149,6 +169,9 @@ public:
     int64_t topRecoveries = 0;  // applies re-run after a time-out (aniso_stats)
     int64_t oneXApplies = 0;    // sharded matvecs through the one-collective exchange (aniso_stats)
     bool forceUnfused = false;
+    // set while a call that recovers its own time-outs (the block solve) runs: the
+    // entry checks of the applies it enqueues leave the flag to its recovery points
+    bool ownTimeline = false;
     // wait for every apply enqueued by this handle (both streams), then check
     void sync();
     // development timeline of the last fused top-of-tree launch (ANISO_TOP_TRACE=1,
@@ -231,6 +254,7 @@ private:
     DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
     DevBuf dTopTrace;           // ANISO_TOP_TRACE=1: the launch's per-block timeline
     DevBuf dKryPart;            // partial sums of the Krylov primitives
+    void arnoldiParts(int rows);  // dKryPart for sweeps of `rows` rows
     bool topTraceOn = false;
     int hmRing = 0;  // the cluster M2L's LDS ring depth (ANISO_HM_RING; 0: the one-block-in-flight form)
     int hmWpe = 0;   // ANISO_HM_WPE=3/4/8: the one-block form's occupancy (0: 4 where LDS allows)
@@ -266,6 +290,7 @@ private:
     int64_t oxNsendPts = 0, oxNrecvPts = 0, oxNsendNodes = 0, oxNrecvNodes = 0;
     bool oxReady = false, oneXActive = false, oneXOn = true;
     bool oneExchangeUsable(int which);
+    bool oneExchangeLocal() const;  // this rank's (shard- and process-dependent) part, gathered at commInit
     // sticky time-out flag of the fused launch's in-kernel hand-offs, in host-visible
     // memory (the kernel stores 1 there when a wait gives up; checked at every API
     // entry and by sync(), never read on the device)

@@ -551,43 +551,65 @@ int aniso_tree_list(aniso_handle h, int which, int64_t* ptr, int* idx) {
     });
 }
 
+constexpr int kStatsV1 = 19, kStats = 27;
+
+static void stats_fill(aniso::Operator& op, int64_t* s) {
+    s[0] = op.nearEntries();
+    s[1] = op.m2lEntries();
+    s[2] = op.plan.pairsM2L;
+    s[3] = (int64_t)op.plan.leaves.size();
+    s[4] = (int64_t)op.plan.m2lTgt.size();
+    s[5] = op.tree.nn;
+    int64_t mx = 0;
+    for (int i = 0; i < op.tree.nn; ++i)
+        if (op.tree.isLeaf[i]) mx = std::max<int64_t>(mx, op.tree.count[i]);
+    s[6] = mx;
+    s[7] = op.geo.N;
+    s[8] = op.plan.storedNear;
+    s[9] = op.plan.storedM2L;
+    s[10] = op.plan.m2lCanon;
+    s[11] = op.plan.nearPartTotal;
+    s[12] = op.harmonicReady() ? 1 : 0;
+    s[13] = (int64_t)op.plan.attOwner.size();
+    const bool cl = op.harmonicReady() && op.clustersOn();
+    s[14] = cl ? (int64_t)op.plan.hmClPtr.size() - 1 : 0;
+    s[15] = cl ? op.plan.hmDual : 0;
+    s[16] = cl ? (int64_t)op.plan.hmSrc.size() : (int64_t)op.plan.attSrc.size();
+    s[17] = op.f32Bytes();  // config 5's fp32 operator caches (0 before its first apply)
+    s[18] = cl && op.topFusedOn() ? 1 : 0;
+    // the cluster plan itself (block handles; host-side, no GPU needed)
+    s[19] = (int64_t)op.plan.hmHaloNode.size();
+    s[20] = op.plan.hmMaxLds;
+    s[21] = (int64_t)op.plan.hmSrc.size();
+    s[22] = op.topRecoveries;
+    // the harmonic near field's symmetric U storage (0: directed, Plan::nearSymHsOn)
+    s[23] = op.plan.nearSymHsOn ? op.plan.hsStored : 0;
+    s[24] = op.plan.nearSymHsOn ? op.plan.hsPartTotal : 0;
+    s[25] = op.oneXApplies;  // sharded matvecs through the one-collective exchange
+    s[26] = op.mrhsM2LPairs();  // directed M2L pairs of the 16-RHS MFMA operators (0 before their plan)
+}
+
+// the round-2 entry: the first kStatsV1 entries only (callers sized for them)
 int aniso_stats(aniso_handle h, int64_t* s) {
     ENTER(h);
     return guarded([&] {
         CHECK_PTR(s);
-        auto& op = get(h);
-        s[0] = op.nearEntries();
-        s[1] = op.m2lEntries();
-        s[2] = op.plan.pairsM2L;
-        s[3] = (int64_t)op.plan.leaves.size();
-        s[4] = (int64_t)op.plan.m2lTgt.size();
-        s[5] = op.tree.nn;
-        int64_t mx = 0;
-        for (int i = 0; i < op.tree.nn; ++i)
-            if (op.tree.isLeaf[i]) mx = std::max<int64_t>(mx, op.tree.count[i]);
-        s[6] = mx;
-        s[7] = op.geo.N;
-        s[8] = op.plan.storedNear;
-        s[9] = op.plan.storedM2L;
-        s[10] = op.plan.m2lCanon;
-        s[11] = op.plan.nearPartTotal;
-        s[12] = op.harmonicReady() ? 1 : 0;
-        s[13] = (int64_t)op.plan.attOwner.size();
-        const bool cl = op.harmonicReady() && op.clustersOn();
-        s[14] = cl ? (int64_t)op.plan.hmClPtr.size() - 1 : 0;
-        s[15] = cl ? op.plan.hmDual : 0;
-        s[16] = cl ? (int64_t)op.plan.hmSrc.size() : (int64_t)op.plan.attSrc.size();
-        s[17] = op.f32Bytes();  // config 5's fp32 operator caches (0 before its first apply)
-        s[18] = cl && op.topFusedOn() ? 1 : 0;
-        // the cluster plan itself (block handles; host-side, no GPU needed)
-        s[19] = (int64_t)op.plan.hmHaloNode.size();
-        s[20] = op.plan.hmMaxLds;
-        s[21] = (int64_t)op.plan.hmSrc.size();
-        s[22] = op.topRecoveries;
-        // the harmonic near field's symmetric U storage (0: directed, Plan::nearSymHsOn)
-        s[23] = op.plan.nearSymHsOn ? op.plan.hsStored : 0;
-        s[24] = op.plan.nearSymHsOn ? op.plan.hsPartTotal : 0;
-        s[25] = op.oneXApplies;  // sharded matvecs through the one-collective exchange
+        int64_t all[kStats];
+        stats_fill(get(h), all);
+        std::copy(all, all + kStatsV1, s);
+    });
+}
+
+int aniso_stats_n(aniso_handle h, int64_t* s, int cap, int* n) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(n);
+        if (cap < 0) throw std::invalid_argument("aniso_stats_n: cap must be >= 0");
+        if (cap > 0) CHECK_PTR(s);
+        int64_t all[kStats];
+        stats_fill(get(h), all);
+        std::copy(all, all + std::min(cap, kStats), s);
+        *n = kStats;
     });
 }
 
@@ -673,6 +695,116 @@ int aniso_krylov_update(aniso_handle h, int64_t n, int nv, const double* V, int6
         CHECK_PTR(out);
         auto& op = get(h);
         op.krylovUpdate(n, nv, V, ldv, c, w, out, dots != 0, (hipStream_t)stream);
+    });
+}
+
+int aniso_arnoldi_state_size(int m, int64_t* doubles) {
+    return guarded([&] {
+        CHECK_PTR(doubles);
+        if (m < 1) throw std::invalid_argument("arnoldi: restart length m >= 1");
+        *doubles = aniso::arn_state_doubles(m);
+    });
+}
+
+int aniso_arnoldi_begin(aniso_handle h, int64_t n, int m, const double* V, int64_t ldv, double* state,
+                        const double* rr, double normb, double* status, void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(state);
+        if (!rr) CHECK_PTR(V);
+        get(h).arnoldiBegin(n, m, V, ldv, state, rr, normb, status, (hipStream_t)stream);
+    });
+}
+
+int aniso_arnoldi_step(aniso_handle h, int64_t n, int m, int j, double* V, int64_t ldv, const double* w,
+                       double* state, double* status, void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(V);
+        CHECK_PTR(w);
+        CHECK_PTR(state);
+        get(h).arnoldiStep(n, m, j, V, ldv, w, state, status, (hipStream_t)stream);
+    });
+}
+
+int aniso_arnoldi_project(aniso_handle h, int64_t n, int j, const double* V, int64_t ldv, const double* w,
+                          double* out, void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(V);
+        CHECK_PTR(w);
+        CHECK_PTR(out);
+        get(h).arnoldiProject(n, j, V, ldv, w, out, (hipStream_t)stream);
+    });
+}
+
+int aniso_arnoldi_coef(aniso_handle h, int m, int j, double* state, const double* red, void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(state);
+        CHECK_PTR(red);
+        get(h).arnoldiCoef(m, j, state, red, (hipStream_t)stream);
+    });
+}
+
+int aniso_arnoldi_update(aniso_handle h, int64_t n, int m, int j, double* V, int64_t ldv, const double* w,
+                         const double* state, double* out, void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(V);
+        CHECK_PTR(w);
+        CHECK_PTR(state);
+        CHECK_PTR(out);
+        get(h).arnoldiUpdate(n, m, j, V, ldv, w, state, out, (hipStream_t)stream);
+    });
+}
+
+int aniso_arnoldi_column(aniso_handle h, int m, int j, double* state, const double* red, double* status,
+                         void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(state);
+        CHECK_PTR(red);
+        get(h).arnoldiColumn(m, j, state, red, status, (hipStream_t)stream);
+    });
+}
+
+int aniso_arnoldi_solution(aniso_handle h, int64_t n, int m, int used, const double* V, int64_t ldv, double* state,
+                           double* x, void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(state);
+        if (used > 0) {
+            CHECK_PTR(V);
+            CHECK_PTR(x);
+        }
+        get(h).arnoldiSolution(n, m, used, V, ldv, state, x, (hipStream_t)stream);
+    });
+}
+
+int aniso_mapped_alloc(size_t bytes, void** host, void** dev) {
+    return guarded([&] {
+        CHECK_PTR(host);
+        CHECK_PTR(dev);
+        *host = *dev = nullptr;
+        if (bytes == 0) throw std::invalid_argument("aniso_mapped_alloc: bytes > 0");
+        hipError_t e = hipHostMalloc(host, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) aniso::throw_hip(e, __FILE__, __LINE__);
+        std::memset(*host, 0, bytes);
+        e = hipHostGetDevicePointer(dev, *host, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(*host);
+            *host = nullptr;
+            aniso::throw_hip(e, __FILE__, __LINE__);
+        }
+    });
+}
+
+int aniso_mapped_free(void* host) {
+    return guarded([&] {
+        if (!host) return;
+        const hipError_t e = hipHostFree(host);
+        if (e != hipSuccess) aniso::throw_hip(e, __FILE__, __LINE__);
     });
 }
 

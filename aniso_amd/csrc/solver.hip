@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "aniso_op.hpp"
+#include "arnoldi.hpp"
 #include "kernels.hpp"
 
 namespace aniso {
@@ -464,6 +465,100 @@ void Operator::krylovUpdate(int64_t n, int nv, const double* V, int64_t ldv, con
     else kr.updateNorm(nv, V, ldv, c, w, out);
 }
 
+// ---- DCGS2 Arnoldi on a never-rewritten basis (arnoldi.hpp): the library primitives
+// (aniso_arnoldi_*) and the block solve on them.  dKryPart holds the sweeps' partial
+// sums (arn::kParts per row).
+int64_t arn_state_doubles(int m) { return arn::Layout(m).total; }
+
+static void check_arnoldi(int m, int j) {
+    if (m < 1 || j < 0 || j >= m) throw std::invalid_argument("arnoldi: need 0 <= j < m");
+}
+
+void Operator::arnoldiParts(int rows) {
+    dKryPart.alloc(std::max(dKryPart.bytes, (size_t)arn::kParts * (rows + 2) * sizeof(double)));
+}
+
+void Operator::arnoldiBegin(int64_t n, int m, const double* V, int64_t ldv, double* st, const double* rr,
+                            double normb, double* status, hipStream_t s) {
+    if (m < 1 || n < 0 || ldv < n || !(normb > 0.0)) throw std::invalid_argument("arnoldi begin: bad sizes or |b|");
+    ensureDevice();
+    if (rr) {
+        arn::k_arn_begin<<<1, arn::kThreads, 0, s>>>(m, st, rr, 1, normb, status);
+        return;
+    }
+    arnoldiParts(1);
+    arn::launch_project(n, 1, V, ldv, V, dKryPart.as<double>(), s);
+    arn::k_arn_begin<<<1, arn::kThreads, 0, s>>>(m, st, dKryPart.as<double>(), arn::kParts, normb, status);
+}
+
+void Operator::arnoldiStep(int64_t n, int m, int j, double* V, int64_t ldv, const double* w, double* st,
+                           double* status, hipStream_t s) {
+    check_arnoldi(m, j);
+    if (n < 0 || ldv < n) throw std::invalid_argument("arnoldi step: bad sizes");
+    ensureDevice();
+    arnoldiParts(j + 2);
+    double* part = dKryPart.as<double>();
+    arn::launch_project(n, j + 1, V, ldv, w, part, s);
+    arn::k_arn_coef<<<1, arn::kThreads, arn::coef_lds(j), s>>>(m, j, st, part, arn::kParts);
+    arn::launch_update(n, j + 1, V, ldv, w, st, m, part, s);
+    arn::k_arn_column<<<1, arn::kThreads, arn::column_lds(j), s>>>(m, j, st, part, arn::kParts, status);
+}
+
+void Operator::arnoldiProject(int64_t n, int j, const double* V, int64_t ldv, const double* w, double* out,
+                              hipStream_t s) {
+    if (n < 0 || j < 0 || ldv < n) throw std::invalid_argument("arnoldi project: bad sizes");
+    ensureDevice();
+    arnoldiParts(j + 1);
+    arn::launch_project(n, j + 1, V, ldv, w, dKryPart.as<double>(), s);
+    arn::k_arn_rows<<<1, arn::kThreads, (size_t)(j + 1) * sizeof(double), s>>>(dKryPart.as<double>(), arn::kParts,
+                                                                                 j + 1, out);
+}
+
+void Operator::arnoldiCoef(int m, int j, double* st, const double* red, hipStream_t s) {
+    check_arnoldi(m, j);
+    ensureDevice();
+    arn::k_arn_coef<<<1, arn::kThreads, arn::coef_lds(j), s>>>(m, j, st, red, 1);
+}
+
+void Operator::arnoldiUpdate(int64_t n, int m, int j, double* V, int64_t ldv, const double* w, const double* st,
+                             double* out, hipStream_t s) {
+    check_arnoldi(m, j);
+    if (n < 0 || ldv < n) throw std::invalid_argument("arnoldi update: bad sizes");
+    ensureDevice();
+    arnoldiParts(j + 2);
+    arn::launch_update(n, j + 1, V, ldv, w, st, m, dKryPart.as<double>(), s);
+    arn::k_arn_rows<<<1, arn::kThreads, (size_t)(j + 2) * sizeof(double), s>>>(dKryPart.as<double>(), arn::kParts,
+                                                                                 j + 2, out);
+}
+
+void Operator::arnoldiColumn(int m, int j, double* st, const double* red, double* status, hipStream_t s) {
+    check_arnoldi(m, j);
+    ensureDevice();
+    arn::k_arn_column<<<1, arn::kThreads, arn::column_lds(j), s>>>(m, j, st, red, 1, status);
+}
+
+void Operator::arnoldiSolution(int64_t n, int m, int used, const double* V, int64_t ldv, double* st, double* x,
+                               hipStream_t s) {
+    if (m < 1 || used < 0 || used > m || n < 0 || ldv < n) throw std::invalid_argument("arnoldi solution: bad sizes");
+    ensureDevice();
+    if (used == 0) return;
+    arn::k_arn_solve<<<1, arn::kThreads, arn::solve_lds(used), s>>>(m, used, st);
+    if (n > 0)
+        arn::k_arn_axpy<<<nblk(n), arn::kThreads, (size_t)used * sizeof(double), s>>>(n, used, V, ldv,
+                                                                                        st + arn::Layout(m).y, x);
+}
+
+// aniso.m:159-173: u = gmres(A, rhs, restart, tol, maxit) with A(x) = x - mforward(x)
+// (aniso.m:155) on the nb = ks stacked blocks.  MATLAB's restarted GMRES semantics:
+// x0 = the given guess, at most maxit cycles of at most `restart` steps, converged
+// when ||rhs - A x|| / ||rhs|| <= tol (the estimate inside a cycle, confirmed by the
+// explicit residual at its end).  The vectors are permuted once into tree order and
+// every Krylov vector ((restart + 1) x ks x N doubles) stays in HBM; the Arnoldi
+// process is DCGS2 on the device (arnoldi.hpp): per step the matvec, two sweeps over
+// the basis and two one-block kernels; the host reads one status word per step
+// while the GPU already runs the next step's matvec.  rhs / x: device, original
+// order, block b at b * N.  Returns the total step count (negative if not converged);
+// hist gets the relative residual estimate after every step.
 int Operator::blockSolveDev(const double* rhs, double* x, int restart, double tol, int maxit, double* hist,
                             int maxhist, double* relresOut, hipStream_t s) {
     if (plan.nranks != 1) throw std::logic_error("block solve on a sharded handle");
@@ -475,44 +570,43 @@ int Operator::blockSolveDev(const double* rhs, double* x, int restart, double to
     checkDeviceErrors();
     const int64_t N = geo.N, L = (int64_t)ks * N;
     const int m = restart;
-    DevBuf bB, bX, bW, bR, bV, bPart, bH, bY;
+    const arn::Layout lay(m);
+    DevBuf bB, bX, bW, bV, bSt;
     bB.alloc(L * sizeof(double));
     bX.alloc(L * sizeof(double));
     bW.alloc(L * sizeof(double));
-    bR.alloc(L * sizeof(double));
     bV.alloc((size_t)(m + 1) * L * sizeof(double));
-    bPart.alloc((size_t)kMdotBlocks * (m + 2) * sizeof(double));
-    bH.alloc((size_t)(m + 2) * sizeof(double));  // Hessenberg column (m + 1 entries), then ||w||^2
-    bY.alloc((size_t)(m + 2) * sizeof(double));  // h2 (m + 1 entries), then ||w||^2
-    double *b = bB.as<double>(), *xt = bX.as<double>(), *w = bW.as<double>(), *r = bR.as<double>();
+    bSt.alloc((size_t)lay.total * sizeof(double));
+    arnoldiParts(m + 2);
+    double *b = bB.as<double>(), *xt = bX.as<double>(), *w = bW.as<double>();
     double* V = bV.as<double>();
-    double* hd = bH.as<double>();
+    double* st = bSt.as<double>();
     const int* perm = dPerm.as<int>();
     for (int k = 0; k < ks; ++k) {  // tree order: the operator needs no permutation gathers
         launch_permute(N, perm, rhs + (size_t)k * N, b + (size_t)k * N, s);
         launch_permute(N, perm, x + (size_t)k * N, xt + (size_t)k * N, s);
     }
-    Krylov kr{L, s, bPart.as<double>()};
-    // the Hessenberg column's host copy (pinned: an asynchronous read the host waits
-    // for with an event, not a stream drain)
-    struct HostCol {
+    // the status word {relres, r', steps} in mapped host memory: the column kernel
+    // stores it there and the host waits for an event behind it, not a stream drain
+    struct HostStat {
         double* p = nullptr;
         hipEvent_t ev = nullptr;
-        ~HostCol() {
+        ~HostStat() {
             if (p) (void)hipHostFree(p);
             if (ev) (void)hipEventDestroy(ev);
         }
-    } col;
-    HIP_CHECK(hipHostMalloc((void**)&col.p, (size_t)(m + 2) * sizeof(double), hipHostMallocDefault));
-    HIP_CHECK(hipEventCreateWithFlags(&col.ev, hipEventDisableTiming));
-    double* hcPinned = col.p;
-    hipEvent_t evH = col.ev;
-    auto norm2 = [&](const double* v) {  // ||v||^2 into hd[m + 1], returned on the host
-        kr.dot(1, v, L, v, hd + m + 1);
-        double h = 0;
-        HIP_CHECK(hipMemcpyAsync(&h, hd + m + 1, sizeof(double), hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipStreamSynchronize(s));
-        return h;
+    } hs;
+    HIP_CHECK(hipHostMalloc((void**)&hs.p, 4 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_CHECK(hipEventCreateWithFlags(&hs.ev, hipEventDisableTiming));
+    double* stat = nullptr;
+    HIP_CHECK(hipHostGetDevicePointer((void**)&stat, hs.p, 0));
+    auto post = [&] { HIP_CHECK(hipEventRecord(hs.ev, s)); };
+    auto sumsq = [&](const double* v) {  // |v|^2 on the host (once per solve)
+        arn::launch_project(L, 1, v, L, v, dKryPart.as<double>(), s);
+        arn::k_arn_rows<<<1, arn::kThreads, sizeof(double), s>>>(dKryPart.as<double>(), arn::kParts, 1, stat);
+        post();
+        HIP_CHECK(hipEventSynchronize(hs.ev));
+        return hs.p[0];
     };
     // a fused-launch time-out (recoverTopTimeout) re-runs the apply it spoiled on the
     // tier launches, and the rest of the solve keeps them
@@ -520,19 +614,26 @@ int Operator::blockSolveDev(const double* rhs, double* x, int restart, double to
         bool& f;
         bool v;
         ~Restore() { f = v; }
-    } restore{forceUnfused, forceUnfused};
-    auto residual = [&] {  // r = b - A x
-        blockOpDev(2, xt, N, w, N, true, s);
-        k_sub<<<nblk(L), 256, 0, s>>>(L, b, w, r);
-        double h = norm2(r);
-        if (recoverTopTimeout(s)) {
-            blockOpDev(2, xt, N, w, N, true, s);
-            k_sub<<<nblk(L), 256, 0, s>>>(L, b, w, r);
-            h = norm2(r);
+    } restore{forceUnfused, forceUnfused}, own{ownTimeline, ownTimeline};
+    ownTimeline = true;  // the look-ahead matvec may be enqueued after a spoiled one: recovered below
+    const double normb = std::sqrt(sumsq(b));
+    // A 0 = 0: a zero initial guess needs no matvec for its residual
+    bool xZero = normb > 0.0 && sumsq(xt) == 0.0;
+    // r = b - A x into V[0], then the cycle's start; returns |r| / |b|
+    auto residual = [&] {
+        for (int tries = 0;; ++tries) {
+            if (xZero) {
+                HIP_CHECK(hipMemcpyAsync(V, b, L * sizeof(double), hipMemcpyDeviceToDevice, s));
+            } else {
+                blockOpDev(2, xt, N, w, N, true, s);
+                k_sub<<<nblk(L), 256, 0, s>>>(L, b, w, V);
+            }
+            arnoldiBegin(L, m, V, L, st, nullptr, normb, stat, s);
+            post();
+            HIP_CHECK(hipEventSynchronize(hs.ev));
+            if (!recoverTopTimeout(s) || tries > 0) return hs.p[0];
         }
-        return std::sqrt(h);
     };
-    const double normb = std::sqrt(norm2(b));
     int nh = 0, total = 0;
     double relres = 0.0;
     bool conv = false;
@@ -540,85 +641,59 @@ int Operator::blockSolveDev(const double* rhs, double* x, int restart, double to
         HIP_CHECK(hipMemsetAsync(xt, 0, L * sizeof(double), s));
         conv = true;
     } else {
-        double beta = residual();
-        relres = beta / normb;
+        relres = residual();
         conv = relres <= tol;
-        const int ld = m + 1;
-        std::vector<double> H((size_t)ld * m, 0.0), g(ld, 0.0), cs(m, 0.0), sn(m, 0.0), hc(m + 2), y(m);
+        std::vector<double> hrel;
         for (int cyc = 0; cyc < maxit && !conv; ++cyc) {
-            if (beta == 0.0) break;
-            k_scale<<<nblk(L), 256, 0, s>>>(L, 1.0 / beta, r, V);
-            std::fill(g.begin(), g.end(), 0.0);
-            g[0] = beta;
+            if (hs.p[1] == 0.0) break;  // |r| = 0 in floating point
             int used = 0;
-            bool ahead = false;  // the matvec of V[i] is already enqueued
-            for (int i = 0; i < m; ++i) {
-                double* vi = V + (size_t)i * L;
-                // CGS2: h = V^T w, w -= V h, twice (the second pass adds its correction),
-                // as three sweeps over V: h; w -= V h with h2 = V^T w; w -= V h2 with
-                // ||w||^2; then the next basis vector and the column's host copy
-                auto orth = [&] {
-                    kr.dot(i + 1, V, L, w, hd);
-                    kr.updateDot(i + 1, V, L, hd, w, bY.as<double>());
-                    kr.updateNorm(i + 1, V, L, bY.as<double>(), w, hd + m + 1);
-                    k_axpby<<<nblk(i + 1), 256, 0, s>>>(i + 1, 1.0, bY.as<double>(), 1.0, hd);
-                    k_scale_rsqrt<<<nblk(L), 256, 0, s>>>(L, w, hd + m + 1, V + (size_t)(i + 1) * L);
-                    HIP_CHECK(hipMemcpyAsync(hcPinned, hd, (size_t)(m + 2) * sizeof(double), hipMemcpyDeviceToHost, s));
-                    HIP_CHECK(hipEventRecord(evH, s));
-                };
-                if (!ahead) blockOpDev(2, vi, N, w, N, true, s);
-                orth();
-                // the next step's matvec goes in before the host reads the column: the GPU
-                // runs it while the host applies the rotations (wasted once per cycle, at
-                // the step that converges)
-                ahead = i + 1 < m;
-                if (ahead) blockOpDev(2, V + (size_t)(i + 1) * L, N, w, N, true, s);
-                HIP_CHECK(hipEventSynchronize(evH));
-                if (recoverTopTimeout(s)) {  // this step's matvec (or the next one's) timed out: redo both
-                    blockOpDev(2, vi, N, w, N, true, s);
-                    orth();
-                    if (ahead) blockOpDev(2, V + (size_t)(i + 1) * L, N, w, N, true, s);
-                    HIP_CHECK(hipEventSynchronize(evH));
+            bool ahead = false;  // the matvec of V[j] is already enqueued
+            hrel.clear();
+            for (int j = 0; j < m; ++j) {
+                double* vj = V + (size_t)j * L;
+                if (!ahead) blockOpDev(2, vj, N, w, N, true, s);
+                arnoldiStep(L, m, j, V, L, w, st, stat, s);
+                post();
+                // the next step's matvec goes in before the host reads the status: the GPU
+                // runs it while the host decides (wasted once per cycle, at the step that
+                // converges) -- except where the residual estimate is predicted to reach tol
+                // at this step (geometric extrapolation of the last two estimates, 10x margin)
+                bool near = false;
+                if (hrel.size() >= 2) {
+                    const double q = std::min(1.0, hrel.back() / hrel[hrel.size() - 2]);
+                    near = hrel.back() * q <= 10.0 * tol;
+                } else if (!hrel.empty()) {
+                    near = hrel.back() <= 10.0 * tol;
                 }
-                std::copy(hcPinned, hcPinned + m + 2, hc.begin());
-                double* Hc = H.data() + (size_t)i * ld;
-                for (int k = 0; k <= i; ++k) Hc[k] = hc[k];
-                Hc[i + 1] = std::sqrt(std::max(hc[m + 1], 0.0));
-                for (int k = 0; k < i; ++k) {  // the previous rotations
-                    const double t = cs[k] * Hc[k] + sn[k] * Hc[k + 1];
-                    Hc[k + 1] = -sn[k] * Hc[k] + cs[k] * Hc[k + 1];
-                    Hc[k] = t;
+                ahead = j + 1 < m && !near;
+                if (ahead) blockOpDev(2, V + (size_t)(j + 1) * L, N, w, N, true, s);
+                HIP_CHECK(hipEventSynchronize(hs.ev));
+                if (recoverTopTimeout(s)) {
+                    // this step's matvec (or the look-ahead one) ran on an invalid fused launch:
+                    // the cycle ends before this step (columns 0 .. j - 1 are valid) and restarts
+                    // from its update on the tier launches
+                    ahead = false;
+                    break;
                 }
-                const double den = std::hypot(Hc[i], Hc[i + 1]);
-                cs[i] = den == 0.0 ? 1.0 : Hc[i] / den;
-                sn[i] = den == 0.0 ? 0.0 : Hc[i + 1] / den;
-                Hc[i] = den;
-                Hc[i + 1] = 0.0;
-                g[i + 1] = -sn[i] * g[i];
-                g[i] = cs[i] * g[i];
+                const double rel = hs.p[0], rnext = hs.p[1];
                 ++total;
-                used = i + 1;
-                relres = std::fabs(g[i + 1]) / normb;
-                if (hist && nh < maxhist) hist[nh++] = relres;
-                if (relres <= tol || hc[m + 1] <= 0.0) break;  // converged (estimate) or lucky breakdown
+                used = j + 1;
+                relres = rel;
+                hrel.push_back(rel);
+                if (hist && nh < maxhist) hist[nh++] = rel;
+                if (rel <= tol || rnext == 0.0) break;  // converged (estimate) or lucky breakdown
             }
-            // x += V y, H y = g (upper triangular)
-            for (int k = used - 1; k >= 0; --k) {
-                double t = g[k];
-                for (int j = k + 1; j < used; ++j) t -= H[(size_t)j * ld + k] * y[j];
-                y[k] = H[(size_t)k * ld + k] != 0.0 ? t / H[(size_t)k * ld + k] : 0.0;
-            }
-            HIP_CHECK(hipMemcpyAsync(bY.p, y.data(), (size_t)used * sizeof(double), hipMemcpyHostToDevice, s));
-            kr.maxpy(used, V, L, bY.as<double>(), 1.0, xt);
-            beta = residual();
-            relres = beta / normb;
+            arnoldiSolution(L, m, used, V, L, st, xt, s);  // x += P T R^-1 g
+            xZero = xZero && used == 0;
+            relres = residual();
             conv = relres <= tol;
         }
     }
     for (int k = 0; k < ks; ++k)
         k_unpermute<<<nblk(N), 256, 0, s>>>(N, perm, xt + (size_t)k * N, x + (size_t)k * N);
     HIP_CHECK(hipStreamSynchronize(s));
-    checkDeviceErrors();
+    ownTimeline = false;
+    checkDeviceErrors();  // every apply was checked at its recovery point: a flag here is new
     if (relresOut) *relresOut = relres;
     return conv ? total : -std::max(total, 1);
 }

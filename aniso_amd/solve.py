@@ -250,11 +250,12 @@ def gmres_dist(apply, b, restart=400, tol=1e-11, maxit=400, x0=None, allreduce=N
     Returns (x, total steps (negative if not converged), final relative residual).
     hist (a list) receives the estimate after every step.
 
-    kry (an aniso_amd.Aniso handle, CUDA vectors): the orthogonalisation runs on the
-    library's sweeps (aniso_krylov_dot / _update: three reads of the basis per step
-    instead of four, fixed-order reductions), the new basis vector is scaled on the
-    device, and the next step's matvec is enqueued before the host reads the
-    Hessenberg column for its rotations."""
+    kry (an aniso_amd.Aniso handle, CUDA vectors): the Arnoldi process runs on the
+    library's DCGS2 primitives (aniso_arnoldi_*: two sweeps over the basis per step,
+    Hessenberg matrix, rotations and residual estimate on the device; with allreduce,
+    the step's two sets of inner products are summed over the ranks between its
+    parts), and the next step's matvec is enqueued before the host reads the step's
+    residual estimate (except where it is predicted to reach tol)."""
     import torch
 
     red = allreduce or (lambda t: t)
@@ -274,14 +275,14 @@ def gmres_dist(apply, b, restart=400, tol=1e-11, maxit=400, x0=None, allreduce=N
     normb = nrm(b)
     if normb == 0.0:
         return torch.zeros_like(b), 0, 0.0
+    m = restart
+    V = torch.empty((m + 1, n), dtype=b.dtype, device=b.device)
+    if kry is not None:
+        return _gmres_dist_dev(apply, b, x, w, V, m, tol, maxit, allreduce, normb, x0 is None, hist, kry)
     r = residual()
     beta = nrm(r)
     relres = beta / normb
     total = 0
-    m = restart
-    V = torch.empty((m + 1, n), dtype=b.dtype, device=b.device)
-    if kry is not None:
-        return _gmres_dist_dev(apply, b, x, w, V, m, tol, maxit, red, normb, r, beta, hist, kry)
     for _ in range(maxit):
         if relres <= tol or beta == 0.0:
             break
@@ -331,76 +332,81 @@ def gmres_dist(apply, b, restart=400, tol=1e-11, maxit=400, x0=None, allreduce=N
     return x, (total if relres <= tol else -max(total, 1)), relres
 
 
-def _gmres_dist_dev(apply, b, x, w, V, m, tol, maxit, red, normb, r, beta, hist, kry):
-    """gmres_dist's loop on the library's Krylov sweeps (see gmres_dist: kry)."""
+def _gmres_dist_dev(apply, b, x, w, V, m, tol, maxit, allreduce, normb, x_zero, hist, kry):
+    """gmres_dist's loop on the library's DCGS2 primitives (see gmres_dist: kry).  V[0]
+    holds each cycle's residual; the stored vectors are never rewritten (arnoldi.hpp)."""
     import torch
 
-    dev = b.device
-    hb = torch.zeros(m + 2, dtype=torch.float64, device=dev)   # V^T w
-    h2 = torch.zeros(m + 2, dtype=torch.float64, device=dev)   # V^T w', then ||w'||^2
-    sq = torch.zeros(1, dtype=torch.float64, device=dev)
-    col = torch.zeros(m + 2, dtype=torch.float64, device=dev)  # [h, ||w''||]
-    host = torch.zeros(m + 2, dtype=torch.float64).pin_memory()
-    wv = w.reshape(-1)
-    relres = beta / normb
-    total = 0
-    for _ in range(maxit):
-        if relres <= tol or beta == 0.0:
-            break
-        V[0] = r.reshape(-1) / beta
-        H = np.zeros((m + 1, m))
-        cs, sn, g = np.zeros(m), np.zeros(m), np.zeros(m + 1)
-        g[0] = beta
-        used = 0
-        ahead = False
-        for i in range(m):
-            if not ahead:
-                apply(V[i].view_as(b), w)
-            Vi = V[: i + 1]
-            kry.krylov_dot(Vi, wv, hb)
-            red(hb[: i + 1])
-            kry.krylov_update(Vi, hb, wv, h2, dots=True)  # h2[:i+1] = V^T w', h2[i+1] = ||w'||^2
-            red(h2[: i + 2])
-            kry.krylov_update(Vi, h2, wv, sq, dots=False)
-            hn2 = torch.clamp(h2[i + 1] - (h2[: i + 1] * h2[: i + 1]).sum(), min=0.0)
-            hn = torch.sqrt(hn2)
-            V[i + 1] = wv * torch.where(hn > 0, 1.0 / torch.where(hn > 0, hn, 1.0), 0.0)
-            col[: i + 1] = hb[: i + 1] + h2[: i + 1]
-            col[i + 1] = hn
-            host[: i + 2].copy_(col[: i + 2], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            ahead = i + 1 < m
-            if ahead:  # the next matvec runs while the host applies the rotations
-                apply(V[i + 1].view_as(b), w)
-            ev.synchronize()
-            hc = host[: i + 2].numpy()
-            H[: i + 1, i] = hc[: i + 1]
-            H[i + 1, i] = hc[i + 1]
-            for k in range(i):  # the previous rotations (gmres.cpp:136-139)
-                t = cs[k] * H[k, i] + sn[k] * H[k + 1, i]
-                H[k + 1, i] = -sn[k] * H[k, i] + cs[k] * H[k + 1, i]
-                H[k, i] = t
-            den = np.hypot(H[i, i], H[i + 1, i])
-            cs[i], sn[i] = (1.0, 0.0) if den == 0 else (H[i, i] / den, H[i + 1, i] / den)
-            H[i, i], H[i + 1, i] = den, 0.0
-            g[i + 1] = -sn[i] * g[i]
-            g[i] = cs[i] * g[i]
-            total += 1
-            used = i + 1
-            relres = abs(g[i + 1]) / normb
-            if hist is not None:
-                hist.append(relres)
-            if relres <= tol or hc[i + 1] == 0.0:
+    from . import MappedStatus
+
+    n = b.numel()
+    st = kry.arnoldi_state(m)
+    stat = MappedStatus(4)
+    out = torch.zeros(m + 2, dtype=torch.float64, device=b.device)
+    ev = torch.cuda.Event()
+    bv, wv, xv = b.reshape(-1), w.reshape(-1), x.reshape(-1)
+    total, relres = 0, 1.0
+
+    def begin():  # r = b - A x into V[0], the cycle's start; (|r| / |b|, |r|)
+        if x_zero:
+            V[0].copy_(bv)
+        else:
+            apply(x, w)
+            torch.sub(bv, wv, out=V[0])
+        if allreduce is None:
+            kry.arnoldi_begin(V, m, st, normb, status=stat)
+        else:  # this rank's |r|^2 in the one-rank path's summation order, then summed over the ranks
+            kry.arnoldi_project(V, 0, V[0], out)
+            allreduce(out[:1])
+            kry.arnoldi_begin(V, m, st, normb, rr=out, status=stat)
+        ev.record()
+        ev.synchronize()
+        return float(stat.host[0]), float(stat.host[1])
+
+    try:
+        for _ in range(maxit):
+            relres, rnorm = begin()
+            if relres <= tol or rnorm == 0.0:
                 break
-        y = np.zeros(used)
-        for k in range(used - 1, -1, -1):
-            y[k] = (g[k] - H[k, k + 1:used] @ y[k + 1:]) / H[k, k] if H[k, k] != 0 else 0.0
-        x += (V[:used].t() @ torch.tensor(y, dtype=b.dtype, device=b.device)).view_as(b)
-        apply(x, w)
-        r = b - w
-        t = (r.reshape(-1) @ r.reshape(-1)).reshape(1)
-        red(t)
-        beta = float(t.sqrt())
-        relres = beta / normb
+            used, ahead, hrel = 0, False, []
+            for j in range(m):
+                if not ahead:
+                    apply(V[j].view_as(b), w)
+                if allreduce is None:
+                    kry.arnoldi_step(V, m, j, wv, st, status=stat)
+                else:
+                    kry.arnoldi_project(V, j, wv, out)
+                    allreduce(out[: j + 1])
+                    kry.arnoldi_coef(m, j, st, out)
+                    kry.arnoldi_update(V, m, j, wv, st, out)
+                    allreduce(out[: j + 2])
+                    kry.arnoldi_column(m, j, st, out, status=stat)
+                ev.record()
+                # the next matvec runs while the host reads this step's estimate, unless
+                # that estimate is predicted to reach tol (the last two estimates' ratio,
+                # 10x margin)
+                near = False
+                if len(hrel) >= 2:
+                    near = hrel[-1] * min(1.0, hrel[-1] / hrel[-2]) <= 10.0 * tol
+                elif hrel:
+                    near = hrel[-1] <= 10.0 * tol
+                ahead = j + 1 < m and not near
+                if ahead:
+                    apply(V[j + 1].view_as(b), w)
+                ev.synchronize()
+                rel, rn = float(stat.host[0]), float(stat.host[1])
+                total += 1
+                used = j + 1
+                relres = rel
+                hrel.append(rel)
+                if hist is not None:
+                    hist.append(rel)
+                if rel <= tol or rn == 0.0:
+                    break
+            kry.arnoldi_solution(V, m, used, st, xv)
+            x_zero = x_zero and used == 0
+        else:
+            relres, _ = begin()
+    finally:
+        stat.close()
     return x, (total if relres <= tol else -max(total, 1)), relres

@@ -43,6 +43,7 @@ Also reported on the same JSON line:
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -53,6 +54,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
 FP64_VALU_PEAK_TF = 78.6  # MI355X fp64 vector (spec): half the 157.3 TF fp32 vector rate of the chip table
+FP32_MATRIX_PEAK_TF = 157.3  # MI355X_MICROARCH.md chip table: fp32-input MFMA = the fp32 vector rate
+FP64_MATRIX_PEAK_TF = 78.6  # MI355X dense fp64 MFMA (spec; equal to the fp64 vector peak on CDNA4)
 
 
 def main_coeffs(xy):
@@ -89,20 +92,48 @@ def ref_bytes(sz, d, ns, s):
     return 8 * (2 * s["near_entries"] + 2 * s["m2l_entries"] + p_r + 8 * ns * ns * N) + 8 * 6 * N
 
 
+def _round_key(path):
+    """Profiles are named r<round><letters>_...: r04at comes after r04n (a < b < ... < z <
+    aa < ab ...), so order by round, then by the letters' length, then the letters."""
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/rNN_pmc_summary.json, made by tools/profile_round.sh + tools/pmc_summary.py
-    on this same bench command; FETCH_SIZE doubled per the gfx950 correction)."""
+    """HBM bytes per launch of `kernel` (a name prefix with the template arguments that
+    pick the kernel family) from the newest committed rocprofv3 PMC summary that holds
+    it (profiles/rNN_pmc_summary.json, made by tools/profile_round.sh +
+    tools/pmc_summary.py on this same bench command; FETCH_SIZE doubled per the gfx950
+    correction).  Among that summary's instantiations of the family, the one the bench
+    launched most often -- the shipped variant -- is taken.  Returns (bytes, source,
+    kernel name)."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
-    if not files:
-        return None, None
-    ks = json.load(open(files[-1]))["kernels"]
-    k = ks.get(kernel) or next((v for n, v in ks.items() if n.startswith(kernel)), None)
-    if not k:
-        return None, None
-    return int(k["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")), key=_round_key)
+    for f in reversed(files):
+        ks = json.load(open(f))["kernels"]
+        hits = [(v.get("launches", 0), n, v) for n, v in ks.items() if n == kernel or n.startswith(kernel)]
+        if hits:
+            _, name, k = max(hits, key=lambda h: h[0])
+            return int(k["traffic_bytes"]), os.path.relpath(f, ROOT), name
+    return None, None, None
+
+
+def mfma_busy(kernel):
+    """MFMA pipe busy % of `kernel` from the newest committed counter summary that holds
+    it (profiles/rNN*_mfma_summary.json or profiles/rNN*/mfma_summary.json, made by
+    tools/f32op_prof.sh / f64op_prof.sh + tools/counter_summary.py:
+    SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs))."""
+    import glob
+
+    files = glob.glob(os.path.join(ROOT, "profiles", "r*_mfma_summary.json")) + \
+        glob.glob(os.path.join(ROOT, "profiles", "r*", "mfma_summary.json"))
+    files.sort(key=lambda f: _round_key(os.path.relpath(f, os.path.join(ROOT, "profiles")).replace("/", "_")))
+    for f in reversed(files):
+        for n, v in json.load(open(f)).items():
+            if n.split("<")[0].endswith("::" + kernel) and "mfma_util_pct" in v:
+                return round(v["mfma_util_pct"], 2), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def block_ref(o, U, ss, g):
@@ -240,11 +271,34 @@ def config5_leg(args):
         its.append(it)
         errs.append(float(np.linalg.norm(Xh[k] - x) / np.linalg.norm(x)))
     t_ref = time.perf_counter() - t0
+    # north_star's "MFMA utilisation on M2L": the two MFMA operators' M2L launches (k32_m2l,
+    # k64_m2l: one 16 x 16 x 16 product per directed pair, 2 x 16^3 flops) timed by the
+    # operators' HIP stage events over 5 applies each; the MFMA pipe's busy share from
+    # the newest committed PMC pass of the same kernels (SQ_VALU_MFMA_BUSY_CYCLES)
+    mfma = {}
+    pairs = a.stats()["mrhs_m2l_pairs"]
+    flops = 2.0 * 16 ** 3 * pairs
+    for kern, dt, fn, peak in (("k32_m2l", torch.float32, a.forward_f32_dev, FP32_MATRIX_PEAK_TF),
+                               ("k64_m2l", torch.float64, a.forward16_f64_dev, FP64_MATRIX_PEAK_TF)):
+        Xm = torch.rand((a.N, 16), dtype=dt, device="cuda")
+        Ym = torch.empty_like(Xm)
+        fn(Xm, Ym)
+        a.set_timing(1)
+        for _ in range(5):
+            fn(Xm, Ym)
+        ms = a.stage_times()["m2l"]
+        a.set_timing(0)
+        tf = flops / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        busy, bsrc = mfma_busy(kern)
+        mfma[kern] = {"bound": "mfma" if dt == torch.float64 else "hbm", "achieved": round(tf, 2), "peak": peak,
+                      "unit": "TFLOP/s", "frac": round(tf / peak, 4), "kernel_ms": round(ms, 5),
+                      "algorithmic_flops": int(flops), "directed_pairs": int(pairs),
+                      "mfma_busy_pct": busy, "mfma_busy_source": bsrc}
     leg = {"workload": "configs[4]: configs[2] geometry (N=1048576, d=1, ns=10), mode 0, 16 RHS, fp32 mixed precision: "
                        "fp32 Krylov basis + fp32 16-RHS MFMA inner operator, fp64 refinement on the fp64 MFMA operator",
            "seconds": round(t_mixed, 4), "outer_refinements": outer, "inner_iterations": inner,
            "final_rel_residual_max": float(rel.max()), "rel_err_vs_fp64_gmres_max": max(errs),
-           "fp64_gmres_16_solves_s": round(t_ref, 4), "fp64_gmres_iterations": its}
+           "fp64_gmres_16_solves_s": round(t_ref, 4), "fp64_gmres_iterations": its, "mfma_m2l": mfma}
     a.close()
     return leg
 
@@ -536,10 +590,12 @@ def main():
         pmc_name = f"void aniso::k_m2l<{nb}, {4 if nb <= 2 else 2}>"
     m2l_ms = times["m2l"]
     achieved = m2l_bytes / (m2l_ms * 1e-3) / 1e9 if m2l_ms > 0 else 0.0
-    traffic, tsrc = pmc_traffic(pmc_name) if world == 1 and args.sz == 1024 and args.d == 1 else (None, None)
+    traffic, tsrc, tkern = (pmc_traffic(pmc_name) if world == 1 and args.sz == 1024 and args.d == 1
+                            else (None, None, None))
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
-                "kernel_ms": round(m2l_ms, 5), "algorithmic_bytes": int(m2l_bytes), "traffic_source": tsrc}
+                "kernel_ms": round(m2l_ms, 5), "algorithmic_bytes": int(m2l_bytes), "traffic_source": tsrc,
+                "traffic_kernel": tkern}
     if harmonic:
         # the harmonic M2L is fp64-VALU work per matrix entry: r^2,
         # 1/r, c = dx/r, T_2..T_{K-1}, V = sum_b T_b xw_b, (E/r) V, K output FMAs =
@@ -559,10 +615,11 @@ def main():
         near_gbs = near_bytes / (near_ms * 1e-3) / 1e9 if near_ms > 0 else 0.0
         # leaves <= 16 points (this geometry) run k_near_hs (sources staged in LDS)
         nkern = "k_near_hs" if my_stats["max_leaf"] <= 16 else "k_near_hm"
-        ntraffic, _ = pmc_traffic(f"void aniso::{nkern}<{nb},") if world == 1 and args.sz == 1024 and args.d == 1 \
-            else (None, None)
+        ntraffic, nsrc, nkname = (pmc_traffic(f"void aniso::{nkern}<{nb},") if world == 1 and args.sz == 1024
+                                  and args.d == 1 else (None, None, None))
         roofline["near"] = {"bound": "hbm", "achieved": round(near_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(near_gbs / HBM_PEAK_GBS, 4), "traffic": ntraffic,
+                            "traffic_source": nsrc, "traffic_kernel": nkname,
                             "kernel": f"{nkern}<{nb}>", "kernel_ms": round(near_ms, 5),
                             "algorithmic_bytes": int(near_bytes), "overlapped_with": roofline["kernel"]}
         roofline["m2l_rsqrt"] = "v_rsq_f64 + 1 Newton step (~1e-13 relative per entry); near field 2 steps (full fp64)"
@@ -620,9 +677,10 @@ def main():
                 "multipoles_received": o1["need_nodes"], "input_points_received": o1["halo_points"]})
     line.update(sec)  # mode-0 operator and deterministic block matvec (measured before the headline leg)
     if args.gmres > 0 and block:
-        # GMRES over this run's (possibly sharded) block matvec: aniso_amd.solve.gmres_dist,
-        # CGS2 with two all-reduces of its inner products per step, one cycle of exactly
-        # --gmres steps (tol 0); the initial and final residuals add two matvecs
+        # GMRES over this run's (possibly sharded) block matvec: aniso_amd.solve.gmres_dist
+        # on the library's DCGS2 Arnoldi (two all-reduces of its inner products per step on
+        # N > 1), one cycle of exactly --gmres steps (tol 0) from x0 = 0 (no matvec for its
+        # residual); the final explicit residual adds one matvec
         from aniso_amd.solve import gmres_dist
 
         rhs0 = torch.zeros(nb, N, dtype=torch.float64, device="cuda")
@@ -652,12 +710,13 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             gel = float(t.item())
         line["gmres"] = {"steps": args.gmres, "steps_per_s": round(args.gmres / gel, 3),
-                         "ms_per_step": round(1e3 * gel / args.gmres, 4), "matvecs": args.gmres + 2,
+                         "ms_per_step": round(1e3 * gel / args.gmres, 4), "matvecs": args.gmres + 1,
                          "relres_after": grel,
-                         "method": "aniso_amd.solve.gmres_dist: restarted GMRES, CGS2 (2 all-reduces per step) on "
-                                   "the library's sweeps (aniso_krylov_dot/_update), Krylov basis in HBM, the next "
-                                   "matvec enqueued ahead of the host's rotations; tol 0 so exactly `steps` Arnoldi "
-                                   "steps are timed"}
+                         "method": "aniso_amd.solve.gmres_dist: restarted GMRES on the library's DCGS2 Arnoldi "
+                                   "(aniso_arnoldi_*: two sweeps over the Krylov basis per step, Hessenberg matrix, "
+                                   "rotations and residual estimate on the device; 2 all-reduces per step on N > 1), "
+                                   "the next matvec enqueued before the host reads the step's estimate; tol 0 so "
+                                   "exactly `steps` Arnoldi steps are timed"}
     if args.config4_sz > 0 and block:
         # BASELINE configs[3]: sz = 2048 (4,194,304 points), d = 1, mode 0 -- main.cpp's GMRES
         # matvec u - K_0(sigma_s .* u), the configuration BASELINE names for 8 GPUs --

@@ -1607,7 +1607,7 @@ class _ThreadCollectives:
 
 @pytest.mark.parametrize("sz,world,one,d,ml", [(64, 2, "1", 1, 20), (64, 2, "0", 1, 20), (64, 4, "1", 1, 20),
                                                (64, 8, "1", 1, 20), (64, 3, "1", 1, 20), (96, 3, "1", 1, 20),
-                                               (40, 2, "1", 1, 3), (32, 2, "1", 2, 20)])
+                                               (40, 2, "1", 1, 3), (32, 2, "1", 2, 20), (64, 3, "mixed", 1, 20)])
 def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     """The library's one-call sharded block matvec (aniso_block_op_sharded_dev) with
     `world` ranks as threads of one process on the box's GPU, each rank's input valid
@@ -1617,13 +1617,16 @@ def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     one grouped exchange) and, with ANISO_ONE_EXCHANGE=0 or where the cuts split a
     tier-0 subtree, the two-collective one; the owned slices equal the unsharded
     matvec.  The maxLevel-limited tree (leaves above 16 points: no staged near field)
-    and d = 2 (no fused corrections) take the two-collective form by themselves."""
+    and d = 2 (no fused corrections) take the two-collective form by themselves.
+    "mixed": rank 0's process would allow the one-collective form and the others' not
+    (ANISO_ONE_EXCHANGE differs per handle): the ranks must still agree (ADVICE r04:
+    the decision is all-gathered at comm_init), here on the two-collective form."""
     torch = _torch()
     import threading
 
     import aniso_amd
 
-    monkeypatch.setenv("ANISO_ONE_EXCHANGE", one)
+    monkeypatch.setenv("ANISO_ONE_EXCHANGE", "1" if one == "mixed" else one)
     ks = 5
     full = aniso_amd.Aniso(sz, d, ks, 0.8, 10, 4, ml)
     xy = full.getNodes()
@@ -1637,6 +1640,8 @@ def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     torch.cuda.synchronize()
     hs = []
     for r in range(world):
+        if one == "mixed":
+            monkeypatch.setenv("ANISO_ONE_EXCHANGE", "1" if r == 0 else "0")
         h = aniso_amd.Aniso(sz, d, ks, 0.8, 10, 4, ml)
         h.set_shard(r, world)
         h.setCoeff(*coef)

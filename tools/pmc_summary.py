@@ -17,12 +17,12 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
             agg[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+    return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
 
 
 def main():
-    fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
-    write = per_kernel(sys.argv[2], "WRITE_SIZE")
+    fetch, launches = per_kernel(sys.argv[1], "FETCH_SIZE")
+    write, _ = per_kernel(sys.argv[2], "WRITE_SIZE")
     out = {"note": "bytes per launch; fetch_bytes = 2 x FETCH_SIZE(KB) x 1024 (gfx950 correction), "
                    "write_bytes = WRITE_SIZE(KB) x 1024; traffic = fetch + write",
            "kernels": {}}
@@ -30,7 +30,8 @@ def main():
         f = 2.0 * fetch.get(k, 0.0) * 1024.0
         w = write.get(k, 0.0) * 1024.0
         out["kernels"][k] = {"fetch_size_kb_raw": fetch.get(k), "write_size_kb_raw": write.get(k),
-                             "fetch_bytes": f, "write_bytes": w, "traffic_bytes": f + w}
+                             "fetch_bytes": f, "write_bytes": w, "traffic_bytes": f + w,
+                             "launches": launches.get(k, 0)}
     json.dump(out, open(sys.argv[3], "w"), indent=1)
     for k, v in out["kernels"].items():
         print(f"{k:40s} traffic {v['traffic_bytes'] / 1e9:9.4f} GB")
