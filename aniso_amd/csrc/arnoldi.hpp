@@ -35,7 +35,8 @@ namespace arn {
 
 constexpr int kThreads = 256;
 constexpr int kMaxRegs = 48;  // basis rows one sweep holds in registers
-constexpr int kParts = 512;   // blocks (partial sums per row) of a sweep: the measured best (tools/arnoldi_micro.hip)
+constexpr int kSweepThreads = 512;  // threads per sweep block
+constexpr int kParts = 256;   // blocks (partial sums per row) of a sweep: 512 x 256 measured best (tools/arnoldi_micro.hip)
 constexpr int kRedRows = 16;  // rows per round of the small kernels' reductions (4 per wave)
 constexpr int kUpdateVar = 0;    // k_arn_update's variant (below)
 constexpr int kStageDoubles = 7000;  // LDS (55 KB) the small kernels stage T and H in
@@ -70,7 +71,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 // chunk b's contiguous element range [j0, j1)
 __device__ __forceinline__ void block_range(int64_t n, int b, int64_t& j0, int64_t& j1) {
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const int64_t chunk = (per + 255) & ~(int64_t)255;
+    const int64_t chunk = (per + 511) & ~(int64_t)511;
     j0 = min(n, (int64_t)b * chunk);
     j1 = min(n, j0 + chunk);
 }
@@ -78,7 +79,7 @@ __device__ __forceinline__ void block_range(int64_t n, int b, int64_t& j0, int64
 // per-block sums into part[row * gridDim.x + b] (b: the block's chunk): acc[k] is row k
 // for k < used, acc[NA - 1] is row extraRow (if >= 0); wave sums by xor shuffles, then
 // the 4 waves in a fixed order
-template <int NA>
+template <int NA, int TB = kThreads>
 __device__ __forceinline__ void block_store(const double (&acc)[NA], int used, int extraRow, double* red,
                                             double* part, int b) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -89,26 +90,30 @@ __device__ __forceinline__ void block_store(const double (&acc)[NA], int used, i
             if (lane == 0) red[wv * NA + k] = v;
         }
     __syncthreads();
-    for (int k = threadIdx.x; k <= used; k += kThreads) {
+    for (int k = threadIdx.x; k <= used; k += TB) {
         const int i = k < used ? k : NA - 1;
         const int row = k < used ? k : extraRow;
-        if (row >= 0)
-            part[(size_t)row * gridDim.x + b] = ((red[i] + red[NA + i]) + red[2 * NA + i]) + red[3 * NA + i];
+        if (row >= 0) {
+            double a = red[i];
+#pragma unroll
+            for (int q = 1; q < TB / 64; ++q) a += red[q * NA + i];
+            part[(size_t)row * gridDim.x + b] = a;
+        }
     }
 }
 
 // sweep A: part[k][blk] = sum over the block's range of V[k][e] w[e], k < nv <= NV
-template <int NV>
-__global__ void __launch_bounds__(kThreads) k_arn_project(int64_t n, int nv, const double* __restrict__ V,
-                                                          int64_t ldv, const double* __restrict__ w,
-                                                          double* __restrict__ part) {
-    __shared__ double red[4 * NV];
+template <int NV, int TB = kSweepThreads>
+__global__ void __launch_bounds__(TB) k_arn_project(int64_t n, int nv, const double* __restrict__ V,
+                                                    int64_t ldv, const double* __restrict__ w,
+                                                    double* __restrict__ part) {
+    __shared__ double red[(TB / 64) * NV];
     int64_t j0, j1;
     block_range(n, blockIdx.x, j0, j1);
     double acc[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) acc[k] = 0.0;
-    for (int64_t e = j0 + threadIdx.x; e < j1; e += kThreads) {
+    for (int64_t e = j0 + threadIdx.x; e < j1; e += TB) {
         double v[NV];
 #pragma unroll
         for (int k = 0; k < NV; ++k)
@@ -118,24 +123,26 @@ __global__ void __launch_bounds__(kThreads) k_arn_project(int64_t n, int nv, con
         for (int k = 0; k < NV; ++k)
             if (k < nv) acc[k] = __builtin_fma(v[k], we, acc[k]);
     }
-    block_store<NV>(acc, nv, -1, red, part, blockIdx.x);
+    block_store<NV, TB>(acc, nv, -1, red, part, blockIdx.x);
 }
 
 // sweep B for nv = j + 1 <= NV stored rows: p = w inv_r - sum_k e_k V_k -> V[nv]; the
 // partials of V_k . p (rows k < nv) and p . p (row nv)
-// VAR (development variants, tools/arnoldi_micro.hip): bit 0 chunks in reverse launch
-// order (the chunks sweep A read last, still in the Infinity Cache, first); bit 1 no
-// compiler barrier per element; bit 2 non-temporal stores of p
-template <int NV, int VAR = kUpdateVar>
-__global__ void __launch_bounds__(kThreads) k_arn_update(int64_t n, int nv, double* __restrict__ V, int64_t ldv,
+// VAR (development variants, tools/arnoldi_micro.hip, neither faster): bit 0 chunks in
+// reverse launch order (the chunks sweep A read last first, for Infinity-Cache hits);
+// bit 2 non-temporal stores of p.  The one store stream costs ~50 us at 1M x 5 among the
+// nv + 1 read streams (4.7-4.9 against 5.9-6.0 TB/s without it; row padding, store
+// placement and store kind do not change it: profiles/r05h-j_micro.log)
+template <int NV, int VAR = kUpdateVar, int TB = kSweepThreads>
+__global__ void __launch_bounds__(TB) k_arn_update(int64_t n, int nv, double* __restrict__ V, int64_t ldv,
                                                          const double* __restrict__ w,
                                                          const double* __restrict__ st, int m,
                                                          double* __restrict__ part) {
     constexpr int NA = NV + 1;
-    __shared__ double red[4 * NA];
+    __shared__ double red[(TB / 64) * NA];
     __shared__ double cf[NV + 1];  // -e[0 .. nv), inv_r
     const Layout L(m);
-    for (int k = threadIdx.x; k < nv; k += kThreads) cf[k] = -st[L.e + k];
+    for (int k = threadIdx.x; k < NV; k += TB) cf[k] = k < nv ? -st[L.e + k] : 0.0;
     if (threadIdx.x == 0) cf[NV] = st[L.sc + kInvR];
     __syncthreads();
     const double ir = cf[NV];
@@ -146,25 +153,37 @@ __global__ void __launch_bounds__(kThreads) k_arn_update(int64_t n, int nv, doub
 #pragma unroll
     for (int k = 0; k < NA; ++k) acc[k] = 0.0;
     double* __restrict__ Vn = V + (size_t)nv * ldv;
-    for (int64_t e = j0 + threadIdx.x; e < j1; e += kThreads) {
-        // keeps the coefficients in LDS (read per element) instead of NV registers
-        if constexpr (!(VAR & 2)) asm volatile("" ::: "memory");
+    // p of the previous element is stored after this element's loads are issued: vmcnt
+    // counts stores with loads (MI355X_MICROARCH.md, s_waitcnt), so a store issued before
+    // them would hold the later load waits to its acknowledgement
+    // (unconditional: the first iteration stores 0 into its own element's slot, which the
+    // second overwrites -- a store under a branch would again drain with the loads)
+    double pPrev = 0.0;
+    int64_t ePrev = j0 + threadIdx.x;
+    for (int64_t e = j0 + threadIdx.x; e < j1; e += TB) {
+        // rows past nv re-read row nv - 1 (an L1 hit) with a zero coefficient: no branch
+        // per row, so the compiler can count the loads in its vmcnt waits instead of
+        // draining the store below with them
         double v[NV];
 #pragma unroll
-        for (int k = 0; k < NV; ++k)
-            if (k < nv) v[k] = V[(size_t)k * ldv + e];
-        double p = w[e] * ir;
+        for (int k = 0; k < NV; ++k) v[k] = V[(size_t)(k < nv ? k : nv - 1) * ldv + e];
+        const double we = w[e];
+        // the loads above are issued before the store below, and cf is re-read from LDS
+        // per element instead of held in NV registers
+        asm volatile("" ::: "memory");
+        if constexpr ((VAR & 4) != 0) __builtin_nontemporal_store(pPrev, Vn + ePrev);
+        else Vn[ePrev] = pPrev;
+        double p = we * ir;
 #pragma unroll
-        for (int k = 0; k < NV; ++k)
-            if (k < nv) p = __builtin_fma(cf[k], v[k], p);
-        if constexpr ((VAR & 4) != 0) __builtin_nontemporal_store(p, Vn + e);
-        else Vn[e] = p;
+        for (int k = 0; k < NV; ++k) p = __builtin_fma(cf[k], v[k], p);
+        pPrev = p;
+        ePrev = e;
 #pragma unroll
-        for (int k = 0; k < NV; ++k)
-            if (k < nv) acc[k] = __builtin_fma(v[k], p, acc[k]);
+        for (int k = 0; k < NV; ++k) acc[k] = __builtin_fma(v[k], p, acc[k]);  // rows >= nv: not stored
         acc[NA - 1] = __builtin_fma(p, p, acc[NA - 1]);
     }
-    block_store<NA>(acc, nv, nv, red, part, b);
+    if (ePrev < j1) Vn[ePrev] = pPrev;
+    block_store<NA, TB>(acc, nv, nv, red, part, b);
 }
 
 // sweep B beyond kMaxRegs rows, first half: p -> V[nv] (one read of V, no register
@@ -219,11 +238,16 @@ __device__ __forceinline__ void reduce_rows(const double* __restrict__ part, int
             if (wv + 4 * q < nr) scratch[(wv + 4 * q) * 64 + lane] = a;
         }
         __syncthreads();
-        for (int r = threadIdx.x; r < nr; r += kThreads) {
-            double a = 0.0;
-#pragma unroll 16
-            for (int l = 0; l < 64; ++l) a += scratch[r * 64 + l];
-            out[k0 + r] = a;
+        for (int r = threadIdx.x; r < nr; r += kThreads) {  // fast_rows_finish's order
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+            for (int l = 0; l < 64; l += 4) {
+                a0 += scratch[r * 64 + l];
+                a1 += scratch[r * 64 + l + 1];
+                a2 += scratch[r * 64 + l + 2];
+                a3 += scratch[r * 64 + l + 3];
+            }
+            out[k0 + r] = (a0 + a1) + (a2 + a3);
         }
         __syncthreads();
     }
@@ -273,6 +297,224 @@ __device__ __forceinline__ void stage(const double* __restrict__ A, int64_t lda,
         }
     }
 }
+
+// ---- one-round fast paths of the small kernels (rows <= kFast): every global load of
+// the kernel (partials, the staged matrices, vectors) is issued before the first is
+// used.  Wave wv owns partial rows wv + 4q and matrix columns wv + 4q (q < 16); a
+// lane reads kParts / 64 consecutive partials of a row, or one matrix row.
+constexpr int kFast = 64;
+typedef double d2f __attribute__((ext_vector_type(2)));
+
+struct FastRows {
+    d2f v[16][kParts / 128];
+};
+
+__device__ __forceinline__ void fast_rows_load(const double* __restrict__ part, int P, int rows, FastRows& fr) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (P == 1) return;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int r = wv + 4 * q;
+        if (r < rows) {
+            const d2f* pr = (const d2f*)(part + (size_t)r * kParts + (size_t)lane * (kParts / 64));
+#pragma unroll
+            for (int b = 0; b < kParts / 128; ++b) fr.v[q][b] = pr[b];
+        }
+    }
+}
+
+// the rows' sums into out (LDS) in a fixed order; scratch: kFast x 64 doubles
+__device__ __forceinline__ void fast_rows_finish(const double* __restrict__ part, int P, int rows, const FastRows& fr,
+                                                 double* scratch, double* out) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (P == 1) {
+        for (int k = threadIdx.x; k < rows; k += kThreads) out[k] = part[k];
+        return;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int r = wv + 4 * q;
+        if (r < rows) {
+            double a = 0.0;
+#pragma unroll
+            for (int b = 0; b < kParts / 128; ++b) a += fr.v[q][b].x + fr.v[q][b].y;
+            scratch[r * 64 + lane] = a;
+        }
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < rows; r += kThreads) {
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+        for (int l = 0; l < 64; l += 4) {
+            a0 += scratch[r * 64 + l];
+            a1 += scratch[r * 64 + l + 1];
+            a2 += scratch[r * 64 + l + 2];
+            a3 += scratch[r * 64 + l + 3];
+        }
+        out[r] = (a0 + a1) + (a2 + a3);
+    }
+}
+
+// columns [0, cols) of a column-major matrix (rows <= 64 at lda) into registers, then LDS
+// (dense at ld rows)
+struct FastCols {
+    double v[16];
+};
+
+__device__ __forceinline__ void fast_cols_load(const double* __restrict__ A, int64_t lda, int rows, int cols,
+                                               FastCols& fc) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int c = wv + 4 * q;
+        if (c < cols && lane < rows) fc.v[q] = A[lane + (int64_t)c * lda];
+    }
+}
+
+__device__ __forceinline__ void fast_cols_store(const FastCols& fc, int rows, int cols, double* S) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int c = wv + 4 * q;
+        if (c < cols && lane < rows) S[c * rows + lane] = fc.v[q];
+    }
+}
+
+// k_arn_coef for j + 1 <= kFast.  LDS: scratch (kFast x 64) | u s tc c d (5 x 64) | T (n1 x j) | H (n1 x j)
+__device__ __forceinline__ void coef_fast(int m, int j, double* __restrict__ st, const double* __restrict__ part,
+                                          int P, double* sm) {
+    const int n1 = j + 1;
+    double* scratch = sm;
+    double *u = sm + kFast * 64, *s = u + kFast, *tc = s + kFast, *c = tc + kFast, *d = c + kFast;
+    double* Ts = d + kFast;
+    double* Hs = Ts + n1 * j;
+    const Layout L(m);
+    double* Tg = st + L.T;
+    FastRows fr;
+    FastCols ft, fh;
+    fast_rows_load(part, P, n1, fr);
+    fast_cols_load(Tg, L.M1, n1, j, ft);
+    fast_cols_load(st + L.Hu, L.M1, n1, j, fh);
+    const double sv = threadIdx.x < j ? st[L.s + threadIdx.x] : 0.0;
+    const double r = st[L.sc + kR];
+    fast_cols_store(ft, n1, j, Ts);
+    fast_cols_store(fh, n1, j, Hs);
+    if (threadIdx.x < j) s[threadIdx.x] = sv;
+    fast_rows_finish(part, P, n1, fr, scratch, u);
+    __syncthreads();
+    const double ir = 1.0 / r;
+    band_matvec(Ts, n1, j, j, 0, s, tc);  // T s
+    band_matvec(Hs, n1, n1, j, 1, s, c);  // H s
+    __syncthreads();
+    for (int i = threadIdx.x; i <= j; i += kThreads) {
+        const double t = i < j ? -tc[i] * ir : ir;  // column j of T: (e_j - T s) / r
+        tc[i] = t;
+        Tg[i + (size_t)j * L.M1] = t;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i <= j; i += kThreads) {  // z = T^T u, h, d
+        double a = 0.0;
+        if (i < j) {
+            for (int k = 0; k <= i; ++k) a = __builtin_fma(Ts[i * n1 + k], u[k], a);
+        } else {
+            for (int k = 0; k <= j; ++k) a = __builtin_fma(tc[k], u[k], a);
+        }
+        const double hi = (a - c[i]) * ir;
+        st[L.h + i] = hi;
+        d[i] = __builtin_fma(c[i], ir, hi);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i <= j; i += kThreads) {  // e = T d
+        double a = 0.0;
+        for (int k = i; k < j; ++k) a = __builtin_fma(Ts[k * n1 + i], d[k], a);
+        st[L.e + i] = __builtin_fma(tc[i], d[j], a);
+    }
+    if (threadIdx.x == 0) st[L.sc + kInvR] = ir;
+}
+
+inline __host__ __device__ size_t coef_fast_lds(int j) { return ((size_t)kFast * 69 + (size_t)2 * (j + 1) * j) * 8; }
+
+// k_arn_column for j + 2 <= kFast.  LDS: scratch (kFast x 64) | u' s' col cs sn h (6 x 64) | T (n1 x n1)
+__device__ __forceinline__ void column_fast(int m, int j, double* __restrict__ st, const double* __restrict__ part,
+                                            int P, double* __restrict__ status, double* sm) {
+    const int n1 = j + 1;
+    double* scratch = sm;
+    double *up = sm + kFast * 64, *sp = up + kFast, *col = sp + kFast, *csl = col + kFast, *snl = csl + kFast,
+           *hl = snl + kFast;
+    double* Ts = hl + kFast;
+    __shared__ double ssum;
+    const Layout L(m);
+    FastRows fr;
+    FastCols ft;
+    fast_rows_load(part, P, j + 2, fr);
+    fast_cols_load(st + L.T, L.M1, n1, n1, ft);
+    const int t = threadIdx.x;
+    const double cv = t < j ? st[L.cs + t] : 0.0, sv = t < j ? st[L.sn + t] : 0.0;
+    const double hv = t <= j ? st[L.h + t] : 0.0;
+    const double gj = st[L.g + j], normb = st[L.sc + kNormb];
+    fast_cols_store(ft, n1, n1, Ts);
+    if (t < j) {
+        csl[t] = cv;
+        snl[t] = sv;
+    }
+    if (t <= j) hl[t] = hv;
+    fast_rows_finish(part, P, j + 2, fr, scratch, up);
+    __syncthreads();
+    for (int i = t; i <= j; i += kThreads) {  // s' = T^T u' = Q^T p
+        double a = 0.0;
+        for (int k = 0; k <= i; ++k) a = __builtin_fma(Ts[i * n1 + k], up[k], a);
+        sp[i] = a;
+    }
+    __syncthreads();
+    if (t < 64) {
+        double ss = 0.0;
+        for (int k = t; k <= j; k += 64) ss = __builtin_fma(sp[k], sp[k], ss);
+        ss = wave_sum(ss);
+        if (t == 0) ssum = ss;
+    }
+    double* Hu = st + L.Hu + (size_t)j * L.M1;
+    double* R = st + L.R + (size_t)j * L.M1;
+    for (int i = t; i <= j; i += kThreads) {
+        const double v = hl[i] + sp[i];
+        Hu[i] = v;
+        col[i] = v;
+        st[L.s + i] = sp[i];
+    }
+    __syncthreads();
+    if (t == 0) {
+        const double a2 = up[j + 1] - ssum;
+        const double r = sqrt(a2 > 0.0 ? a2 : 0.0);
+        Hu[j + 1] = r;
+        st[L.sc + kR] = r;
+        double a = col[0];
+        for (int k = 0; k < j; ++k) {  // the previous rotations, R[k + 1] carried in a register
+            const double b = col[k + 1];
+            col[k] = csl[k] * a + snl[k] * b;
+            a = -snl[k] * a + csl[k] * b;
+        }
+        const double den = hypot(a, r);
+        const double c = den == 0.0 ? 1.0 : a / den;
+        const double sn = den == 0.0 ? 0.0 : r / den;
+        st[L.cs + j] = c;
+        st[L.sn + j] = sn;
+        col[j] = den;
+        col[j + 1] = 0.0;
+        st[L.g + j + 1] = -sn * gj;
+        st[L.g + j] = c * gj;
+        const double rel = fabs(sn * gj) / normb;
+        st[L.sc + kRelres] = rel;
+        st[L.sc + kSteps] = j + 1;
+        if (status) {
+            status[0] = rel;
+            status[1] = r;
+            status[2] = j + 1;
+        }
+    }
+    __syncthreads();
+    for (int i = t; i <= j + 1; i += kThreads) R[i] = col[i];
+}
+
+inline __host__ __device__ size_t column_fast_lds(int j) { return ((size_t)kFast * 70 + (size_t)(j + 1) * (j + 1)) * 8; }
 
 // cycle start: V[0] holds the residual r; rr = |r|^2 (P partials, or P = 1: reduced);
 // status (may be null): {|r| / normb, |r|, 0}
@@ -360,8 +602,12 @@ inline __host__ __device__ bool coef_staged(int j) { return (int64_t)2 * (j + 1)
 
 __global__ void __launch_bounds__(kThreads) k_arn_coef(int m, int j, double* __restrict__ st,
                                                        const double* __restrict__ part, int P) {
-    extern __shared__ double sm[];  // u, s, tcol, z, c, d: 6 (j + 1); staged T, H
+    extern __shared__ double sm[];  // fast path: coef_fast's layout; else u, s, tcol, z, c, d: 6 (j + 1); staged T, H
     __shared__ double scratch[kRedRows * 64];
+    if (j + 1 <= kFast) {
+        coef_fast(m, j, st, part, P, sm);
+        return;
+    }
     const Layout L(m);
     reduce_rows(part, P, j + 1, sm, scratch);
     for (int k = threadIdx.x; k < j; k += kThreads) sm[j + 1 + k] = st[L.s + k];
@@ -380,9 +626,13 @@ inline __host__ __device__ bool column_staged(int j) {
 __global__ void __launch_bounds__(kThreads) k_arn_column(int m, int j, double* __restrict__ st,
                                                          const double* __restrict__ part, int P,
                                                          double* __restrict__ status) {
-    extern __shared__ double sm[];  // u'[0 .. j + 1] | s' | col[0 .. j + 1] | cs | sn
+    extern __shared__ double sm[];  // fast path: column_fast's layout; else u'[0 .. j + 1] | s' | col[0 .. j + 1] | cs | sn
     __shared__ double scratch[kRedRows * 64];
     __shared__ double ssum;
+    if (j + 2 <= kFast) {
+        column_fast(m, j, st, part, P, status, sm);
+        return;
+    }
     double* up = sm;
     double* sp = up + (j + 2);
     double* col = sp + (j + 1);
@@ -517,37 +767,50 @@ inline void nv_dispatch(int nv, F&& f) {
 }
 
 // part[k * kParts + b] (k < nv): sweep A, in groups of kMaxRegs rows (w re-read per group)
+template <int TB = kSweepThreads, int PP = kParts>
 inline void launch_project(int64_t n, int nv, const double* V, int64_t ldv, const double* w, double* part,
                            hipStream_t s) {
     for (int k0 = 0; k0 < nv; k0 += kMaxRegs) {
         const int g = nv - k0 < kMaxRegs ? nv - k0 : kMaxRegs;
         const double* Vg = V + (size_t)k0 * ldv;
-        double* pg = part + (size_t)k0 * kParts;
+        double* pg = part + (size_t)k0 * PP;
         nv_dispatch(g, [&](auto c) {
-            k_arn_project<decltype(c)::value><<<kParts, kThreads, 0, s>>>(n, g, Vg, ldv, w, pg);
+            k_arn_project<decltype(c)::value, TB><<<PP, TB, 0, s>>>(n, g, Vg, ldv, w, pg);
         });
     }
 }
 
 // sweep B of step j (nv = j + 1 stored rows): V[nv] written, part rows 0 .. nv
-template <int VAR = kUpdateVar>
+template <int VAR = kUpdateVar, int TB = kSweepThreads, int PP = kParts>
 inline void launch_update(int64_t n, int nv, double* V, int64_t ldv, const double* w, const double* st, int m,
                           double* part, hipStream_t s) {
     if (nv <= kMaxRegs) {
         nv_dispatch(nv, [&](auto c) {
-            k_arn_update<decltype(c)::value, VAR><<<kParts, kThreads, 0, s>>>(n, nv, V, ldv, w, st, m, part);
+            k_arn_update<decltype(c)::value, VAR, TB><<<PP, TB, 0, s>>>(n, nv, V, ldv, w, st, m, part);
         });
         return;
     }
     k_arn_update_wide<<<(unsigned)((n + kThreads - 1) / kThreads), kThreads, (size_t)nv * sizeof(double), s>>>(
         n, nv, V, ldv, w, st, m);
-    launch_project(n, nv + 1, V, ldv, V + (size_t)nv * ldv, part, s);
+    launch_project<TB, PP>(n, nv + 1, V, ldv, V + (size_t)nv * ldv, part, s);
+}
+
+// the small kernels' fast paths stage up to ~110 KB of LDS: raise their dynamic limit
+// once per process (gfx950: 160 KB per CU, one such block per CU)
+inline void small_kernel_attrs() {
+    static bool done = false;
+    if (done) return;
+    (void)hipFuncSetAttribute((const void*)k_arn_coef, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_arn_column, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
+    done = true;
 }
 
 inline size_t coef_lds(int j) {
+    if (j + 1 <= kFast) return coef_fast_lds(j);
     return ((size_t)6 * (j + 1) + (coef_staged(j) ? (size_t)2 * (j + 1) * j : 0)) * sizeof(double);
 }
 inline size_t column_lds(int j) {
+    if (j + 2 <= kFast) return column_fast_lds(j);
     return ((size_t)(3 * (j + 2) + 2 * j) + (column_staged(j) ? (size_t)(j + 1) * (j + 1) : 0)) * sizeof(double);
 }
 inline size_t solve_lds(int used) { return ((size_t)2 * used + (solve_staged(used) ? (size_t)used * used : 0)) * sizeof(double); }

@@ -475,6 +475,7 @@ static void check_arnoldi(int m, int j) {
 }
 
 void Operator::arnoldiParts(int rows) {
+    arn::small_kernel_attrs();
     dKryPart.alloc(std::max(dKryPart.bytes, (size_t)arn::kParts * (rows + 2) * sizeof(double)));
 }
 

@@ -102,42 +102,29 @@ int main(int argc, char** argv) {
         const float ms = time([&] { arn::launch_project(n, nv, V, n, w, part, 0); }, 10);
         std::printf("project nv %2d: %.4f ms %.1f GB/s\n", nv, ms, (nv + 1) * vecGB / (ms * 1e-3));
     }
-    for (int nv : {8, 16, 24, 32, 40, 48}) {
-        const int m1 = 50;
-        auto run = [&](auto tec) {
-            constexpr int TE = decltype(tec)::value;
-            const int64_t nt = n / TE;
-            const float ms = time([&] {
-                arn::nv_dispatch(nv, [&](auto c) {
-                    k_project_tiled<decltype(c)::value, TE><<<arn::kParts, 256>>>(nt, nv, m1, V, w, part);
-                });
-            }, 10);
-            std::printf("project tiled TE %4d nv %2d: %.4f ms %.1f GB/s\n", TE, nv, ms, (nv + 1) * vecGB / (ms * 1e-3));
-        };
-        run(std::integral_constant<int, 256>{});
-        run(std::integral_constant<int, 1024>{});
-    }
     auto var = [&](auto vc, const char* name) {
         constexpr int VAR = decltype(vc)::value;
-        for (int nv : {8, 16, 24, 32, 40, 48}) {
+        for (int nv : {8, 16, 24, 32, 48}) {
             CK(hipMemcpy(V2, V, (size_t)(nv + 1) * n * sizeof(double), hipMemcpyDeviceToDevice));
             const float ms = time([&] { arn::launch_update<VAR>(n, nv, V2, n, w, st, m, part, 0); }, 10);
-            // sweep A then sweep B over the same rows (the step's order): the pair's time
-            const float mp = time([&] {
-                arn::launch_project(n, nv, V2, n, w, part, 0);
-                arn::launch_update<VAR>(n, nv, V2, n, w, st, m, part, 0);
-            }, 10);
-            std::printf("update %-8s nv %2d: %.4f ms %.1f GB/s   A+B %.4f ms (%.1f GB/s)\n", name, nv, ms,
-                        (nv + 2) * vecGB / (ms * 1e-3), mp, (2 * nv + 3) * vecGB / (mp * 1e-3));
+            std::printf("update %-8s nv %2d: %.4f ms %.1f GB/s (reads %d vectors)\n", name, nv, ms,
+                        (nv + 2) * vecGB / (ms * 1e-3), nv + 1);
         }
     };
     var(std::integral_constant<int, 0>{}, "base");
-    var(std::integral_constant<int, 1>{}, "rev");
-    var(std::integral_constant<int, 2>{}, "noclob");
+    var(std::integral_constant<int, 1>{}, "reverse");
     var(std::integral_constant<int, 4>{}, "nt");
-    var(std::integral_constant<int, 5>{}, "rev+nt");
-    var(std::integral_constant<int, 3>{}, "rev+ncl");
+    for (int64_t pad : {256, 576, 4224, 65536 + 192}) {
+        const int64_t ld = n + pad;
+        for (int nv : {8, 24, 48}) {
+            const float ma = time([&] { arn::launch_project(n, nv, V2, ld, w, part, 0); }, 10);
+            const float mb = time([&] { arn::launch_update(n, nv, V2, ld, w, st, m, part, 0); }, 10);
+            std::printf("pad %6lld nv %2d: project %.4f ms %.1f GB/s  update %.4f ms %.1f GB/s\n", (long long)pad, nv,
+                        ma, (nv + 1) * vecGB / (ma * 1e-3), mb, (nv + 2) * vecGB / (mb * 1e-3));
+        }
+    }
     // the small kernels on kParts partials
+    arn::small_kernel_attrs();
     for (int j : {0, 15, 39, 63}) {
         k_fill<<<2048, 256>>>(L.total, st, 3);
         const float mc = time([&] { arn::k_arn_coef<<<1, 256, arn::coef_lds(j)>>>(m, j, st, part, arn::kParts); }, 20);
