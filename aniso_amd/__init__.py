@@ -746,7 +746,8 @@ class Aniso:
                 "stored_near", "stored_m2l", "m2l_canon", "near_partial", "harmonic", "att_m2l_blocks",
                 "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "top_fused",
                 "plan_halo_slots", "plan_max_lds_slots", "plan_block_reads", "top_recoveries",
-                "near_hs_stored", "near_hs_partials", "one_exchange_applies", "mrhs_m2l_pairs"]
+                "near_hs_stored", "near_hs_partials", "one_exchange_applies", "mrhs_m2l_pairs",
+                "top_steals"]
         return dict(zip(keys, (int(v) for v in s)))
 
     def sync(self):

@@ -318,6 +318,8 @@ void Operator::uploadPlan() {
         up(dHmHaloPtr, plan.hmHaloPtr);
         up(dHmHaloPos, plan.hmHaloPos);
         dTopCnt.alloc((kMaxTopTiers + 1) * sizeof(unsigned));
+        dTopSteals.alloc(sizeof(unsigned));
+        HIP_CHECK(hipMemset(dTopSteals.p, 0, sizeof(unsigned)));
         attReady = false;
     }
     up(dM2LCanonBase, plan.m2lCanonBase);
@@ -1031,6 +1033,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             ta.cnt = dTopCnt.as<unsigned>();
             ta.recv1 = phase == 2 ? rootsRecv : nullptr;
             ta.spinLimit = topSpinLimit;
+            ta.steals = dTopSteals.as<unsigned>();
             HIP_CHECK(hipHostGetDevicePointer((void**)&ta.err, topErr, 0));
             const NearHsArgs na{(int)plan.leaves.size(), plan.nsMax, dLeafInfo.as<int4>(), hmPtsPtr, hmLoc,
                           dNsPtr.as<int64_t>(), dNsPts.as<int>(), hmKOff, dAttNear.as<double>(), dPxT.as<double>(),
@@ -1892,6 +1895,14 @@ bool Operator::recoverTopTimeout(hipStream_t s) {
     forceUnfused = true;
     ++topRecoveries;
     return true;
+}
+
+int64_t Operator::topSteals() {
+    if (device < 0 || !dTopSteals.p) return 0;
+    HIP_CHECK(hipSetDevice(device));
+    unsigned v = 0;
+    HIP_CHECK(hipMemcpy(&v, dTopSteals.p, sizeof(unsigned), hipMemcpyDeviceToHost));
+    return v;
 }
 
 void Operator::sync() {

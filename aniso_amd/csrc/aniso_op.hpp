@@ -167,6 +167,7 @@ public:
     // and count it; the caller then re-runs the apply on the tier launches
     bool recoverTopTimeout(hipStream_t s);
     int64_t topRecoveries = 0;  // applies re-run after a time-out (aniso_stats)
+    int64_t topSteals();        // tier tasks the fused launch's waiting blocks computed themselves (aniso_stats)
     int64_t oneXApplies = 0;    // sharded matvecs through the one-collective exchange (aniso_stats)
     bool forceUnfused = false;
     // set while a call that recovers its own time-outs (the block solve) runs: the
@@ -252,6 +253,7 @@ private:
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
     DevBuf dHmHaloPtr, dHmHaloPos, dHmPart, dDnChainFold;  // the halo form (Plan::hmHaloPtr)
     DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
+    DevBuf dTopSteals;          // tier tasks computed by waiting blocks of the fused launch (persistent)
     DevBuf dTopTrace;           // ANISO_TOP_TRACE=1: the launch's per-block timeline
     DevBuf dKryPart;            // partial sums of the Krylov primitives
     void arnoldiParts(int rows);  // dKryPart for sweeps of `rows` rows
@@ -295,7 +297,9 @@ private:
     // memory (the kernel stores 1 there when a wait gives up; checked at every API
     // entry and by sync(), never read on the device)
     unsigned* topErr = nullptr;
-    unsigned topSpinLimit = 1u << 24;  // ANISO_TOP_SPIN_LIMIT (tests: 0 forces the time-out path)
+    // ANISO_TOP_SPIN_LIMIT: polls of a tier counter (~1 us each) before a waiting block of
+    // the fused launch computes the tier itself (tests: 0 makes every waiter compute)
+    unsigned topSpinLimit = 1u << 16;
     bool useClusters = true;
     std::map<std::string, DevBuf> modeTabs;
     const CorrFold& corrTable(int K, int nterm, const int* ids, const double* mixes);

@@ -551,7 +551,7 @@ int aniso_tree_list(aniso_handle h, int which, int64_t* ptr, int* idx) {
     });
 }
 
-constexpr int kStatsV1 = 19, kStats = 27;
+constexpr int kStatsV1 = 19, kStats = 28;
 
 static void stats_fill(aniso::Operator& op, int64_t* s) {
     s[0] = op.nearEntries();
@@ -587,6 +587,7 @@ static void stats_fill(aniso::Operator& op, int64_t* s) {
     s[24] = op.plan.nearSymHsOn ? op.plan.hsPartTotal : 0;
     s[25] = op.oneXApplies;  // sharded matvecs through the one-collective exchange
     s[26] = op.mrhsM2LPairs();  // directed M2L pairs of the 16-RHS MFMA operators (0 before their plan)
+    s[27] = op.topSteals();     // upper-tier tasks computed by waiting blocks of the fused launch
 }
 
 // the round-2 entry: the first kStatsV1 entries only (callers sized for them)

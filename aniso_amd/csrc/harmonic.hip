@@ -807,30 +807,58 @@ k_m2l_hc(HcArgs a) {
 // Hand-off per tier: a counter of finished tasks, published after an agent-scope
 // release by each task and polled (relaxed, agent scope) by one lane of a waiting
 // block, which then acquires before its block reads (MI355X_MICROARCH.md, cross-
-// workgroup visibility).  Waiting blocks have higher ids than every block they wait
-// for and the up blocks (a few hundred) all fit on the chip at once, so the
-// producers are always resident.  The spin is still bounded: a wait that gives up
-// counts in cnt[0] and stores 1 into the host-visible flag err, which the host turns
-// into ANISO_ERR_RUNTIME at its next entry / sync (Operator::checkDeviceErrors) --
-// the apply's output is then invalid, never silently accepted.
+// workgroup visibility).
+// No dispatch-order assumption: a wait that has polled spinLimit times without
+// seeing the tier complete computes the tier's tasks itself (top_ensure), after the
+// tiers below it, the same way.  up_task only assigns (mult, the gathered roots), so
+// a task computed twice -- by its own block and by a waiter -- writes the same bits,
+// and a waiter reads only what it computed itself or what a completed counter
+// published.  So the launch cannot hang on, or be spoiled by, a producer block that
+// is not resident; each such computation counts in TopArgs.steals (aniso_stats).
 typedef __attribute__((address_space(1))) unsigned gu32;
 
-__device__ __forceinline__ void top_wait(const TopArgs& t, int k, unsigned target) {
+// one lane polls tier k's counter up to spinLimit times; true (and acquired) if the tier completed
+__device__ __forceinline__ bool top_poll(const TopArgs& t, int k, unsigned target) {
+    __shared__ int done;
     if (threadIdx.x == 0) {
         gu32* c = (gu32*)(t.cnt + k);
+        bool ok = false;
         for (unsigned spins = 0;; ++spins) {
-            if (spins >= t.spinLimit) {
-                __hip_atomic_fetch_add((gu32*)t.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(t.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
+                ok = true;
                 break;
             }
-            if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+            if (spins >= t.spinLimit) break;
             __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        done = ok ? 1 : 0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const bool ok = done != 0;
+    __syncthreads();  // `done` is reused by the next poll
+    return ok;
+}
+
+// tiers 1 .. k complete for this block: the highest tier whose counter completes within
+// the poll bound, then every task of the tiers above it computed here, bottom up
+template <int K>
+__device__ __forceinline__ void top_ensure(const TopArgs& t, const UpArgs& u, int k, double* sm) {
+    int j = k;
+    while (j >= 1 && !top_poll(t, j, (unsigned)(t.blk0[j + 1] - t.blk0[j]))) --j;
+    for (int jj = j + 1; jj <= k; ++jj) {
+        const int nj = t.blk0[jj + 1] - t.blk0[jj];
+        for (int i = 0; i < nj; ++i) {
+            up_task<K>(t.task0[jj] + i, u.maxTask, u.desc, u.grpFix, u.node, u.code, u.geom, u.leafRange, u.pxT,
+                       u.pyT, u.xin, u.ldi, u.treeIn, u.perm, u.sigT, u.wT, u.fT, u.cT, u.P, u.mult, u.rootSlot,
+                       jj == 1 ? t.recv1 : nullptr, nullptr, nullptr, sm);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its mult stores, read by the next task
+            __syncthreads();
+        }
+        if (threadIdx.x == 0 && t.steals)
+            __hip_atomic_fetch_add((gu32*)t.steals, (unsigned)nj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __device__ __forceinline__ void top_publish(unsigned* cnt, int k) {
@@ -880,7 +908,7 @@ k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a, NearHsArgs n) {
     if (b < t.nUp) {
         int k = 1;
         while (b >= t.blk0[k + 1]) ++k;
-        if (k >= 2) top_wait(t, k - 1, (unsigned)(t.blk0[k] - t.blk0[k - 1]));
+        if (k >= 2) top_ensure<K>(t, u, k - 1, sm);
         top_mark<TRACE>(t, 1);
         up_task<K>(t.task0[k] + (b - t.blk0[k]), u.maxTask, u.desc, u.grpFix, u.node, u.code, u.geom, u.leafRange,
                    u.pxT, u.pyT, u.xin, u.ldi, u.treeIn, u.perm, u.sigT, u.wT, u.fT, u.cT, u.P, u.mult, u.rootSlot,
@@ -900,7 +928,7 @@ k_top_m2l_hc(UpArgs u, TopArgs t, HcArgs a, NearHsArgs n) {
     }
     const int w = t.clWait[cid];
     if (w > 0) {  // its own copy: behind the wait's fence the source boxes load through the vector path
-        top_wait(t, w, (unsigned)(t.blk0[w + 1] - t.blk0[w]));
+        top_ensure<K>(t, u, w, sm);
         top_mark<TRACE>(t, 1);
         m2l_cluster_form<K, NR, D, XL, kHcLR<WPE>>(cid, a, sm);
         top_mark<TRACE>(t, 2);

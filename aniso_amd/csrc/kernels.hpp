@@ -235,10 +235,12 @@ struct TopArgs {
     int blk0[kMaxTopTiers + 1];   // first block of tier k; blk0[ntier] = nUp
     int task0[kMaxTopTiers];      // first task of tier k
     const int* clWait;            // per cluster: the upper tier it waits for (0: none)
-    unsigned* cnt;                // finished tasks per tier; cnt[0] = spin time-outs (zeroed by tier 0)
+    unsigned* cnt;                // finished tasks per tier (zeroed by tier 0)
     const double* recv1;          // sharded phase 2: the gathered tier-0 roots tier 1 reads
-    unsigned spinLimit;           // polls before a wait gives up (0: give up at once -- tests only)
-    unsigned* err;                // host-visible sticky flag: set to 1 when a wait gave up
+    unsigned spinLimit;           // polls of a tier's counter before the waiting block computes the tier itself
+                                  // (0: at once -- tests only)
+    unsigned* steals;             // persistent count of tier tasks computed by a waiting block (aniso_stats)
+    unsigned* err;                // host-visible sticky flag (kept for the ABI; the launch no longer sets it)
     int64_t* trace;               // development (ANISO_TOP_TRACE=1): per block {start, waited, end, hw id}
     int nCl;                      // cluster blocks (set by the launcher); near-field groups follow them
 };

@@ -62,9 +62,11 @@ int aniso_tree_list(aniso_handle h, int which, int64_t *ptr, int *idx);
  * the harmonic near field's symmetric U storage: its stored E entries and partner
  * partial entries (both 0 when it reads every near block directed); then the
  * sharded matvecs run through the one-collective exchange (section 5); then the
- * directed M2L pairs of the 16-right-hand-side MFMA operators (0 before their plan).
+ * directed M2L pairs of the 16-right-hand-side MFMA operators (0 before their plan);
+ * then the upper-tier tasks that waiting blocks of the fused top-of-tree launch
+ * computed themselves after ANISO_TOP_SPIN_LIMIT polls (section 3.10).
  * aniso_stats_n writes the first min(cap, *n) of them and sets *n to their count
- * (27 here); aniso_stats, the round-2 form, writes the first 19 only. */
+ * (28 here); aniso_stats, the round-2 form, writes the first 19 only. */
 int aniso_stats_n(aniso_handle h, int64_t *stats, int cap, int *n);
 int aniso_stats(aniso_handle h, int64_t *stats);
 /* per-stage device times (ms), averaged over every apply since aniso_set_timing(h, 1)
