@@ -107,6 +107,8 @@ def lib():
             "aniso_shard_exchange": [P, I, lp],
             "aniso_shard_exchange_one": [P, lp],
             "aniso_shard_one_halo": [P, lp],
+            "aniso_shard_upper_partials": [P, lp],
+            "aniso_shard_upper_records": [P, ip],
             "aniso_shard_halo": [P, lp],
             "aniso_shard_roots": [P, ip, ip, ip],
             "aniso_forward_tree_begin_dev": [P, P, P, P, P],
@@ -686,6 +688,19 @@ class Aniso:
         keys = ["ok", "own_t0_tasks", "need_nodes", "halo_ranges", "halo_points"]
         return dict(zip(keys, (int(v) for v in info)))
 
+    def shard_upper_partials(self):
+        """The upper multipoles as partial sums of this shard (aniso_shard_upper_partials), host only:
+        whether the plan forms them, its tasks, records, the topmost level an M2L reads, the
+        tier-0 root level, the roots the tasks cover, and the node of each record."""
+        info = np.zeros(6, dtype=np.int64)
+        _check(lib().aniso_shard_upper_partials(self.address, info.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        keys = ["on", "tasks", "records", "top_level", "root_level", "roots"]
+        d = dict(zip(keys, (int(v) for v in info)))
+        nodes = np.zeros(max(d["records"], 1), dtype=np.int32)
+        _check(lib().aniso_shard_upper_records(self.address, nodes.ctypes.data_as(ctypes.POINTER(ctypes.c_int))))
+        d["record_nodes"] = nodes[: d["records"]]
+        return d
+
     def shard_one_halo(self):
         """(n, 2) ranges of the input the one-collective exchange fills outside the own range."""
         n = self.shard_exchange_one()["halo_ranges"]
@@ -747,7 +762,7 @@ class Aniso:
                 "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "top_fused",
                 "plan_halo_slots", "plan_max_lds_slots", "plan_block_reads", "top_recoveries",
                 "near_hs_stored", "near_hs_partials", "one_exchange_applies", "mrhs_m2l_pairs",
-                "top_steals"]
+                "top_steals", "upper_partial_applies"]
         return dict(zip(keys, (int(v) for v in s)))
 
     def sync(self):

@@ -77,6 +77,9 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     // at one wave per SIMD).  Off by default: measured slower
     plan.nearSymHs = false;
     if (const char* e = std::getenv("ANISO_NEAR_HS_SYM")) plan.nearSymHs = ks > 1 && ks <= 5 && e[0] == '1';
+    // ANISO_UPPER_PARTIAL=0: a sharded one-collective matvec exchanges the tier-0 roots
+    // and runs the upper up tiers on every rank (the round-4 form)
+    if (const char* e = std::getenv("ANISO_UPPER_PARTIAL")) plan.xUpPartialIn = std::atoi(e) != 0;
     plan.build(tree, np, 0, 1);
     plan.buildExchange(tree, geo.sz, geo.d2);
     plan.buildTopWait(tree);
@@ -91,6 +94,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_NEAR_IN_TOP")) nearInTop = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_EARLY")) nearEarly = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_ONE_EXCHANGE")) oneXOn = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ANISO_SHARD_NEAR_EARLY")) shardNearEarly = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_ORDER")) nearOrderUp = std::strcmp(e, "first") != 0;
     hmRing = hm_ring_depth();
     if (const char* e = std::getenv("ANISO_HM_WPE")) hmWpe = std::atoi(e);
@@ -358,6 +362,7 @@ void Operator::uploadPlan() {
     up(dNearPts, plan.nearPts);
     up(dXT0Tasks, plan.xT0Tasks);
     up(dXOwnT0Tasks, plan.xOwnT0Tasks);
+    up(dXUpTask, plan.xUpTask);
     up(dNearGrpEarly, plan.nearGrpEarly);
     up(dNearGrpLate, plan.nearGrpLate);
     up(dXRootRecv, plan.xRootRecv);
@@ -793,9 +798,13 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     const NearCorr nc{dNearCorrRow.as<uint16_t>(), dPerm.as<int>(), dIperm.as<int>(), dCT.as<double>(),
                       cf.Wc.as<double>(), cf.Wm.as<double>(), P};
     const int ntier = (int)plan.upTierTask.size() - 1;  // 0: a lone leaf
+    // a sharded one-collective matvec with the upper multipoles as partial sums
+    // (blockOpShardedDev, Plan::xUpPartial): phase 1 forms this rank's records, the
+    // exchange's unpack sums them, phase 2 runs no up tier
+    const bool upPartial = oneXActive && upActive && phase != 0;
     // the upper tiers ride in the M2L launch (k_top_m2l_hc) when every leaf is in the
     // bottom tier: the near field then forks after it
-    const bool topFused = harmonic && (mask & kStageFar) && topFusedOn();
+    const bool topFused = harmonic && (mask & kStageFar) && topFusedOn() && !upPartial;
     // ANISO_NEAR_IN_TOP: the near field (+ corrections) as the last blocks of that
     // launch (the one-block M2L form; a shard's phase 1 then leaves it to phase 2)
     const bool ringOn = hmRing > 0 && hm_ring_xl(K, plan.hmMaxLds, hmRing) >= 0;
@@ -930,7 +939,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         // up pass: tiers bottom-up; its P2M also forms the weighted charges fT (tree
         // order) the near field and the corrections read
         e0 = tm ? mark(s) : -1;
-        if (nearIn && oneX && !plan.nearGrpEarly.empty()) {
+        if (nearIn && oneX && !plan.nearGrpEarly.empty() && shardNearEarly) {
             // one-collective form: the groups that read only the own range start now,
             // beside the own tier-0 tasks; the rest waits for the exchange (phase 2)
             nin.grpList = dNearGrpEarly.as<int>();
@@ -958,7 +967,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             if (fork) HIP_CHECK(hipEventRecord(evFork, s));
         }
         if (phase == 1 && ntier >= 1) {
-            if (oneX) upTier(0, dXOwnT0Tasks.as<int>(), (int)plan.xOwnT0Tasks.size(), nullptr, rootsSend);
+            if (oneX) upTier(0, dXOwnT0Tasks.as<int>(), (int)plan.xOwnT0Tasks.size(), nullptr, upPartial ? nullptr : rootsSend);
             else upTier(0, dXT0Tasks.as<int>(), (int)plan.xT0Tasks.size(), nullptr, rootsSend);
         }
         for (int k = 0; k < (topFused ? 1 : ntier) && phase == 0; ++k) {
@@ -989,15 +998,17 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         const int ex = tm ? mark(s) : -1;
         span(0, pend.ePack, ex);  // the caller's root exchange
         if (oneX && !nearDone) {  // the rest of the near field after the one exchange (it filled the input's halo)
-            nin.grpList = dNearGrpLate.as<int>();
-            nin.ngrp = (int)plan.nearGrpLate.size();
+            // (ANISO_SHARD_NEAR_EARLY=0: every group here, in one launch)
+            nin.grpList = shardNearEarly ? dNearGrpLate.as<int>() : nullptr;
+            nin.ngrp = shardNearEarly ? (int)plan.nearGrpLate.size() : 0;
             if (fork) HIP_CHECK(hipEventRecord(evFork, s));
             nearStage();
             nin.grpList = nullptr;
             nin.ngrp = 0;
             nearDone = true;
         }
-        if (topFused) {  // the upper tiers run inside the M2L launch below
+        if (upPartial) {  // the exchange's unpack summed the upper multipoles
+        } else if (topFused) {  // the upper tiers run inside the M2L launch below
         } else if (ntier >= 2) {  // the first upper tier reads the gathered roots (and stores them for the M2L)
             upTier(1, nullptr, tierTasks(1), rootsRecv, nullptr);
             for (int k = 2; k < ntier; ++k) upTier(k, nullptr, tierTasks(k), nullptr, nullptr);
@@ -1561,7 +1572,7 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
     // loopback communicator (development: one rank's schedule on one GPU) has no
     // peers, so their lists come from their plans built here
     struct PeerLists {
-        std::vector<double> halo, oneHalo, needNodes, ok;
+        std::vector<double> halo, oneHalo, needNodes, ok, upRec;
     };
     std::vector<PeerLists> peerLists;
     if (c->loopback()) {
@@ -1572,6 +1583,7 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
                 q.nearSymmetric = plan.nearSymmetric;
                 q.nearSymHs = plan.nearSymHs;
                 q.maxCanon = plan.maxCanon;
+                q.xUpPartialIn = plan.xUpPartialIn;
                 q.build(tree, np, r, P);
                 q.buildExchange(tree, geo.sz, geo.d2);
             }
@@ -1579,7 +1591,8 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
             peerLists[r].halo.assign(src.xHalo.begin(), src.xHalo.end());
             peerLists[r].oneHalo.assign(src.xOneHalo.begin(), src.xOneHalo.end());
             peerLists[r].needNodes.assign(src.xNeedNodes.begin(), src.xNeedNodes.end());
-            peerLists[r].ok.assign(1, (r == me ? oneExchangeLocal() : src.xOneOk) ? 1.0 : 0.0);
+            peerLists[r].ok = {(r == me ? oneExchangeLocal() : src.xOneOk) ? 1.0 : 0.0, src.xUpPartial ? 1.0 : 0.0};
+            peerLists[r].upRec.assign(src.xUpRecNode.begin(), src.xUpRecNode.end());
         }
     }
     auto gatherList = [&](std::vector<double> PeerLists::*field, const std::vector<double>& mineV,
@@ -1674,14 +1687,33 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
     // staged near field, its knobs): the one-collective form only where all of them
     // hold, so that oxReady, and with it the collectives each matvec issues, is the
     // same on every rank (oneExchangeUsable adds only rank-independent checks)
-    gatherList(&PeerLists::ok, std::vector<double>(1, oneExchangeLocal() ? 1.0 : 0.0), oksAll);
-    bool allOk = true;
-    for (const auto& o : oksAll) allOk = allOk && !o.empty() && o[0] > 0.5;
+    // (and whether its plan has the upper multipoles as partial sums: only if every
+    // rank's has, since the parts then carry records instead of roots)
+    gatherList(&PeerLists::ok, {oneExchangeLocal() ? 1.0 : 0.0, plan.xUpPartial ? 1.0 : 0.0}, oksAll);
+    bool allOk = true, allUp = true;
+    for (const auto& o : oksAll) {
+        allOk = allOk && !o.empty() && o[0] > 0.5;
+        allUp = allUp && o.size() > 1 && o[1] > 0.5;
+    }
+    oxUp = false;
     if (allOk) {  // every rank decides alike: all take part in the same collectives
-        std::vector<std::vector<double>> oneAll, nodesAll;
+        std::vector<std::vector<double>> oneAll, nodesAll, upAll;
         gatherList(&PeerLists::oneHalo, std::vector<double>(plan.xOneHalo.begin(), plan.xOneHalo.end()), oneAll);
         gatherList(&PeerLists::needNodes, std::vector<double>(plan.xNeedNodes.begin(), plan.xNeedNodes.end()), nodesAll);
+        if (allUp)
+            gatherList(&PeerLists::upRec, std::vector<double>(plan.xUpRecNode.begin(), plan.xUpRecNode.end()), upAll);
         const int RK = kRank * rootRhs(nb);
+        // the partial-sum records: (node, rank, record, source offset), summed per node in
+        // (rank, record) order; this rank's own from its record buffer (~offset)
+        struct UpSum {
+            int node, rank, j;
+            int64_t src;
+        };
+        std::vector<UpSum> sums;
+        const int64_t myRec = allUp ? (int64_t)plan.xUpRecNode.size() * RK : 0;
+        if (allUp)
+            for (size_t j = 0; j < plan.xUpRecNode.size(); ++j)
+                sums.push_back({plan.xUpRecNode[j], me, (int)j, ~((int64_t)j * RK)});
         auto ownerOf = [&](int n) {
             return (int)(std::upper_bound(cuts.begin() + 1, cuts.end() - 1, tree.begin[n]) - (cuts.begin() + 1));
         };
@@ -1709,7 +1741,15 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
             oxSoff[p] = so;
             oxRoff[p] = ro;
             if (p == me) continue;
-            if (rec > 0) {
+            if (allUp) {  // this rank's records to p; p's records from it
+                if (myRec > 0) {
+                    rtS.push_back(so);
+                    so += myRec;
+                }
+                for (size_t j = 0; j < upAll[p].size(); ++j)
+                    sums.push_back({(int)upAll[p][j], p, (int)j, ro + (int64_t)j * RK});
+                ro += (int64_t)upAll[p].size() * RK;
+            } else if (rec > 0) {
                 rtS.push_back(so);
                 rtR.push_back(ro);
                 rtD.push_back((int64_t)p * rec);
@@ -1745,6 +1785,27 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
             ro += (int64_t)rp.size() * nb + (int64_t)rn.size() * RK;
             oxScount[p] = so - oxSoff[p];
             oxRcount[p] = ro - oxRoff[p];
+        }
+        if (allUp) {
+            std::sort(sums.begin(), sums.end(), [](const UpSum& a, const UpSum& b) {
+                return a.node != b.node ? a.node < b.node : a.rank != b.rank ? a.rank < b.rank : a.j < b.j;
+            });
+            std::vector<int> sNode, sPtr(1, 0);
+            std::vector<int64_t> sSrc;
+            for (size_t i = 0; i < sums.size(); ++i) {
+                if (i == 0 || sums[i].node != sums[i - 1].node) {
+                    if (i > 0) sPtr.push_back((int)sSrc.size());
+                    sNode.push_back(sums[i].node);
+                }
+                sSrc.push_back(sums[i].src);
+            }
+            if (!sums.empty()) sPtr.push_back((int)sSrc.size());
+            oxUpSums = (int64_t)sNode.size();
+            up(dOxUpSumNode, sNode);
+            up(dOxUpSumPtr, sPtr);
+            up(dOxUpSumSrc, sSrc);
+            dXUpRec.alloc((size_t)std::max<int64_t>(myRec, 1) * sizeof(double));
+            oxUp = true;
         }
         oxRootParts = (int64_t)rtS.size();
         up(dOxRootSend, rtS);
@@ -1814,18 +1875,20 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
         // rank, and from each owner the input positions and multipoles this rank reads;
         // then phase 2 (near field, upper tiers + M2L, down pass)
         oneXActive = true;
+        upActive = oxUp;
         try {
             blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 1, dXRootsSend.as<double>(), nullptr);
             const int RK = kRank * rootRhs(nb);
-            // one pack launch (this rank's roots into every peer's part, the input
-            // positions and the multipole rows each peer reads), one all-to-all-v, one
-            // unpack launch (the peers' roots into the slot layout, the own roots, the
+            // one pack launch (this rank's roots -- or its partial-sum records -- into
+            // every peer's part, the input positions and the multipole rows each peer
+            // reads), one all-to-all-v, one unpack launch (the peers' roots into the slot
+            // layout and the own roots -- or every upper node's records summed -- the
             // input's halo, the multipoles)
             OxArgs pk;
             pk.nRoot = oxRootParts;
-            pk.rec = rec;
+            pk.rec = oxUp ? (int64_t)plan.xUpRecNode.size() * RK : rec;
             pk.rootOff = dOxRootSend.as<int64_t>();
-            pk.roots = dXRootsSend.as<double>();
+            pk.roots = oxUp ? dXUpRec.as<double>() : dXRootsSend.as<double>();
             pk.nPts = oxNsendPts;
             pk.nb = nb;
             pk.pos = dOxSendPos.as<int64_t>();
@@ -1839,7 +1902,15 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
             pk.nodeBase = dOxSendNodeBase.as<int64_t>();
             pk.mult = dMult.as<double>();
             pk.buf = dOxSendBuf.as<double>();
-            launch_ox(pk, true, s);
+            if (oxUp) {  // the pack launch forms this rank's records (its first workgroups)
+                OxArgs pr = pk;
+                pr.nRoot = 0;
+                launch_ox_pack_up(rootRhs(nb), (int)(plan.xUpTask.size() / Plan::kUpTaskInts), dXUpTask.as<int>(),
+                                  dMult.as<double>(), dParams.as<Params>(), dXUpRec.as<double>(), (int)oxRootParts,
+                                  dOxRootSend.as<int64_t>(), pr, s);
+            } else {
+                launch_ox(pk, true, s);
+            }
             comm->alltoallv(dOxSendBuf.as<double>(), oxScount.data(), oxSoff.data(), dOxRecvBuf.as<double>(),
                             oxRcount.data(), oxRoff.data(), s);
             OxArgs uk = pk;
@@ -1856,14 +1927,26 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
             uk.node = dOxRecvNode.as<int>();
             uk.nodeBase = dOxRecvNodeBase.as<int64_t>();
             uk.buf = dOxRecvBuf.as<double>();
+            if (oxUp) {
+                uk.nRoot = 0;
+                uk.ownRoots = nullptr;
+                uk.nSum = oxUpSums;
+                uk.sumNode = dOxUpSumNode.as<int>();
+                uk.sumPtr = dOxUpSumPtr.as<int>();
+                uk.sumSrc = dOxUpSumSrc.as<int64_t>();
+                uk.ownRec = dXUpRec.as<double>();
+            }
             launch_ox(uk, false, s);
             blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 2, nullptr, dXRootsRecv.as<double>());
         } catch (...) {
             oneXActive = false;
+            upActive = false;
             throw;
         }
         oneXActive = false;
+        upActive = false;
         ++oneXApplies;
+        if (oxUp) ++upPartialApplies;
         return;
     }
     // the input's halo from its owners

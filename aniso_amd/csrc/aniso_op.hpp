@@ -169,6 +169,7 @@ public:
     int64_t topRecoveries = 0;  // applies re-run after a time-out (aniso_stats)
     int64_t topSteals();        // tier tasks the fused launch's waiting blocks computed themselves (aniso_stats)
     int64_t oneXApplies = 0;    // sharded matvecs through the one-collective exchange (aniso_stats)
+    int64_t upPartialApplies = 0;  // ... of them with the upper multipoles as partial sums (aniso_stats)
     bool forceUnfused = false;
     // set while a call that recovers its own time-outs (the block solve) runs: the
     // entry checks of the applies it enqueues leave the flag to its recovery points
@@ -269,6 +270,9 @@ private:
     // of the block apply, beside the up pass (ANISO_NEAR_EARLY=0: after it, from fT)
     bool nearEarly = true;
     bool nearOrderUp = true;  // the near launch issued after the bottom up tier's (ANISO_NEAR_ORDER=first: before)
+    // a one-collective sharded matvec starts the near field's own-range groups beside
+    // phase 1 (ANISO_SHARD_NEAR_EARLY=0: every group after the exchange)
+    bool shardNearEarly = true;
     int topTraceBlocks = 0, topTraceNear = 0;
     // the attached communicator and its halo exchange plan (commInit): per element of
     // the send / receive position lists its tree position and its place in the
@@ -291,6 +295,13 @@ private:
     std::vector<int64_t> oxScount, oxSoff, oxRcount, oxRoff;
     int64_t oxNsendPts = 0, oxNrecvPts = 0, oxNsendNodes = 0, oxNrecvNodes = 0;
     bool oxReady = false, oneXActive = false, oneXOn = true;
+    // the upper multipoles as partial sums (Plan::xUpPartial on every rank): the parts
+    // carry every rank's records instead of the roots; the unpack sums each upper
+    // node's records (oxUpSumNode / Ptr / Src: >= 0 an offset into the receive buffer,
+    // < 0 ~offset into this rank's own records); upActive marks such a matvec
+    bool oxUp = false, upActive = false;
+    DevBuf dXUpTask, dXUpRec, dOxUpSumNode, dOxUpSumPtr, dOxUpSumSrc;
+    int64_t oxUpSums = 0;
     bool oneExchangeUsable(int which);
     bool oneExchangeLocal() const;  // this rank's (shard- and process-dependent) part, gathered at commInit
     // sticky time-out flag of the fused launch's in-kernel hand-offs, in host-visible

@@ -1034,6 +1034,154 @@ void launch_roots_unpack(int K, int nslots, const int* nodes, const double* recv
     HIP_LAUNCH_CHECK();
 }
 
+// the one-collective exchange's pack / unpack (kernels.hpp OxArgs): one thread per
+// double of the roots, then of the input positions, then of the multipole rows
+template <bool PACK>
+__device__ __forceinline__ void ox_element(const OxArgs& a, const int64_t e) {
+    const int64_t nr = a.nRoot * a.rec, np = a.nPts * a.nb, nn = a.nNode * a.len;
+    if (e < nr) {
+        const int64_t j = e / a.rec, c = e - j * a.rec;
+        if (PACK) a.buf[a.rootOff[j] + c] = a.roots[c];
+        else a.roots[a.rootDst[j] + c] = a.buf[a.rootOff[j] + c];
+    } else if (e < nr + np) {
+        const int64_t t = e - nr, b = t / a.nPts, i = t - b * a.nPts;  // consecutive lanes: consecutive positions
+        const int64_t q = a.base[i] + b * a.stride[i];
+        if (PACK) a.buf[q] = a.x[(size_t)b * a.ldx + a.pos[i]];
+        else a.x[(size_t)b * a.ldx + a.pos[i]] = a.buf[q];
+    } else if (e < nr + np + nn) {
+        const int64_t t = e - nr - np, j = t / a.len, c = t - j * a.len;
+        if (PACK) a.buf[a.nodeBase[j] + c] = a.mult[(size_t)a.node[j] * a.len + c];
+        else a.mult[(size_t)a.node[j] * a.len + c] = a.buf[a.nodeBase[j] + c];
+    } else if (!PACK && a.ownRoots && e < nr + np + nn + a.rec) {
+        const int64_t c = e - nr - np - nn;
+        a.roots[a.ownDst + c] = a.ownRoots[c];
+    } else if (!PACK && a.nSum > 0) {  // an upper node: its records summed in (rank, record) order
+        const int64_t t = e - nr - np - nn - (a.ownRoots ? a.rec : 0), j = t / a.len, c = t - j * a.len;
+        if (j >= a.nSum) return;
+        // 8 records per round: their offsets, then their values, all loads of a round
+        // independent (one dependent pair per record measured 16 us at 16 records)
+        const int k0 = a.sumPtr[j], k1 = a.sumPtr[j + 1];
+        double v = 0.0;
+        for (int kb = k0; kb < k1; kb += 8) {
+            int64_t o[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) o[u] = kb + u < k1 ? a.sumSrc[kb + u] : INT64_MIN;
+            double x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                x[u] = o[u] == INT64_MIN ? 0.0 : o[u] >= 0 ? a.buf[o[u] + c] : a.ownRec[~o[u] + c];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (kb + u < k1) v += x[u];
+        }
+        a.mult[(size_t)a.sumNode[j] * a.len + c] = v;
+    }
+}
+
+template <bool PACK>
+__global__ void k_ox(OxArgs a) {
+    ox_element<PACK>(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+void launch_ox(const OxArgs& a, bool pack, hipStream_t s) {
+    const int64_t n = a.nRoot * a.rec + a.nPts * a.nb + a.nNode * a.len + (!pack && a.ownRoots ? a.rec : 0) +
+                      (!pack ? a.nSum * a.len : 0);
+    if (n <= 0) return;
+    if (pack) k_ox<true><<<blocks_for(n, 256), 256, 0, s>>>(a);
+    else k_ox<false><<<blocks_for(n, 256), 256, 0, s>>>(a);
+    HIP_LAUNCH_CHECK();
+}
+
+// The upper multipoles as partial sums (Plan::xUpTask), in the
+// exchange's pack launch: its first workgroups take one partial task each -- this
+// rank's tier-0 roots under one node A two levels above them.  M2M (bbfmm.h:855-859)
+// of the roots to the mid level and to A, then A's contribution to each ancestor up
+// to the topmost level an M2L reads, one transfer matrix per level.  M2M is linear,
+// so this rank's share of an upper multipole is the M2M of its own roots alone; each
+// share an M2L reads is a record, stored into this rank's record buffer and into
+// every peer's part; the unpack sums every rank's records of a node in a fixed order
+// (ox_element).  The other workgroups pack the input positions and multipole rows.
+struct UpPack {
+    int ntask = 0;
+    const int* task = nullptr;  // Plan::kUpTaskInts ints per task
+    const double* mult = nullptr;
+    const Params* P = nullptr;
+    double* rec = nullptr;            // this rank's records
+    int nPeer = 0;
+    const int64_t* peerOff = nullptr;  // each peer part's first record (doubles into the send buffer)
+};
+
+template <int K>
+__global__ void __launch_bounds__(256) k_ox_pack_up(UpPack u, OxArgs a) {
+    if ((int)blockIdx.x >= u.ntask) {
+        ox_element<true>(a, (int64_t)(blockIdx.x - u.ntask) * blockDim.x + threadIdx.x);
+        return;
+    }
+    constexpr int RK = kRank * K;
+    constexpr int NI = Plan::kUpTaskInts;
+    __shared__ int T[NI];
+    __shared__ double Rm[4 * kRank * kRank];  // R[q][r * 16 + rr]: row r of quadrant q's M2M
+    __shared__ double X[16 * RK];             // the roots, slot 4 q1 + q0
+    __shared__ double Mid[4 * RK];
+    __shared__ double C[2][RK];               // A's share, then its contributions up the chain
+    const int* tk = u.task + (size_t)blockIdx.x * NI;
+    for (int i = threadIdx.x; i < NI; i += blockDim.x) T[i] = tk[i];
+    for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) Rm[i] = (&u.P->R[0][0])[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < 16 * RK; i += blockDim.x) {
+        const int r = T[i / RK];
+        X[i] = r >= 0 ? u.mult[(size_t)r * RK + i % RK] : 0.0;
+    }
+    __syncthreads();
+    auto store = [&](int ri, int e, double v) {  // record ri, entry e: own buffer and every peer part
+        if (ri < 0) return;
+        u.rec[(size_t)ri * RK + e] = v;
+        for (int p = 0; p < u.nPeer; ++p) a.buf[u.peerOff[p] + (int64_t)ri * RK + e] = v;
+    };
+    // parent entry (r, b) = sum over quadrants q and rows rr of R[q][r, rr] child_q[rr, b]
+    auto m2m = [&](const double* child, int q, int r, int b, double acc) {
+        const double* R = Rm + q * kRank * kRank + r * kRank;
+#pragma unroll
+        for (int rr = 0; rr < kRank; ++rr) acc += R[rr] * child[rr * K + b];
+        return acc;
+    };
+    for (int it = threadIdx.x; it < 4 * RK; it += blockDim.x) {
+        const int q1 = it / RK, e = it - q1 * RK, r = e / K, b = e - r * K;
+        double acc = 0.0;
+        for (int q0 = 0; q0 < 4; ++q0) acc = m2m(X + (4 * q1 + q0) * RK, q0, r, b, acc);
+        Mid[it] = acc;
+        store(T[16 + q1], e, acc);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < RK; e += blockDim.x) {
+        const int r = e / K, b = e - r * K;
+        double acc = 0.0;
+        for (int q1 = 0; q1 < 4; ++q1) acc = m2m(Mid + q1 * RK, q1, r, b, acc);
+        C[0][e] = acc;
+        store(T[20], e, acc);
+    }
+    for (int c = 0; c < T[21]; ++c) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < RK; e += blockDim.x) {
+            const int r = e / K, b = e - r * K;
+            const double v = m2m(C[c & 1], T[22 + c], r, b, 0.0);
+            C[(c + 1) & 1][e] = v;
+            store(T[30 + c], e, v);
+        }
+    }
+}
+
+void launch_ox_pack_up(int K, int ntask, const int* task, const double* mult, const Params* P, double* rec,
+                       int nPeer, const int64_t* peerOff, const OxArgs& a, hipStream_t s) {
+    if (a.nRoot != 0) throw std::invalid_argument("pack with partial sums: the records replace the root parts");
+    const int64_t n = a.nPts * a.nb + a.nNode * a.len;
+    const unsigned nb = (unsigned)ntask + (unsigned)blocks_for(n, 256);
+    if (nb == 0) return;
+    const UpPack u{ntask, task, mult, P, rec, nPeer, peerOff};
+    ANISO_DISPATCH_K(K, (k_ox_pack_up<KK><<<nb, 256, 0, s>>>(u, a)));
+    HIP_LAUNCH_CHECK();
+}
+
 void launch_m2l(int K, int ntgt, const int* tgt, const int64_t* ptr, const int* nDir, const int* canonBase,
                 const int* outSlot, const int* src, const ModeArgs* tab, int nterm, const double* mult, int maxCanon,
                 double* partial, double* local, hipStream_t s) {

@@ -446,6 +446,32 @@ int aniso_shard_exchange_one(aniso_handle h, int64_t* info) {
     });
 }
 
+int aniso_shard_upper_partials(aniso_handle h, int64_t* info) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(info);
+        const auto& p = get(h).plan;
+        info[0] = p.xUpPartial ? 1 : 0;
+        info[1] = (int64_t)(p.xUpTask.size() / aniso::Plan::kUpTaskInts);
+        info[2] = (int64_t)p.xUpRecNode.size();
+        info[3] = p.xUpTop;
+        info[4] = p.tierRootLevel.empty() ? -1 : p.tierRootLevel[0];
+        int64_t roots = 0;
+        for (size_t t = 0; t < p.xUpTask.size(); t += aniso::Plan::kUpTaskInts)
+            for (int i = 0; i < 16; ++i) roots += p.xUpTask[t + i] >= 0;
+        info[5] = roots;
+    });
+}
+
+int aniso_shard_upper_records(aniso_handle h, int* nodes) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(nodes);
+        const auto& p = get(h).plan;
+        std::copy(p.xUpRecNode.begin(), p.xUpRecNode.end(), nodes);
+    });
+}
+
 int aniso_shard_one_halo(aniso_handle h, int64_t* ranges) {
     ENTER(h);
     return guarded([&] {
@@ -551,7 +577,7 @@ int aniso_tree_list(aniso_handle h, int which, int64_t* ptr, int* idx) {
     });
 }
 
-constexpr int kStatsV1 = 19, kStats = 28;
+constexpr int kStatsV1 = 19, kStats = 29;
 
 static void stats_fill(aniso::Operator& op, int64_t* s) {
     s[0] = op.nearEntries();
@@ -588,6 +614,7 @@ static void stats_fill(aniso::Operator& op, int64_t* s) {
     s[25] = op.oneXApplies;  // sharded matvecs through the one-collective exchange
     s[26] = op.mrhsM2LPairs();  // directed M2L pairs of the 16-RHS MFMA operators (0 before their plan)
     s[27] = op.topSteals();     // upper-tier tasks computed by waiting blocks of the fused launch
+    s[28] = op.upPartialApplies;  // one-collective matvecs with the upper multipoles as partial sums
 }
 
 // the round-2 entry: the first kStatsV1 entries only (callers sized for them)

@@ -250,6 +250,24 @@ struct Plan {
     std::vector<int64_t> xOneHalo;
     int64_t xOneHaloPoints = 0;
     bool xOneOk = false;
+    // The upper multipoles as partial sums (the one-collective
+    // form over a tree whose points all lie under tier-0 roots).  M2M is linear, so a
+    // rank forms its own roots' share of every upper multipole in phase 1: per partial
+    // task -- its roots under one node A two levels above them -- the mid level, A,
+    // and A's contribution to each ancestor up to xUpTop, the topmost level any M2L
+    // reads.  Every rank receives every rank's records and sums each node's in a fixed
+    // order (rank, record), so phase 2 runs no up tier and every cluster starts at
+    // once; the level-L0 roots an M2L reads travel as multipole rows (xNeedNodes).
+    // Task record (kUpTaskInts ints): [0, 16) root at slot 4 q1 + q0 (-1 none), [16, 20)
+    // record of mid q1, [20] record of A, [21] chain length, [22, 30) chain quadrants
+    // (A's, then its parent's ...), [30, 38) chain records (-1: a level no M2L reads).
+    static constexpr int kUpTaskInts = 40;
+    static constexpr int kUpChainMax = 8;
+    bool xUpPartialIn = true;  // input: ANISO_UPPER_PARTIAL
+    bool xUpPartial = false;
+    int xUpTop = 0;
+    std::vector<int> xUpTask;
+    std::vector<int> xUpRecNode;  // per record of this rank: its upper node
 
     void build(const Tree& t, int np, int rank, int nranks);
     // the exchange plan above; sz / d2: the square grid of the correction stencil

@@ -249,11 +249,12 @@ std::vector<int64_t> shard_cuts(const Tree& t, int nranks) {
 void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     (void)np;
     if (nranks_ < 1 || rank_ < 0 || rank_ >= nranks_) throw std::invalid_argument("bad shard rank/nranks");
-    const bool symNear = nearSymmetric, symHs = nearSymHs;
+    const bool symNear = nearSymmetric, symHs = nearSymHs, upIn = xUpPartialIn;
     const int capCanon = maxCanon;
     *this = Plan();
     nearSymmetric = symNear;
     nearSymHs = symHs;
+    xUpPartialIn = upIn;
     maxCanon = std::max(0, std::min(kMaxCanon, capCanon));
     rank = rank_;
     nranks = nranks_;
@@ -1022,6 +1023,10 @@ void Plan::buildExchange(const Tree& t, int sz, int d2) {
     xOneHalo.clear();
     xOneHaloPoints = 0;
     xOneOk = false;
+    xUpPartial = false;
+    xUpTop = 0;
+    xUpTask.clear();
+    xUpRecNode.clear();
     xRootSend.clear();
     xRootRecv.clear();
     xRootSlot.clear();
@@ -1128,9 +1133,14 @@ void Plan::buildExchange(const Tree& t, int sz, int d2) {
         ok = ok && t.begin[r] >= ownBegin && t.begin[r] + t.count[r] <= ownEnd;
     }
     std::sort(xOwnT0Tasks.begin(), xOwnT0Tasks.end());
+    // the upper multipoles as partial sums: every point under a tier-0 root (no P2M
+    // above L0), two levels above the roots, and this rank's roots inside its range
+    bool allCovered = true;
+    for (int64_t p = 0; p < N && allCovered; ++p) allCovered = covered[p] != 0;
+    xUpPartial = xUpPartialIn && ok && nranks > 1 && allCovered && L0 >= 2;
     std::vector<char> needNode(t.nn, 0);
-    auto markNeed = [&](int n) {  // a multipole below L0 in another rank's subtree
-        if (t.level[n] > L0 && ownerOf(t.begin[n]) != rank) needNode[n] = 1;
+    auto markNeed = [&](int n) {  // a multipole below L0 (at L0: partial sums) in another rank's subtree
+        if (t.level[n] >= (xUpPartial ? L0 : L0 + 1) && ownerOf(t.begin[n]) != rank) needNode[n] = 1;
     };
     for (int n : m2lTgt) {
         for (int64_t k = t.vPtr[n]; k < t.vPtr[n + 1]; ++k)
@@ -1154,6 +1164,74 @@ void Plan::buildExchange(const Tree& t, int sz, int d2) {
         p = e;
     }
     xOneOk = ok && nranks > 1;
+    if (xUpPartial) {
+        // xUpTop: the topmost level above L0 whose multipoles an M2L reads (V / X
+        // sources, or targets with a list: their own multipole feeds the dual products)
+        xUpTop = L0;
+        for (int n = 0; n < t.nn; ++n) {
+            if (t.isEmpty[n]) continue;
+            const bool lists = t.vPtr[n + 1] > t.vPtr[n] || t.xPtr[n + 1] > t.xPtr[n];
+            if (lists) xUpTop = std::min(xUpTop, t.level[n]);
+            for (int64_t k = t.xPtr[n]; k < t.xPtr[n + 1]; ++k) xUpTop = std::min(xUpTop, t.level[t.xIdx[k]]);
+        }
+        const int La = L0 - 2;
+        if (La - xUpTop > kUpChainMax) throw std::logic_error("upper partials: chain deeper than its record");
+        auto quadrant = [&](int n) {
+            const int p = t.parent[n];
+            for (int q = 0; q < 4; ++q)
+                if (t.child[p][q] == n) return q;
+            throw std::logic_error("upper partials: a node is not its parent's child");
+        };
+        // tasks in tree order of A; a task's roots by their slot under A
+        std::vector<int> tops;
+        std::vector<int> taskOfTop(t.nn, -1);
+        for (int r : xRootSend) {
+            const int A = t.parent[t.parent[r]];
+            if (taskOfTop[A] < 0) {
+                taskOfTop[A] = (int)tops.size();
+                tops.push_back(A);
+            }
+        }
+        std::vector<int> order(tops.size());
+        for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+        std::sort(order.begin(), order.end(), [&](int a, int b) { return t.begin[tops[a]] < t.begin[tops[b]]; });
+        std::vector<std::array<int, kUpTaskInts>> recs(tops.size());
+        for (auto& a : recs) a.fill(-1);
+        for (int r : xRootSend) {
+            const int mid = t.parent[r];
+            auto& a = recs[taskOfTop[t.parent[mid]]];
+            a[4 * quadrant(mid) + quadrant(r)] = r;
+        }
+        for (int i : order) {
+            auto& a = recs[i];
+            const int A = tops[i];
+            for (int q1 = 0; q1 < 4; ++q1) {
+                const bool has = a[4 * q1] >= 0 || a[4 * q1 + 1] >= 0 || a[4 * q1 + 2] >= 0 || a[4 * q1 + 3] >= 0;
+                if (has && L0 - 1 >= xUpTop) {
+                    a[16 + q1] = (int)xUpRecNode.size();
+                    xUpRecNode.push_back(t.child[A][q1]);
+                }
+            }
+            if (La >= xUpTop) {
+                a[20] = (int)xUpRecNode.size();
+                xUpRecNode.push_back(A);
+            }
+            const int nc = std::max(La - xUpTop, 0);
+            a[21] = nc;
+            int n = A;
+            for (int c = 0; c < kUpChainMax; ++c) {
+                a[22 + c] = 0;
+                if (c >= nc) continue;
+                a[22 + c] = quadrant(n);
+                n = t.parent[n];
+                a[30 + c] = (int)xUpRecNode.size();
+                xUpRecNode.push_back(n);
+            }
+            a[38] = A;
+            a[39] = 0;
+            xUpTask.insert(xUpTask.end(), a.begin(), a.end());
+        }
+    }
     nearGrpEarly.clear();
     nearGrpLate.clear();
     for (size_t g = 0; g + 1 < nsPtr.size(); ++g) {

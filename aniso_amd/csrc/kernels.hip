@@ -334,37 +334,5 @@ void launch_halo_unpack(int64_t n, int nb, const int64_t* pos, const int64_t* ba
     HIP_LAUNCH_CHECK();
 }
 
-// the one-collective exchange's pack / unpack (kernels.hpp OxArgs): one thread per
-// double of the roots, then of the input positions, then of the multipole rows
-template <bool PACK>
-__global__ void k_ox(OxArgs a) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t nr = a.nRoot * a.rec, np = a.nPts * a.nb, nn = a.nNode * a.len;
-    if (e < nr) {
-        const int64_t j = e / a.rec, c = e - j * a.rec;
-        if (PACK) a.buf[a.rootOff[j] + c] = a.roots[c];
-        else a.roots[a.rootDst[j] + c] = a.buf[a.rootOff[j] + c];
-    } else if (e < nr + np) {
-        const int64_t t = e - nr, b = t / a.nPts, i = t - b * a.nPts;  // consecutive lanes: consecutive positions
-        const int64_t q = a.base[i] + b * a.stride[i];
-        if (PACK) a.buf[q] = a.x[(size_t)b * a.ldx + a.pos[i]];
-        else a.x[(size_t)b * a.ldx + a.pos[i]] = a.buf[q];
-    } else if (e < nr + np + nn) {
-        const int64_t t = e - nr - np, j = t / a.len, c = t - j * a.len;
-        if (PACK) a.buf[a.nodeBase[j] + c] = a.mult[(size_t)a.node[j] * a.len + c];
-        else a.mult[(size_t)a.node[j] * a.len + c] = a.buf[a.nodeBase[j] + c];
-    } else if (!PACK && a.ownRoots && e < nr + np + nn + a.rec) {
-        const int64_t c = e - nr - np - nn;
-        a.roots[a.ownDst + c] = a.ownRoots[c];
-    }
-}
-
-void launch_ox(const OxArgs& a, bool pack, hipStream_t s) {
-    const int64_t n = a.nRoot * a.rec + a.nPts * a.nb + a.nNode * a.len + (!pack && a.ownRoots ? a.rec : 0);
-    if (n <= 0) return;
-    if (pack) k_ox<true><<<blocks_for(n, 256), 256, 0, s>>>(a);
-    else k_ox<false><<<blocks_for(n, 256), 256, 0, s>>>(a);
-    HIP_LAUNCH_CHECK();
-}
 
 }  // namespace aniso

@@ -372,8 +372,22 @@ struct OxArgs {
     const int64_t* nodeBase = nullptr;
     double* mult = nullptr;
     double* buf = nullptr;
+    // unpack, the upper multipoles as partial sums (Plan::xUpPartial): node sumNode[j]
+    // = the sum of its records sumSrc[sumPtr[j] .. sumPtr[j + 1]) in that order (>= 0:
+    // offset into buf, < 0: ~offset into ownRec), len doubles each
+    int64_t nSum = 0;
+    const int* sumNode = nullptr;
+    const int* sumPtr = nullptr;
+    const int64_t* sumSrc = nullptr;
+    const double* ownRec = nullptr;
 };
 void launch_ox(const OxArgs& a, bool pack, hipStream_t s);
+// the pack launch with the upper multipoles as partial sums (apply.hip k_ox_pack_up):
+// one workgroup per task of Plan::xUpTask (kUpTaskInts ints each) stores its records
+// into rec and into each of nPeer parts at peerOff (doubles into a.buf), the rest pack
+// a's input positions and multipole rows (a.nRoot must be 0)
+void launch_ox_pack_up(int K, int ntask, const int* task, const double* mult, const Params* P, double* rec,
+                       int nPeer, const int64_t* peerOff, const OxArgs& a, hipStream_t s);
 
 
 // host-callable device helpers used by tests through the C ABI

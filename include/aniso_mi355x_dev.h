@@ -38,6 +38,14 @@ int aniso_forward_f32_stages_dev(aniso_handle h, const float *x, int mask, float
 int aniso_shard_exchange_one(aniso_handle h, int64_t *info);
 /* its input ranges: 2 x info[3] tree positions [b, e) */
 int aniso_shard_one_halo(aniso_handle h, int64_t *ranges);
+/* the upper multipoles as partial sums of the one-collective exchange (section 5,
+ * round 5; ANISO_UPPER_PARTIAL=0 keeps the root records): info[0..5] = 1 if this
+ * rank's plan forms them, its partial tasks, its records (one per upper node share
+ * an M2L reads), the topmost level an M2L reads, the tier-0 root level, the roots
+ * its tasks cover (= its own tier-0 roots) */
+int aniso_shard_upper_partials(aniso_handle h, int64_t *info);
+/* the node of each of this rank's records (info[2] ints, record order) */
+int aniso_shard_upper_records(aniso_handle h, int *nodes);
 int aniso_tree_size(aniso_handle h, int *nnodes, int *max_level);
 /* per node ints[11*i ..]: parent, child0..3, level, slot, isLeaf, isEmpty, nSource, begin;
  * geom[4*i ..]: cx, cy, rx, ry */
@@ -64,9 +72,10 @@ int aniso_tree_list(aniso_handle h, int which, int64_t *ptr, int *idx);
  * sharded matvecs run through the one-collective exchange (section 5); then the
  * directed M2L pairs of the 16-right-hand-side MFMA operators (0 before their plan);
  * then the upper-tier tasks that waiting blocks of the fused top-of-tree launch
- * computed themselves after ANISO_TOP_SPIN_LIMIT polls (section 3.10).
+ * computed themselves after ANISO_TOP_SPIN_LIMIT polls (section 3.10); then the
+ * one-collective matvecs that exchanged the upper multipoles as partial sums.
  * aniso_stats_n writes the first min(cap, *n) of them and sets *n to their count
- * (28 here); aniso_stats, the round-2 form, writes the first 19 only. */
+ * (29 here); aniso_stats, the round-2 form, writes the first 19 only. */
 int aniso_stats_n(aniso_handle h, int64_t *stats, int cap, int *n);
 int aniso_stats(aniso_handle h, int64_t *stats);
 /* per-stage device times (ms), averaged over every apply since aniso_set_timing(h, 1)

@@ -1603,7 +1603,8 @@ class _ThreadCollectives:
 @pytest.mark.parametrize("sz,world,one,d,ml", [(64, 2, "1", 1, 20), (64, 2, "0", 1, 20), (64, 4, "1", 1, 20),
                                                (64, 8, "1", 1, 20), (64, 3, "1", 1, 20), (96, 3, "1", 1, 20),
                                                (40, 2, "1", 1, 3), (32, 2, "1", 2, 20), (64, 3, "mixed", 1, 20),
-                                               (64, 2, "spin0", 1, 20)])
+                                               (64, 2, "spin0", 1, 20), (256, 4, "1", 1, 20), (512, 8, "1", 1, 20),
+                                               (256, 4, "partial0", 1, 20)])
 def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     """The library's one-call sharded block matvec (aniso_block_op_sharded_dev) with
     `world` ranks as threads of one process on the box's GPU, each rank's input valid
@@ -1618,13 +1619,18 @@ def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     (ANISO_ONE_EXCHANGE differs per handle): the ranks must still agree (ADVICE r04:
     the decision is all-gathered at comm_init), here on the two-collective form.
     "spin0": ANISO_TOP_SPIN_LIMIT=0, every waiting block of the fused launch computes
-    the upper tiers it reads (the sharded phase 2, from the gathered roots)."""
+    the upper tiers it reads (the sharded phase 2, from the gathered roots; with
+    ANISO_UPPER_PARTIAL=0, since the partial sums leave phase 2 no up tier).
+    The one-collective form exchanges the upper multipoles as partial sums where every
+    rank's plan forms them (records at 256 and 512 points per side; "partial0":
+    ANISO_UPPER_PARTIAL=0, the root records and the upper tiers on every rank)."""
     torch = _torch()
     import threading
 
     import aniso_amd
 
-    monkeypatch.setenv("ANISO_ONE_EXCHANGE", "1" if one in ("mixed", "spin0") else one)
+    monkeypatch.setenv("ANISO_ONE_EXCHANGE", "1" if one in ("mixed", "spin0", "partial0") else one)
+    monkeypatch.setenv("ANISO_UPPER_PARTIAL", "0" if one in ("spin0", "partial0") else "1")
     ks = 5
     full = aniso_amd.Aniso(sz, d, ks, 0.8, 10, 4, ml)
     xy = full.getNodes()
@@ -1680,6 +1686,11 @@ def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     assert not torch.isnan(Y).any()
     assert float(torch.linalg.norm(Y - ref) / torch.linalg.norm(ref)) <= 1e-13
     used = [h.stats()["one_exchange_applies"] for h in hs]
-    assert used == [2 * int(one in ("1", "spin0") and all(oks) and staged)] * world
+    one_used = one in ("1", "spin0", "partial0") and all(oks) and staged
+    assert used == [2 * int(one_used)] * world
+    ups = [h.shard_upper_partials() for h in hs]
+    assert [h.stats()["upper_partial_applies"] for h in hs] == [2 * int(one_used and all(u["on"] for u in ups))] * world
+    if sz >= 256 and one == "1":
+        assert all(u["on"] and u["records"] > 0 for u in ups)
     if one == "spin0":
         assert all(h.stats()["top_steals"] > 0 for h in hs)

@@ -202,3 +202,40 @@ def test_one_collective_exchange_plan(sz, ks, nranks):
     assert all(oks) == (nranks != 3)
     a.set_shard(0, 1)
     assert a.shard_exchange_one()["ok"] == 0  # one rank: nothing to exchange
+
+
+@pytest.mark.parametrize("sz,nranks", [(256, 2), (256, 4), (512, 8), (128, 3)])
+def test_upper_partial_sum_plan(sz, nranks, monkeypatch):
+    """The upper multipoles as partial sums (Plan::xUpPartial, DESIGN.md §5): each rank's
+    partial tasks cover exactly its own tier-0 roots, its records lie on the levels
+    between the topmost one an M2L reads and the root level, and the ranks' records
+    together reach every non-empty node there (each upper multipole is the sum of its
+    records over the ranks).  Where the one-collective form is refused (3 ranks of 16,384
+    points split tier-0 subtrees) or ANISO_UPPER_PARTIAL=0, no plan forms them."""
+    a = aniso_amd.Aniso(sz, 1, 5, 0.8, 10, 4, 20)
+    ints, _ = a.tree_nodes()
+    level, empty = ints[:, 5], ints[:, 8]
+    reached = set()
+    ons = []
+    for r in range(nranks):
+        a.set_shard(r, nranks)
+        one, u = a.shard_exchange_one(), a.shard_upper_partials()
+        ons.append(u["on"])
+        assert u["on"] == one["ok"]
+        if not u["on"]:
+            assert u["tasks"] == u["records"] == 0
+            continue
+        assert u["roots"] == one["own_t0_tasks"]
+        lv = level[u["record_nodes"]]
+        assert ((lv >= u["top_level"]) & (lv < u["root_level"])).all()
+        reached.update(int(n) for n in u["record_nodes"])
+    if all(ons):
+        top, root = u["top_level"], u["root_level"]
+        want = {n for n in range(len(level)) if top <= level[n] < root and not empty[n]}
+        assert want and reached == want
+    else:
+        assert nranks == 3
+    monkeypatch.setenv("ANISO_UPPER_PARTIAL", "0")
+    b = aniso_amd.Aniso(sz, 1, 5, 0.8, 10, 4, 20)
+    b.set_shard(0, nranks)
+    assert b.shard_upper_partials()["on"] == 0
