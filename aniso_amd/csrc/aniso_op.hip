@@ -811,10 +811,10 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     // symmetric U storage (Plan::nearSymHsOn): the harmonic near field reads its own
     // column lists and leaves the partner products of other groups to the down pass
     const bool hsSym = harmonic && plan.nearSymHsOn;
-    const bool nearFused = topFused && overlap && nearInTop && !ringOn && !hsSym && plan.nearCorrOk &&
+    const bool nearFused = topFused && overlapOn() && nearInTop && !ringOn && !hsSym && plan.nearCorrOk &&
                            near_hs_fusable((int)plan.leaves.size(), plan.nearMaxLeaf, plan.nsMax,
                                            dNearLoc.as<uint16_t>(), &nc, mask);
-    const bool fork = harmonic && overlap && !nearFused;
+    const bool fork = harmonic && overlapOn() && !nearFused;
     const hipStream_t sn = fork ? side : s;
     // the staged near field with its fused corrections forms its charges from the
     // input itself (NearHsArgs::xin), so it needs nothing from the up pass: it forks

@@ -170,6 +170,7 @@ public:
     int64_t topSteals();        // tier tasks the fused launch's waiting blocks computed themselves (aniso_stats)
     int64_t oneXApplies = 0;    // sharded matvecs through the one-collective exchange (aniso_stats)
     int64_t upPartialApplies = 0;  // ... of them with the upper multipoles as partial sums (aniso_stats)
+    bool nearOverlaps() const { return overlapOn(); }  // the block apply's near field on a side stream
     bool forceUnfused = false;
     // set while a call that recovers its own time-outs (the block solve) runs: the
     // entry checks of the applies it enqueues leave the flag to its recovery points
@@ -332,7 +333,13 @@ private:
     bool fuseSub = true;
     const double* subX = nullptr;
     int64_t subLd = 0;
-    int overlap = 1;
+    // the near field beside the up pass and the M2L on a side stream: -1 (default) on a
+    // shard only -- one GPU runs them serially, 1.190 against 1.202 ms per block matvec
+    // (same-process A/B, r05r; 1.148 against 1.162, r04ar): each kernel alone keeps
+    // the load path busy, and the fork and join cost more than the overlap saves; a
+    // rank of 8 overlaps (0.208 against 0.229 ms, r04ar).  ANISO_OVERLAP=0/1 forces it.
+    int overlap = -1;
+    bool overlapOn() const { return overlap < 0 ? plan.nranks > 1 : overlap != 0; }
     // stage timing: events recorded in-stream, (stage, start, end) spans per apply
     std::vector<hipEvent_t> evPool;
     int evUsed = 0;

@@ -303,6 +303,9 @@ def config5_leg(args):
     return leg
 
 
+SOCKET_CORES = 64  # physical cores of one socket of the GPU box's CPU (AMD EPYC 9575F)
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -396,6 +399,12 @@ def cpu_baseline(args, coeffs, op, block_check):
                                 for (m, a), (lo, hi) in spread.items()},
         "reps_per_mode": args.cpu_reps,
         "port_value": 1.0 / (per_matvec * t_port),
+        # SURVEY §8(d) / BASELINE.md name one socket's physical cores (64 on the EPYC
+        # 9575F); the box gives one GPU's job 16 CPUs and its OMP_NUM_THREADS is left as
+        # set, so the 64-core figure is the measured rate scaled linearly: an upper bound
+        # on the reference's rate at 64 threads (its own runs scale sub-linearly)
+        "socket_cores": SOCKET_CORES,
+        "value_linear_to_socket": 1.0 / (per_matvec * t_apply) * SOCKET_CORES / max(cores, 1),
         "port_mode_apply_s": {str(m): round(t, 4) for m, t in port_mode.items()},
     }, errs
 
@@ -621,7 +630,8 @@ def main():
                             "frac": round(near_gbs / HBM_PEAK_GBS, 4), "traffic": ntraffic,
                             "traffic_source": nsrc, "traffic_kernel": nkname,
                             "kernel": f"{nkern}<{nb}>", "kernel_ms": round(near_ms, 5),
-                            "algorithmic_bytes": int(near_bytes), "overlapped_with": roofline["kernel"]}
+                            "algorithmic_bytes": int(near_bytes),
+                            "overlapped_with": roofline["kernel"] if my_stats.get("near_overlap") else None}
         roofline["m2l_rsqrt"] = "v_rsq_f64 + 1 Newton step (~1e-13 relative per entry); near field 2 steps (full fp64)"
     applies = ks * (2 * ks - 1) if block else 1  # the reference's mapping calls per matvec
     cfg = (f"configs[2] (1M points, d=1, ns=10, np=4, maxLevel=20, g={args.g}): aniso.m GMRES block matvec "

@@ -73,9 +73,11 @@ int aniso_tree_list(aniso_handle h, int which, int64_t *ptr, int *idx);
  * directed M2L pairs of the 16-right-hand-side MFMA operators (0 before their plan);
  * then the upper-tier tasks that waiting blocks of the fused top-of-tree launch
  * computed themselves after ANISO_TOP_SPIN_LIMIT polls (section 3.10); then the
- * one-collective matvecs that exchanged the upper multipoles as partial sums.
+ * one-collective matvecs that exchanged the upper multipoles as partial sums; then 1
+ * if the block apply runs its near field on a side stream beside the up pass and the
+ * M2L (a shard, or ANISO_OVERLAP=1), 0 if serially (one GPU's default).
  * aniso_stats_n writes the first min(cap, *n) of them and sets *n to their count
- * (29 here); aniso_stats, the round-2 form, writes the first 19 only. */
+ * (30 here); aniso_stats, the round-2 form, writes the first 19 only. */
 int aniso_stats_n(aniso_handle h, int64_t *stats, int cap, int *n);
 int aniso_stats(aniso_handle h, int64_t *stats);
 /* per-stage device times (ms), averaged over every apply since aniso_set_timing(h, 1)
