@@ -762,7 +762,7 @@ class Aniso:
                 "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "top_fused",
                 "plan_halo_slots", "plan_max_lds_slots", "plan_block_reads", "top_recoveries",
                 "near_hs_stored", "near_hs_partials", "one_exchange_applies", "mrhs_m2l_pairs",
-                "top_steals", "upper_partial_applies", "near_overlap"]
+                "top_steals", "upper_partial_applies", "near_overlap", "near_up_tier"]
         return dict(zip(keys, (int(v) for v in s)))
 
     def sync(self):

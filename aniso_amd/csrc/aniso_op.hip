@@ -95,6 +95,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_NEAR_EARLY")) nearEarly = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_ONE_EXCHANGE")) oneXOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_SHARD_NEAR_EARLY")) shardNearEarly = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ANISO_NEAR_UP")) nearUpOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_ORDER")) nearOrderUp = std::strcmp(e, "first") != 0;
     hmRing = hm_ring_depth();
     if (const char* e = std::getenv("ANISO_HM_WPE")) hmWpe = std::atoi(e);
@@ -363,6 +364,7 @@ void Operator::uploadPlan() {
     up(dXT0Tasks, plan.xT0Tasks);
     up(dXOwnT0Tasks, plan.xOwnT0Tasks);
     up(dXUpTask, plan.xUpTask);
+    up(dNearUpGrp, plan.nearUpGrp);
     up(dNearGrpEarly, plan.nearGrpEarly);
     up(dNearGrpLate, plan.nearGrpLate);
     up(dXRootRecv, plan.xRootRecv);
@@ -856,6 +858,20 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         nin.sigT = sigT;
         nin.wT = dWT.as<double>();
     }
+    // the bottom up tier inside the staged near field (one GPU, serial: the near field
+    // runs first, so tier 1 -- in the fused launch or its own -- finds the tier-0 roots)
+    // (K <= 5: the 4-wave near kernel with the tail spills at K = 8)
+    const bool nearUp = phase == 0 && nearIn && !fork && nearUpTier() && ntier >= 1 && !hsSym && K <= 5;
+    if (nearUp) {
+        nin.upMult = dMult.as<double>();
+        nin.upGrp = dNearUpGrp.as<int>();
+        nin.upP = P;
+        nin.upNcx = dNcx.as<double>();
+        nin.upNcy = dNcy.as<double>();
+        nin.upNrx = dNrx.as<double>();
+        nin.upNry = dNry.as<double>();
+        nin.zeroCnt = topFused ? dTopCnt.as<unsigned>() : nullptr;
+    }
     if (hsSym) {
         nin.nearSym = dHsSym.as<int2>();
         nin.colDst = dHsDst.as<int>();
@@ -970,7 +986,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             if (oneX) upTier(0, dXOwnT0Tasks.as<int>(), (int)plan.xOwnT0Tasks.size(), nullptr, upPartial ? nullptr : rootsSend);
             else upTier(0, dXT0Tasks.as<int>(), (int)plan.xT0Tasks.size(), nullptr, rootsSend);
         }
-        for (int k = 0; k < (topFused ? 1 : ntier) && phase == 0; ++k) {
+        for (int k = nearUp ? 1 : 0; k < (topFused ? 1 : ntier) && phase == 0; ++k) {
             upTier(k, nullptr, tierTasks(k), nullptr, nullptr);
             if (k == 0 && nearAfterUp) {
                 nearStage();

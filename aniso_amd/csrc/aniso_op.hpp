@@ -171,6 +171,8 @@ public:
     int64_t oneXApplies = 0;    // sharded matvecs through the one-collective exchange (aniso_stats)
     int64_t upPartialApplies = 0;  // ... of them with the upper multipoles as partial sums (aniso_stats)
     bool nearOverlaps() const { return overlapOn(); }  // the block apply's near field on a side stream
+    // the one-GPU block apply forms its bottom up tier inside the near field
+    bool nearUpTier() const { return nearUpOn && plan.nearUpOk && !overlapOn(); }
     bool forceUnfused = false;
     // set while a call that recovers its own time-outs (the block solve) runs: the
     // entry checks of the applies it enqueues leave the flag to its recovery points
@@ -262,7 +264,9 @@ private:
     bool topTraceOn = false;
     int hmRing = 0;  // the cluster M2L's LDS ring depth (ANISO_HM_RING; 0: the one-block-in-flight form)
     int hmWpe = 0;   // ANISO_HM_WPE=3/4/8: the one-block form's occupancy (0: 4 where LDS allows)
-    int nearWpe = 3;  // ANISO_NEAR_WPE: the staged near field at 3 (132 VGPRs, the default since r03zj) or 4 waves per SIMD (<= 128)
+    // ANISO_NEAR_WPE: the staged near field capped at 128 VGPRs, 4 waves per SIMD (the default
+    // since round 5: 0.312 against 0.329 ms standalone, r05y), or 3 (121 VGPRs, the round-4 form)
+    int nearWpe = 4;
     int topFusedMode = 1;  // ANISO_TOP_FUSED=0: the upper up tiers as launches of their own
     // the near field's groups ride at the end of the fused top-of-tree + M2L launch
     // instead of a side-stream launch (ANISO_NEAR_IN_TOP=1; on a shard in phase 2)
@@ -274,6 +278,10 @@ private:
     // a one-collective sharded matvec starts the near field's own-range groups beside
     // phase 1 (ANISO_SHARD_NEAR_EARLY=0: every group after the exchange)
     bool shardNearEarly = true;
+    // the bottom up tier inside the staged near field on one GPU (Plan::nearUpOk, serial
+    // schedule; ANISO_NEAR_UP=0: its own launch)
+    bool nearUpOn = true;
+    DevBuf dNearUpGrp;
     int topTraceBlocks = 0, topTraceNear = 0;
     // the attached communicator and its halo exchange plan (commInit): per element of
     // the send / receive position lists its tree position and its place in the

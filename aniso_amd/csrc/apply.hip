@@ -774,11 +774,20 @@ __global__ void __launch_bounds__(kTierThreads) k_down_tier(
         // a node's local = its cluster's store + the halo partials other clusters left
         // for it (the halo form of the cluster M2L: packed (first << 3) | count, one
         // receiver-contiguous range), all loads of one round
+        // (every load of an entry issued before its sum: the partials' count is a
+        // runtime value, and a loop over it waited on each load in turn)
         auto total = [&](int n, int fold, int e) {
+            const int cnt = fold & 7;  // fold = 0 when there are no partials (hpart may be null)
             double v = local[(size_t)n * RK + e];
-            const int cnt = fold & 7;
-            const double* hp = hpart + (size_t)(fold >> 3) * RK + e;
-            for (int j = 0; j < cnt; ++j) v += hp[(size_t)j * RK];
+            if (cnt > 0) {
+                const double* hp = hpart + (size_t)(fold >> 3) * RK + e;
+                double p[7];
+#pragma unroll
+                for (int j = 0; j < 7; ++j) p[j] = hp[(size_t)min(j, cnt - 1) * RK];  // clamped: a valid slot
+#pragma unroll
+                for (int j = 0; j < 7; ++j)
+                    if (j < cnt) v += p[j];
+            }
             return v;
         };
         for (int it = threadIdx.x; it < nt * RK; it += blockDim.x) {

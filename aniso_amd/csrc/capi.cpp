@@ -577,7 +577,7 @@ int aniso_tree_list(aniso_handle h, int which, int64_t* ptr, int* idx) {
     });
 }
 
-constexpr int kStatsV1 = 19, kStats = 30;
+constexpr int kStatsV1 = 19, kStats = 31;
 
 static void stats_fill(aniso::Operator& op, int64_t* s) {
     s[0] = op.nearEntries();
@@ -616,6 +616,7 @@ static void stats_fill(aniso::Operator& op, int64_t* s) {
     s[27] = op.topSteals();     // upper-tier tasks computed by waiting blocks of the fused launch
     s[28] = op.upPartialApplies;  // one-collective matvecs with the upper multipoles as partial sums
     s[29] = op.nearOverlaps() ? 1 : 0;  // the block apply's near field on the side stream (else serial)
+    s[30] = op.nearUpTier() ? 1 : 0;  // the one-GPU block apply's bottom up tier inside the near field
 }
 
 // the round-2 entry: the first kStatsV1 entries only (callers sized for them)

@@ -893,7 +893,7 @@ __device__ __forceinline__ void m2l_cluster_form(int cid, const HcArgs& a, doubl
     else m2l_hcr_cluster<K, NR, D, XL>(cid, a, sm);
 }
 
-template <int K, int U, int NR, bool FUSE, bool SYM = false>
+template <int K, int U, int NR, bool FUSE, bool SYM = false, bool UP = false>
 __device__ __forceinline__ void near_hs_group(int g, const NearHsArgs& n, double* tab);
 
 // NEAR: the staged near field's groups (k_near_hs with fused corrections) are the last
@@ -1086,7 +1086,118 @@ __global__ void __launch_bounds__(256) k_near_hm(int nl, const int4* __restrict_
 template <int K>
 constexpr int kTabRow = (K + 2) | 1;
 
-template <int K, int U, int NR, bool FUSE, bool SYM>
+// The bottom up tier in the staged near field (NearHsArgs::upMult): group g's 16
+// leaves are one tier-0 subtree, leaf slots 4m .. 4m + 3 under parent m
+// (Plan::nearUpGrp).  Out of the group's table region once the epilogue is done with it:
+//  * each lane stores its point's Chebyshev weights and weighted charges (the
+//    epilogue's point t = 4 (ln & 3) + (ln >> 2) of leaf slot l; zero past the leaf);
+//  * P2M (bbfmm.h:737-748): lane ln of leaf l sums entry ln = (i, j) of the leaf's
+//    multipole over the leaf's 16 points, every right-hand side, in point order;
+//  * M2M (bbfmm.h:855-859) to the parents: one lane per (parent, row, child), the 4
+//    children's partial rows of a parent added by a DPP quad reduction (fixed order,
+//    as up_task's), then the root the same way from the parents.
+// Transfer matrices from global memory (8 KB, cache-resident).
+template <int K>
+__device__ __forceinline__ void near_up_tail(int g, bool active, int nT, int64_t tb, int leafNode,
+                                             const NearHsArgs& n, double (&f)[K], double* tab) {
+    constexpr int RK = kRank * K;
+    constexpr int PW = 2 * kNP + K;  // per point: Sx, Sy, f
+    const int ln = threadIdx.x & 15, l = (int)(threadIdx.x >> 4);
+    const int t = 4 * (ln & 3) + (ln >> 2);
+    const bool on = active && t < nT;
+    const int64_t kp = tb + (on ? t : 0);
+    const int* G = n.upGrp + (size_t)g * kNearUpInts;
+    const Params* __restrict__ P = n.upP;
+    double Sx[kNP], Sy[kNP];
+    {
+        const int nd = active ? leafNode : 0;
+        const double cx = n.upNcx[nd], cy = n.upNcy[nd], irx = 1.0 / n.upNrx[nd], iry = 1.0 / n.upNry[nd];
+        cheb_weights(P, (n.pxT[kp] - cx) * irx, Sx);
+        cheb_weights(P, (n.pyT[kp] - cy) * iry, Sy);
+    }
+    double* PT = tab;              // 256 points x PW; leaf l's rows reused for its multipole (16 x K <= 16 PW)
+    double* PM = tab + 256 * PW;   // the 4 parents, 16 x K each
+    __syncthreads();  // every lane is done with the source table (the epilogue's corrections read it)
+    {
+        double* q = PT + (size_t)threadIdx.x * PW;
+#pragma unroll
+        for (int i = 0; i < kNP; ++i) {
+            q[i] = Sx[i];
+            q[kNP + i] = Sy[i];
+        }
+#pragma unroll
+        for (int b = 0; b < K; ++b) q[2 * kNP + b] = on ? f[b] : 0.0;
+    }
+    __syncthreads();
+    {
+        const int i = ln & 3, j = ln >> 2;
+        const double* q = PT + (size_t)l * 16 * PW;
+        double acc[K];
+#pragma unroll
+        for (int b = 0; b < K; ++b) acc[b] = 0.0;
+#pragma unroll 2
+        for (int p = 0; p < 16; ++p) {
+            const double* r = q + p * PW;
+            const double w = r[i] * r[kNP + j];
+#pragma unroll
+            for (int b = 0; b < K; ++b) acc[b] = __builtin_fma(w, r[2 * kNP + b], acc[b]);
+        }
+        // the 16 lanes of leaf l read all of its rows before any writes (one wave, in order)
+        double* LM = PT + (size_t)l * 16 * PW;  // [16][K]
+#pragma unroll
+        for (int b = 0; b < K; ++b) LM[ln * K + b] = acc[b];
+        if (active)
+#pragma unroll
+            for (int b = 0; b < K; ++b) n.upMult[((size_t)leafNode * kRank + ln) * K + b] = acc[b];
+    }
+    __syncthreads();
+    {  // parent m, row r, child c (leaf slot 4 m + c, quadrant G[4 m + c] & 3)
+        const int m = threadIdx.x >> 6, r = (threadIdx.x >> 2) & 15, c = threadIdx.x & 3;
+        const int code = G[4 * m + c];
+        const double* R = &P->R[code & 3][r * kRank];
+        const double* x = PT + (size_t)(4 * m + c) * 16 * PW;
+        double acc[K];
+#pragma unroll
+        for (int b = 0; b < K; ++b) acc[b] = 0.0;
+#pragma unroll 2
+        for (int rr = 0; rr < kRank; ++rr) {  // 2 rows per step: the near loop's register budget
+            const double rv = R[rr];
+#pragma unroll
+            for (int b = 0; b < K; ++b) acc[b] = __builtin_fma(rv, x[rr * K + b], acc[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < K; ++b) acc[b] = quad_sum(acc[b]);
+        if (c == 0) {
+#pragma unroll
+            for (int b = 0; b < K; ++b) {
+                PM[(m * kRank + r) * K + b] = acc[b];
+                n.upMult[((size_t)G[20 + m] * kRank + r) * K + b] = acc[b];
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // the root: row r, parent m
+        const int r = threadIdx.x >> 2, m = threadIdx.x & 3;
+        const double* R = &P->R[G[16 + m]][r * kRank];
+        const double* x = PM + (size_t)m * RK;
+        double acc[K];
+#pragma unroll
+        for (int b = 0; b < K; ++b) acc[b] = 0.0;
+#pragma unroll 2
+        for (int rr = 0; rr < kRank; ++rr) {  // 2 rows per step: the near loop's register budget
+            const double rv = R[rr];
+#pragma unroll
+            for (int b = 0; b < K; ++b) acc[b] = __builtin_fma(rv, x[rr * K + b], acc[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < K; ++b) acc[b] = quad_sum(acc[b]);
+        if (m == 0)
+#pragma unroll
+            for (int b = 0; b < K; ++b) n.upMult[((size_t)G[24] * kRank + r) * K + b] = acc[b];
+    }
+}
+
+template <int K, int U, int NR, bool FUSE, bool SYM, bool UP>
 __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, double* tab) {
     constexpr int KS = kStride<K>;
     constexpr int RW = kTabRow<K>;  // table row: x, y, the charges (padded)
@@ -1289,6 +1400,9 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
             a[j][i] = v;
         }
     if (sym) __syncthreads();  // every partner product of the group is in LDS
+    double fq[K];  // the lane's point's weighted charges (the fused up tail's P2M)
+#pragma unroll
+    for (int i = 0; i < K; ++i) fq[i] = 0.0;
     if (rowOk) {  // lane (rq, cph) finishes row 4 rq + cph: one pass with every lane active
         const int t = 4 * rq + cph;
         double av[K];
@@ -1315,6 +1429,8 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
             const int64_t k = tb + t;
             double f[K];
             wcharges(k, f);
+#pragma unroll
+            for (int i = 0; i < K; ++i) fq[i] = f[i];
             const double sd = nearOn ? sigDiag[k] : 0.0;
             const int64_t oi = out_index(operm, obase, k);
             double cr[K];  // FUSE: k_corr's contribution (d = 1), its neighbour charges from the table
@@ -1341,23 +1457,28 @@ __device__ __forceinline__ void near_hs_group(const int g, const NearHsArgs& n, 
                     __builtin_fma(hw.om[i] * scale, __builtin_fma(hw.dw[i] * sd, f[i], av[i]), cr[i] * scale);
         }
     }
+    if constexpr (UP) near_up_tail<K>(g, active, nT, tb, info.x, n, fq, tab);
 }
 
 // the staged near field's LDS: the source table, and with symmetric U storage the
 // group's partner product slots (16 rows x K each)
 template <int K>
 static size_t near_hs_lds(const NearHsArgs& n) {
-    return (size_t)n.nsMax * kTabRow<K> * sizeof(double) + (n.colDst ? (size_t)n.grpSlots * 16 * K * sizeof(double) : 0);
+    const size_t tab = (size_t)n.nsMax * kTabRow<K> * sizeof(double) +
+                       (n.colDst ? (size_t)n.grpSlots * 16 * K * sizeof(double) : 0);
+    return std::max(tab, n.upMult ? near_up_lds_doubles(K) * sizeof(double) : (size_t)0);  // the up tail reuses the table
 }
 
 // W4: capped at 128 VGPRs (4 waves per SIMD; ANISO_NEAR_WPE=4)
 #ifndef ANISO_NEAR_SYM_WPE
 #define ANISO_NEAR_SYM_WPE 1
 #endif
-template <int K, int U, int NR, bool FUSE, bool W4 = false, bool SYM = false>
+template <int K, int U, int NR, bool FUSE, bool W4 = false, bool SYM = false, bool UP = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W4 ? 4 : SYM ? ANISO_NEAR_SYM_WPE : 1))) k_near_hs(NearHsArgs n) {
     extern __shared__ double tab[];
-    near_hs_group<K, U, NR, FUSE, SYM>(n.grpList ? n.grpList[blockIdx.x] : (int)blockIdx.x, n, tab);
+    // the fused top-of-tree launch's counters (the bottom tier launch that zeroes them is skipped)
+    if (n.zeroCnt && blockIdx.x == 0 && threadIdx.x <= kMaxTopTiers) n.zeroCnt[threadIdx.x] = 0u;
+    near_hs_group<K, U, NR, FUSE, SYM, UP>(n.grpList ? n.grpList[blockIdx.x] : (int)blockIdx.x, n, tab);
 }
 
 
@@ -1575,6 +1696,18 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
             n.sigT = in->sigT;
             n.wT = in->wT;
         }
+        if (in && in->upMult) {  // the bottom up tier in the near field (the caller checked near_up_fits)
+            if (!fuse || in->colDst)
+                throw std::invalid_argument("near field with the up tier: not the staged directed kernel with its table");
+            n.upMult = in->upMult;
+            n.upGrp = in->upGrp;
+            n.upP = in->upP;
+            n.upNcx = in->upNcx;
+            n.upNcy = in->upNcy;
+            n.upNrx = in->upNrx;
+            n.upNry = in->upNry;
+            n.zeroCnt = in->zeroCnt;
+        }
         if (in && in->grpList) {  // a subset of the groups
             n.grpList = in->grpList;
             n.ngrp = in->ngrp;
@@ -1595,7 +1728,9 @@ bool launch_near_hm(int K, int nl, int maxLeaf, const int4* leafInfo, const int6
         ANISO_HM_DISPATCH_K(K, ({
             const size_t shm = near_hs_lds<KK>(n);
             auto f = n.colDst ? (fuse ? k_near_hs<KK, 4, 2, true, false, true> : k_near_hs<KK, 4, 2, false, false, true>)
-                     : fuse ? (wpe == 4 ? k_near_hs<KK, 2, 2, true, true> : k_near_hs<KK, 2, 2, true>)
+                     // with the up tail: the 4-wave form (<= 128 VGPRs)
+                     : fuse ? (n.upMult ? k_near_hs<KK, 2, 2, true, true, false, true>
+                               : wpe == 4 ? k_near_hs<KK, 2, 2, true, true> : k_near_hs<KK, 2, 2, true>)
                             : (wpe == 4 ? k_near_hs<KK, 2, 2, false, true> : k_near_hs<KK, 2, 2, false>);
             f<<<ng, 256, shm, s>>>(n);
         }));

@@ -129,6 +129,12 @@ struct Plan {
     // partials): per leaf the slots it receives (CSR, ascending), summed in that
     // fixed order -- no atomics, so the apply stays deterministic
     static constexpr int kNearGrpSlots = 48;
+    // the bottom up tier inside the staged near field (one rank): every
+    // 16-leaf group is exactly one tier-0 subtree (a root, 4 parents, 16 leaves, all
+    // non-empty) -- then per group 25 ints (NearHsArgs::upGrp): per leaf (parent slot
+    // << 2 | quadrant), per parent its quadrant, the parents' nodes, the root node
+    std::vector<int> nearUpGrp;
+    bool nearUpOk = false;
     std::vector<int> nearGrpInPtr, nearGrpIn;
     int nearGrpSlots = 0;
     int64_t nearKTotal = 0;
@@ -280,6 +286,7 @@ struct Plan {
     void buildClusters(const Tree& t);
     void buildDownTasks(const Tree& t);
     void buildNearHs(const Tree& t, const std::vector<int>& leafIdx);
+    void buildNearUp(const Tree& t);
 };
 
 std::vector<int64_t> shard_cuts(const Tree& t, int nranks);

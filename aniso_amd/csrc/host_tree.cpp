@@ -471,6 +471,47 @@ void Plan::build(const Tree& t, int np, int rank_, int nranks_) {
     }
     buildNearHs(t, leafIdx);
     buildDownTasks(t);
+    buildNearUp(t);
+}
+
+void Plan::buildNearUp(const Tree& t) {
+    nearUpGrp.clear();
+    nearUpOk = false;
+    const size_t ng = nsPtr.size() - 1;
+    if (nranks != 1 || nsMax <= 0 || ng == 0 || leaves.size() != 16 * ng || upTierTask.size() < 2 ||
+        (size_t)(upTierTask[1] - upTierTask[0]) != ng)
+        return;
+    std::vector<int> taskOf(t.nn, -1);
+    for (int k = upTierTask[0]; k < upTierTask[1]; ++k) taskOf[upTaskRoot[k]] = k;
+    for (size_t g = 0; g < ng; ++g) {
+        const int* L = leaves.data() + 16 * g;
+        if (t.parent[L[0]] < 0 || t.parent[t.parent[L[0]]] < 0) return;
+        const int A = t.parent[t.parent[L[0]]];
+        const int k = taskOf[A];
+        if (k < 0 || upTaskPtr[k + 1] - upTaskPtr[k] != 21) return;  // a 3-level tier-0 task rooted at A
+        std::array<int, 25> G{};
+        int found = 0;
+        for (int c = 0; c < 16; ++c) {
+            const int p = t.parent[L[c]];
+            if (t.parent[p] != A || !t.isLeaf[L[c]] || t.isEmpty[L[c]]) return;
+            int m = -1, q = -1;
+            for (int i = 0; i < 4; ++i) {
+                if (t.child[A][i] == p) m = i;
+                if (t.child[p][i] == L[c]) q = i;
+            }
+            if (m < 0 || q < 0 || m != c / 4) return;  // wave m of the group holds parent m's leaves
+            G[c] = (m << 2) | q;
+            found |= 1 << (4 * m + q);
+        }
+        if (found != 0xFFFF) return;  // the 16 leaves are all of A's grandchildren
+        for (int m = 0; m < 4; ++m) {
+            G[16 + m] = m;
+            G[20 + m] = t.child[A][m];
+        }
+        G[24] = A;
+        nearUpGrp.insert(nearUpGrp.end(), G.begin(), G.end());
+    }
+    nearUpOk = true;
 }
 
 // The staged near field of the harmonic block apply with symmetric U storage (see

@@ -304,7 +304,27 @@ struct NearHsArgs {
     // the exchange and the rest after it (Plan::nearGrpEarly / nearGrpLate)
     const int* grpList = nullptr;
     int ngrp = 0;
+    // the bottom up tier in the staged near field (one GPU, serial schedule;
+    // Plan::nearUpGrp): every 16-leaf group is one tier-0 subtree (its
+    // 16 leaves, their 4 parents, the root).  Its lanes form the leaves' P2M from the
+    // charges the epilogue loads, the workgroup the subtree's M2M, into upMult (the
+    // multipoles of an up tier; the tier launch is skipped).  upGrp: per group
+    // kNearUpInts ints -- per leaf (parent slot << 2 | quadrant), per parent its
+    // quadrant, the 4 parent nodes, the root node.  zeroCnt: the fused top-of-tree
+    // launch's counters, zeroed here instead of by the skipped tier launch.
+    double* upMult = nullptr;
+    const int* upGrp = nullptr;
+    const Params* upP = nullptr;
+    const double* upNcx = nullptr;
+    const double* upNcy = nullptr;
+    const double* upNrx = nullptr;
+    const double* upNry = nullptr;
+    unsigned* zeroCnt = nullptr;
 };
+constexpr int kNearUpInts = 25;
+// LDS the fused up tail needs in the group's table region (doubles): 256 points x
+// (8 Chebyshev weights + K charges), then the 4 parents' 16 x K
+inline size_t near_up_lds_doubles(int K) { return (size_t)256 * (8 + K) + 4 * 16 * K; }
 bool top_fused_enabled();
 // near: the staged near field with its corrections fused (near_hs_fusable) as the
 // launch's last blocks, or nullptr (it runs as a launch of its own)

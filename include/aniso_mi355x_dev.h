@@ -75,9 +75,11 @@ int aniso_tree_list(aniso_handle h, int which, int64_t *ptr, int *idx);
  * computed themselves after ANISO_TOP_SPIN_LIMIT polls (section 3.10); then the
  * one-collective matvecs that exchanged the upper multipoles as partial sums; then 1
  * if the block apply runs its near field on a side stream beside the up pass and the
- * M2L (a shard, or ANISO_OVERLAP=1), 0 if serially (one GPU's default).
+ * M2L (a shard, or ANISO_OVERLAP=1), 0 if serially (one GPU's default); then 1 if
+ * the serial block apply forms its bottom up tier inside the staged near field
+ * (section 3.11; ANISO_NEAR_UP=0 keeps its own launch).
  * aniso_stats_n writes the first min(cap, *n) of them and sets *n to their count
- * (30 here); aniso_stats, the round-2 form, writes the first 19 only. */
+ * (31 here); aniso_stats, the round-2 form, writes the first 19 only. */
 int aniso_stats_n(aniso_handle h, int64_t *stats, int cap, int *n);
 int aniso_stats(aniso_handle h, int64_t *stats);
 /* per-stage device times (ms), averaged over every apply since aniso_set_timing(h, 1)
