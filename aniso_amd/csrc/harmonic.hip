@@ -62,6 +62,17 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
     }
 }
 
+// a wave-uniform double in SGPRs.  Loop-invariant table values (the Chebyshev nodes)
+// read through a generic pointer are re-loaded inside loops that also do atomics on
+// generic pointers (no hoisting across a possible alias); such a reload issued after a
+// prefetch makes the compiler's vmcnt wait drain the prefetch as well.
+__device__ __forceinline__ double uniform_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // XCD-aware workgroup order: the dispatcher deals workgroups round-robin over the
 // 8 XCDs (bid % 8), so consecutive logical tiles would land on 8 different L2s.
 // Renumber so each XCD runs one contiguous range of logical workgroups: targets
@@ -376,6 +387,11 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
     const int lane = threadIdx.x & (kWave - 1);
     const int s = lane >> 2, q = lane & 3;
     const double chx = P->cheb[s & 3], chy = P->cheb[s >> 2];
+    // the canonical loop's Chebyshev nodes, held in SGPRs: re-loaded per pair they cost
+    // a vmcnt(0) that drained every other pair's prefetch (1-2 % of the M2L, r05zk)
+    double chu[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) chu[j] = uniform_f64(P->cheb[j]);
     for (int ti = w; ti < nt;) {
         const int n = tgt[c0 + ti];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous target's xa reads are done
@@ -491,7 +507,7 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                     const double e4[4] = {a0.x, a0.y, a1.x, a1.y};
     #pragma unroll
                     for (int j = 0; j < 4; ++j)
-                        hm_entry2<K, NR>(e4[j], cheb_dx_lr(j, axs, trx, P), dy2, xw, xa + (4 * q + j) * K, c[j], ob);
+                        hm_entry2<K, NR>(e4[j], __builtin_fma(-trx, chu[j], axs), dy2, xw, xa + (4 * q + j) * K, c[j], ob);
     #pragma unroll
                     for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // rows 4q'+j over the quad
                     if (q == 0) {
