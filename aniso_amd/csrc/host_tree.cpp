@@ -876,11 +876,36 @@ void Plan::buildClusters(const Tree& t) {
     if (const char* e = std::getenv("ANISO_HM_UPPER_DEPTH"))  // experiments only (0..2)
         upperDepth = std::max(0, std::min(2, std::atoi(e)));
     std::vector<int64_t> key(nt);
-    for (int w = 0; w < nt; ++w) {
+    auto keyAt = [&](int w, int dp) {
         int a = m2lTgt[w];
-        const int dp = upper(w) ? std::min(depth, upperDepth) : depth;
         for (int k = 0; k < dp && t.parent[a] != -1; ++k) a = t.parent[a];
-        key[w] = ((int64_t)t.level[m2lTgt[w]] << 32) | (uint32_t)a;
+        return ((int64_t)t.level[m2lTgt[w]] << 32) | (uint32_t)a;
+    };
+    for (int w = 0; w < nt; ++w) key[w] = keyAt(w, upper(w) ? std::min(depth, upperDepth) : depth);
+    // the launch's tail: its last round of clusters drains over one cluster run time
+    // (one GPU: 768 slots, 5,462 near-equal clusters of ~106 us; r05zo trace).  The
+    // tailSplit lightest regular clusters are split into depth-1 (4-target) ones that
+    // run after the upper clusters, so the last units are ~4x shorter: min(400, 1/4 of
+    // the regular clusters) -- one GPU 1.155 -> 1.122 ms per block matvec (300-600 alike),
+    // a rank of 8 (812 clusters) 0.202 -> 0.200 / 0.210 -> 0.206 ms with 200 (r05zq, r05zr)
+    std::vector<char> split(nt, 0);
+    if (depth > 1) {
+        std::unordered_map<int64_t, int64_t> wk;
+        for (int w = 0; w < nt; ++w)
+            if (!upper(w)) wk[key[w]] += attPtr[w + 1] - attPtr[w];
+        int tailSplit = std::min(400, (int)wk.size() / 4);
+        if (const char* e = std::getenv("ANISO_HM_TAIL")) tailSplit = std::max(0, std::atoi(e));  // experiments
+        std::vector<std::pair<int64_t, int64_t>> ws(wk.begin(), wk.end());  // key, weight
+        std::sort(ws.begin(), ws.end(), [](const auto& a, const auto& b) {
+            return a.second != b.second ? a.second < b.second : a.first < b.first;
+        });
+        std::unordered_map<int64_t, char> lite;
+        for (size_t i = 0; i < ws.size() && (int)i < tailSplit; ++i) lite[ws[i].first] = 1;
+        for (int w = 0; w < nt; ++w)
+            if (!upper(w) && lite.count(key[w])) {
+                split[w] = 1;
+                key[w] = keyAt(w, 1);
+            }
     }
     std::vector<int> order(nt);
     for (int w = 0; w < nt; ++w) order[w] = w;
@@ -888,13 +913,13 @@ void Plan::buildClusters(const Tree& t) {
     {
         // launch order: heaviest cluster first (its att pairs), so the workgroups
         // dispatched last are short ones and the tail of the launch stays full; the
-        // upper-level clusters after all others
-        std::vector<std::array<int64_t, 4>> seg;  // upper, -weight, begin, end in `order`
+        // upper-level clusters after the others, the split tail clusters last
+        std::vector<std::array<int64_t, 4>> seg;  // class, -weight, begin, end in `order`
         for (int k = 0; k < nt;) {
             int e = k;
             int64_t wgt = 0;
             for (; e < nt && key[order[e]] == key[order[k]]; ++e) wgt += attPtr[order[e] + 1] - attPtr[order[e]];
-            seg.push_back({upper(order[k]) ? 1 : 0, -wgt, k, e});
+            seg.push_back({split[order[k]] ? 2 : upper(order[k]) ? 1 : 0, -wgt, k, e});
             k = e;
         }
         std::stable_sort(seg.begin(), seg.end(), [](const auto& a, const auto& b) {

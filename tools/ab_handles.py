@@ -97,4 +97,5 @@ for r in runs:
     rel = float(torch.linalg.norm(d - ref) / torch.linalg.norm(ref))  # same input: outputs agree to rounding
     print(json.dumps({"cfg": r["cfg"], "world": world, "rank": rank, "ms": r["ms"], "best_ms": min(r["ms"]),
                       "stage_ms": r["st"], "clusters": s["hm_clusters"],
-                      "block_reads": s["hm_block_reads"], "rel_vs_first": rel}), flush=True)
+                      "block_reads": s["hm_block_reads"], "dual_pairs": s["hm_dual_pairs"],
+                      "rel_vs_first": rel}), flush=True)
