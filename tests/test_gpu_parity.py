@@ -730,13 +730,16 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
                                   "ANISO_HM_HALO=0", "ANISO_NEAR_EARLY=0", "ANISO_NEAR_EARLY=0,ANISO_OVERLAP=1",
                                   "ANISO_NEAR_HS_SYM=1", "ANISO_NEAR_HS_SYM=1,ANISO_NEAR_EARLY=0",
                                   "ANISO_NEAR_HS_SYM=1,ANISO_OVERLAP=1", "ANISO_NEAR_HS_SYM=1,ANISO_TOP_FUSED=0",
-                                  "ANISO_NEAR_ORDER=first,ANISO_OVERLAP=1", "ANISO_NEAR_UP=0"])
+                                  "ANISO_NEAR_ORDER=first,ANISO_OVERLAP=1", "ANISO_NEAR_UP=0", "ANISO_HM_TAIL=0",
+                                  "ANISO_HM_TAIL=100000"])
 def test_block_matvec_knobs_agree(knob, monkeypatch):
     """Every remaining environment knob of the block apply:
     the near field on a side stream beside the up pass and the M2L (one GPU's
     default is serial since round 5), the bottom up tier as its own launch instead of
-    inside the near field (ANISO_NEAR_UP=0), the separate x - mforward(x) subtraction
-    and the per-mode operator stream give the default's block matvec to rounding."""
+    inside the near field (ANISO_NEAR_UP=0), the cluster M2L without its split tail
+    clusters or with every regular cluster split (ANISO_HM_TAIL), the separate
+    x - mforward(x) subtraction and the per-mode operator stream give the default's
+    block matvec to rounding."""
     torch = _torch()
     import aniso_amd
 
