@@ -93,6 +93,7 @@ def lib():
             "aniso_gmres": [P, dp, dp, I, I, D, dp, I, ip, dp],
             "aniso_block_solve": [P, dp, dp, I, D, I, dp, I, ip, dp],
             "aniso_block_solve_dev": [P, P, P, I, D, I, dp, I, ip, dp, P],
+            "aniso_solve16_mixed_dev": [P, P, I64, P, I64, I, D, D, I, I, ip, ip, dp, P],
             "aniso_apply_block_dev": [P, I, P, I64, I, I, ip, dp, P, I64, I, P],
             "aniso_block_op_dev": [P, I, P, I64, P, I64, I, P],
             "aniso_block_mixes": [I, D, I, dp],
@@ -526,6 +527,26 @@ class Aniso:
                                            len(hist), ctypes.byref(it), ctypes.byref(rr), ctypes.c_void_p(s)))
         return it.value, hist[: min(abs(it.value), len(hist))], rr.value
 
+    def solve16_mixed_dev(self, B, X, m=40, tol=1e-12, inner_tol=1e-6, max_outer=30, max_cycles=20, stream=None):
+        """Config 5's solve A X = B (aniso_solve16_mixed_dev): 16 right-hand sides, the
+        rows of B and X ((16, N) float64 CUDA tensors, original order, unit inner stride),
+        fp64 refinement over fp32 inner GMRES(m), every step in the library.  Returns
+        (outer refinements, inner steps, the 16 final relative residuals)."""
+        import torch
+
+        for t, name in ((B, "B"), (X, "X")):
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64 and t.dim() == 2
+                    and t.shape[0] == 16 and t.shape[1] == self.N and t.stride(1) == 1):
+                raise ValueError(f"{name}: (16, N) float64 CUDA tensor with unit inner stride")
+        s = torch.cuda.current_stream().cuda_stream if stream is None else stream
+        outer, inner = ctypes.c_int(), ctypes.c_int()
+        rel = np.zeros(16)
+        _check(lib().aniso_solve16_mixed_dev(self.address, ctypes.c_void_p(B.data_ptr()), int(B.stride(0)),
+                                             ctypes.c_void_p(X.data_ptr()), int(X.stride(0)), int(m), float(tol),
+                                             float(inner_tol), int(max_outer), int(max_cycles), ctypes.byref(outer),
+                                             ctypes.byref(inner), _dp(rel), ctypes.c_void_p(s)))
+        return outer.value, inner.value, rel
+
     # ---- the library's own multi-GPU exchange (aniso_comm_*; DESIGN.md §5)
     def comm_init_rccl(self, unique_id):
         """Attach an RCCL communicator (every rank together, after set_shard)."""
@@ -589,6 +610,14 @@ class Aniso:
         return ctypes.c_void_p(t.data_ptr())
 
     @staticmethod
+    def _arn_state(state, m):
+        """the state block must hold arnoldi_state(m)'s entries: the device kernels index
+        it by m's layout (H, T and R columns, g, y)"""
+        n = ctypes.c_int64()
+        _check(lib().aniso_arnoldi_state_size(int(m), ctypes.byref(n)))
+        return Aniso._arn_t(state, n.value, f"state (arnoldi_state({int(m)}))")
+
+    @staticmethod
     def _arn_s(stream):
         import torch
 
@@ -596,14 +625,14 @@ class Aniso:
 
     def arnoldi_begin(self, V, m, state, normb, rr=None, status=None, stream=None):
         pv, n, ld = self._arn_v(V, 1)
-        _check(lib().aniso_arnoldi_begin(self.address, n, int(m), pv, ld, self._arn_t(state, 1, "state"),
+        _check(lib().aniso_arnoldi_begin(self.address, n, int(m), pv, ld, self._arn_state(state, m),
                                          None if rr is None else self._arn_t(rr, 1, "rr"), float(normb),
                                          None if status is None else status.dev, self._arn_s(stream)))
 
     def arnoldi_step(self, V, m, j, w, state, status=None, stream=None):
         pv, n, ld = self._arn_v(V, j + 2)
         _check(lib().aniso_arnoldi_step(self.address, n, int(m), int(j), pv, ld, self._arn_t(w, n, "w"),
-                                        self._arn_t(state, 1, "state"), None if status is None else status.dev,
+                                        self._arn_state(state, m), None if status is None else status.dev,
                                         self._arn_s(stream)))
 
     def arnoldi_project(self, V, j, w, out, stream=None):
@@ -612,24 +641,24 @@ class Aniso:
                                            self._arn_t(out, j + 1, "out"), self._arn_s(stream)))
 
     def arnoldi_coef(self, m, j, state, red, stream=None):
-        _check(lib().aniso_arnoldi_coef(self.address, int(m), int(j), self._arn_t(state, 1, "state"),
+        _check(lib().aniso_arnoldi_coef(self.address, int(m), int(j), self._arn_state(state, m),
                                         self._arn_t(red, j + 1, "red"), self._arn_s(stream)))
 
     def arnoldi_update(self, V, m, j, w, state, out, stream=None):
         pv, n, ld = self._arn_v(V, j + 2)
         _check(lib().aniso_arnoldi_update(self.address, n, int(m), int(j), pv, ld, self._arn_t(w, n, "w"),
-                                          self._arn_t(state, 1, "state"), self._arn_t(out, j + 2, "out"),
+                                          self._arn_state(state, m), self._arn_t(out, j + 2, "out"),
                                           self._arn_s(stream)))
 
     def arnoldi_column(self, m, j, state, red, status=None, stream=None):
-        _check(lib().aniso_arnoldi_column(self.address, int(m), int(j), self._arn_t(state, 1, "state"),
+        _check(lib().aniso_arnoldi_column(self.address, int(m), int(j), self._arn_state(state, m),
                                           self._arn_t(red, j + 2, "red"), None if status is None else status.dev,
                                           self._arn_s(stream)))
 
     def arnoldi_solution(self, V, m, used, state, x, stream=None):
         pv, n, ld = self._arn_v(V, max(int(used), 1))
         _check(lib().aniso_arnoldi_solution(self.address, n, int(m), int(used), pv, ld,
-                                            self._arn_t(state, 1, "state"), self._arn_t(x, n, "x"),
+                                            self._arn_state(state, m), self._arn_t(x, n, "x"),
                                             self._arn_s(stream)))
 
     def comm_init_loopback(self):

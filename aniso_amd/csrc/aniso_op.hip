@@ -950,11 +950,13 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         launch_m2l_hc(K, c1 - c0, plan.hmMaxLds, a, st);
     };
     int e0 = -1;
+    int eStart = -1;  // the apply's first event: the total span covers every stage
     bool nearDone = false;
     if (phase != 2) {
         // up pass: tiers bottom-up; its P2M also forms the weighted charges fT (tree
         // order) the near field and the corrections read
         e0 = tm ? mark(s) : -1;
+        eStart = e0;
         if (nearIn && oneX && !plan.nearGrpEarly.empty() && shardNearEarly) {
             // one-collective form: the groups that read only the own range start now,
             // beside the own tier-0 tasks; the rest waits for the exchange (phase 2)
@@ -1004,11 +1006,13 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             pend.nearDone = nearDone;
             pend.K = K;
             pend.e0 = e0;
+            pend.eStart = eStart;
             pend.ePack = ep;
             return;
         }
     } else {
         e0 = pend.e0;
+        eStart = pend.eStart;
         nearDone = pend.nearDone;
         pend.active = false;
         const int ex = tm ? mark(s) : -1;
@@ -1112,7 +1116,7 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     if (tr) {
         const int e2 = tm ? mark(s) : -1;
         span(5, ep, e2);
-        span(7, e0, e2);
+        span(7, eStart, e2);
         ++applies;
     }
 }
@@ -1607,7 +1611,8 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
             peerLists[r].halo.assign(src.xHalo.begin(), src.xHalo.end());
             peerLists[r].oneHalo.assign(src.xOneHalo.begin(), src.xOneHalo.end());
             peerLists[r].needNodes.assign(src.xNeedNodes.begin(), src.xNeedNodes.end());
-            peerLists[r].ok = {(r == me ? oneExchangeLocal() : src.xOneOk) ? 1.0 : 0.0, src.xUpPartial ? 1.0 : 0.0};
+            peerLists[r].ok = {(r == me ? oneExchangeLocal() : src.xOneOk) ? 1.0 : 0.0, src.xUpPartial ? 1.0 : 0.0,
+                               cachesReady() ? 1.0 : 0.0};
             peerLists[r].upRec.assign(src.xUpRecNode.begin(), src.xUpRecNode.end());
         }
     }
@@ -1705,11 +1710,19 @@ void Operator::commInit(std::unique_ptr<Collectives> c) {
     // same on every rank (oneExchangeUsable adds only rank-independent checks)
     // (and whether its plan has the upper multipoles as partial sums: only if every
     // rank's has, since the parts then carry records instead of roots)
-    gatherList(&PeerLists::ok, {oneExchangeLocal() ? 1.0 : 0.0, plan.xUpPartial ? 1.0 : 0.0}, oksAll);
+    // (and whether it has cached every mode: a sharded matvec on a rank without its
+    // caches could only fail on that rank while its peers wait inside the exchange, so
+    // comm_init fails on EVERY rank instead, after this gather)
+    gatherList(&PeerLists::ok, {oneExchangeLocal() ? 1.0 : 0.0, plan.xUpPartial ? 1.0 : 0.0, cachesReady() ? 1.0 : 0.0},
+               oksAll);
     bool allOk = true, allUp = true;
-    for (const auto& o : oksAll) {
-        allOk = allOk && !o.empty() && o[0] > 0.5;
-        allUp = allUp && o.size() > 1 && o[1] > 0.5;
+    for (int r = 0; r < P; ++r) {
+        const auto& o = oksAll[r];
+        if (o.size() < 3 || o[2] < 0.5)
+            throw std::logic_error("comm_init: rank " + std::to_string(r) +
+                                   " has not cached every mode; every rank caches its modes before comm_init");
+        allOk = allOk && o[0] > 0.5;
+        allUp = allUp && o[1] > 0.5;
     }
     oxUp = false;
     if (allOk) {  // every rank decides alike: all take part in the same collectives
@@ -1865,6 +1878,14 @@ bool Operator::oneExchangeLocal() const {
     const NearCorr probe{dNearCorrRow.as<uint16_t>(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     return near_hs_fusable((int)plan.leaves.size(), plan.nearMaxLeaf, plan.nsMax, dNearLoc.as<uint16_t>(), &probe,
                            kStageAll);
+}
+
+// every mode cached (and the mode-shared caches built, where the handle uses them):
+// what a sharded block matvec needs on every rank
+bool Operator::cachesReady() const {
+    for (int m = 0; m < kernelSize; ++m)
+        if (!modes[m].ready) return false;
+    return !useAtt || attReady;
 }
 
 bool Operator::oneExchangeUsable(int which) {

@@ -122,6 +122,8 @@ public:
     // ks stacked blocks (original order, block b at b * N); device / host pointers
     int blockSolveDev(const double* rhs, double* x, int restart, double tol, int maxit, double* hist, int maxhist,
                       double* relres, hipStream_t s);
+    int solve16Mixed(const double* B, int64_t ldb, double* X, int64_t ldx, int m, double tol, double innerTol,
+                     int maxOuter, int maxCycles, int* outer, double* rel, hipStream_t s);
     int blockSolveHost(const double* rhs, double* x, int restart, double tol, int maxit, double* hist, int maxhist,
                        double* relres);
     // config 5's fp32 operator (f32op.hip): Y = X - K_0(sigma_s .* X)
@@ -231,7 +233,7 @@ private:
                     int phase = 0, double* rootsSend = nullptr, const double* rootsRecv = nullptr);
     struct Pending {  // state between the two phases of a sharded apply
         bool active = false, nearDone = false;
-        int K = 0, e0 = -1, ePack = -1;
+        int K = 0, e0 = -1, ePack = -1, eStart = -1;
     } pend;
     // the public call that started a pending sharded apply: its _end must repeat it
     // (operation, which, vectors, strides, sigma_s, g)
@@ -312,6 +314,7 @@ private:
     DevBuf dXUpTask, dXUpRec, dOxUpSumNode, dOxUpSumPtr, dOxUpSumSrc;
     int64_t oxUpSums = 0;
     bool oneExchangeUsable(int which);
+    bool cachesReady() const;
     bool oneExchangeLocal() const;  // this rank's (shard- and process-dependent) part, gathered at commInit
     // sticky time-out flag of the fused launch's in-kernel hand-offs, in host-visible
     // memory (the kernel stores 1 there when a wait gives up; checked at every API

@@ -204,11 +204,14 @@ __global__ void __launch_bounds__(kThreads) k_arn_update_wide(int64_t n, int nv,
     V[(size_t)nv * ldv + e] = p;
 }
 
-// ---- the small kernels (one block).  Row sums of partials part[k * P + b], b < P = kParts,
-// in a fixed order: lane l sums its kParts / 64 consecutive partials, the 64 lane sums
-// go through LDS, thread k adds them in lane order.  P = 1: the values themselves (a
-// caller's all-reduced sums).  scratch: kRedRows x 64 doubles of LDS; out: LDS.
-__device__ __forceinline__ void reduce_rows(const double* __restrict__ part, int P, int rows, double* out,
+// ---- the small kernels (one block per column: the one-vector solves launch one, the
+// 16-column solve of config 5 one per column, blockIdx.x = the column).  Row sums of
+// partials part[k * rs + b], b < P = kParts (rs = kParts for one column, 16 kParts for
+// 16 interleaved columns), in a fixed order: lane l sums its kParts / 64 consecutive
+// partials, the 64 lane sums go through LDS, thread k adds them in lane order.  P = 1:
+// the values themselves (a caller's all-reduced sums, one column).  scratch: kRedRows
+// x 64 doubles of LDS; out: LDS.
+__device__ __forceinline__ void reduce_rows(const double* __restrict__ part, int P, int64_t rs, int rows, double* out,
                                             double* scratch) {
     if (P == 1) {
         for (int k = threadIdx.x; k < rows; k += kThreads) out[k] = part[k];
@@ -226,7 +229,7 @@ __device__ __forceinline__ void reduce_rows(const double* __restrict__ part, int
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int r = wv + 4 * q;
-            const d2* pr = (const d2*)(part + (size_t)(k0 + (r < nr ? r : 0)) * kParts + (size_t)lane * kPer);
+            const d2* pr = (const d2*)(part + (size_t)(k0 + (r < nr ? r : 0)) * rs + (size_t)lane * kPer);
 #pragma unroll
             for (int b = 0; b < kPer / 2; ++b) v[q][b] = pr[b];
         }
@@ -309,14 +312,15 @@ struct FastRows {
     d2f v[16][kParts / 128];
 };
 
-__device__ __forceinline__ void fast_rows_load(const double* __restrict__ part, int P, int rows, FastRows& fr) {
+__device__ __forceinline__ void fast_rows_load(const double* __restrict__ part, int P, int64_t rs, int rows,
+                                               FastRows& fr) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (P == 1) return;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         const int r = wv + 4 * q;
         if (r < rows) {
-            const d2f* pr = (const d2f*)(part + (size_t)r * kParts + (size_t)lane * (kParts / 64));
+            const d2f* pr = (const d2f*)(part + (size_t)r * rs + (size_t)lane * (kParts / 64));
 #pragma unroll
             for (int b = 0; b < kParts / 128; ++b) fr.v[q][b] = pr[b];
         }
@@ -382,7 +386,7 @@ __device__ __forceinline__ void fast_cols_store(const FastCols& fc, int rows, in
 
 // k_arn_coef for j + 1 <= kFast.  LDS: scratch (kFast x 64) | u s tc c d (5 x 64) | T (n1 x j) | H (n1 x j)
 __device__ __forceinline__ void coef_fast(int m, int j, double* __restrict__ st, const double* __restrict__ part,
-                                          int P, double* sm) {
+                                          int P, int64_t rs, double* sm) {
     const int n1 = j + 1;
     double* scratch = sm;
     double *u = sm + kFast * 64, *s = u + kFast, *tc = s + kFast, *c = tc + kFast, *d = c + kFast;
@@ -392,7 +396,7 @@ __device__ __forceinline__ void coef_fast(int m, int j, double* __restrict__ st,
     double* Tg = st + L.T;
     FastRows fr;
     FastCols ft, fh;
-    fast_rows_load(part, P, n1, fr);
+    fast_rows_load(part, P, rs, n1, fr);
     fast_cols_load(Tg, L.M1, n1, j, ft);
     fast_cols_load(st + L.Hu, L.M1, n1, j, fh);
     const double sv = threadIdx.x < j ? st[L.s + threadIdx.x] : 0.0;
@@ -402,7 +406,7 @@ __device__ __forceinline__ void coef_fast(int m, int j, double* __restrict__ st,
     if (threadIdx.x < j) s[threadIdx.x] = sv;
     fast_rows_finish(part, P, n1, fr, scratch, u);
     __syncthreads();
-    const double ir = 1.0 / r;
+    const double ir = r > 0.0 ? 1.0 / r : 0.0;  // r = 0: a finished column, q_j = 0 (no NaN)
     band_matvec(Ts, n1, j, j, 0, s, tc);  // T s
     band_matvec(Hs, n1, n1, j, 1, s, c);  // H s
     __syncthreads();
@@ -436,7 +440,7 @@ inline __host__ __device__ size_t coef_fast_lds(int j) { return ((size_t)kFast *
 
 // k_arn_column for j + 2 <= kFast.  LDS: scratch (kFast x 64) | u' s' col cs sn h (6 x 64) | T (n1 x n1)
 __device__ __forceinline__ void column_fast(int m, int j, double* __restrict__ st, const double* __restrict__ part,
-                                            int P, double* __restrict__ status, double* sm) {
+                                            int P, int64_t rs, double* __restrict__ status, double* sm) {
     const int n1 = j + 1;
     double* scratch = sm;
     double *up = sm + kFast * 64, *sp = up + kFast, *col = sp + kFast, *csl = col + kFast, *snl = csl + kFast,
@@ -446,7 +450,7 @@ __device__ __forceinline__ void column_fast(int m, int j, double* __restrict__ s
     const Layout L(m);
     FastRows fr;
     FastCols ft;
-    fast_rows_load(part, P, j + 2, fr);
+    fast_rows_load(part, P, rs, j + 2, fr);
     fast_cols_load(st + L.T, L.M1, n1, n1, ft);
     const int t = threadIdx.x;
     const double cv = t < j ? st[L.cs + t] : 0.0, sv = t < j ? st[L.sn + t] : 0.0;
@@ -516,14 +520,29 @@ __device__ __forceinline__ void column_fast(int m, int j, double* __restrict__ s
 
 inline __host__ __device__ size_t column_fast_lds(int j) { return ((size_t)kFast * 70 + (size_t)(j + 1) * (j + 1)) * 8; }
 
+// Column c = blockIdx.x of a solve with several interleaved columns: its state block at
+// st + c * sts, its partials at part + c * pc (row stride rs), its status at status +
+// c * ss; one column: sts = pc = 0, rs = kParts.
+struct ColArgs {
+    int64_t sts, pc, rs;
+    int ss;
+};
+constexpr ColArgs kOneCol{0, 0, kParts, 0};
+
 // cycle start: V[0] holds the residual r; rr = |r|^2 (P partials, or P = 1: reduced);
-// status (may be null): {|r| / normb, |r|, 0}
+// normb: |b| (normbv: per column, else the scalar); status (may be null): {|r| / normb, |r|, 0}
 __global__ void __launch_bounds__(kThreads) k_arn_begin(int m, double* __restrict__ st, const double* __restrict__ rr,
-                                                        int P, double normb, double* __restrict__ status) {
+                                                        int P, double normb, double* __restrict__ status,
+                                                        ColArgs ca = kOneCol, const double* __restrict__ normbv = nullptr) {
     __shared__ double scratch[kRedRows * 64];
     __shared__ double a[1];
+    const int c = blockIdx.x;
+    st += c * ca.sts;
+    rr += P == 1 ? c : c * ca.pc;
+    if (status) status += c * ca.ss;
+    if (normbv) normb = normbv[c];
     const Layout L(m);
-    reduce_rows(rr, P, 1, a, scratch);
+    reduce_rows(rr, P, ca.rs, 1, a, scratch);
     const double r = sqrt(a[0] > 0.0 ? a[0] : 0.0);
     for (int k = threadIdx.x; k < L.M1; k += kThreads) st[L.g + k] = k == 0 ? r : 0.0;
     if (threadIdx.x == 0) {
@@ -539,29 +558,20 @@ __global__ void __launch_bounds__(kThreads) k_arn_begin(int m, double* __restric
     }
 }
 
-// coefficients of step j from sweep A's sums u = P^T w (rows 0 .. j).  T (columns
-// 0 .. j - 1) and H are staged in LDS where they fit (kStageDoubles), else read from the
-// state block.
-template <bool STAGED>
+// coefficients of step j from sweep A's sums u = P^T w (rows 0 .. j), for j + 1 > kFast:
+// T (columns 0 .. j - 1) and H read from the state block (2 (j + 1) j doubles exceed the
+// LDS stage, kStageDoubles, for every such j)
 __device__ __forceinline__ void coef_body(int m, int j, double* __restrict__ st, double* sm) {
     const int n1 = j + 1;
     double *u = sm, *s = u + n1, *tc = s + n1, *z = tc + n1, *c = z + n1, *d = c + n1;
+    (void)z;
     const Layout L(m);
     double* Tg = st + L.T;
     const double* T = Tg;
     const double* H = st + L.Hu;
-    int64_t ldt = L.M1, ldh = L.M1;
-    if constexpr (STAGED) {
-        double* Ts = d + n1;
-        double* Hs = Ts + (size_t)n1 * j;
-        stage(Tg, L.M1, n1, j, Ts);
-        stage(st + L.Hu, L.M1, n1, j, Hs);
-        __syncthreads();
-        T = Ts;
-        H = Hs;
-        ldt = ldh = n1;
-    }
-    const double ir = 1.0 / st[L.sc + kR];
+    const int64_t ldt = L.M1, ldh = L.M1;
+    const double r = st[L.sc + kR];
+    const double ir = r > 0.0 ? 1.0 / r : 0.0;
     // column j of T: (e_j - T s) / r
     band_matvec(T, ldt, j, j, 0, s, tc);
     // c = H s
@@ -598,22 +608,21 @@ __device__ __forceinline__ void coef_body(int m, int j, double* __restrict__ st,
     if (threadIdx.x == 0) st[L.sc + kInvR] = ir;
 }
 
-inline __host__ __device__ bool coef_staged(int j) { return (int64_t)2 * (j + 1) * j + 6 * (j + 1) <= kStageDoubles; }
-
 __global__ void __launch_bounds__(kThreads) k_arn_coef(int m, int j, double* __restrict__ st,
-                                                       const double* __restrict__ part, int P) {
-    extern __shared__ double sm[];  // fast path: coef_fast's layout; else u, s, tcol, z, c, d: 6 (j + 1); staged T, H
+                                                       const double* __restrict__ part, int P, ColArgs ca = kOneCol) {
+    extern __shared__ double sm[];  // fast path: coef_fast's layout; else u, s, tcol, z, c, d: 6 (j + 1)
     __shared__ double scratch[kRedRows * 64];
+    st += blockIdx.x * ca.sts;
+    part += P == 1 ? 0 : blockIdx.x * ca.pc;
     if (j + 1 <= kFast) {
-        coef_fast(m, j, st, part, P, sm);
+        coef_fast(m, j, st, part, P, ca.rs, sm);
         return;
     }
     const Layout L(m);
-    reduce_rows(part, P, j + 1, sm, scratch);
+    reduce_rows(part, P, ca.rs, j + 1, sm, scratch);
     for (int k = threadIdx.x; k < j; k += kThreads) sm[j + 1 + k] = st[L.s + k];
     __syncthreads();
-    if (coef_staged(j)) coef_body<true>(m, j, st, sm);
-    else coef_body<false>(m, j, st, sm);
+    coef_body(m, j, st, sm);
 }
 
 inline __host__ __device__ bool column_staged(int j) {
@@ -625,12 +634,15 @@ inline __host__ __device__ bool column_staged(int j) {
 // null): {relres, r', steps}
 __global__ void __launch_bounds__(kThreads) k_arn_column(int m, int j, double* __restrict__ st,
                                                          const double* __restrict__ part, int P,
-                                                         double* __restrict__ status) {
+                                                         double* __restrict__ status, ColArgs ca = kOneCol) {
     extern __shared__ double sm[];  // fast path: column_fast's layout; else u'[0 .. j + 1] | s' | col[0 .. j + 1] | cs | sn
     __shared__ double scratch[kRedRows * 64];
     __shared__ double ssum;
+    st += blockIdx.x * ca.sts;
+    part += P == 1 ? 0 : blockIdx.x * ca.pc;
+    if (status) status += blockIdx.x * ca.ss;
     if (j + 2 <= kFast) {
-        column_fast(m, j, st, part, P, status, sm);
+        column_fast(m, j, st, part, P, ca.rs, status, sm);
         return;
     }
     double* up = sm;
@@ -639,7 +651,7 @@ __global__ void __launch_bounds__(kThreads) k_arn_column(int m, int j, double* _
     double* csl = col + (j + 2);
     double* snl = csl + j;
     const Layout L(m);
-    reduce_rows(part, P, j + 2, up, scratch);
+    reduce_rows(part, P, ca.rs, j + 2, up, scratch);
     for (int k = threadIdx.x; k < j; k += kThreads) {
         csl[k] = st[L.cs + k];
         snl[k] = st[L.sn + k];
@@ -709,8 +721,9 @@ inline __host__ __device__ bool solve_staged(int used) { return (int64_t)used * 
 
 // the cycle's update coefficients on the stored vectors: R yh = g over the used columns
 // (back substitution column by column), then y = T yh
-__global__ void __launch_bounds__(kThreads) k_arn_solve(int m, int used, double* __restrict__ st) {
+__global__ void __launch_bounds__(kThreads) k_arn_solve(int m, int used, double* __restrict__ st, int64_t sts = 0) {
     extern __shared__ double t[];  // t[0 .. used), yh[0 .. used), staged R
+    st += blockIdx.x * sts;
     double* yh = t + used;
     double* Rs = yh + used;
     const Layout L(m);
@@ -751,7 +764,7 @@ __global__ void __launch_bounds__(kThreads) k_arn_rows(const double* __restrict_
                                                        double* __restrict__ out) {
     __shared__ double scratch[kRedRows * 64];
     extern __shared__ double o[];
-    reduce_rows(part, P, rows, o, scratch);
+    reduce_rows(part, P, kParts, rows, o, scratch);
     for (int k = threadIdx.x; k < rows; k += kThreads) out[k] = o[k];
 }
 
@@ -795,19 +808,9 @@ inline void launch_update(int64_t n, int nv, double* V, int64_t ldv, const doubl
     launch_project<TB, PP>(n, nv + 1, V, ldv, V + (size_t)nv * ldv, part, s);
 }
 
-// the small kernels' fast paths stage up to ~110 KB of LDS: raise their dynamic limit
-// once per process (gfx950: 160 KB per CU, one such block per CU)
-inline void small_kernel_attrs() {
-    static bool done = false;
-    if (done) return;
-    (void)hipFuncSetAttribute((const void*)k_arn_coef, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_arn_column, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
-    done = true;
-}
-
 inline size_t coef_lds(int j) {
     if (j + 1 <= kFast) return coef_fast_lds(j);
-    return ((size_t)6 * (j + 1) + (coef_staged(j) ? (size_t)2 * (j + 1) * j : 0)) * sizeof(double);
+    return (size_t)6 * (j + 1) * sizeof(double);
 }
 inline size_t column_lds(int j) {
     if (j + 2 <= kFast) return column_fast_lds(j);

@@ -396,6 +396,23 @@ int aniso_block_solve_dev(aniso_handle h, const double* rhs, double* x, int rest
     });
 }
 
+int aniso_solve16_mixed_dev(aniso_handle h, const double* b, int64_t ldb, double* x, int64_t ldx, int m, double tol,
+                            double inner_tol, int max_outer, int max_cycles, int* outer, int* inner, double* relres,
+                            void* stream) {
+    ENTER(h);
+    return guarded([&] {
+        CHECK_PTR(b);
+        CHECK_PTR(x);
+        double rel[16];
+        int o = 0;
+        const int it = get(h).solve16Mixed(b, ldb, x, ldx, m, tol, inner_tol, max_outer, max_cycles, &o, rel,
+                                           (hipStream_t)stream);
+        if (outer) *outer = o;
+        if (inner) *inner = it;
+        if (relres) std::copy(rel, rel + 16, relres);
+    });
+}
+
 int aniso_set_shard(aniso_handle h, int rank, int nranks) {
     ENTER(h);
     return guarded([&] { get(h).setShard(rank, nranks); });
@@ -577,7 +594,7 @@ int aniso_tree_list(aniso_handle h, int which, int64_t* ptr, int* idx) {
     });
 }
 
-constexpr int kStatsV1 = 19, kStats = 31;
+constexpr int kStatsV1 = 26, kStats = 31;  // aniso_stats: the 26 entries its round-4 contract promised
 
 static void stats_fill(aniso::Operator& op, int64_t* s) {
     s[0] = op.nearEntries();
@@ -619,7 +636,8 @@ static void stats_fill(aniso::Operator& op, int64_t* s) {
     s[30] = op.nearUpTier() ? 1 : 0;  // the one-GPU block apply's bottom up tier inside the near field
 }
 
-// the round-2 entry: the first kStatsV1 entries only (callers sized for them)
+// the fixed-size entry: the first kStatsV1 = 26 entries, as aniso_mi355x_dev.h has
+// promised since round 4 (entries 26.. only through aniso_stats_n)
 int aniso_stats(aniso_handle h, int64_t* s) {
     ENTER(h);
     return guarded([&] {

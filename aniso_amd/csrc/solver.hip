@@ -4,6 +4,7 @@
 // BLAS-1 reductions use a fixed two-level tree so results are deterministic.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <stdexcept>
 #include <type_traits>
@@ -11,6 +12,8 @@
 
 #include "aniso_op.hpp"
 #include "arnoldi.hpp"
+#include "arnoldi16.hpp"
+#include "device_common.hpp"
 #include "kernels.hpp"
 
 namespace aniso {
@@ -474,9 +477,30 @@ static void check_arnoldi(int m, int j) {
     if (m < 1 || j < 0 || j >= m) throw std::invalid_argument("arnoldi: need 0 <= j < m");
 }
 
+// the small kernels' fast paths stage up to ~100 KB of LDS: their dynamic limit is
+// raised once per device (a function attribute binds to the device current at the
+// call), checked, before any launch of them on that device
+static void arn_small_kernel_attrs() {
+    static std::atomic<uint64_t> done{0};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load(std::memory_order_acquire) & bit) return;
+    for (const void* f : {(const void*)arn::k_arn_coef, (const void*)arn::k_arn_column}) {
+        e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
+        if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
+    }
+    done.fetch_or(bit, std::memory_order_acq_rel);
+}
+
+// dKryPart for sweeps of `rows` rows.  DevBuf::alloc frees and reallocates (a device
+// synchronisation) on every size change, so it grows geometrically; the Arnoldi entry
+// points that know the restart length size it for the whole cycle at once
 void Operator::arnoldiParts(int rows) {
-    arn::small_kernel_attrs();
-    dKryPart.alloc(std::max(dKryPart.bytes, (size_t)arn::kParts * (rows + 2) * sizeof(double)));
+    arn_small_kernel_attrs();
+    const size_t need = (size_t)arn::kParts * (rows + 2) * sizeof(double);
+    if (need > dKryPart.bytes) dKryPart.alloc(std::max(need, 2 * dKryPart.bytes));
 }
 
 void Operator::arnoldiBegin(int64_t n, int m, const double* V, int64_t ldv, double* st, const double* rr,
@@ -485,11 +509,13 @@ void Operator::arnoldiBegin(int64_t n, int m, const double* V, int64_t ldv, doub
     ensureDevice();
     if (rr) {
         arn::k_arn_begin<<<1, arn::kThreads, 0, s>>>(m, st, rr, 1, normb, status);
+        HIP_LAUNCH_CHECK();
         return;
     }
-    arnoldiParts(1);
+    arnoldiParts(m + 2);
     arn::launch_project(n, 1, V, ldv, V, dKryPart.as<double>(), s);
     arn::k_arn_begin<<<1, arn::kThreads, 0, s>>>(m, st, dKryPart.as<double>(), arn::kParts, normb, status);
+    HIP_LAUNCH_CHECK();
 }
 
 void Operator::arnoldiStep(int64_t n, int m, int j, double* V, int64_t ldv, const double* w, double* st,
@@ -497,12 +523,14 @@ void Operator::arnoldiStep(int64_t n, int m, int j, double* V, int64_t ldv, cons
     check_arnoldi(m, j);
     if (n < 0 || ldv < n) throw std::invalid_argument("arnoldi step: bad sizes");
     ensureDevice();
-    arnoldiParts(j + 2);
+    arnoldiParts(m + 2);
     double* part = dKryPart.as<double>();
     arn::launch_project(n, j + 1, V, ldv, w, part, s);
     arn::k_arn_coef<<<1, arn::kThreads, arn::coef_lds(j), s>>>(m, j, st, part, arn::kParts);
+    HIP_LAUNCH_CHECK();
     arn::launch_update(n, j + 1, V, ldv, w, st, m, part, s);
     arn::k_arn_column<<<1, arn::kThreads, arn::column_lds(j), s>>>(m, j, st, part, arn::kParts, status);
+    HIP_LAUNCH_CHECK();
 }
 
 void Operator::arnoldiProject(int64_t n, int j, const double* V, int64_t ldv, const double* w, double* out,
@@ -513,12 +541,15 @@ void Operator::arnoldiProject(int64_t n, int j, const double* V, int64_t ldv, co
     arn::launch_project(n, j + 1, V, ldv, w, dKryPart.as<double>(), s);
     arn::k_arn_rows<<<1, arn::kThreads, (size_t)(j + 1) * sizeof(double), s>>>(dKryPart.as<double>(), arn::kParts,
                                                                                  j + 1, out);
+    HIP_LAUNCH_CHECK();
 }
 
 void Operator::arnoldiCoef(int m, int j, double* st, const double* red, hipStream_t s) {
     check_arnoldi(m, j);
     ensureDevice();
+    arn_small_kernel_attrs();
     arn::k_arn_coef<<<1, arn::kThreads, arn::coef_lds(j), s>>>(m, j, st, red, 1);
+    HIP_LAUNCH_CHECK();
 }
 
 void Operator::arnoldiUpdate(int64_t n, int m, int j, double* V, int64_t ldv, const double* w, const double* st,
@@ -526,16 +557,19 @@ void Operator::arnoldiUpdate(int64_t n, int m, int j, double* V, int64_t ldv, co
     check_arnoldi(m, j);
     if (n < 0 || ldv < n) throw std::invalid_argument("arnoldi update: bad sizes");
     ensureDevice();
-    arnoldiParts(j + 2);
+    arnoldiParts(m + 2);
     arn::launch_update(n, j + 1, V, ldv, w, st, m, dKryPart.as<double>(), s);
     arn::k_arn_rows<<<1, arn::kThreads, (size_t)(j + 2) * sizeof(double), s>>>(dKryPart.as<double>(), arn::kParts,
                                                                                  j + 2, out);
+    HIP_LAUNCH_CHECK();
 }
 
 void Operator::arnoldiColumn(int m, int j, double* st, const double* red, double* status, hipStream_t s) {
     check_arnoldi(m, j);
     ensureDevice();
+    arn_small_kernel_attrs();
     arn::k_arn_column<<<1, arn::kThreads, arn::column_lds(j), s>>>(m, j, st, red, 1, status);
+    HIP_LAUNCH_CHECK();
 }
 
 void Operator::arnoldiSolution(int64_t n, int m, int used, const double* V, int64_t ldv, double* st, double* x,
@@ -544,9 +578,11 @@ void Operator::arnoldiSolution(int64_t n, int m, int used, const double* V, int6
     ensureDevice();
     if (used == 0) return;
     arn::k_arn_solve<<<1, arn::kThreads, arn::solve_lds(used), s>>>(m, used, st);
+    HIP_LAUNCH_CHECK();
     if (n > 0)
         arn::k_arn_axpy<<<nblk(n), arn::kThreads, (size_t)used * sizeof(double), s>>>(n, used, V, ldv,
                                                                                         st + arn::Layout(m).y, x);
+    HIP_LAUNCH_CHECK();
 }
 
 // aniso.m:159-173: u = gmres(A, rhs, restart, tol, maxit) with A(x) = x - mforward(x)
@@ -677,6 +713,8 @@ int Operator::blockSolveDev(const double* rhs, double* x, int restart, double to
                     break;
                 }
                 const double rel = hs.p[0], rnext = hs.p[1];
+                if (hs.p[2] != (double)(j + 1))  // the column kernel of this step did not run
+                    throw std::runtime_error("block solve: Arnoldi step " + std::to_string(j) + " left no status");
                 ++total;
                 used = j + 1;
                 relres = rel;
@@ -697,6 +735,172 @@ int Operator::blockSolveDev(const double* rhs, double* x, int restart, double to
     checkDeviceErrors();  // every apply was checked at its recovery point: a flag here is new
     if (relresOut) *relresOut = relres;
     return conv ? total : -std::max(total, 1);
+}
+
+// Config 5 (main.cpp:121-141 for 16 right-hand sides): A X = B with
+// A(u) = u - K_0(sigma_s .* u), fp64 iterative refinement over fp32 inner GMRES(m)
+// solves -- the algorithm of aniso_amd.solve.gmres_mixed, every step in the library:
+//   outer: R = B - A64 X (the fp64 16-RHS MFMA operator), rel_c = |R_c| / |B_c|; stop
+//          when every rel_c <= tol (or after maxOuter refinements); X += inner(R);
+//   inner: GMRES(m) per column on an fp32 basis (arnoldi16.hpp: the DCGS2 Arnoldi of
+//          the block solve, 16 columns in lockstep), the fp32 16-RHS MFMA operator,
+//          to |g_c| <= innerTol |R_c| for every column, at most maxCycles cycles.
+// B, X: 16 rows of N doubles (original order, strides ldb / ldx; X is written, the
+// initial guess is 0); device pointers, stream s.  Returns the inner steps; *outer the
+// refinements; rel: the 16 final relative residuals.
+int Operator::solve16Mixed(const double* B, int64_t ldb, double* X, int64_t ldx, int m, double tol, double innerTol,
+                           int maxOuter, int maxCycles, int* outerOut, double* rel, hipStream_t s) {
+    using namespace arn16;
+    if (plan.nranks != 1) throw std::logic_error("16-RHS solve on a sharded handle");
+    if (!coeffSet) throw std::runtime_error("16-RHS solve before setCoeff");
+    if (!modes[0].ready) throw std::runtime_error("16-RHS solve before cache(0)");
+    if (m < 1 || m >= kMaxRows) throw std::invalid_argument("16-RHS solve: restart must be in [1, 47]");
+    if (!(tol > 0.0) || !(innerTol > 0.0) || maxOuter < 0 || maxCycles < 1)
+        throw std::invalid_argument("16-RHS solve needs tol, inner_tol > 0, max_outer >= 0, max_cycles >= 1");
+    const int64_t N = geo.N, n16 = KC * N;
+    if (ldb < N || ldx < N) throw std::invalid_argument("16-RHS solve: leading dimension below N");
+    ensureDevice();
+    checkDeviceErrors();
+    const arn::Layout lay(m);
+    const int64_t sts = lay.total;
+    arn::ColArgs ca = kCols;
+    ca.sts = sts;
+    DevBuf bB, bX, bR, bW, bD, bDf, bW32, bV, bSt, bPart, bNb;
+    bB.alloc(n16 * sizeof(double));
+    bX.alloc(n16 * sizeof(double));
+    bR.alloc(n16 * sizeof(double));
+    bW.alloc(n16 * sizeof(double));
+    bD.alloc(n16 * sizeof(double));
+    bDf.alloc(n16 * sizeof(float));
+    bW32.alloc(n16 * sizeof(float));
+    bV.alloc((size_t)(m + 1) * n16 * sizeof(float));
+    bSt.alloc((size_t)KC * sts * sizeof(double));
+    bPart.alloc((size_t)kParts * KC * (m + 2) * sizeof(double));
+    bNb.alloc(KC * sizeof(double));
+    arn_small_kernel_attrs();
+    double *Bt = bB.as<double>(), *Xt = bX.as<double>(), *R = bR.as<double>(), *W = bW.as<double>();
+    double *D = bD.as<double>(), *st = bSt.as<double>(), *part = bPart.as<double>(), *r0d = bNb.as<double>();
+    float *Df = bDf.as<float>(), *W32 = bW32.as<float>(), *V = bV.as<float>();
+    const int* perm = dPerm.as<int>();
+    // status words in mapped host memory: per column {relres, r', steps, -}, then 16 sums
+    struct HostStat {
+        double* p = nullptr;
+        hipEvent_t ev = nullptr;
+        ~HostStat() {
+            if (p) (void)hipHostFree(p);
+            if (ev) (void)hipEventDestroy(ev);
+        }
+    } hs;
+    HIP_CHECK(hipHostMalloc((void**)&hs.p, 5 * KC * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_CHECK(hipEventCreateWithFlags(&hs.ev, hipEventDisableTiming));
+    double* stat = nullptr;
+    HIP_CHECK(hipHostGetDevicePointer((void**)&stat, hs.p, 0));
+    double* sums = stat + 4 * KC;
+    const double* hsums = hs.p + 4 * KC;
+    auto wait = [&] {
+        HIP_CHECK(hipEventRecord(hs.ev, s));
+        HIP_CHECK(hipEventSynchronize(hs.ev));
+    };
+    auto colsums = [&] {  // the one-row partials in `part` -> hsums[c]
+        k16_rows<<<KC, arn::kThreads, 0, s>>>(part, sums);
+        HIP_LAUNCH_CHECK();
+        wait();
+    };
+    const unsigned g16 = nblk(n16);
+    k16_gather<<<g16, 256, 0, s>>>(N, perm, B, ldb, Bt);
+    k16_sub_norm<double><<<kParts, kT, 0, s>>>(n16, Bt, nullptr, R, nullptr, part);  // R = B (X = 0)
+    HIP_LAUNCH_CHECK();
+    HIP_CHECK(hipMemsetAsync(Xt, 0, n16 * sizeof(double), s));
+    colsums();
+    double bn[KC], rn[KC], r0[KC];
+    for (int c = 0; c < KC; ++c) bn[c] = std::sqrt(hsums[c]);
+    int outer = 0, inner = 0;
+    for (;; ++outer) {
+        if (outer > 0) {
+            mrhs64Dev(0, true, Xt, W, s);  // W = X - K_0(sigma_s .* X), fp64
+            k16_sub_norm<double><<<kParts, kT, 0, s>>>(n16, Bt, W, R, nullptr, part);
+            HIP_LAUNCH_CHECK();
+            colsums();
+        }
+        bool all = true;
+        for (int c = 0; c < KC; ++c) {
+            rn[c] = std::sqrt(hsums[c]);
+            rel[c] = bn[c] > 0.0 ? rn[c] / bn[c] : 0.0;
+            all = all && rel[c] <= tol;
+        }
+        if (all || outer == maxOuter) break;
+        for (int c = 0; c < KC; ++c) r0[c] = rn[c] > 0.0 ? rn[c] : 1.0;
+        HIP_CHECK(hipMemcpyAsync(r0d, r0, KC * sizeof(double), hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemsetAsync(D, 0, n16 * sizeof(double), s));
+        int its = 0;
+        for (int cyc = 0; cyc < maxCycles; ++cyc) {
+            // the cycle's residual R - A32 D into V[0] (fp32) and its norm per column
+            if (its > 0) {
+                k16_round<<<g16, 256, 0, s>>>(n16, D, Df);
+                forwardF32Dev(Df, W32, s);
+                k16_sub_norm<float><<<kParts, kT, 0, s>>>(n16, R, W32, nullptr, V, part);
+            } else {
+                k16_sub_norm<double><<<kParts, kT, 0, s>>>(n16, R, nullptr, nullptr, V, part);
+            }
+            HIP_LAUNCH_CHECK();
+            arn::k_arn_begin<<<KC, arn::kThreads, 0, s>>>(m, st, part, kParts, 1.0, stat, ca, r0d);
+            HIP_LAUNCH_CHECK();
+            wait();
+            bool done = true;
+            for (int c = 0; c < KC; ++c) done = done && hs.p[4 * c] <= innerTol;
+            if (done) break;
+            int used = 0;
+            bool ahead = false;
+            std::vector<double> hrel;
+            for (int j = 0; j < m; ++j) {
+                float* vj = V + (size_t)j * n16;
+                if (!ahead) forwardF32Dev(vj, W32, s);
+                rows_dispatch(j + 1, [&](auto c) {
+                    k16_project<decltype(c)::value><<<kParts, kT, 0, s>>>(n16, j + 1, V, n16, W32, part);
+                });
+                HIP_LAUNCH_CHECK();
+                arn::k_arn_coef<<<KC, arn::kThreads, arn::coef_lds(j), s>>>(m, j, st, part, kParts, ca);
+                HIP_LAUNCH_CHECK();
+                rows_dispatch(j + 1, [&](auto c) {
+                    k16_update<decltype(c)::value><<<kParts, kT, 0, s>>>(n16, j + 1, V, n16, W32, st, sts, m, part);
+                });
+                HIP_LAUNCH_CHECK();
+                arn::k_arn_column<<<KC, arn::kThreads, arn::column_lds(j), s>>>(m, j, st, part, kParts, stat, ca);
+                HIP_LAUNCH_CHECK();
+                HIP_CHECK(hipEventRecord(hs.ev, s));
+                // the next step's matvec before the host reads the estimates (as blockSolveDev)
+                bool near = false;
+                if (hrel.size() >= 2) near = hrel.back() * std::min(1.0, hrel.back() / hrel[hrel.size() - 2]) <= 10.0 * innerTol;
+                else if (!hrel.empty()) near = hrel.back() <= 10.0 * innerTol;
+                ahead = j + 1 < m && !near;
+                if (ahead) forwardF32Dev(V + (size_t)(j + 1) * n16, W32, s);
+                HIP_CHECK(hipEventSynchronize(hs.ev));
+                double worst = 0.0;
+                for (int c = 0; c < KC; ++c) {
+                    if (hs.p[4 * c + 2] != (double)(j + 1))
+                        throw std::runtime_error("16-RHS solve: Arnoldi step " + std::to_string(j) + " left no status");
+                    worst = std::max(worst, hs.p[4 * c]);
+                }
+                ++its;
+                used = j + 1;
+                hrel.push_back(worst);
+                if (worst <= innerTol) break;
+            }
+            arn::k_arn_solve<<<KC, arn::kThreads, arn::solve_lds(used), s>>>(m, used, st, sts);
+            HIP_LAUNCH_CHECK();
+            k16_axpy<<<g16, 256, (size_t)used * KC * sizeof(double), s>>>(n16, used, V, n16, st, sts, m, D);
+            HIP_LAUNCH_CHECK();
+        }
+        k16_add<<<g16, 256, 0, s>>>(n16, D, Xt);
+        HIP_LAUNCH_CHECK();
+        inner += its;
+    }
+    k16_scatter<<<g16, 256, 0, s>>>(N, perm, Xt, X, ldx);
+    HIP_LAUNCH_CHECK();
+    HIP_CHECK(hipStreamSynchronize(s));
+    checkDeviceErrors();
+    if (outerOut) *outerOut = outer;
+    return inner;
 }
 
 // the same on host pointers (the MEX shim's 'solve' op): one staging copy each way

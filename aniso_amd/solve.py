@@ -182,9 +182,17 @@ def _inner_gmres(apply, R, m, tol, max_cycles, rd=1):
     return D, its
 
 
-def gmres_mixed(op, B, tol=1e-12, m=40, inner_tol=1e-6, max_outer=30, max_cycles=20, fp32_op=None, fp64_mfma=None):
+def gmres_mixed(op, B, tol=1e-12, m=40, inner_tol=1e-6, max_outer=30, max_cycles=20, fp32_op=None, fp64_mfma=None,
+                native=None):
     """Solve A X = B (rows) to ||B - A X|| / ||B|| <= tol per row.  Returns
     (X, outer iterations, inner iterations, final relative residuals).
+
+    native (default: 16 rows on a handle with the library solve, both MFMA operators):
+    the whole solve runs in the library (Aniso.solve16_mixed_dev,
+    aniso_solve16_mixed_dev: the same refinement and inner GMRES with the DCGS2
+    Arnoldi of the block solve on an fp32 basis, no torch op and no host round trip
+    inside a step).  native=False keeps the torch-orchestrated loop below (the
+    reference the library's solve is tested against).
 
     fp32_op (default: when B has 16 rows): the inner solves run on the fp32 MFMA
     operator (Aniso.forward_f32_dev, fp32 caches) in tree order, point-major; the
@@ -197,6 +205,13 @@ def gmres_mixed(op, B, tol=1e-12, m=40, inner_tol=1e-6, max_outer=30, max_cycles
         fp32_op = B.shape[0] == 16
     if fp64_mfma is None:
         fp64_mfma = B.shape[0] == 16 and hasattr(op, "forward16_f64_dev")
+    if native is None:
+        native = fp32_op and fp64_mfma and hasattr(op, "solve16_mixed_dev") and B.is_cuda
+    if native:
+        X = torch.zeros_like(B)
+        outer, inner, rel = op.solve16_mixed_dev(B.contiguous(), X, m=m, tol=tol, inner_tol=inner_tol,
+                                                 max_outer=max_outer, max_cycles=max_cycles)
+        return X, outer, inner, rel
     X = torch.zeros_like(B)
     W = torch.empty_like(B)
     bn = torch.linalg.norm(B, dim=1)

@@ -16,11 +16,16 @@ path).  fp64 throughout.  --workload mode0 instead times main.cpp's matvec
 u - K_0(sigma_s .* u) (main.cpp:125-136) with main.cpp's coefficients; the block
 run also reports that number as `mode0_matvec_per_s`.
 
-N GPUs (torchrun, one process per GPU, RCCL): the targets are sharded by FMM
-subtree (strong scaling: total work fixed).  Each rank runs the up pass over its
-own and halo subtrees, exchanges the tier-0 root multipoles with one all-gather
-mid-apply, computes its targets into its slice of the next iterate, and one halo
-all-to-all refreshes the points its neighbours read (aniso_amd/dist.py).
+N GPUs (one process per GPU, RCCL over xGMI; `bench.py --gpus N` run bare starts its
+N ranks itself under torch.distributed.run, and under a launcher WORLD_SIZE must equal
+--gpus): the targets are sharded by FMM subtree (strong scaling: total work fixed).
+Each rank forms the multipoles of its own tier-0 subtrees and its partial sums of the
+upper tiers, then ONE grouped all-to-all-v per matvec (the library's own exchange,
+aniso_block_op_sharded_dev over RCCL) brings it the upper multipoles,
+the multipoles below the root level and the input points it reads from each owner;
+it then computes its targets into its slice of the next iterate.  Config 4 (one
+right-hand side) keeps the two-collective form: a halo all-to-all and the tier-0
+root all-gather.
 
 Also reported on the same JSON line:
   roofline      HBM roofline of the dominant kernel (the clustered M2L with the upper up
@@ -290,10 +295,20 @@ def config5_leg(args):
         a.set_timing(0)
         tf = flops / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
         busy, bsrc = mfma_busy(kern)
-        mfma[kern] = {"bound": "mfma" if dt == torch.float64 else "hbm", "achieved": round(tf, 2), "peak": peak,
+        # the bound from the counters: the kernel's PMC HBM bytes per launch over its
+        # time against HBM peak, beside its flops against the MFMA peak -- the larger
+        # fraction of peak is what bounds it
+        traffic, tsrc, _ = pmc_traffic(f"aniso::{kern}")
+        hbm_gbs = traffic / (ms * 1e-3) / 1e9 if traffic and ms > 0 else None
+        hbm_frac = hbm_gbs / HBM_PEAK_GBS if hbm_gbs else None
+        bound = ("hbm" if hbm_frac is not None and hbm_frac > tf / peak else "mfma") if hbm_frac is not None else None
+        mfma[kern] = {"bound": bound, "achieved": round(tf, 2), "peak": peak,
                       "unit": "TFLOP/s", "frac": round(tf / peak, 4), "kernel_ms": round(ms, 5),
                       "algorithmic_flops": int(flops), "directed_pairs": int(pairs),
-                      "mfma_busy_pct": busy, "mfma_busy_source": bsrc}
+                      "mfma_busy_pct": busy, "mfma_busy_source": bsrc,
+                      "traffic": traffic, "traffic_source": tsrc,
+                      "hbm_GBps_from_traffic": round(hbm_gbs, 1) if hbm_gbs else None,
+                      "hbm_frac_from_traffic": round(hbm_frac, 4) if hbm_frac else None}
     leg = {"workload": "configs[4]: configs[2] geometry (N=1048576, d=1, ns=10), mode 0, 16 RHS, fp32 mixed precision: "
                        "fp32 Krylov basis + fp32 16-RHS MFMA inner operator, fp64 refinement on the fp64 MFMA operator",
            "seconds": round(t_mixed, 4), "outer_refinements": outer, "inner_iterations": inner,
@@ -314,6 +329,23 @@ def cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def cgroup_cpu_quota():
+    """The job's CPU quota from its cgroup (v2 cpu.max "quota period", or v1
+    cfs_quota_us / cfs_period_us): (cpus, raw text), or (None, reason)."""
+    try:
+        raw = open("/sys/fs/cgroup/cpu.max").read().strip()
+        q, p = raw.split()[:2]
+        return (None if q == "max" else round(int(q) / int(p), 2)), f"cpu.max={raw}"
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return (None if q < 0 else round(q / p, 2)), f"cfs_quota_us={q} cfs_period_us={p}"
+    except (OSError, ValueError):
+        return None, "no cgroup cpu quota readable"
 
 
 def cpu_baseline(args, coeffs, op, block_check):
@@ -373,6 +405,7 @@ def cpu_baseline(args, coeffs, op, block_check):
     t_port = float(np.mean(list(port_mode.values())))
     per_matvec = ks * (2 * ks - 1) if block else 1  # aniso.m's loop: ks x (2ks-1) mapping calls per mforward
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    quota, quota_raw = cgroup_cpu_quota()
     try:
         visible = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
@@ -392,8 +425,10 @@ def cpu_baseline(args, coeffs, op, block_check):
                    f"not timed; OMP threads={cores}"),
         # OpenMP threads: OMP_NUM_THREADS as the GPU box sets it for one GPU's job (16: the
         # box's CPU share per GPU; the reference's own runs used one thread per core)
-        "thread_policy": (f"OMP_NUM_THREADS={cores} (the job's CPU share on the GPU box); "
-                          f"{visible} CPUs visible to the process, os.cpu_count()={os.cpu_count()}"),
+        "thread_policy": (f"OMP_NUM_THREADS={cores} (the job's CPU share on the GPU box, set by the box and left "
+                          f"as set: one GPU's job may use 16 CPUs); {visible} CPUs visible to the process, "
+                          f"os.cpu_count()={os.cpu_count()}; cgroup quota: {quota_raw}"),
+        "cgroup_cpu_quota": quota,
         "mode_apply_s": {str(m): round(t, 4) for m, t in per_mode.items()},
         "mode_apply_spread_s": {f"{m}{'' if a else '_port'}": [round(lo, 4), round(hi, 4)]
                                 for (m, a), (lo, hi) in spread.items()},
@@ -407,6 +442,27 @@ def cpu_baseline(args, coeffs, op, block_check):
         "value_linear_to_socket": 1.0 / (per_matvec * t_apply) * SOCKET_CORES / max(cores, 1),
         "port_mode_apply_s": {str(m): round(t, 4) for m, t in port_mode.items()},
     }, errs
+
+
+def free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` run bare: N ranks of this same command under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1); rank 0 prints
+    the JSON line.  Returns the launcher's exit code."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (the box's driver)
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -444,6 +500,17 @@ def main():
                     help="secondary leg (one GPU): BASELINE configs[4], 16-RHS fp32 mixed-precision solve; 0 skips")
     args = ap.parse_args()
 
+    # --gpus N > 1 without a launcher: start N ranks under torch.distributed.run as a
+    # child process and exit with its code (before torch or HIP is touched here, so
+    # nothing in this process has initialised the GPU); under a launcher the world
+    # size must agree with --gpus
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if world_env is not None and int(world_env) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+        sys.exit(2)
+
     import torch
     import torch.distributed as dist
 
@@ -465,7 +532,14 @@ def main():
     ks = args.ks if block else 1
     nb = ks if block else 1
     coeffs = demo_coeffs if block else main_coeffs
+    # setup, timed per step: create (geometry, quadtree, interaction
+    # lists, the cluster plan), the shard's plan, setCoeff (device upload of the
+    # plan and coefficients), cache (every mode's operators and the mode-shared E
+    # caches, built on the device), the communicator
+    setup = {}
+    t0 = time.perf_counter()
     op = aniso_amd.Aniso(args.sz, args.d, ks, args.g, args.ns, 4, args.max_level)
+    setup["create"] = time.perf_counter() - t0
     N = op.N
     xy = op.getNodes()
     ss, st = coeffs(xy)
@@ -474,19 +548,31 @@ def main():
     if world > 1:
         # sharded apply: own subtrees + halo up pass, one all-gather
         # of the tier-0 root multipoles mid-apply, one halo all-to-all per iterate
+        t0 = time.perf_counter()
         op.set_shard(rank, world)
+        setup["set_shard"] = time.perf_counter() - t0
         xchg = adist.ShardExchange(op, rank, world, nb, "cuda", args.backend)
         xchg0 = adist.ShardExchange(op, rank, world, 1, "cuda", args.backend) if block else xchg
         ob, oe = xchg.own
+    t0 = time.perf_counter()
     op.setCoeff(ss, st)
+    torch.cuda.synchronize()
+    setup["set_coeff"] = time.perf_counter() - t0
     native = world > 1 and block and args.comm == "native"
-    coll = adist.native_comm_init(op, world, args.backend) if native else None  # noqa: F841 (kept alive)
     modes = list(range(2 * ks - 1))
     t0 = time.time()
     for m in modes:
         op.cache(m)
     torch.cuda.synchronize()
     t_cache = time.time() - t0
+    setup["cache"] = t_cache
+    # the library's communicator after the caches: comm_init all-gathers every rank's
+    # readiness and fails on every rank if one has not cached
+    t0 = time.perf_counter()
+    coll = adist.native_comm_init(op, world, args.backend) if native else None  # noqa: F841 (kept alive)
+    if native:
+        setup["comm_init"] = time.perf_counter() - t0
+    setup["total"] = sum(setup.values())
     # GMRES vectors live in tree order (a fixed relabelling of the unknowns): the
     # operator then needs no permutation gathers, and the shards' output slices
     # concatenate to the next iterate.  Block 0 holds the Gaussian (demo.m:27-29).
@@ -668,6 +754,7 @@ def main():
                                  if harmonic and world == 1 else None),
         "stage_ms": {k: round(v_, 5) for k, v_ in times.items()},
         "cache_build_s": round(t_cache, 3),
+        "setup_s": {k: round(v_, 3) for k, v_ in setup.items()},
         "roofline": roofline,
     }
     one_x = world > 1 and native and op.stats()["one_exchange_applies"] > 0
@@ -732,15 +819,29 @@ def main():
         # matvec u - K_0(sigma_s .* u), the configuration BASELINE names for 8 GPUs --
         # sharded over this run's ranks like the headline (the library's one-call exchange at
         # N > 1); its per-N rates give the strong scaling of the multi-GPU config
+        setup4 = {}
+        t0 = time.perf_counter()
         op4 = aniso_amd.Aniso(args.config4_sz, args.d, 1, args.g, args.ns, 4, args.max_level)
+        setup4["create"] = time.perf_counter() - t0
         xy4 = op4.getNodes()
         perm4 = torch.tensor(op4.tree_perm(), device="cuda", dtype=torch.int64)
         if world > 1:
+            t0 = time.perf_counter()
             op4.set_shard(rank, world)
+            setup4["set_shard"] = time.perf_counter() - t0
+        t0 = time.perf_counter()
         op4.setCoeff(*main_coeffs(xy4))
+        torch.cuda.synchronize()
+        setup4["set_coeff"] = time.perf_counter() - t0
+        t0 = time.perf_counter()
         op4.cache(0)
+        torch.cuda.synchronize()
+        setup4["cache"] = time.perf_counter() - t0
         if world > 1:
+            t0 = time.perf_counter()
             coll4 = adist.native_comm_init(op4, world, args.backend)  # noqa: F841 (kept alive)
+            setup4["comm_init"] = time.perf_counter() - t0
+        setup4["total"] = sum(setup4.values())
         x4 = torch.zeros(1, op4.N, dtype=torch.float64, device="cuda")
         x4[0] = torch.tensor(gaussian(xy4), device="cuda")[perm4]
         y4 = torch.zeros_like(x4)
@@ -777,6 +878,7 @@ def main():
                            "ms_per_step": round(1e3 * el4 / args.steps, 4), "steps": args.steps,
                            "scaling": "strong", "n_gpus": world,
                            "stage_ms": {k: round(v_, 5) for k, v_ in times4.items()},
+                           "setup_s": {k: round(v_, 3) for k, v_ in setup4.items()},
                            # this rank's M2L and near-field streams (its shard's stored blocks)
                            "roofline": fwd_roofline(op4.stats(), times4)}
         del op4

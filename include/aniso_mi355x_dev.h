@@ -79,7 +79,8 @@ int aniso_tree_list(aniso_handle h, int which, int64_t *ptr, int *idx);
  * the serial block apply forms its bottom up tier inside the staged near field
  * (section 3.11; ANISO_NEAR_UP=0 keeps its own launch).
  * aniso_stats_n writes the first min(cap, *n) of them and sets *n to their count
- * (31 here); aniso_stats, the round-2 form, writes the first 19 only. */
+ * (31 here); aniso_stats, the fixed-size form, writes the first 26 (stats must hold
+ * 26 entries). */
 int aniso_stats_n(aniso_handle h, int64_t *stats, int cap, int *n);
 int aniso_stats(aniso_handle h, int64_t *stats);
 /* per-stage device times (ms), averaged over every apply since aniso_set_timing(h, 1)

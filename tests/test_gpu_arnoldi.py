@@ -77,17 +77,20 @@ def _mgs_gmres(A, b, m, tol):
     return hist
 
 
-@pytest.mark.parametrize("m", [10, 60])
+@pytest.mark.parametrize("m", [10, 60, 110])
 def test_arnoldi_basis_is_orthonormal_and_satisfies_the_arnoldi_relation(m):
-    """m steps of the primitives (m = 60 runs the > 48-row sweeps): Q = P T orthonormal
-    and A Q_m = Q_{m+1} H to <= 1e-12, residual estimates as torch MGS GMRES."""
+    """m steps of the primitives (m = 60 runs the > 48-row sweeps; m = 110 the small
+    kernels past their one-round fast paths: k_arn_coef from j = 64, k_arn_column with
+    T staged in LDS up to j = 81 and read from the state block past it, and the
+    unstaged k_arn_solve): Q = P T orthonormal and A Q_m = Q_{m+1} H to <= 1e-12,
+    residual estimates as torch MGS GMRES, arnoldi_solution = Q_m argmin |beta e_1 - H y|."""
     torch = _torch()
     import aniso_amd
     from aniso_amd import MappedStatus
 
     a = aniso_amd.Aniso(8, 1, 2, 0.8, 10, 4, 20)  # any handle: the primitives use only its device
     n = 100_003
-    A = LowRankOp(n, 70, 1)
+    A = LowRankOp(n, 70 if m <= 64 else 160, 1)  # rank > m: no convergence to rounding level inside the m steps
     b = torch.rand(n, dtype=torch.float64, device="cuda", generator=torch.Generator(device="cuda").manual_seed(2))
     V = torch.zeros(m + 1, n, dtype=torch.float64, device="cuda")
     st = a.arnoldi_state(m)
@@ -122,6 +125,15 @@ def test_arnoldi_basis_is_orthonormal_and_satisfies_the_arnoldi_relation(m):
     rhs = Q @ H[:m, : m - 1]
     err_a = float(torch.linalg.norm(lhs - rhs) / torch.linalg.norm(lhs))
     assert err_a <= 1e-12, err_a
+    # the cycle's update x = Q_m y, y the least-squares solution of H y = |b| e_1
+    x = torch.zeros(n, dtype=torch.float64, device="cuda")
+    a.arnoldi_solution(V, m, m, st, x)
+    g = torch.zeros(M1, dtype=torch.float64, device="cuda")
+    g[0] = nb
+    y = torch.linalg.lstsq(H.cpu(), g.cpu().unsqueeze(1)).solution.squeeze(1).cuda()
+    xr = Q @ y
+    err_x = float(torch.linalg.norm(x - xr) / torch.linalg.norm(xr))
+    assert err_x <= 1e-9, err_x
 
 
 @pytest.mark.parametrize("restart", [7, 40])

@@ -255,22 +255,27 @@ def test_uncached_mode_fails_loudly():
     assert e.value.code == 3
 
 
-@pytest.mark.parametrize("comm,port", [("native", 29533), ("python", 29534)])
+@pytest.mark.parametrize("comm,port", [("native", 29533), ("python", 29534), ("native", None)])
 def test_bench_sharded_path_rehearsal_two_ranks(comm, port):
     """bench.py's N>1 matvec (subtree shards, halo all-to-all, root all-gather) with
     two ranks sharing the one GPU of the box over gloo: through the library's own
     exchange (one C call per matvec, aniso_comm_init_callbacks) and through
     aniso_amd.dist.ShardExchange; each rank's input holds only its own range (native)
     or own range + halo (python), NaN elsewhere; checked against the unsharded op,
-    with the GMRES leg over the shards."""
+    with the GMRES leg over the shards.  port None: `bench.py --gpus 2` run bare, the
+    way the driver may call it -- bench.py starts its two ranks itself."""
     import subprocess
     import sys
 
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--sz", "128", "--backend", "gloo",
-           "--same-device", "--verify", "--no-cpu", "--comm", comm, "--gmres", "6", "--config4-sz", "256"]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    launcher = [] if port is None else [
+        "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+        f"--master-port={port}"]
+    cmd = [sys.executable] + launcher + [
+        os.path.join(ROOT, "bench.py"),
+        "--gpus", "2", "--steps", "2", "--warmup", "1", "--sz", "128", "--backend", "gloo",
+        "--same-device", "--verify", "--no-cpu", "--comm", comm, "--gmres", "6", "--config4-sz", "256"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
     res = json.loads(line)
@@ -904,6 +909,37 @@ def test_config5_mixed_precision_16_rhs_matches_fp64_gmres(sz):
         its, x, hist, fr = a.gmres(Q[s], m=80, maxit=400, tol=1e-12)
         assert its > 0
         assert _rel(Xh[s], x) <= 1e-10, (s, _rel(Xh[s], x))
+
+
+def test_config5_library_solve_matches_torch_loop():
+    """aniso_solve16_mixed_dev (config 5's whole solve in the library: fp64 refinement,
+    fp32 inner GMRES on the DCGS2 Arnoldi of arnoldi16.hpp) against the torch-
+    orchestrated loop it replaces (gmres_mixed(native=False), modified Gram-Schmidt):
+    both reach 1e-12 in the same number of refinements and their solutions agree to
+    1e-10; a zero right-hand side gives a zero column (no NaN from its zero residual);
+    the restart length is checked."""
+    torch = _torch()
+    import aniso_amd
+    from aniso_amd.solve import config5_charges, gmres_mixed, rhs_block
+
+    a = aniso_amd.Aniso(256, 1, 1, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    a.setCoeff(*main_coeffs(xy))
+    a.cache(0)
+    Q = np.stack([config5_charges(xy, s) for s in range(16)])
+    Q[5] = 0.0
+    B = rhs_block(a, torch.tensor(Q, device="cuda"))
+    X1, o1, i1, r1 = gmres_mixed(a, B, tol=1e-12, m=40, inner_tol=1e-6)
+    X0, o0, i0, r0 = gmres_mixed(a, B, tol=1e-12, m=40, inner_tol=1e-6, native=False)
+    assert not torch.isnan(X1).any()
+    assert (r1 <= 1e-12).all() and o1 == o0 and o1 >= 2, (r1, o1, o0)
+    assert abs(i1 - i0) <= max(2, i0 // 10), (i1, i0)
+    assert float(torch.linalg.norm(X1[5])) == 0.0 and r1[5] == 0.0
+    for s in range(16):
+        if s != 5:
+            assert float(torch.linalg.norm(X1[s] - X0[s]) / torch.linalg.norm(X0[s])) <= 1e-10, s
+    with pytest.raises(aniso_amd.AnisoError):
+        a.solve16_mixed_dev(B, torch.zeros_like(B), m=48)
 
 
 def test_config5_fp64_gmres_matches_oracle():
@@ -1700,3 +1736,50 @@ def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
         assert all(u["on"] and u["records"] > 0 for u in ups)
     if one == "spin0":
         assert all(h.stats()["top_steals"] > 0 for h in hs)
+
+
+@pytest.mark.parametrize("world,uncached", [(2, 1), (3, 0)])
+def test_comm_init_fails_on_every_rank_when_one_rank_is_uncached(world, uncached):
+    """A rank that has not cached its modes cannot run its part of a sharded matvec;
+    the ranks learn it together: comm_init all-gathers every rank's cache readiness
+    and fails on EVERY rank (no rank is left waiting inside a collective), and a
+    sharded matvec without a communicator is an error as well."""
+    _torch()
+    import threading
+
+    import aniso_amd
+
+    ks, sz = 3, 32
+    hs = []
+    for r in range(world):
+        h = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
+        h.set_shard(r, world)
+        h.setCoeff(*rough_coeffs(h.getNodes(), 2))
+        if r != uncached:
+            for m in range(2 * ks - 1):
+                h.cache(m)
+        hs.append(h)
+    shared = dict(bar=threading.Barrier(world, timeout=60), slot=[None] * world, errors=[])
+    colls = [_ThreadCollectives(world, r, shared) for r in range(world)]
+    codes = [None] * world
+
+    def run(r):
+        try:
+            hs[r].comm_init_callbacks(colls[r].struct)
+            codes[r] = 0
+        except aniso_amd.AnisoError as ex:
+            codes[r] = ex.code
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(60)
+    assert not any(t.is_alive() for t in threads)
+    assert not shared["errors"], shared["errors"]
+    assert all(c not in (None, 0) for c in codes), codes
+    import torch
+
+    x = torch.zeros(ks, hs[0].N, dtype=torch.float64, device="cuda")
+    with pytest.raises(aniso_amd.AnisoError):
+        hs[0].block_op_sharded_dev(2, x, torch.zeros_like(x))

@@ -239,3 +239,32 @@ def test_upper_partial_sum_plan(sz, nranks, monkeypatch):
     b = aniso_amd.Aniso(sz, 1, 5, 0.8, 10, 4, 20)
     b.set_shard(0, nranks)
     assert b.shard_upper_partials()["on"] == 0
+
+
+def test_bench_gpus_must_match_launcher_world_size():
+    """bench.py --gpus N under a launcher whose WORLD_SIZE differs exits non-zero before
+    touching torch or the GPU (the driver's N-GPU line must come from N ranks)."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"],
+                         capture_output=True, text=True, timeout=120, env=env)
+    assert out.returncode != 0
+    assert "WORLD_SIZE=1" in out.stderr
+
+
+def test_fixed_size_stats_writes_its_26_entries():
+    """aniso_stats keeps the contract aniso_mi355x_dev.h gives it (26 entries, the same
+    values aniso_stats_n reports first) and writes nothing past them."""
+    a = aniso_amd.Aniso(16, 1, 3, 0.8, 10, 4, 20)
+    full = np.zeros(40, dtype=np.int64)
+    n = ctypes.c_int()
+    P64 = ctypes.POINTER(ctypes.c_int64)
+    assert aniso_amd.lib().aniso_stats_n(a.address, full.ctypes.data_as(P64), len(full), ctypes.byref(n)) == 0
+    assert n.value == 31
+    fixed = np.full(40, -7, dtype=np.int64)
+    assert aniso_amd.lib().aniso_stats(a.address, fixed.ctypes.data_as(P64)) == 0
+    assert np.array_equal(fixed[:26], full[:26])
+    assert np.all(fixed[26:] == -7)
+    a.close()

@@ -124,7 +124,8 @@ int main(int argc, char** argv) {
         }
     }
     // the small kernels on kParts partials
-    arn::small_kernel_attrs();
+    (void)hipFuncSetAttribute((const void*)arn::k_arn_coef, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
+    (void)hipFuncSetAttribute((const void*)arn::k_arn_column, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
     for (int j : {0, 15, 39, 63}) {
         k_fill<<<2048, 256>>>(L.total, st, 3);
         const float mc = time([&] { arn::k_arn_coef<<<1, 256, arn::coef_lds(j)>>>(m, j, st, part, arn::kParts); }, 20);
