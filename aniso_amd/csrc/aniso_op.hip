@@ -95,6 +95,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_NEAR_EARLY")) nearEarly = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_ONE_EXCHANGE")) oneXOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_SHARD_NEAR_EARLY")) shardNearEarly = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ANISO_UP_TAILS")) upTailsOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_UP")) nearUpOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_ORDER")) nearOrderUp = std::strcmp(e, "first") != 0;
     hmRing = hm_ring_depth();
@@ -364,6 +365,10 @@ void Operator::uploadPlan() {
     up(dXT0Tasks, plan.xT0Tasks);
     up(dXOwnT0Tasks, plan.xOwnT0Tasks);
     up(dXUpTask, plan.xUpTask);
+    up(dXT0Part, plan.xT0Part);
+    up(dXUpRoots, plan.xUpRoots);
+    dXUpCnt.alloc(std::max<size_t>(plan.xUpRoots.size(), 1) * sizeof(unsigned));
+    HIP_CHECK(hipMemset(dXUpCnt.p, 0, dXUpCnt.bytes));  // each tail resets its counter after use
     up(dNearUpGrp, plan.nearUpGrp);
     up(dNearGrpEarly, plan.nearGrpEarly);
     up(dNearGrpLate, plan.nearGrpLate);
@@ -839,13 +844,29 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     const int forkTier = phase == 0 && !topFused ? std::max(ntier - 1, 0) : plan.upLastLeafTier;
     // one up tier; a sharded apply's bottom tier runs this rank's tasks only (list)
     // and stores its tier-0 roots into send, its next tier reads the gathered ones
-    auto upTier = [&](int k, const int* list, int ntask, const double* recv, double* send) {
+    // the partial tasks of the upper multipoles ride as tails of the own tier-0 launch
+    // (blockOpShardedDev decides: upTailActive; they write into the send buffer)
+    UpTail tail;
+    if (upPartial && upTailActive) {
+        tail.partOf = dXT0Part.as<int2>();
+        const size_t sb = plan.xUpRoots.size() * 16 * kRank * K * sizeof(double);
+        if (dXUpStage.bytes < sb) dXUpStage.alloc(sb);
+        tail.stage = dXUpStage.as<double>();
+        tail.cnt = dXUpCnt.as<unsigned>();
+        tail.nroots = dXUpRoots.as<int>();
+        tail.task = dXUpTask.as<int>();
+        tail.rec = dXUpRec.as<double>();
+        tail.nPeer = (int)oxRootParts;
+        tail.peerOff = dOxRootSend.as<int64_t>();
+        tail.buf = dOxSendBuf.as<double>();
+    }
+    auto upTier = [&](int k, const int* list, int ntask, const double* recv, double* send, const UpTail* tl = nullptr) {
         launch_up_tier(K, ntask, plan.upTierTask[k], list, plan.upTierMaxTask[k], dUpDesc.as<int4>(), dUpGrpFix.as<int>(),
                        dUpNode.as<int>(), dUpCode.as<int4>(), dUpGeom.as<double4>(), dUpLeaf.as<int2>(),
                        dPxT.as<double>(), dPyT.as<double>(), x, ldx, treeIn ? 1 : 0, dPerm.as<int>(), sigT,
                        dWT.as<double>(), fTw, cTw, P, dMult.as<double>(),
                        recv ? dXRootSlot.as<int>() : nullptr, recv, send ? dXSendSlot.as<int>() : nullptr, send, s,
-                       topFused && k == 0 ? dTopCnt.as<unsigned>() : nullptr);
+                       topFused && k == 0 ? dTopCnt.as<unsigned>() : nullptr, tl);
         if (fork && !nearIn && k == forkTier) HIP_CHECK(hipEventRecord(evFork, s));
     };
     auto tierTasks = [&](int k) { return plan.upTierTask[k + 1] - plan.upTierTask[k]; };
@@ -985,7 +1006,9 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
             if (fork) HIP_CHECK(hipEventRecord(evFork, s));
         }
         if (phase == 1 && ntier >= 1) {
-            if (oneX) upTier(0, dXOwnT0Tasks.as<int>(), (int)plan.xOwnT0Tasks.size(), nullptr, upPartial ? nullptr : rootsSend);
+            if (oneX)
+                upTier(0, dXOwnT0Tasks.as<int>(), (int)plan.xOwnT0Tasks.size(), nullptr, upPartial ? nullptr : rootsSend,
+                       tail.partOf ? &tail : nullptr);
             else upTier(0, dXT0Tasks.as<int>(), (int)plan.xT0Tasks.size(), nullptr, rootsSend);
         }
         for (int k = nearUp ? 1 : 0; k < (topFused ? 1 : ntier) && phase == 0; ++k) {
@@ -1913,6 +1936,8 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
         // then phase 2 (near field, upper tiers + M2L, down pass)
         oneXActive = true;
         upActive = oxUp;
+        upTailActive = oxUp && upTailsOn && !plan.xUpRoots.empty();
+        if (oxUp && oxRootParts > 63) throw std::logic_error("partial-sum records: more than 63 peer parts");
         try {
             blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 1, dXRootsSend.as<double>(), nullptr);
             const int RK = kRank * rootRhs(nb);
@@ -1939,12 +1964,13 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
             pk.nodeBase = dOxSendNodeBase.as<int64_t>();
             pk.mult = dMult.as<double>();
             pk.buf = dOxSendBuf.as<double>();
-            if (oxUp) {  // the pack launch forms this rank's records (its first workgroups)
+            if (oxUp) {  // the pack launch forms this rank's records (its first workgroups) unless the
+                         // bottom tier's tails already did
                 OxArgs pr = pk;
                 pr.nRoot = 0;
-                launch_ox_pack_up(rootRhs(nb), (int)(plan.xUpTask.size() / Plan::kUpTaskInts), dXUpTask.as<int>(),
-                                  dMult.as<double>(), dParams.as<Params>(), dXUpRec.as<double>(), (int)oxRootParts,
-                                  dOxRootSend.as<int64_t>(), pr, s);
+                launch_ox_pack_up(rootRhs(nb), upTailActive ? 0 : (int)(plan.xUpTask.size() / Plan::kUpTaskInts),
+                                  dXUpTask.as<int>(), dMult.as<double>(), dParams.as<Params>(), dXUpRec.as<double>(),
+                                  (int)oxRootParts, dOxRootSend.as<int64_t>(), pr, s);
             } else {
                 launch_ox(pk, true, s);
             }
@@ -1978,10 +2004,12 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
         } catch (...) {
             oneXActive = false;
             upActive = false;
+            upTailActive = false;
             throw;
         }
         oneXActive = false;
         upActive = false;
+        upTailActive = false;
         ++oneXApplies;
         if (oxUp) ++upPartialApplies;
         return;

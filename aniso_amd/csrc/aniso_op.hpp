@@ -311,6 +311,10 @@ private:
     // node's records (oxUpSumNode / Ptr / Src: >= 0 an offset into the receive buffer,
     // < 0 ~offset into this rank's own records); upActive marks such a matvec
     bool oxUp = false, upActive = false;
+    // the partial tasks as tails of the bottom tier (ANISO_UP_TAILS=1; default: in the
+    // pack launch, measured faster on a rank of 8: r06h)
+    bool upTailsOn = false, upTailActive = false;
+    DevBuf dXT0Part, dXUpRoots, dXUpCnt, dXUpStage;
     DevBuf dXUpTask, dXUpRec, dOxUpSumNode, dOxUpSumPtr, dOxUpSumSrc;
     int64_t oxUpSums = 0;
     bool oneExchangeUsable(int which);

@@ -91,6 +91,101 @@ __global__ void k_sub_slice(int64_t n, int nrhs, const double* __restrict__ x, i
 
 // ----------------------------------------------------------------- up pass
 
+// One partial task of the upper multipoles (Plan::xUpTask): this rank's
+// tier-0 roots under one node A two levels above them.  M2M (bbfmm.h:855-859) of the
+// roots to the mid level and to A, then A's contribution to each ancestor up to the
+// topmost level an M2L reads, one transfer matrix per level; each share an M2L reads is
+// a record, stored into rec and into every peer part.  sm: up_partial_lds<K>() doubles
+// of LDS; 256 threads.
+constexpr int kUpMaxPeers = 63;  // peer parts whose offsets the partial task holds in LDS
+template <int K>
+constexpr int up_partial_lds() {
+    return Plan::kUpTaskInts + (kUpMaxPeers + 1) + 4 * kRank * kRank + 16 * kRank * K +
+           (5 + Plan::kUpChainMax) * kRank * K;
+}
+// stage (tails): the roots from the write-through staging copies, slot q at
+// stage + q * RK, read with sc1 loads (no acquire fence; MI355X_MICROARCH.md, the
+// last-adder hand-off with write-through payload); else from mult by node id.
+// Every record is formed in LDS first and stored in one final pass: a barrier
+// between the levels then waits for LDS work only, not for the records' global
+// stores (with a store pass per level the task took ~30 us under the near field).
+template <int K>
+__device__ __forceinline__ void up_partial_task(const int* __restrict__ tk, const Params* __restrict__ P,
+                                                const double* __restrict__ mult, double* __restrict__ rec, int nPeer,
+                                                const int64_t* __restrict__ peerOff, double* __restrict__ buf,
+                                                double* sm, double* stage = nullptr) {
+    constexpr int RK = kRank * K;
+    constexpr int NI = Plan::kUpTaskInts;
+    int* T = reinterpret_cast<int*>(sm);                // NI ints (NI doubles reserved)
+    int64_t* PO = reinterpret_cast<int64_t*>(sm + NI);  // the peer parts' offsets
+    double* Rm = sm + NI + kUpMaxPeers + 1;             // R[q][r * 16 + rr]: row r of quadrant q's M2M
+    double* X = Rm + 4 * kRank * kRank;                 // the roots, slot 4 q1 + q0
+    double* Mid = X + 16 * RK;                          // the 4 mid-level records
+    double* C0 = Mid + 4 * RK;                          // A's share, then its contributions up the chain
+    for (int i = threadIdx.x; i < NI; i += blockDim.x) T[i] = tk[i];
+    for (int i = threadIdx.x; i < nPeer; i += blockDim.x) PO[i] = peerOff[i];
+    for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) Rm[i] = (&P->R[0][0])[i];
+    if (stage) {  // slot q's root at stage + q RK (absent slots: never staged, read as 0 below)
+        for (int i = threadIdx.x; i < 16 * RK; i += blockDim.x)
+            X[i] = __hip_atomic_load(stage + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        for (int i = threadIdx.x; i < 16 * RK; i += blockDim.x)
+            if (T[i / RK] < 0) X[i] = 0.0;
+    } else {
+        __syncthreads();
+        for (int i = threadIdx.x; i < 16 * RK; i += blockDim.x) {
+            const int r = T[i / RK];
+            X[i] = r >= 0 ? mult[(size_t)r * RK + i % RK] : 0.0;
+        }
+    }
+    __syncthreads();
+    // parent entry (r, b) = sum over quadrants q and rows rr of R[q][r, rr] child_q[rr, b]
+    auto m2m = [&](const double* child, int q, int r, int b, double acc) {
+        const double* R = Rm + q * kRank * kRank + r * kRank;
+#pragma unroll
+        for (int rr = 0; rr < kRank; ++rr) acc += R[rr] * child[rr * K + b];
+        return acc;
+    };
+    for (int it = threadIdx.x; it < 4 * RK; it += blockDim.x) {
+        const int q1 = it / RK, e = it - q1 * RK, r = e / K, b = e - r * K;
+        double acc = 0.0;
+        for (int q0 = 0; q0 < 4; ++q0) acc = m2m(X + (4 * q1 + q0) * RK, q0, r, b, acc);
+        Mid[it] = acc;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < RK; e += blockDim.x) {
+        const int r = e / K, b = e - r * K;
+        double acc = 0.0;
+        for (int q1 = 0; q1 < 4; ++q1) acc = m2m(Mid + q1 * RK, q1, r, b, acc);
+        C0[e] = acc;
+    }
+    const int nc = T[21];
+    for (int c = 0; c < nc; ++c) {
+        __syncthreads();
+        const double* Cin = C0 + c * RK;
+        double* Cout = C0 + (c + 1) * RK;
+        for (int e = threadIdx.x; e < RK; e += blockDim.x) {
+            const int r = e / K, b = e - r * K;
+            Cout[e] = m2m(Cin, T[22 + c], r, b, 0.0);
+        }
+    }
+    __syncthreads();
+    // the records (mid q1: T[16 + q1]; A: T[20]; chain level c: T[30 + c]), each into
+    // this rank's record buffer and every peer part
+    const int nrec = 5 + nc;
+    for (int f = threadIdx.x; f < nrec * RK; f += blockDim.x) {
+        const int j = f / RK, e = f - j * RK;
+        const int ri = j < 4 ? T[16 + j] : j == 4 ? T[20] : T[30 + j - 5];
+        if (ri < 0) continue;
+        const double v = j < 4 ? Mid[f] : C0[f - 4 * RK];
+        const int64_t o = (int64_t)ri * RK + e;
+        rec[o] = v;
+        for (int p = 0; p < nPeer; ++p) buf[PO[p] + o] = v;
+    }
+}
+
+typedef __attribute__((address_space(1))) unsigned gu32_up;
+
 template <int K>
 __global__ void __launch_bounds__(kUpThreads) k_up_tier(
     int taskBase, const int* __restrict__ taskList, int maxTask, const int4* __restrict__ desc, const int* __restrict__ grpFix,
@@ -100,13 +195,50 @@ __global__ void __launch_bounds__(kUpThreads) k_up_tier(
     const double* __restrict__ sigT, const double* __restrict__ wT, double* __restrict__ fT, double* __restrict__ cT,
     const Params* __restrict__ P, double* __restrict__ mult, const int* __restrict__ rootSlot,
     const double* __restrict__ recv, const int* __restrict__ sendSlot, double* __restrict__ send,
-    unsigned* __restrict__ zeroCnt) {
+    unsigned* __restrict__ zeroCnt, UpTail tail) {
     extern __shared__ double sm[];
     // the counters of the fused top-of-tree launch that follows (k_top_m2l_hc)
     if (zeroCnt && blockIdx.x == 0 && threadIdx.x <= kMaxTopTiers) zeroCnt[threadIdx.x] = 0u;
     const int task = taskList ? taskList[blockIdx.x] : taskBase + (int)blockIdx.x;
     up_task<K>(task, maxTask, desc, grpFix, node, code, geom, leafRange, pxT, pyT, xin, ldi, treeIn, perm, sigT, wT,
                fT, cT, P, mult, rootSlot, recv, sendSlot, send, sm);
+    if (!tail.partOf) return;
+    // the partial task's last root (MI355X_MICROARCH.md, inter-workgroup visibility:
+    // the last-adder hand-off with a write-through payload, no fences): this block's
+    // root multipole (its own plain stores, re-read after the barrier) is copied into
+    // the staging slot with sc1 (write-through) stores; every storing wave waits for
+    // them, then one lane adds to the partial task's counter; the block whose add
+    // completes the count resets the counter for the next apply and runs the partial
+    // task, loading the staged roots with sc1 loads.  No block waits for another, so
+    // dispatch order does not matter.
+    constexpr int RK = kRank * K;
+    __shared__ int lastOf;
+    const int2 pq = tail.partOf[blockIdx.x];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the root's plain stores by every wave of this block
+    __syncthreads();
+    if (pq.x >= 0)
+        for (int e = threadIdx.x; e < RK; e += blockDim.x)
+            __hip_atomic_store(tail.stage + (size_t)pq.x * RK + e, mult[(size_t)pq.y * RK + e], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        if (pq.x >= 0) {
+            const int p = pq.x >> 4;
+            const unsigned old = __hip_atomic_fetch_add((gu32_up*)(tail.cnt + p), 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (old + 1u == (unsigned)tail.nroots[p]) {
+                __hip_atomic_store((gu32_up*)(tail.cnt + p), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                run = p + 1;
+            }
+        }
+        lastOf = run;
+    }
+    __syncthreads();
+    if (lastOf)
+        up_partial_task<K>(tail.task + (size_t)(lastOf - 1) * Plan::kUpTaskInts, P, mult, tail.rec, tail.nPeer,
+                           tail.peerOff, tail.buf, sm, tail.stage + (size_t)(lastOf - 1) * 16 * RK);
 }
 
 
@@ -1010,7 +1142,7 @@ void launch_up_tier(int K, int ntask, int taskBase, const int* taskList, int max
                     const double* pxT, const double* pyT, const double* xin, int64_t ldi, int treeIn, const int* perm,
                     const double* sigT, const double* wT, double* fT, double* cT, const Params* P, double* mult,
                     const int* rootSlot, const double* recv, const int* sendSlot, double* send, hipStream_t s,
-                    unsigned* zeroCnt) {
+                    unsigned* zeroCnt, const UpTail* tail) {
     if (ntask <= 0) {
         if (zeroCnt) {
             const hipError_t e = hipMemsetAsync(zeroCnt, 0, (kMaxTopTiers + 1) * sizeof(unsigned), s);
@@ -1018,11 +1150,14 @@ void launch_up_tier(int K, int ntask, int taskBase, const int* taskList, int max
         }
         return;
     }
-    const size_t shm = up_tier_lds(maxTask, K);
-    ANISO_DISPATCH_K(K, (k_up_tier<KK><<<ntask, kUpThreads, shm, s>>>(taskBase, taskList, maxTask, desc, grpFix, node,
-                                                                      code, geom, leafRange, pxT, pyT, xin, ldi, treeIn,
-                                                                      perm, sigT, wT, fT, cT, P, mult, rootSlot, recv,
-                                                                      sendSlot, send, zeroCnt)));
+    const UpTail tl = tail ? *tail : UpTail{};
+    ANISO_DISPATCH_K(K, ({
+        const size_t shm = std::max(up_tier_lds(maxTask, KK),
+                                    tl.partOf ? (size_t)up_partial_lds<KK>() * sizeof(double) : (size_t)0);
+        k_up_tier<KK><<<ntask, kUpThreads, shm, s>>>(taskBase, taskList, maxTask, desc, grpFix, node, code, geom,
+                                                     leafRange, pxT, pyT, xin, ldi, treeIn, perm, sigT, wT, fT, cT, P,
+                                                     mult, rootSlot, recv, sendSlot, send, zeroCnt, tl);
+    }));
     HIP_LAUNCH_CHECK();
 }
 
@@ -1128,61 +1263,12 @@ __global__ void __launch_bounds__(256) k_ox_pack_up(UpPack u, OxArgs a) {
         ox_element<true>(a, (int64_t)(blockIdx.x - u.ntask) * blockDim.x + threadIdx.x);
         return;
     }
-    constexpr int RK = kRank * K;
-    constexpr int NI = Plan::kUpTaskInts;
-    __shared__ int T[NI];
-    __shared__ double Rm[4 * kRank * kRank];  // R[q][r * 16 + rr]: row r of quadrant q's M2M
-    __shared__ double X[16 * RK];             // the roots, slot 4 q1 + q0
-    __shared__ double Mid[4 * RK];
-    __shared__ double C[2][RK];               // A's share, then its contributions up the chain
+    __shared__ double sm[up_partial_lds<K>()];
     // the exchange waits on these few latency-bound workgroups, and the near field's own
     // groups run beside them: their waves issue first on a contended SIMD
     if (u.prio) __builtin_amdgcn_s_setprio(3);
-    const int* tk = u.task + (size_t)blockIdx.x * NI;
-    for (int i = threadIdx.x; i < NI; i += blockDim.x) T[i] = tk[i];
-    for (int i = threadIdx.x; i < 4 * kRank * kRank; i += blockDim.x) Rm[i] = (&u.P->R[0][0])[i];
-    __syncthreads();
-    for (int i = threadIdx.x; i < 16 * RK; i += blockDim.x) {
-        const int r = T[i / RK];
-        X[i] = r >= 0 ? u.mult[(size_t)r * RK + i % RK] : 0.0;
-    }
-    __syncthreads();
-    auto store = [&](int ri, int e, double v) {  // record ri, entry e: own buffer and every peer part
-        if (ri < 0) return;
-        u.rec[(size_t)ri * RK + e] = v;
-        for (int p = 0; p < u.nPeer; ++p) a.buf[u.peerOff[p] + (int64_t)ri * RK + e] = v;
-    };
-    // parent entry (r, b) = sum over quadrants q and rows rr of R[q][r, rr] child_q[rr, b]
-    auto m2m = [&](const double* child, int q, int r, int b, double acc) {
-        const double* R = Rm + q * kRank * kRank + r * kRank;
-#pragma unroll
-        for (int rr = 0; rr < kRank; ++rr) acc += R[rr] * child[rr * K + b];
-        return acc;
-    };
-    for (int it = threadIdx.x; it < 4 * RK; it += blockDim.x) {
-        const int q1 = it / RK, e = it - q1 * RK, r = e / K, b = e - r * K;
-        double acc = 0.0;
-        for (int q0 = 0; q0 < 4; ++q0) acc = m2m(X + (4 * q1 + q0) * RK, q0, r, b, acc);
-        Mid[it] = acc;
-        store(T[16 + q1], e, acc);
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < RK; e += blockDim.x) {
-        const int r = e / K, b = e - r * K;
-        double acc = 0.0;
-        for (int q1 = 0; q1 < 4; ++q1) acc = m2m(Mid + q1 * RK, q1, r, b, acc);
-        C[0][e] = acc;
-        store(T[20], e, acc);
-    }
-    for (int c = 0; c < T[21]; ++c) {
-        __syncthreads();
-        for (int e = threadIdx.x; e < RK; e += blockDim.x) {
-            const int r = e / K, b = e - r * K;
-            const double v = m2m(C[c & 1], T[22 + c], r, b, 0.0);
-            C[(c + 1) & 1][e] = v;
-            store(T[30 + c], e, v);
-        }
-    }
+    up_partial_task<K>(u.task + (size_t)blockIdx.x * Plan::kUpTaskInts, u.P, u.mult, u.rec, u.nPeer, u.peerOff, a.buf,
+                       sm);
 }
 
 void launch_ox_pack_up(int K, int ntask, const int* task, const double* mult, const Params* P, double* rec,

@@ -274,6 +274,10 @@ struct Plan {
     int xUpTop = 0;
     std::vector<int> xUpTask;
     std::vector<int> xUpRecNode;  // per record of this rank: its upper node
+    // the partial tasks as tails of the bottom tier: per xOwnT0Tasks entry {16 p + q
+    // (its root is slot q of partial task p; -1: none), its root node}, and per partial
+    // task its root count
+    std::vector<int> xT0Part, xUpRoots;
 
     void build(const Tree& t, int np, int rank, int nranks);
     // the exchange plan above; sz / d2: the square grid of the correction stencil

@@ -1093,6 +1093,8 @@ void Plan::buildExchange(const Tree& t, int sz, int d2) {
     xUpTop = 0;
     xUpTask.clear();
     xUpRecNode.clear();
+    xT0Part.clear();
+    xUpRoots.clear();
     xRootSend.clear();
     xRootRecv.clear();
     xRootSlot.clear();
@@ -1296,6 +1298,27 @@ void Plan::buildExchange(const Tree& t, int sz, int d2) {
             a[38] = A;
             a[39] = 0;
             xUpTask.insert(xUpTask.end(), a.begin(), a.end());
+        }
+        // the tails: each own tier-0 task's partial task (its root's grandparent), in
+        // xUpTask's order, and how many roots each one waits for
+        std::vector<int> pos(tops.size());
+        for (size_t k = 0; k < order.size(); ++k) pos[order[k]] = (int)k;
+        xUpRoots.assign(tops.size(), 0);
+        xT0Part.assign(2 * xOwnT0Tasks.size(), -1);
+        for (size_t i = 0; i < xOwnT0Tasks.size(); ++i) {
+            const int r = upTaskRoot[xOwnT0Tasks[i]];
+            const int pt = pos[taskOfTop[t.parent[t.parent[r]]]];
+            int q = 0;
+            while (q < 16 && xUpTask[(size_t)pt * kUpTaskInts + q] != r) ++q;
+            if (q == 16) throw std::logic_error("upper partials: a root is not in its task");
+            xT0Part[2 * i] = 16 * pt + q;
+            xT0Part[2 * i + 1] = r;
+            ++xUpRoots[pt];
+        }
+        for (size_t pt = 0; pt < xUpRoots.size(); ++pt) {  // every tail waits for exactly its task's roots
+            int slots = 0;
+            for (int i = 0; i < 16; ++i) slots += xUpTask[pt * kUpTaskInts + i] >= 0;
+            if (slots != xUpRoots[pt]) throw std::logic_error("upper partials: a tail's root count differs from its task");
         }
     }
     nearGrpEarly.clear();

@@ -82,12 +82,30 @@ size_t down_tier_lds(int maxTask, int maxLeaves, int maxNear, int maxChain, int 
 // are tier-0 roots with a slot are read from the all-gathered records recv (and
 // stored to mult for the M2L); sendSlot / send -- a task root with a send slot also
 // stores its record into this rank's all-gather buffer.
+// The upper multipoles' partial tasks (Plan::xUpTask) as tails of the sharded
+// bottom tier: block b's task root (node partOf[b].y) is slot q of
+// partial task p (partOf[b].x = 16 p + q; -1: none).  The block copies its root
+// multipole write-through into stage[16 p + q]; the last of a partial task's
+// nroots[p] roots to finish (an agent-scope counter, cnt[p], reset by that block)
+// runs it from the staged roots, storing its records into rec and into each of nPeer
+// parts at peerOff (doubles into buf, the exchange's send buffer).
+struct UpTail {
+    const int2* partOf = nullptr;
+    double* stage = nullptr;
+    unsigned* cnt = nullptr;
+    const int* nroots = nullptr;
+    const int* task = nullptr;
+    double* rec = nullptr;
+    int nPeer = 0;
+    const int64_t* peerOff = nullptr;
+    double* buf = nullptr;
+};
 void launch_up_tier(int K, int ntask, int taskBase, const int* taskList, int maxTask, const int4* desc,
                     const int* grpFix, const int* node, const int4* code, const double4* geom, const int2* leafRange,
                     const double* pxT, const double* pyT, const double* xin, int64_t ldi, int treeIn, const int* perm,
                     const double* sigT, const double* wT, double* fT, double* cT, const Params* P, double* mult,
                     const int* rootSlot, const double* recv, const int* sendSlot, double* send, hipStream_t s,
-                    unsigned* zeroCnt = nullptr);
+                    unsigned* zeroCnt = nullptr, const UpTail* tail = nullptr);
 // config 5's fp32 operator (f32op.hip): node expansions as 64 lanes x float4
 // (void* below), vectors point-major N x 16 floats
 void launch32_p2m(int nleaf, const int* leaves, const int64_t* begin, const int64_t* count, const double* ncx,

@@ -1650,7 +1650,7 @@ class _ThreadCollectives:
                                                (64, 8, "1", 1, 20), (64, 3, "1", 1, 20), (96, 3, "1", 1, 20),
                                                (40, 2, "1", 1, 3), (32, 2, "1", 2, 20), (64, 3, "mixed", 1, 20),
                                                (64, 2, "spin0", 1, 20), (256, 4, "1", 1, 20), (512, 8, "1", 1, 20),
-                                               (256, 4, "partial0", 1, 20)])
+                                               (256, 4, "partial0", 1, 20), (512, 8, "tails", 1, 20)])
 def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     """The library's one-call sharded block matvec (aniso_block_op_sharded_dev) with
     `world` ranks as threads of one process on the box's GPU, each rank's input valid
@@ -1675,7 +1675,9 @@ def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
 
     import aniso_amd
 
-    monkeypatch.setenv("ANISO_ONE_EXCHANGE", "1" if one in ("mixed", "spin0", "partial0") else one)
+    monkeypatch.setenv("ANISO_ONE_EXCHANGE", "1" if one in ("mixed", "spin0", "partial0", "tails") else one)
+    # "tails": the upper partial tasks as tails of the own tier-0 launch (ANISO_UP_TAILS=1)
+    monkeypatch.setenv("ANISO_UP_TAILS", "1" if one == "tails" else "0")
     monkeypatch.setenv("ANISO_UPPER_PARTIAL", "0" if one in ("spin0", "partial0") else "1")
     ks = 5
     full = aniso_amd.Aniso(sz, d, ks, 0.8, 10, 4, ml)
@@ -1732,7 +1734,7 @@ def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     assert not torch.isnan(Y).any()
     assert float(torch.linalg.norm(Y - ref) / torch.linalg.norm(ref)) <= 1e-13
     used = [h.stats()["one_exchange_applies"] for h in hs]
-    one_used = one in ("1", "spin0", "partial0") and all(oks) and staged
+    one_used = one in ("1", "spin0", "partial0", "tails") and all(oks) and staged
     assert used == [2 * int(one_used)] * world
     ups = [h.shard_upper_partials() for h in hs]
     assert [h.stats()["upper_partial_applies"] for h in hs] == [2 * int(one_used and all(u["on"] for u in ups))] * world
