@@ -782,7 +782,7 @@ class Aniso:
         return ptr, idx
 
     def stats(self):
-        s = np.zeros(32, dtype=np.int64)
+        s = np.zeros(40, dtype=np.int64)
         n = ctypes.c_int()
         _check(lib().aniso_stats_n(self.address, s.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(s),
                                    ctypes.byref(n)))
@@ -791,7 +791,8 @@ class Aniso:
                 "hm_clusters", "hm_dual_pairs", "hm_block_reads", "f32_cache_bytes", "top_fused",
                 "plan_halo_slots", "plan_max_lds_slots", "plan_block_reads", "top_recoveries",
                 "near_hs_stored", "near_hs_partials", "one_exchange_applies", "mrhs_m2l_pairs",
-                "top_steals", "upper_partial_applies", "near_overlap", "near_up_tier"]
+                "top_steals", "upper_partial_applies", "near_overlap", "near_up_tier", "near_loc_entries",
+                "near_corr_rows", "near_up_nodes"]
         return dict(zip(keys, (int(v) for v in s)))
 
     def sync(self):

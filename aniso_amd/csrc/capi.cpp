@@ -594,7 +594,7 @@ int aniso_tree_list(aniso_handle h, int which, int64_t* ptr, int* idx) {
     });
 }
 
-constexpr int kStatsV1 = 26, kStats = 31;  // aniso_stats: the 26 entries its round-4 contract promised
+constexpr int kStatsV1 = 26, kStats = 34;  // aniso_stats: the 26 entries its round-4 contract promised
 
 static void stats_fill(aniso::Operator& op, int64_t* s) {
     s[0] = op.nearEntries();
@@ -634,6 +634,13 @@ static void stats_fill(aniso::Operator& op, int64_t* s) {
     s[28] = op.upPartialApplies;  // one-collective matvecs with the upper multipoles as partial sums
     s[29] = op.nearOverlaps() ? 1 : 0;  // the block apply's near field on the side stream (else serial)
     s[30] = op.nearUpTier() ? 1 : 0;  // the one-GPU block apply's bottom up tier inside the near field
+    // the staged near field's index streams (bench.py's extended algorithmic bytes): its
+    // 16-bit source-row entries (one per leaf and source point), its correction-stencil
+    // row entries (9 per target), and the bottom-tier nodes whose multipoles its up tail
+    // writes (16 leaves + 4 parents + 1 root per group)
+    s[31] = (int64_t)op.plan.nearLoc.size();
+    s[32] = (int64_t)op.plan.nearCorrRow.size();
+    s[33] = (int64_t)(op.plan.nearUpGrp.size() / aniso::kNearUpInts) * 21;
 }
 
 // the fixed-size entry: the first kStatsV1 = 26 entries, as aniso_mi355x_dev.h has

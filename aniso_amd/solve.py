@@ -356,7 +356,10 @@ def _gmres_dist_dev(apply, b, x, w, V, m, tol, maxit, allreduce, normb, x_zero, 
 
     n = b.numel()
     st = kry.arnoldi_state(m)
-    stat = MappedStatus(4)
+    # the status word: one pinned mapped allocation per handle, reused by its solves
+    stat = getattr(kry, "_gmres_status", None)
+    if stat is None:
+        stat = kry._gmres_status = MappedStatus(4)
     out = torch.zeros(m + 2, dtype=torch.float64, device=b.device)
     ev = torch.cuda.Event()
     bv, wv, xv = b.reshape(-1), w.reshape(-1), x.reshape(-1)
@@ -423,5 +426,5 @@ def _gmres_dist_dev(apply, b, x, w, V, m, tol, maxit, allreduce, normb, x_zero, 
         else:
             relres, _ = begin()
     finally:
-        stat.close()
+        torch.cuda.synchronize()  # no kernel may still write the reused status word
     return x, (total if relres <= tol else -max(total, 1)), relres

@@ -706,7 +706,22 @@ def main():
         # every (target, source) point pair once (8 B each), timed by its own HIP events
         # on the side stream it runs on (overlapped with the M2L)
         near_ms = times["near"]
-        near_bytes = 8.0 * my_stats["stored_near"]
+        # the launch's full algorithmic bytes (verdict r05: the E stream alone left its fused
+        # work uncounted): the directed E entries (8 B each); every point's data once
+        # (x, y, the nb input charges, sigma_s, the quadrature weight: the source table's
+        # and the epilogue's reads); the 16-bit source-row and correction-stencil row
+        # indices; sigma_t at each point (the r = 0 diagonal); the nb outputs per target;
+        # with the up tail (one GPU), the bottom-tier multipoles it writes (16 x nb doubles
+        # per node)
+        n_pts = my_stats["N"] if world == 1 else (oe - ob)
+        parts = {"E_entries": 8.0 * my_stats["stored_near"],
+                 "points_once": 8.0 * (4 + nb) * n_pts,
+                 "row_indices": 2.0 * (my_stats["near_loc_entries"] + my_stats["near_corr_rows"]),
+                 "sigma_t_diag": 8.0 * n_pts,
+                 "outputs": 8.0 * nb * n_pts,
+                 "up_tail_multipoles": (8.0 * 16 * nb * my_stats["near_up_nodes"]
+                                        if my_stats["near_up_tier"] and world == 1 else 0.0)}
+        near_bytes = sum(parts.values())
         near_gbs = near_bytes / (near_ms * 1e-3) / 1e9 if near_ms > 0 else 0.0
         # leaves <= 16 points (this geometry) run k_near_hs (sources staged in LDS)
         nkern = "k_near_hs" if my_stats["max_leaf"] <= 16 else "k_near_hm"
@@ -717,6 +732,8 @@ def main():
                             "traffic_source": nsrc, "traffic_kernel": nkname,
                             "kernel": f"{nkern}<{nb}>", "kernel_ms": round(near_ms, 5),
                             "algorithmic_bytes": int(near_bytes),
+                            "algorithmic_bytes_parts": {k: int(v_) for k, v_ in parts.items()},
+                            "traffic_over_algorithmic": (round(ntraffic / near_bytes, 3) if ntraffic else None),
                             "overlapped_with": roofline["kernel"] if my_stats.get("near_overlap") else None}
         roofline["m2l_rsqrt"] = "v_rsq_f64 + 1 Newton step (~1e-13 relative per entry); near field 2 steps (full fp64)"
     applies = ks * (2 * ks - 1) if block else 1  # the reference's mapping calls per matvec
@@ -792,7 +809,10 @@ def main():
             gb = rhs0[:, ob:oe].contiguous()
             gapply = adist.native_block_matvec(op, nb, "cuda") if native else adist.sharded_block_matvec(op, xchg)
             gred = xchg.allreduce
-        gmres_dist(gapply, gb, restart=2, tol=0.0, maxit=1, allreduce=gred, kry=op)  # warm-up
+        # warm-up: one cycle of the same length (its Krylov basis allocation is then reused,
+        # and the GPU enters the timed cycle busy, not after an idle gap: a cold start ran
+        # the first steps' kernels at lower clocks, r06i trace)
+        gmres_dist(gapply, gb, restart=args.gmres, tol=0.0, maxit=1, allreduce=gred, kry=op)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()

@@ -77,9 +77,11 @@ int aniso_tree_list(aniso_handle h, int which, int64_t *ptr, int *idx);
  * if the block apply runs its near field on a side stream beside the up pass and the
  * M2L (a shard, or ANISO_OVERLAP=1), 0 if serially (one GPU's default); then 1 if
  * the serial block apply forms its bottom up tier inside the staged near field
- * (section 3.11; ANISO_NEAR_UP=0 keeps its own launch).
+ * (section 3.11; ANISO_NEAR_UP=0 keeps its own launch); then the staged near
+ * field's 16-bit source-row entries, its correction-stencil row entries and the
+ * bottom-tier nodes its up tail writes (bench.py's extended algorithmic bytes).
  * aniso_stats_n writes the first min(cap, *n) of them and sets *n to their count
- * (31 here); aniso_stats, the fixed-size form, writes the first 26 (stats must hold
+ * (34 here); aniso_stats, the fixed-size form, writes the first 26 (stats must hold
  * 26 entries). */
 int aniso_stats_n(aniso_handle h, int64_t *stats, int cap, int *n);
 int aniso_stats(aniso_handle h, int64_t *stats);
