@@ -96,6 +96,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_ONE_EXCHANGE")) oneXOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_SHARD_NEAR_EARLY")) shardNearEarly = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_UP_TAILS")) upTailsOn = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ANISO_NEAR_AFTER_PACK")) nearAfterPack = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_UP")) nearUpOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_ORDER")) nearOrderUp = std::strcmp(e, "first") != 0;
     hmRing = hm_ring_depth();
@@ -978,15 +979,19 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
         // order) the near field and the corrections read
         e0 = tm ? mark(s) : -1;
         eStart = e0;
-        if (nearIn && oneX && !plan.nearGrpEarly.empty() && shardNearEarly) {
+        const bool nearEarlyGroups = nearIn && oneX && !plan.nearGrpEarly.empty() && shardNearEarly;
+        const bool earlyAfterPack = nearEarlyGroups && phase == 1 && ntier >= 1 && packHook;
+        auto nearEarlyStage = [&] {
             // one-collective form: the groups that read only the own range start now,
-            // beside the own tier-0 tasks; the rest waits for the exchange (phase 2)
+            // beside the own tier-0 tasks (or after the pack); the rest waits for the
+            // exchange (phase 2)
             nin.grpList = dNearGrpEarly.as<int>();
             nin.ngrp = (int)plan.nearGrpEarly.size();
             if (fork) HIP_CHECK(hipEventRecord(evFork, s));
             nearStage();
             if (!fork && tm) e0 = mark(s);
-        }
+        };
+        if (nearEarlyGroups && !earlyAfterPack) nearEarlyStage();
         // the fork point is the start of the apply, but the near field's launch is issued
         // after the bottom up tier's, so the dispatcher tends to hand the up tasks their
         // workgroup slots first (0.6-1.2 % per block matvec on one GPU, 1.6 % on a rank
@@ -1010,6 +1015,11 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
                 upTier(0, dXOwnT0Tasks.as<int>(), (int)plan.xOwnT0Tasks.size(), nullptr, upPartial ? nullptr : rootsSend,
                        tail.partOf ? &tail : nullptr);
             else upTier(0, dXT0Tasks.as<int>(), (int)plan.xT0Tasks.size(), nullptr, rootsSend);
+            if (earlyAfterPack) {  // the pack's partial tasks take their slots before the near groups do
+                packHook(s);
+                packIssued = true;
+                nearEarlyStage();
+            }
         }
         for (int k = nearUp ? 1 : 0; k < (topFused ? 1 : ntier) && phase == 0; ++k) {
             upTier(k, nullptr, tierTasks(k), nullptr, nullptr);
@@ -1937,43 +1947,53 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
         oneXActive = true;
         upActive = oxUp;
         upTailActive = oxUp && upTailsOn && !plan.xUpRoots.empty();
+        packIssued = false;
         if (oxUp && oxRootParts > 63) throw std::logic_error("partial-sum records: more than 63 peer parts");
         try {
-            blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 1, dXRootsSend.as<double>(), nullptr);
             const int RK = kRank * rootRhs(nb);
             // one pack launch (this rank's roots -- or its partial-sum records -- into
             // every peer's part, the input positions and the multipole rows each peer
             // reads), one all-to-all-v, one unpack launch (the peers' roots into the slot
             // layout and the own roots -- or every upper node's records summed -- the
             // input's halo, the multipoles)
+            // (built when the pack is enqueued: phase 1 may size the work buffers, dMult)
             OxArgs pk;
-            pk.nRoot = oxRootParts;
-            pk.rec = oxUp ? (int64_t)plan.xUpRecNode.size() * RK : rec;
-            pk.rootOff = dOxRootSend.as<int64_t>();
-            pk.roots = oxUp ? dXUpRec.as<double>() : dXRootsSend.as<double>();
-            pk.nPts = oxNsendPts;
-            pk.nb = nb;
-            pk.pos = dOxSendPos.as<int64_t>();
-            pk.base = dOxSendBase.as<int64_t>();
-            pk.stride = dOxSendStride.as<int64_t>();
-            pk.x = x;
-            pk.ldx = ldx;
-            pk.nNode = oxNsendNodes;
-            pk.len = RK;
-            pk.node = dOxSendNode.as<int>();
-            pk.nodeBase = dOxSendNodeBase.as<int64_t>();
-            pk.mult = dMult.as<double>();
-            pk.buf = dOxSendBuf.as<double>();
-            if (oxUp) {  // the pack launch forms this rank's records (its first workgroups) unless the
-                         // bottom tier's tails already did
-                OxArgs pr = pk;
-                pr.nRoot = 0;
-                launch_ox_pack_up(rootRhs(nb), upTailActive ? 0 : (int)(plan.xUpTask.size() / Plan::kUpTaskInts),
-                                  dXUpTask.as<int>(), dMult.as<double>(), dParams.as<Params>(), dXUpRec.as<double>(),
-                                  (int)oxRootParts, dOxRootSend.as<int64_t>(), pr, s);
-            } else {
-                launch_ox(pk, true, s);
-            }
+            auto packArgs = [&] {
+                pk.nRoot = oxRootParts;
+                pk.rec = oxUp ? (int64_t)plan.xUpRecNode.size() * RK : rec;
+                pk.rootOff = dOxRootSend.as<int64_t>();
+                pk.roots = oxUp ? dXUpRec.as<double>() : dXRootsSend.as<double>();
+                pk.nPts = oxNsendPts;
+                pk.nb = nb;
+                pk.pos = dOxSendPos.as<int64_t>();
+                pk.base = dOxSendBase.as<int64_t>();
+                pk.stride = dOxSendStride.as<int64_t>();
+                pk.x = x;
+                pk.ldx = ldx;
+                pk.nNode = oxNsendNodes;
+                pk.len = RK;
+                pk.node = dOxSendNode.as<int>();
+                pk.nodeBase = dOxSendNodeBase.as<int64_t>();
+                pk.mult = dMult.as<double>();
+                pk.buf = dOxSendBuf.as<double>();
+            };
+            auto pack = [&](hipStream_t st) {
+                packArgs();
+                if (oxUp) {  // the pack launch forms this rank's records (its first workgroups) unless the
+                             // bottom tier's tails already did
+                    OxArgs pr = pk;
+                    pr.nRoot = 0;
+                    launch_ox_pack_up(rootRhs(nb), upTailActive ? 0 : (int)(plan.xUpTask.size() / Plan::kUpTaskInts),
+                                      dXUpTask.as<int>(), dMult.as<double>(), dParams.as<Params>(),
+                                      dXUpRec.as<double>(), (int)oxRootParts, dOxRootSend.as<int64_t>(), pr, st);
+                } else {
+                    launch_ox(pk, true, st);
+                }
+            };
+            if (nearAfterPack) packHook = pack;
+            blockOpDev(which, x, ldx, yo, ldy, true, s, NAN, nullptr, 1, dXRootsSend.as<double>(), nullptr);
+            packHook = nullptr;
+            if (!packIssued) pack(s);
             comm->alltoallv(dOxSendBuf.as<double>(), oxScount.data(), oxSoff.data(), dOxRecvBuf.as<double>(),
                             oxRcount.data(), oxRoff.data(), s);
             OxArgs uk = pk;
@@ -2005,6 +2025,7 @@ void Operator::blockOpShardedDev(int which, double* x, int64_t ldx, double* y, i
             oneXActive = false;
             upActive = false;
             upTailActive = false;
+            packHook = nullptr;
             throw;
         }
         oneXActive = false;

@@ -10,6 +10,7 @@
 #include <array>
 #include <cmath>
 #include <map>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -314,6 +315,11 @@ private:
     // the partial tasks as tails of the bottom tier (ANISO_UP_TAILS=1; default: in the
     // pack launch, measured faster on a rank of 8: r06h)
     bool upTailsOn = false, upTailActive = false;
+    // the one-collective exchange's pack launch, enqueued by phase 1 right after the own
+    // tier-0 launch when the near field's early groups fork after it
+    // (ANISO_NEAR_AFTER_PACK=1): packHook set by blockOpShardedDev, packIssued by phase 1
+    bool nearAfterPack = false, packIssued = false;
+    std::function<void(hipStream_t)> packHook;
     DevBuf dXT0Part, dXUpRoots, dXUpCnt, dXUpStage;
     DevBuf dXUpTask, dXUpRec, dOxUpSumNode, dOxUpSumPtr, dOxUpSumSrc;
     int64_t oxUpSums = 0;

@@ -1228,6 +1228,21 @@ __global__ void k_ox(OxArgs a) {
     ox_element<PACK>(a, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
+// Development (the loopback communicator, ANISO_LOOPBACK_XCHG_US): a stand-in for an
+// exchange's latency on the stream -- `blocks` one-wave workgroups that each sleep
+// until `us` microseconds of the 100 MHz real-time clock have passed (bounded: every
+// wave exits), occupying a few CUs as the collective's kernels would.
+__global__ void __launch_bounds__(64) k_spin_us(long long ticks) {
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+void launch_spin_us(int us, int blocks, hipStream_t s) {
+    if (us <= 0 || blocks <= 0) return;
+    k_spin_us<<<blocks, 64, 0, s>>>((long long)us * 100);
+    HIP_LAUNCH_CHECK();
+}
+
 void launch_ox(const OxArgs& a, bool pack, hipStream_t s) {
     const int64_t n = a.nRoot * a.rec + a.nPts * a.nb + a.nNode * a.len + (!pack && a.ownRoots ? a.rec : 0) +
                       (!pack ? a.nSum * a.len : 0);

@@ -1,9 +1,11 @@
 // comm.cpp -- the collectives of the library's own multi-GPU exchange (comm.hpp).
 #include "comm.hpp"
+#include "kernels.hpp"
 
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -150,8 +152,17 @@ class LoopbackCollectives : public Collectives {
                                             hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
     }
+    // ANISO_LOOPBACK_XCHG_US: a stand-in for the exchange's latency over xGMI (a spin
+    // kernel of that duration on 8 workgroups), so a rank's schedule is timed with the
+    // exchange in its critical path
     void alltoallv(const double*, const int64_t*, const int64_t*, double*, const int64_t*, const int64_t*,
-                   hipStream_t) override {}
+                   hipStream_t s) override {
+        static const int us = [] {
+            const char* e = std::getenv("ANISO_LOOPBACK_XCHG_US");
+            return e ? std::atoi(e) : 0;
+        }();
+        launch_spin_us(us, 8, s);
+    }
     void allreduce(double*, size_t, hipStream_t) override {}
     bool loopback() const override { return true; }
 };

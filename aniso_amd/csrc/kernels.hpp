@@ -420,6 +420,7 @@ struct OxArgs {
     const double* ownRec = nullptr;
 };
 void launch_ox(const OxArgs& a, bool pack, hipStream_t s);
+void launch_spin_us(int us, int blocks, hipStream_t s);  // development: a stand-in exchange latency
 // the pack launch with the upper multipoles as partial sums (apply.hip k_ox_pack_up):
 // one workgroup per task of Plan::xUpTask (kUpTaskInts ints each) stores its records
 // into rec and into each of nPeer parts at peerOff (doubles into a.buf), the rest pack
