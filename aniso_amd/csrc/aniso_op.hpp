@@ -263,6 +263,9 @@ private:
     DevBuf dTopSteals;          // tier tasks computed by waiting blocks of the fused launch (persistent)
     DevBuf dTopTrace;           // ANISO_TOP_TRACE=1: the launch's per-block timeline
     DevBuf dKryPart;            // partial sums of the Krylov primitives
+    // config 5's library solve (solve16Mixed): its vectors and fp32 basis, kept between
+    // solves (grown, never shrunk: a hipFree synchronises the device)
+    DevBuf s16B, s16X, s16R, s16W, s16D, s16Df, s16W32, s16V, s16St, s16Part, s16R0;
     void arnoldiParts(int rows);  // dKryPart for sweeps of `rows` rows
     bool topTraceOn = false;
     int hmRing = 0;  // the cluster M2L's LDS ring depth (ANISO_HM_RING; 0: the one-block-in-flight form)

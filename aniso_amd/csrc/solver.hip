@@ -765,22 +765,24 @@ int Operator::solve16Mixed(const double* B, int64_t ldb, double* X, int64_t ldx,
     const int64_t sts = lay.total;
     arn::ColArgs ca = kCols;
     ca.sts = sts;
-    DevBuf bB, bX, bR, bW, bD, bDf, bW32, bV, bSt, bPart, bNb;
-    bB.alloc(n16 * sizeof(double));
-    bX.alloc(n16 * sizeof(double));
-    bR.alloc(n16 * sizeof(double));
-    bW.alloc(n16 * sizeof(double));
-    bD.alloc(n16 * sizeof(double));
-    bDf.alloc(n16 * sizeof(float));
-    bW32.alloc(n16 * sizeof(float));
-    bV.alloc((size_t)(m + 1) * n16 * sizeof(float));
-    bSt.alloc((size_t)KC * sts * sizeof(double));
-    bPart.alloc((size_t)kParts * KC * (m + 2) * sizeof(double));
-    bNb.alloc(KC * sizeof(double));
+    auto grow = [](DevBuf& b, size_t bytes) {
+        if (b.bytes < bytes) b.alloc(bytes);
+    };
+    grow(s16B, n16 * sizeof(double));
+    grow(s16X, n16 * sizeof(double));
+    grow(s16R, n16 * sizeof(double));
+    grow(s16W, n16 * sizeof(double));
+    grow(s16D, n16 * sizeof(double));
+    grow(s16Df, n16 * sizeof(float));
+    grow(s16W32, n16 * sizeof(float));
+    grow(s16V, (size_t)(m + 1) * n16 * sizeof(float));
+    grow(s16St, (size_t)KC * sts * sizeof(double));
+    grow(s16Part, (size_t)kParts * KC * (m + 2) * sizeof(double));
+    grow(s16R0, KC * sizeof(double));
     arn_small_kernel_attrs();
-    double *Bt = bB.as<double>(), *Xt = bX.as<double>(), *R = bR.as<double>(), *W = bW.as<double>();
-    double *D = bD.as<double>(), *st = bSt.as<double>(), *part = bPart.as<double>(), *r0d = bNb.as<double>();
-    float *Df = bDf.as<float>(), *W32 = bW32.as<float>(), *V = bV.as<float>();
+    double *Bt = s16B.as<double>(), *Xt = s16X.as<double>(), *R = s16R.as<double>(), *W = s16W.as<double>();
+    double *D = s16D.as<double>(), *st = s16St.as<double>(), *part = s16Part.as<double>(), *r0d = s16R0.as<double>();
+    float *Df = s16Df.as<float>(), *W32 = s16W32.as<float>(), *V = s16V.as<float>();
     const int* perm = dPerm.as<int>();
     // status words in mapped host memory: per column {relres, r', steps, -}, then 16 sums
     struct HostStat {
