@@ -4,7 +4,7 @@
 set -o pipefail
 T=${1:-r06i}
 mkdir -p gpurun_out/$T
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$T/tr -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --config2 0 --config5 0 --config4-sz 0 --no-solve --gmres 30 > gpurun_out/$T/bench.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$T/tr -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu --config2 0 --config5 0 --config4-sz 0 --no-solve --gmres 30 --warmup 5 > gpurun_out/$T/bench.log 2>&1 || exit 1
 python3 - gpurun_out/$T $(find gpurun_out/$T/tr -name "*kernel_trace.csv" | head -1) <<'PY' > gpurun_out/$T/gmres_step.txt
 import csv, sys
 rows = sorted(csv.DictReader(open(sys.argv[2])), key=lambda r: int(r["Start_Timestamp"]))
