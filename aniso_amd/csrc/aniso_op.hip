@@ -97,7 +97,6 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_SHARD_NEAR_EARLY")) shardNearEarly = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_UP_TAILS")) upTailsOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_AFTER_PACK")) nearAfterPack = std::atoi(e) != 0;
-    if (const char* e = std::getenv("ANISO_SIDE_CU_RESERVE")) sideCuReserve = std::max(0, std::min(31, std::atoi(e)));
     if (const char* e = std::getenv("ANISO_NEAR_UP")) nearUpOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_ORDER")) nearOrderUp = std::strcmp(e, "first") != 0;
     hmRing = hm_ring_depth();
@@ -164,19 +163,9 @@ void Operator::ensureDevice() {
     HIP_CHECK(hipGetDevice(&device));
     HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
     // side stream at normal priority (a high-priority one measured slower, r01f; the
-    // lowest priority 11-25 % slower, r04l).  ANISO_SIDE_CU_RESERVE = r: the side stream
-    // (the near field beside the sharded chain) leaves r CUs of every 32 to the apply's
-    // stream, so the bottom tier -> pack -> exchange chain finds workgroup slots
-    if (sideCuReserve > 0) {
-        int ncu = 0;
-        HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-        for (int cu = 0; cu < ncu; ++cu)
-            if (cu % 32 >= sideCuReserve) mask[cu / 32] |= 1u << (cu % 32);
-        HIP_CHECK(hipExtStreamCreateWithCUMask(&side, (uint32_t)mask.size(), mask.data()));
-    } else {
-        HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-    }
+    // lowest priority 11-25 % slower, r04l; a CU-masked one serialised the two streams
+    // on a rank of 8: 0.455 against 0.235 ms, r06q)
+    HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&evFork, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
     HIP_CHECK(hipHostMalloc((void**)&topErr, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));

@@ -322,7 +322,6 @@ private:
     // tier-0 launch when the near field's early groups fork after it
     // (ANISO_NEAR_AFTER_PACK=1): packHook set by blockOpShardedDev, packIssued by phase 1
     bool nearAfterPack = false, packIssued = false;
-    int sideCuReserve = 0;  // ANISO_SIDE_CU_RESERVE: CUs of every 32 the side stream leaves free
     std::function<void(hipStream_t)> packHook;
     DevBuf dXT0Part, dXUpRoots, dXUpCnt, dXUpStage;
     DevBuf dXUpTask, dXUpRec, dOxUpSumNode, dOxUpSumPtr, dOxUpSumSrc;
