@@ -97,6 +97,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_SHARD_NEAR_EARLY")) shardNearEarly = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_UP_TAILS")) upTailsOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_AFTER_PACK")) nearAfterPack = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ANISO_SIDE_PRIO")) sidePrio = std::atoi(e);
     if (const char* e = std::getenv("ANISO_NEAR_UP")) nearUpOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_ORDER")) nearOrderUp = std::strcmp(e, "first") != 0;
     hmRing = hm_ring_depth();
@@ -164,8 +165,14 @@ void Operator::ensureDevice() {
     HIP_CHECK(hipStreamCreateWithFlags(&own, hipStreamNonBlocking));
     // side stream at normal priority (a high-priority one measured slower, r01f; the
     // lowest priority 11-25 % slower, r04l; a CU-masked one serialised the two streams
-    // on a rank of 8: 0.455 against 0.235 ms, r06q)
-    HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    // on a rank of 8: 0.455 against 0.235 ms, r06q).  ANISO_SIDE_PRIO: -1 lowest, 1 highest
+    if (sidePrio != 0) {
+        int lo = 0, hi = 0;
+        HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_CHECK(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, sidePrio < 0 ? lo : hi));
+    } else {
+        HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    }
     HIP_CHECK(hipEventCreateWithFlags(&evFork, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
     HIP_CHECK(hipHostMalloc((void**)&topErr, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));

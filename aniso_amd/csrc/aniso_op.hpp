@@ -322,6 +322,7 @@ private:
     // tier-0 launch when the near field's early groups fork after it
     // (ANISO_NEAR_AFTER_PACK=1): packHook set by blockOpShardedDev, packIssued by phase 1
     bool nearAfterPack = false, packIssued = false;
+    int sidePrio = 0;  // ANISO_SIDE_PRIO: the side stream's priority (-1 lowest, 0 default, 1 highest)
     std::function<void(hipStream_t)> packHook;
     DevBuf dXT0Part, dXUpRoots, dXUpCnt, dXUpStage;
     DevBuf dXUpTask, dXUpRec, dOxUpSumNode, dOxUpSumPtr, dOxUpSumSrc;
