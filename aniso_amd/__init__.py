@@ -805,7 +805,8 @@ class Aniso:
         return k.value
 
     def set_deterministic(self, on):
-        """Bitwise-reproducible block applies (per-target M2L waves) on / off."""
+        """Bitwise-reproducible block applies on / off (the clustered M2L with fixed-point
+        LDS sums; ANISO_DET_PER_TARGET=1: one wave per target)."""
         _check(lib().aniso_set_deterministic(self.address, int(bool(on))))
 
     def set_timing(self, on):

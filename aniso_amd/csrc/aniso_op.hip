@@ -98,6 +98,7 @@ Operator::Operator(int sz, int d, int ks_, double g_, int ns_, int np_, int maxL
     if (const char* e = std::getenv("ANISO_UP_TAILS")) upTailsOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_AFTER_PACK")) nearAfterPack = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_SIDE_PRIO")) sidePrio = std::atoi(e);
+    if (const char* e = std::getenv("ANISO_DET_PER_TARGET")) detPerTarget = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_UP")) nearUpOn = std::atoi(e) != 0;
     if (const char* e = std::getenv("ANISO_NEAR_ORDER")) nearOrderUp = std::strcmp(e, "first") != 0;
     hmRing = hm_ring_depth();
@@ -505,8 +506,44 @@ void Operator::buildAttCache() {
                       dStCoef.as<double>(), P, kAttMode, maxSrc, dAttNear.as<double>(), own);
     launch_sigma_diag(geo.N, dPxT.as<double>(), dPyT.as<double>(), dStCoef.as<double>(), P, dSigDiag.as<double>(),
                       own);
+    if (!dAttMax.bytes) dAttMax.alloc(sizeof(double));
+    launch_abs_max(npairs * 256, dAttM2L.as<double>(), dAttMax.as<double>(), own);
     HIP_CHECK(hipStreamSynchronize(own));
     attReady = true;
+}
+
+// The deterministic sums' geometric bound per cluster (harmonic.hip hc_det_scale):
+// 2 x 16 columns x the most pair products one of its LDS slots receives x the largest
+// 1 / gap over its pairs (gap: the boxes' separation along the wider axis, a lower
+// bound on the distance of any two of their Chebyshev nodes).
+void Operator::detBounds() {
+    const int ncl = (int)plan.hmClPtr.size() - 1;
+    if (ncl <= 0 || dHmClBound.bytes >= (size_t)ncl * sizeof(double)) return;
+    std::vector<double> bound(ncl);
+    std::vector<int> cnt;
+    for (int c = 0; c < ncl; ++c) {
+        const int c0 = plan.hmClPtr[c], nt = plan.hmClPtr[c + 1] - c0;
+        const int nh = plan.hmHaloPtr.empty() ? 0 : plan.hmHaloPtr[c + 1] - plan.hmHaloPtr[c];
+        cnt.assign(nt + nh, 0);
+        double ig = 0.0;
+        for (int ti = 0; ti < nt; ++ti) {
+            const int t = plan.hmTgt[c0 + ti];
+            const int64_t p0 = plan.hmPtr[c0 + ti], pd = p0 + plan.hmNDir[c0 + ti], p1 = plan.hmPtr[c0 + ti + 1];
+            for (int64_t e = p0; e < p1; ++e) {
+                const int n = plan.hmSrc[e];
+                const double gx = std::fabs(tree.ncx[t] - tree.ncx[n]) - tree.nrx[t] - tree.nrx[n];
+                const double gy = std::fabs(tree.ncy[t] - tree.ncy[n]) - tree.nry[t] - tree.nry[n];
+                const double gap = std::max(gx, gy);
+                if (!(gap > 0.0)) throw std::logic_error("deterministic M2L: a V-list pair of touching boxes");
+                ig = std::max(ig, 1.0 / gap);
+                ++cnt[ti];
+                if (e >= pd) ++cnt.at(plan.hmSlot[e]);
+            }
+        }
+        const int most = cnt.empty() ? 0 : *std::max_element(cnt.begin(), cnt.end());
+        bound[c] = 2.0 * 16.0 * most * ig;
+    }
+    up(dHmClBound, bound);
 }
 
 // Do the terms of a batched apply have aniso.m's harmonic structure (harmonic.hip)?
@@ -975,6 +1012,15 @@ void Operator::applyBlock(int K, const double* x, int64_t ldx, bool treeIn, cons
     }
     auto m2lClusters = [&](int c0, int c1, hipStream_t st) {
         HcArgs a = hca;
+        if (detSums) {  // fixed-point cluster sums: the bounds of this apply's multipoles first
+            detBounds();
+            const int nn = (int)tree.ncx.size();
+            if (dNodeWmax.bytes < (size_t)nn * sizeof(double)) dNodeWmax.alloc((size_t)nn * sizeof(double));
+            launch_node_wmax(K, nn, dMult.as<double>(), hw, dNodeWmax.as<double>(), st);
+            a.wmax = dNodeWmax.as<double>();
+            a.clBound = dHmClBound.as<double>() + c0;
+            a.emax = dAttMax.as<double>();
+        }
         a.clPtr += c0;
         if (a.haloPtr) a.haloPtr += c0;
         launch_m2l_hc(K, c1 - c0, plan.hmMaxLds, a, st);

@@ -193,14 +193,19 @@ public:
     // of 8: 0.262 against 0.251 ms, same-process A/B r03ls)
     bool topFusedOn() const {
         const int ntier = (int)plan.upTierTask.size() - 1;
-        return useClusters && topFusedMode != 0 && !forceUnfused && top_fused_enabled() && ntier >= 2 &&
+        return useClusters && !detSums && topFusedMode != 0 && !forceUnfused && top_fused_enabled() && ntier >= 2 &&
                ntier <= kMaxTopTiers &&
                plan.upLastLeafTier == 0 && plan.hmClWait.size() + 1 == plan.hmClPtr.size();
     }
-    // bitwise-reproducible applies: the harmonic M2L as one wave per target (a fixed
-    // summation order) instead of the clustered kernel, whose LDS adds of the partner
-    // products land in run-dependent order (repeat applies agree to ~1e-15)
-    void setDeterministic(bool on) { useClusters = !on; }
+    // bitwise-reproducible applies: the clustered M2L with its LDS
+    // sums in fixed point (integer adds: order-independent) and the upper up tiers as
+    // launches of their own; ANISO_DET_PER_TARGET=1 keeps the round-2 form instead (one
+    // wave per target, every sum in a fixed order, every block read from both ends)
+    void setDeterministic(bool on) {
+        detSums = on && !detPerTarget;
+        useClusters = !(on && detPerTarget);
+    }
+    bool deterministicOn() const { return detSums || !useClusters; }
     bool modeCached(int id) const { return id >= 0 && id < kernelSize && modes[id].ready; }
     int kernelSize = 0;
     // stage timing with HIP events recorded in-stream (no host sync per apply);
@@ -257,6 +262,8 @@ private:
     void buildAttCache();
     bool useAtt = false, attReady = false;
     DevBuf dAttM2L, dAttNear, dSigDiag, dAttPtr, dAttSrc, dAttBlk, dAttOwner, dAttOther;
+    DevBuf dAttMax;                // max |E| of dAttM2L (the deterministic sums' bound)
+    DevBuf dHmClBound, dNodeWmax;  // the deterministic sums: per cluster, per node
     DevBuf dHmClPtr, dHmTgt, dHmPtr, dHmSrc, dHmBlk, dHmSlot, dHmNDir;  // cluster plan
     DevBuf dHmHaloPtr, dHmHaloPos, dHmPart, dDnChainFold;  // the halo form (Plan::hmHaloPtr)
     DevBuf dHmClWait, dTopCnt;  // fused top-of-tree launch: per-cluster wait tier, per-tier counters
@@ -338,6 +345,9 @@ private:
     // the fused launch computes the tier itself (tests: 0 makes every waiter compute)
     unsigned topSpinLimit = 1u << 16;
     bool useClusters = true;
+    bool detSums = false;       // the clustered M2L's fixed-point sums (setDeterministic)
+    bool detPerTarget = false;  // ANISO_DET_PER_TARGET
+    void detBounds();           // dHmClBound from the plan (once)
     std::map<std::string, DevBuf> modeTabs;
     const CorrFold& corrTable(int K, int nterm, const int* ids, const double* mixes);
     std::map<std::string, CorrFold> corrTabs;

@@ -241,8 +241,28 @@ __device__ __forceinline__ void hm_entry2(double e, double dx, double dy2, const
 
 // the end of a target in the cluster M2L: its 4 x K row sums per lane summed over the
 // 16 columns (lane bits 2..5) and added to its LDS locals at `at` (16 x K)
-template <int K>
-__device__ __forceinline__ void m2l_hc_store_target(double (&c)[4][K], double* at, int lane, int s, int q) {
+constexpr int kHcMaxWaves = 8;  // the largest cluster workgroup (512 threads)
+
+// The deterministic cluster sums: every add into a cluster's LDS
+// slots is an integer add of a fixed-point value (a cluster-wide scale 2^S with the
+// slot bound below 2^62, hc_det_scale), so the sums do not depend on the order in which
+// the waves add.  fx_of rounds v 2^S to the nearest integer and splits it into the
+// two 32-bit words of its two's complement form (|v 2^S| < 2^62: hi fits an int).
+__device__ __forceinline__ unsigned long long fx_of(double v, double sc) {
+    const double x = __builtin_rint(v * sc);
+    const double hi = __builtin_floor(x * 0x1p-32);
+    const double lo = __builtin_fma(-hi, 0x1p32, x);  // exact: an integer in [0, 2^32)
+    return ((unsigned long long)(unsigned)(int)hi << 32) | (unsigned long long)(unsigned)lo;
+}
+template <bool DET>
+__device__ __forceinline__ void slot_add(double* d, double v, double sc) {
+    if constexpr (DET) atomicAdd(reinterpret_cast<unsigned long long*>(d), fx_of(v, sc));
+    else atomicAdd(d, v);
+}
+
+template <int K, bool DET = false>
+__device__ __forceinline__ void m2l_hc_store_target(double (&c)[4][K], double* at, int lane, int s, int q,
+                                                    double sc = 0.0) {
     if constexpr (K == 5) {
         // sum over the 16 columns (lane bits 2..5) as a reduce-scatter of the lane's
         // 20 row sums (rows 4q + j, entries i; v = 5 j + i): 20 -> 10 (lane ^ 32),
@@ -272,7 +292,7 @@ __device__ __forceinline__ void m2l_hc_store_target(double (&c)[4][K], double* a
             const int w = u + 2 * h0, v2 = w + 3 * h1;
             if (w <= 2 && v2 <= 4) {
                 const int v0 = v2 + k16 + k32, j = v0 / 5, i = v0 - 5 * j;
-                atomicAdd(d + (4 * q + j) * K + i, sum);
+                slot_add<DET>(d + (4 * q + j) * K + i, sum, sc);
             }
         }
     } else {
@@ -295,7 +315,7 @@ __device__ __forceinline__ void m2l_hc_store_target(double (&c)[4][K], double* a
         for (int i = 0; i < K; ++i) {
             const double sel = jr == 0 ? c[0][i] : jr == 1 ? c[1][i] : jr == 2 ? c[2][i] : c[3][i];
             const double v = __shfl(sel, srcLane);
-            if ((i & 3) == q) atomicAdd(d + i, v);
+            if ((i & 3) == q) slot_add<DET>(d + i, v, sc);
         }
     }
 }
@@ -317,18 +337,48 @@ __device__ __forceinline__ HcSlots hc_slots(int cid, const HcArgs& a) {
 
 // the cluster's end: its targets' locals stored, its halo slots stored to their
 // partials (both scaled by om; the down pass adds the partials, k_down_tier)
-template <int K>
-__device__ __forceinline__ void hc_flush(const HcSlots& c, const HcArgs& a, const double* acc) {
+template <int K, bool DET = false>
+__device__ __forceinline__ void hc_flush(const HcSlots& c, const HcArgs& a, const double* acc, double isc = 1.0) {
     constexpr int RK = kRank * K;
+    auto val = [&](int e) {
+        if constexpr (DET) return (double)reinterpret_cast<const long long*>(acc)[e] * isc;
+        else return acc[e];
+    };
     for (int e = threadIdx.x; e < c.nt * RK; e += blockDim.x) {
         const int k = e / RK, r = e - k * RK;
-        a.local[(size_t)a.tgt[c.c0 + k] * RK + r] = a.hw.om[r % K] * acc[e];
+        a.local[(size_t)a.tgt[c.c0 + k] * RK + r] = a.hw.om[r % K] * val(e);
     }
-    const double* ah = acc + (size_t)c.nt * RK;
+    const int hb = c.nt * RK;
     for (int e = threadIdx.x; e < c.nh * RK; e += blockDim.x) {
         const int k = e / RK, r = e - k * RK;
-        a.hpart[(size_t)a.haloPos[c.h0 + k] * RK + r] = a.hw.om[r % K] * ah[e];
+        a.hpart[(size_t)a.haloPos[c.h0 + k] * RK + r] = a.hw.om[r % K] * val(hb + e);
     }
+}
+
+// DET: the cluster's fixed-point scale.  Every value a slot receives is a sum of
+// entries |E T_i (E/r) sum_b T_b hw_b x_b| <= Emax / gap * W(node) (|T| <= 1, E <= Emax,
+// r >= the box gap), W(node) = max over its columns of sum_b |hw_b x_b| (k_node_wmax);
+// a slot's total is within clBound[c] (the host's 16 columns x the most pairs one
+// slot receives x the largest 1/gap of the cluster's pairs, x 2) times Emax times the
+// largest W of the nodes the cluster reads.  S puts that bound below 2^62.
+__device__ __forceinline__ void hc_det_scale(int cid, const HcSlots& cs, const HcArgs& a, double* red,
+                                             double& sc, double& isc) {
+    double mw = 0.0;
+    for (int k = threadIdx.x; k < cs.nt; k += blockDim.x) mw = fmax(mw, a.wmax[a.tgt[cs.c0 + k]]);
+    const int64_t e0 = a.ptr[cs.c0], e1 = a.ptr[cs.c0 + cs.nt];
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) mw = fmax(mw, a.wmax[a.src[e]]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mw = fmax(mw, __shfl_xor(mw, off));
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = mw;
+    __syncthreads();
+    mw = 0.0;
+    for (int w = 0; w < (int)(blockDim.x / kWave); ++w) mw = fmax(mw, red[w]);
+    const double B = a.clBound[cid] * a.emax[0] * mw;
+    int ex = 0;
+    if (B > 0.0) (void)frexp(B, &ex);  // B < 2^ex
+    const int S = min(1000, max(-1000, 62 - ex));
+    sc = ldexp(1.0, S);
+    isc = ldexp(1.0, -S);
 }
 
 // The same distances for the 4-wave form (LR): from wave-uniform values only,
@@ -350,7 +400,7 @@ __device__ __forceinline__ double cheb_dx_lr(int j, double axs, double r, const 
 // adds is not fixed (results repeat to rounding, not bitwise).
 // LR: the 4-wave-per-SIMD form (<= 128 VGPRs, k_m2l_hc / k_top_m2l_hc with WPE = 4)
 // for launches whose LDS allows 4 workgroups per CU (small clusters: shards)
-template <int K, int NR, bool LR = false>
+template <int K, int NR, bool LR = false, bool DET = false>
 __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, double* sm) {
     const int* __restrict__ clPtr = a.clPtr;
     const int* __restrict__ tgt = a.tgt;
@@ -383,7 +433,13 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
     __shared__ int nextTarget;
     for (int i = threadIdx.x; i < nsl * RK; i += blockDim.x) acc[i] = 0.0;
     if (threadIdx.x == 0) nextTarget = nw;
-    __syncthreads();
+    [[maybe_unused]] double sc = 0.0, isc = 1.0;
+    if constexpr (DET) {
+        __shared__ double red[kHcMaxWaves];
+        hc_det_scale(cid, cs, a, red, sc, isc);  // (its barrier also publishes the zeroed slots)
+    } else {
+        __syncthreads();
+    }
     const int lane = threadIdx.x & (kWave - 1);
     const int s = lane >> 2, q = lane & 3;
     const double chx = P->cheb[s & 3], chy = P->cheb[s >> 2];
@@ -510,8 +566,19 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                         hm_entry2<K, NR>(e4[j], __builtin_fma(-trx, chu[j], axs), dy2, xw, xa + (4 * q + j) * K, c[j], ob);
     #pragma unroll
                     for (int i = 0; i < K; ++i) ob[i] = quad_sum(ob[i]);  // rows 4q'+j over the quad
-                    if (q == 0) {
-                        double* d = acc + ((size_t)sl * kRank + s) * K;
+                    double* d = acc + ((size_t)sl * kRank + s) * K;
+                    if constexpr (DET) {
+                        // the quad's lanes share the K conversions: lane q adds entries q, q + 4, ..
+                        const double sq = (q & 1) ? -sc : sc;
+    #pragma unroll
+                        for (int i0 = 0; i0 < K; i0 += 4) {
+                            double v = ob[i0];
+    #pragma unroll
+                            for (int u = 1; u < 4; ++u)
+                                if (i0 + u < K && q == u) v = ob[i0 + u];
+                            if (i0 + q < K) slot_add<true>(d + i0 + q, v, sq);
+                        }
+                    } else if (q == 0) {
     #pragma unroll
                         for (int i = 0; i < K; ++i) atomicAdd(d + i, (i & 1) ? -ob[i] : ob[i]);
                     }
@@ -529,13 +596,13 @@ __device__ __forceinline__ void m2l_hc_cluster(const int cid, const HcArgs& a, d
                     pair(jj + 1, m0, m1, xn, hcx, hrx, hcy, hry);
                 }
             }
-        m2l_hc_store_target<K>(c, acc + (size_t)ti * kRank * K, lane, s, q);
+        m2l_hc_store_target<K, DET>(c, acc + (size_t)ti * kRank * K, lane, s, q, sc);
         int nx = 0;
         if (lane == 0) nx = atomicAdd(&nextTarget, 1);
         ti = __builtin_amdgcn_readlane(nx, 0);
     }
     __syncthreads();
-    hc_flush<K>(cs, a, acc);
+    hc_flush<K, DET>(cs, a, acc, isc);
 }
 
 // ---- the ring form of the cluster M2L ----
@@ -805,11 +872,11 @@ constexpr int kHcWaves = WPE == 8 ? 4 : WPE == 6 ? 3 : WPE;
 template <int WPE>
 constexpr bool kHcLR = WPE == 4 || WPE == 8;
 
-template <int K, int NR, int WPE>
+template <int K, int NR, int WPE, bool DET = false>
 __global__ void __launch_bounds__(kHcThreads<WPE>) __attribute__((amdgpu_waves_per_eu(kHcWaves<WPE>)))
 k_m2l_hc(HcArgs a) {
     extern __shared__ double sm[];
-    m2l_hc_cluster<K, NR, kHcLR<WPE>>((int)blockIdx.x, a, sm);
+    m2l_hc_cluster<K, NR, kHcLR<WPE>, DET>((int)blockIdx.x, a, sm);
 }
 
 // ----------------------------------------------------------------- fused top of tree + M2L
@@ -1607,6 +1674,17 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s) {
     const int form = depth == 0 ? hm_form(K, a.wpe, shm) : 3;
     if (form != 3) shm = m2l_hc_lds(K, maxCl, depth, xl, hm_waves(form));
     if (shm > 160 * 1024) throw std::invalid_argument("harmonic M2L: a cluster and its halo exceed the LDS");
+    if (a.wmax) {  // the deterministic sums: the one-block 3-wave-per-SIMD forms (whatever the ring knob says)
+        const int fd = hm_form(K, 0, shm);
+        const size_t shd = m2l_hc_lds(K, maxCl, 0, false, hm_waves(fd));
+        ANISO_HM_DISPATCH_K(K, ({
+            auto f = fd == 6 ? k_m2l_hc<KK, 1, 6, true> : k_m2l_hc<KK, 1, 3, true>;
+            set_lds(f, shd);
+            f<<<ncl, hm_threads(fd), shd, s>>>(a);
+        }));
+        HIP_LAUNCH_CHECK();
+        return;
+    }
     ANISO_HM_DISPATCH_K(K, ANISO_HM_DISPATCH_RING(depth, ({
         if constexpr (DD == 0 || KK > kRingMaxK) {
             auto f = form == 6 ? k_m2l_hc<KK, 1, 6> : k_m2l_hc<KK, 1, 3>;
@@ -1622,6 +1700,50 @@ void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s) {
             f<<<ncl, 256, shm, s>>>(a);
         }
     })));
+    HIP_LAUNCH_CHECK();
+}
+
+// The deterministic sums' bounds (hc_det_scale): W per node, the largest |E|
+template <int K>
+__global__ void __launch_bounds__(256) k_node_wmax(int nnodes, const double* __restrict__ mult, HarmWeights hw,
+                                                   double* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (node, column): 16 lanes per node
+    const int64_t n = t >> 4;
+    double w = 0.0;
+    if (n < nnodes) {
+        const double* m = mult + (size_t)t * K;
+#pragma unroll
+        for (int b = 0; b < K; ++b) w += fabs(hw.hw[b] * m[b]);
+    }
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) w = fmax(w, __shfl_xor(w, off));
+    if (n < nnodes && (t & 15) == 0) out[n] = w;
+}
+
+__global__ void __launch_bounds__(256) k_abs_max(int64_t n, const double* __restrict__ x,
+                                                 unsigned long long* __restrict__ out) {
+    double m = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        m = fmax(m, fabs(x[i]));
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = fmax(m, __shfl_xor(m, off));
+    // non-negative doubles order as their bit patterns
+    if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)__double_as_longlong(m));
+}
+
+void launch_node_wmax(int K, int nnodes, const double* mult, const HarmWeights& hw, double* out, hipStream_t s) {
+    if (nnodes <= 0) return;
+    const int nb = (int)(((int64_t)nnodes * 16 + 255) / 256);
+    ANISO_HM_DISPATCH_K(K, (k_node_wmax<KK><<<nb, 256, 0, s>>>(nnodes, mult, hw, out)));
+    HIP_LAUNCH_CHECK();
+}
+
+void launch_abs_max(int64_t n, const double* x, double* out, hipStream_t s) {
+    const hipError_t e = hipMemsetAsync(out, 0, sizeof(double), s);
+    if (e != hipSuccess) throw_hip(e, __FILE__, __LINE__);
+    if (n <= 0) return;
+    const int nb = (int)std::min<int64_t>(4096, (n + 255) / 256);
+    k_abs_max<<<nb, 256, 0, s>>>(n, x, reinterpret_cast<unsigned long long*>(out));
     HIP_LAUNCH_CHECK();
 }
 

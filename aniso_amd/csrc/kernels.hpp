@@ -219,6 +219,12 @@ struct HcArgs {
     const int* haloPtr = nullptr;
     const int* haloPos = nullptr;
     double* hpart = nullptr;
+    // the deterministic sums (k_m2l_hc only): per node the bound W of
+    // its weighted multipole (k_node_wmax), per cluster the host's geometric bound, the
+    // largest stored E (device scalar).  wmax == nullptr: the ds_add_f64 sums
+    const double* wmax = nullptr;
+    const double* clBound = nullptr;
+    const double* emax = nullptr;
 };
 // The fused top-of-tree + clustered M2L launch (harmonic.hip k_top_m2l_hc, DESIGN.md
 // §3.10): blocks 0 .. nUp - 1 run the up tasks of tiers 1 .. ntier - 1 (tier k's
@@ -351,6 +357,10 @@ void launch_top_m2l_hc(int K, int ncl, int maxCl, const UpArgs& u, const TopArgs
 // whether launch_near_hm would run the staged near field with fused corrections
 bool near_hs_fusable(int nl, int maxLeaf, int nsMax, const uint16_t* nearLoc, const NearCorr* corr, int flags);
 void launch_m2l_hc(int K, int ncl, int maxCl, const HcArgs& a, hipStream_t s);
+// the deterministic cluster sums' bounds: out[n] = max over node n's 16 columns of
+// sum_b |hw_b mult_b|; out[0] = max |x|
+void launch_node_wmax(int K, int nnodes, const double* mult, const HarmWeights& hw, double* out, hipStream_t s);
+void launch_abs_max(int64_t n, const double* x, double* out, hipStream_t s);
 
 int hm_ring_depth();  // ANISO_HM_RING (read at handle creation): the cluster M2L's LDS ring depth
 int hm_ring_xl(int K, int maxCl, int depth);  // its target multipole in LDS / VGPRs / ring off (1, 0, -1)

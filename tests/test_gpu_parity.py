@@ -626,8 +626,9 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, ring, monk
     read once too (the halo form: partner products in LDS halo slots, folded into the
     locals after the launch); h: ANISO_HM_HALO=0, the directed copies instead.
     Also checks that in-cluster pairs exist, that the cluster plan reads fewer E
-    blocks (the halo form: exactly the stored blocks), and that the deterministic
-    mode repeats bitwise."""
+    blocks (the halo form: exactly the stored blocks), and that both deterministic
+    forms (one wave per target; the clusters with fixed-point LDS sums, which take the
+    one-block form whatever the ring knob says) repeat bitwise."""
     torch = _torch()
     import aniso_amd
 
@@ -643,9 +644,10 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, ring, monk
     # clusters, which small trees only reach with 4-target clusters: no in-cluster pairs)
     monkeypatch.setenv("ANISO_HM_CLDEPTH", "3")
     outs, st = [], []
-    for det in (False, True):
+    for det in (False, True, "fixed"):
+        monkeypatch.setenv("ANISO_DET_PER_TARGET", "0" if det == "fixed" else "1")
         a = aniso_amd.Aniso(sz, d, ks, 0.8, 8, 4, ml)
-        a.set_deterministic(det)
+        a.set_deterministic(bool(det))
         xy = a.getNodes()
         a.setCoeff(*rough_coeffs(xy, 3))
         for m in range(2 * ks - 1):
@@ -661,6 +663,7 @@ def test_harmonic_clusters_match_per_target_waves(sz, d, ks, ml, sym, ring, monk
             assert torch.equal(out, again)
         a.sync()
         outs.append(out.cpu().numpy())
+    assert _rel(outs[2], outs[1]) <= 1e-13
     assert st[0]["harmonic"] == 1 and st[0]["hm_clusters"] > 0 and st[1]["hm_clusters"] == 0
     assert st[0]["hm_dual_pairs"] > 0 and st[0]["hm_block_reads"] < st[1]["hm_block_reads"]
     if not halo:
@@ -703,14 +706,20 @@ def test_small_clusters_on_shards_match_unsharded(ks, world, ring, monkeypatch):
     assert err <= 1e-13, err
 
 
-def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
+@pytest.mark.parametrize("env", ["", "ANISO_DET_PER_TARGET=1", "ANISO_HM_HALO=0", "ANISO_HM_WPE=6"])
+def test_deterministic_block_matvec_repeats_bitwise_at_config3_size(env, monkeypatch):
     """aniso_set_deterministic at BASELINE's 1M-point block matvec: repeat applies
     are bitwise identical, and equal the default (clustered) matvec to 1e-13.  The
     default runs the upper up tiers inside the M2L launch (k_top_m2l_hc), so this
-    also checks its in-launch hand-offs against the plain tier launches."""
+    also checks its in-launch hand-offs against the plain tier launches.  Forms: the
+    clustered M2L with fixed-point LDS sums (the default deterministic mode; with and
+    without the halo slots, in 6-wave workgroups) and the round-2 per-target M2L."""
     torch = _torch()
     import aniso_amd
 
+    for kv in filter(None, env.split(",")):
+        k, v = kv.split("=")
+        monkeypatch.setenv(k, v)
     a = aniso_amd.Aniso(1024, 1, 5, 0.8, 10, 4, 20)
     xy = a.getNodes()
     a.setCoeff(*rough_coeffs(xy, 2))
@@ -727,6 +736,36 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size():
     torch.cuda.synchronize()
     assert torch.equal(o1, o2)
     assert float(torch.linalg.norm(o1 - ref) / torch.linalg.norm(ref)) <= 1e-13
+
+
+@pytest.mark.parametrize("ks", [2, 4, 5, 8])
+@pytest.mark.parametrize("scale", [1.0, 1e150, 1e-150])
+def test_deterministic_fixed_point_sums_scale_and_block_counts(ks, scale):
+    """The clustered M2L's fixed-point sums (harmonic.hip hc_det_scale) at every
+    harmonic block count and at inputs 1e+-150 times the usual size (the cluster scale
+    follows the multipoles; no overflow, no loss): bitwise repeats, and the default
+    matvec's result to 1e-13.  A zero input gives zero."""
+    torch = _torch()
+    import aniso_amd
+
+    a = aniso_amd.Aniso(256, 1, ks, 0.8, 10, 4, 20)
+    xy = a.getNodes()
+    a.setCoeff(*rough_coeffs(xy, 3))
+    for m in range(2 * ks - 1):
+        a.cache(m)
+    U = scale * torch.tensor(np.random.default_rng(9).uniform(-1, 1, (ks, a.N)), device="cuda")
+    ref = torch.zeros_like(U)
+    a.block_op_dev(2, U, ref, tree=True)
+    a.set_deterministic(True)
+    o1, o2, z = torch.zeros_like(U), torch.zeros_like(U), torch.ones_like(U)
+    a.block_op_dev(2, U, o1, tree=True)
+    a.block_op_dev(2, U, o2, tree=True)
+    a.block_op_dev(2, torch.zeros_like(U), z, tree=True)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert torch.isfinite(o1).all()
+    assert float(torch.linalg.norm(o1 - ref) / torch.linalg.norm(ref)) <= 1e-13
+    assert not torch.any(z)
 
 
 @pytest.mark.parametrize("knob", ["ANISO_OVERLAP=1", "ANISO_FUSE_SUB=0", "ANISO_HARMONIC=0", "ANISO_HM_RING=3",
