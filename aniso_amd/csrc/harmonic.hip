@@ -1191,6 +1191,19 @@ __device__ __forceinline__ void near_up_tail(int g, bool active, int nT, int64_t
     const int64_t kp = tb + (on ? t : 0);
     const int* G = n.upGrp + (size_t)g * kNearUpInts;
     const Params* __restrict__ P = n.upP;
+    // the tail's global reads issued ahead of the stage that uses them (the near loop's
+    // registers are free now): the M2M row of this lane's child quadrant (G[4 m + c] & 3)
+    // here, before the first barrier; the root's row (parent slot m: G[16 + m] = m,
+    // Plan::buildNearUp) at the start of the M2M stage
+    const int um = threadIdx.x >> 6, ur = (threadIdx.x >> 2) & 15, uc = threadIdx.x & 3;
+    const int code = G[4 * um + uc];
+    const int parentNode = G[20 + um], rootNode = G[24];
+    double Rc[kRank];
+    {
+        const double* R = &P->R[code & 3][ur * kRank];
+#pragma unroll
+        for (int rr = 0; rr < kRank; ++rr) Rc[rr] = R[rr];
+    }
     double Sx[kNP], Sy[kNP];
     {
         const int nd = active ? leafNode : 0;
@@ -1234,49 +1247,48 @@ __device__ __forceinline__ void near_up_tail(int g, bool active, int nT, int64_t
             for (int b = 0; b < K; ++b) n.upMult[((size_t)leafNode * kRank + ln) * K + b] = acc[b];
     }
     __syncthreads();
+    double Rr[kRank];
+    {
+        const double* R2 = &P->R[threadIdx.x & 3][((threadIdx.x >> 2) & 15) * kRank];
+#pragma unroll
+        for (int rr = 0; rr < kRank; ++rr) Rr[rr] = threadIdx.x < 64 ? R2[rr] : 0.0;
+    }
     {  // parent m, row r, child c (leaf slot 4 m + c, quadrant G[4 m + c] & 3)
-        const int m = threadIdx.x >> 6, r = (threadIdx.x >> 2) & 15, c = threadIdx.x & 3;
-        const int code = G[4 * m + c];
-        const double* R = &P->R[code & 3][r * kRank];
+        const int m = um, r = ur, c = uc;
         const double* x = PT + (size_t)(4 * m + c) * 16 * PW;
         double acc[K];
 #pragma unroll
         for (int b = 0; b < K; ++b) acc[b] = 0.0;
-#pragma unroll 2
-        for (int rr = 0; rr < kRank; ++rr) {  // 2 rows per step: the near loop's register budget
-            const double rv = R[rr];
 #pragma unroll
-            for (int b = 0; b < K; ++b) acc[b] = __builtin_fma(rv, x[rr * K + b], acc[b]);
-        }
+        for (int rr = 0; rr < kRank; ++rr)
+#pragma unroll
+            for (int b = 0; b < K; ++b) acc[b] = __builtin_fma(Rc[rr], x[rr * K + b], acc[b]);
 #pragma unroll
         for (int b = 0; b < K; ++b) acc[b] = quad_sum(acc[b]);
         if (c == 0) {
 #pragma unroll
             for (int b = 0; b < K; ++b) {
                 PM[(m * kRank + r) * K + b] = acc[b];
-                n.upMult[((size_t)G[20 + m] * kRank + r) * K + b] = acc[b];
+                n.upMult[((size_t)parentNode * kRank + r) * K + b] = acc[b];
             }
         }
     }
     __syncthreads();
     if (threadIdx.x < 64) {  // the root: row r, parent m
         const int r = threadIdx.x >> 2, m = threadIdx.x & 3;
-        const double* R = &P->R[G[16 + m]][r * kRank];
         const double* x = PM + (size_t)m * RK;
         double acc[K];
 #pragma unroll
         for (int b = 0; b < K; ++b) acc[b] = 0.0;
-#pragma unroll 2
-        for (int rr = 0; rr < kRank; ++rr) {  // 2 rows per step: the near loop's register budget
-            const double rv = R[rr];
 #pragma unroll
-            for (int b = 0; b < K; ++b) acc[b] = __builtin_fma(rv, x[rr * K + b], acc[b]);
-        }
+        for (int rr = 0; rr < kRank; ++rr)
+#pragma unroll
+            for (int b = 0; b < K; ++b) acc[b] = __builtin_fma(Rr[rr], x[rr * K + b], acc[b]);
 #pragma unroll
         for (int b = 0; b < K; ++b) acc[b] = quad_sum(acc[b]);
         if (m == 0)
 #pragma unroll
-            for (int b = 0; b < K; ++b) n.upMult[((size_t)G[24] * kRank + r) * K + b] = acc[b];
+            for (int b = 0; b < K; ++b) n.upMult[((size_t)rootNode * kRank + r) * K + b] = acc[b];
     }
 }
 
