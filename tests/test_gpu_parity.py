@@ -1689,7 +1689,8 @@ class _ThreadCollectives:
                                                (64, 8, "1", 1, 20), (64, 3, "1", 1, 20), (96, 3, "1", 1, 20),
                                                (40, 2, "1", 1, 3), (32, 2, "1", 2, 20), (64, 3, "mixed", 1, 20),
                                                (64, 2, "spin0", 1, 20), (256, 4, "1", 1, 20), (512, 8, "1", 1, 20),
-                                               (256, 4, "partial0", 1, 20), (512, 8, "tails", 1, 20)])
+                                               (256, 4, "partial0", 1, 20), (512, 8, "tails", 1, 20),
+                                               (256, 4, "det", 1, 20)])
 def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     """The library's one-call sharded block matvec (aniso_block_op_sharded_dev) with
     `world` ranks as threads of one process on the box's GPU, each rank's input valid
@@ -1708,13 +1709,15 @@ def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     ANISO_UPPER_PARTIAL=0, since the partial sums leave phase 2 no up tier).
     The one-collective form exchanges the upper multipoles as partial sums where every
     rank's plan forms them (records at 256 and 512 points per side; "partial0":
-    ANISO_UPPER_PARTIAL=0, the root records and the upper tiers on every rank)."""
+    ANISO_UPPER_PARTIAL=0, the root records and the upper tiers on every rank).
+    "det": every rank in the deterministic mode (fixed-point cluster sums): the two
+    matvecs are bitwise equal on every rank, and equal the default unsharded one."""
     torch = _torch()
     import threading
 
     import aniso_amd
 
-    monkeypatch.setenv("ANISO_ONE_EXCHANGE", "1" if one in ("mixed", "spin0", "partial0", "tails") else one)
+    monkeypatch.setenv("ANISO_ONE_EXCHANGE", "1" if one in ("mixed", "spin0", "partial0", "tails", "det") else one)
     # "tails": the upper partial tasks as tails of the own tier-0 launch (ANISO_UP_TAILS=1)
     monkeypatch.setenv("ANISO_UP_TAILS", "1" if one == "tails" else "0")
     monkeypatch.setenv("ANISO_UPPER_PARTIAL", "0" if one in ("spin0", "partial0") else "1")
@@ -1740,6 +1743,7 @@ def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
         h.setCoeff(*coef)
         for m in range(2 * ks - 1):
             h.cache(m)
+        h.set_deterministic(one == "det")
         hs.append(h)
     oks = [h.shard_exchange_one()["ok"] for h in hs]
     staged = d == 1 and ml == 20  # the harmonic near field from the input, fused corrections
@@ -1755,10 +1759,15 @@ def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
             x = torch.full_like(X, float("nan"))
             x[:, b:e] = X[:, b:e]
             y = torch.zeros_like(X)
+            first = None
             for _ in range(2):  # a second matvec reuses the exchange plan
                 h.block_op_sharded_dev(2, x, y)
+                if first is None:
+                    first = y[:, b:e].clone()
             h.sync()
             outs[r] = y[:, b:e].clone()
+            if one == "det" and not torch.equal(first, outs[r]):
+                raise AssertionError(f"rank {r}: deterministic matvecs differ")
         except Exception as ex:  # noqa: BLE001
             shared["errors"].append(repr(ex))
             shared["bar"].abort()
@@ -1773,7 +1782,7 @@ def test_native_exchange_ranks_as_threads(sz, world, one, d, ml, monkeypatch):
     assert not torch.isnan(Y).any()
     assert float(torch.linalg.norm(Y - ref) / torch.linalg.norm(ref)) <= 1e-13
     used = [h.stats()["one_exchange_applies"] for h in hs]
-    one_used = one in ("1", "spin0", "partial0", "tails") and all(oks) and staged
+    one_used = one in ("1", "spin0", "partial0", "tails", "det") and all(oks) and staged
     assert used == [2 * int(one_used)] * world
     ups = [h.shard_upper_partials() for h in hs]
     assert [h.stats()["upper_partial_applies"] for h in hs] == [2 * int(one_used and all(u["on"] for u in ups))] * world
