@@ -333,6 +333,7 @@ void Operator::uploadPlan() {
         up(dHmClWait, plan.hmClWait);
         up(dHmHaloPtr, plan.hmHaloPtr);
         up(dHmHaloPos, plan.hmHaloPos);
+        dHmClBound.alloc(0);  // the deterministic sums' bounds follow the plan (detBounds)
         dTopCnt.alloc((kMaxTopTiers + 1) * sizeof(unsigned));
         dTopSteals.alloc(sizeof(unsigned));
         HIP_CHECK(hipMemset(dTopSteals.p, 0, sizeof(unsigned)));

@@ -738,6 +738,63 @@ def test_deterministic_block_matvec_repeats_bitwise_at_config3_size(env, monkeyp
     assert float(torch.linalg.norm(o1 - ref) / torch.linalg.norm(ref)) <= 1e-13
 
 
+def test_deterministic_bounds_follow_a_new_shard_layout():
+    """The fixed-point sums' per-cluster bounds are built from the plan (detBounds): a
+    handle that ran deterministic applies on the whole tree and is then re-sharded
+    must rebuild them, so its two-phase shard apply (with a second rank) still equals
+    the default unsharded matvec and repeats bitwise."""
+    torch = _torch()
+    import aniso_amd
+
+    sz, ks, world = 128, 5, 2
+    full = aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20)
+    xy = full.getNodes()
+    coef = rough_coeffs(xy, 4)
+    full.setCoeff(*coef)
+    for m in range(2 * ks - 1):
+        full.cache(m)
+    X = torch.tensor(np.random.default_rng(3).uniform(-1, 1, (ks, full.N)), device="cuda")
+    ref = torch.zeros_like(X)
+    full.block_op_dev(2, X, ref, tree=True)
+    full.set_deterministic(True)
+    tmp = torch.zeros_like(X)
+    full.block_op_dev(2, X, tmp, tree=True)  # the whole tree's bounds
+    torch.cuda.synchronize()
+    hs = [full] + [aniso_amd.Aniso(sz, 1, ks, 0.8, 10, 4, 20) for _ in range(world - 1)]
+    for r, h in enumerate(hs):
+        h.set_shard(r, world)
+        h.setCoeff(*coef)
+        for m in range(2 * ks - 1):
+            h.cache(m)
+        h.set_deterministic(True)
+    got = []
+    for rep in range(2):
+        sends, outs, info = [], [], []
+        for h in hs:
+            b, e = h.shard()
+            ex = h.shard_exchange(ks)
+            xr = torch.full_like(X, float("nan"))
+            xr[:, b:e] = X[:, b:e]
+            for lo, hi in h.shard_halo():
+                xr[:, lo:hi] = X[:, lo:hi]
+            y = torch.zeros(ks, max(e - b, 1), dtype=torch.float64, device="cuda")
+            rs = torch.zeros(max(ex["root_chunk"] * ex["root_record"], 1), dtype=torch.float64, device="cuda")
+            h.block_op_begin_dev(2, xr, y, rs)
+            sends.append(rs[: ex["root_chunk"] * ex["root_record"]])
+            outs.append(y)
+            info.append((xr, b, e))
+        recv = torch.cat(sends)
+        Y = torch.zeros_like(X)
+        for h, y, (xr, b, e) in zip(hs, outs, info):
+            h.block_op_end_dev(2, xr, y, recv, world)
+            Y[:, b:e] = y[:, : e - b]
+        torch.cuda.synchronize()
+        got.append(Y)
+    assert torch.equal(got[0], got[1])
+    assert not torch.isnan(got[0]).any()
+    assert float(torch.linalg.norm(got[0] - ref) / torch.linalg.norm(ref)) <= 1e-13
+
+
 @pytest.mark.parametrize("ks", [2, 4, 5, 8])
 @pytest.mark.parametrize("scale", [1.0, 1e150, 1e-150])
 def test_deterministic_fixed_point_sums_scale_and_block_counts(ks, scale):
